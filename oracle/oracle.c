@@ -1,0 +1,2215 @@
+/*
+ * ORACLE / TEST INFRASTRUCTURE ONLY -- see oracle.h for scope and the list of
+ * reference files restated here.  Never linked into the product.
+ *
+ * All reference paths below are relative to /root/reference:
+ *   core/ = parser-core/src/main/java/nl/basjes/parse/core/
+ *   hp/   = httpdlog/httpdlog-parser/src/main/java/nl/basjes/parse/httpdlog/
+ */
+#include "oracle.h"
+
+#include <pthread.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "jregex.h"
+#include "ostr.h"
+
+void oracle_md5_hex(const unsigned char *msg, size_t len, char out[33]);
+
+/* ================================================================ utils */
+static void *xmalloc(size_t n) {
+    void *p = calloc(1, n ? n : 1);
+    if (!p) { fprintf(stderr, "oracle: out of memory\n"); abort(); }
+    return p;
+}
+static char *xstrdup(const char *s) {
+    size_t n = strlen(s);
+    char *d = (char *)xmalloc(n + 1);
+    memcpy(d, s, n + 1);
+    return d;
+}
+static char *xfmt(const char *f, ...) {
+    va_list ap;
+    va_start(ap, f);
+    char tmp[4096];
+    vsnprintf(tmp, sizeof tmp, f, ap);
+    va_end(ap);
+    return xstrdup(tmp);
+}
+
+typedef struct { char **v; int n, cap; } slist;
+static void sl_add(slist *l, const char *s) {
+    if (l->n == l->cap) { l->cap = l->cap ? l->cap * 2 : 8; l->v = (char **)realloc(l->v, sizeof(char *) * (size_t)l->cap); }
+    l->v[l->n++] = xstrdup(s);
+}
+static int sl_has(const slist *l, const char *s) {
+    for (int i = 0; i < l->n; i++) if (strcmp(l->v[i], s) == 0) return 1;
+    return 0;
+}
+static void sl_add_unique(slist *l, const char *s) { if (!sl_has(l, s)) sl_add(l, s); }
+static void sl_free(slist *l) {
+    for (int i = 0; i < l->n; i++) free(l->v[i]);
+    free(l->v);
+    l->v = NULL; l->n = l->cap = 0;
+}
+
+static void ascii_lower(char *s) { for (; *s; s++) if (*s >= 'A' && *s <= 'Z') *s += 32; }
+static void ascii_upper(char *s) { for (; *s; s++) if (*s >= 'a' && *s <= 'z') *s -= 32; }
+
+/* code points <-> UTF-8 for setup-time strings */
+static int *cp_of(const char *s, int *n) {
+    int len = (int)strlen(s);
+    int *cp = (int *)xmalloc(sizeof(int) * (size_t)(len + 1));
+    int k = 0;
+    const unsigned char *u = (const unsigned char *)s;
+    for (int i = 0; i < len;) {
+        unsigned c = u[i];
+        if (c < 0x80) { cp[k++] = (int)c; i++; }
+        else if ((c >> 5) == 6 && i + 1 < len) { cp[k++] = (int)(((c & 0x1F) << 6) | (u[i + 1] & 0x3F)); i += 2; }
+        else if ((c >> 4) == 14 && i + 2 < len) { cp[k++] = (int)(((c & 0x0F) << 12) | ((u[i + 1] & 0x3F) << 6) | (u[i + 2] & 0x3F)); i += 3; }
+        else if ((c >> 3) == 30 && i + 3 < len) { cp[k++] = (int)(((c & 0x07) << 18) | ((u[i + 1] & 0x3F) << 12) | ((u[i + 2] & 0x3F) << 6) | (u[i + 3] & 0x3F)); i += 4; }
+        else { cp[k++] = 0xFFFD; i++; }
+    }
+    *n = k;
+    return cp;
+}
+static char *utf8_of(const int *cp, int n) {
+    char *o = (char *)xmalloc((size_t)n * 4 + 1);
+    int k = 0;
+    for (int i = 0; i < n; i++) {
+        unsigned c = (unsigned)cp[i];
+        if (c < 0x80) o[k++] = (char)c;
+        else if (c < 0x800) { o[k++] = (char)(0xC0 | (c >> 6)); o[k++] = (char)(0x80 | (c & 0x3F)); }
+        else if (c < 0x10000) { o[k++] = (char)(0xE0 | (c >> 12)); o[k++] = (char)(0x80 | ((c >> 6) & 0x3F)); o[k++] = (char)(0x80 | (c & 0x3F)); }
+        else { o[k++] = (char)(0xF0 | (c >> 18)); o[k++] = (char)(0x80 | ((c >> 12) & 0x3F)); o[k++] = (char)(0x80 | ((c >> 6) & 0x3F)); o[k++] = (char)(0x80 | (c & 0x3F)); }
+    }
+    o[k] = 0;
+    return o;
+}
+
+static jre *must_compile(const char *pat) {
+    char err[256];
+    jre *r = jre_compile(pat, err, sizeof err);
+    if (!r) { fprintf(stderr, "oracle: internal regex '%s' failed: %s\n", pat, err); abort(); }
+    return r;
+}
+
+/* setup-time regex replaceAll on UTF-8 strings (replacement is literal
+ * except $n) */
+static char *re_replace_all_s(const char *pat, const char *s, const char *repl) {
+    arena a = {0};
+    jre *re = must_compile(pat);
+    js in = js_lit(&a, s);
+    js out = js_replace_all(&a, re, in, repl);
+    char *r = utf8_of(out.c, out.n);
+    jre_free(re);
+    ar_free(&a);
+    return r;
+}
+
+/* ====================================================== token parsers */
+/* Casts bitmask */
+#define C_S 1
+#define C_L 2
+#define C_D 4
+#define STRING_ONLY C_S
+#define STRING_OR_LONG (C_S | C_L)
+#define STRING_OR_LONG_OR_DOUBLE (C_S | C_L | C_D)
+
+/* hp/dissectors/tokenformat/TokenParser.java:35-59 */
+#define FORMAT_DIGIT "[0-9]"
+#define FORMAT_NUMBER FORMAT_DIGIT "+"
+#define FORMAT_CLF_NUMBER FORMAT_NUMBER "|-"
+#define FORMAT_HEXDIGIT "[0-9a-fA-F]"
+#define FORMAT_HEXNUMBER FORMAT_HEXDIGIT "+"
+#define FORMAT_CLF_HEXNUMBER FORMAT_HEXNUMBER "|-"
+#define FORMAT_NON_ZERO_NUMBER "[1-9][0-9]*"
+#define FORMAT_EIGHT_BIT_DECIMAL "(?:25[0-5]|2[0-4][0-9]|[01]?[0-9][0-9]?)"
+#define FORMAT_IPV4 "(?:" FORMAT_EIGHT_BIT_DECIMAL "\\.){3}" FORMAT_EIGHT_BIT_DECIMAL
+#define FORMAT_IPV6 ":?(?:" FORMAT_HEXDIGIT "{1,4}(?::|.)?){0,8}(?::|::)?(?:" FORMAT_HEXDIGIT "{1,4}(?::|.)?){0,8}"
+#define FORMAT_IP FORMAT_IPV4 "|" FORMAT_IPV6
+#define FORMAT_CLF_IP FORMAT_IP "|-"
+#define FORMAT_STRING ".*?"
+#define FORMAT_NO_SPACE_STRING "[^\\s]*"
+#define FORMAT_STANDARD_TIME_US "[0-3][0-9]/(?:[a-zA-Z][a-zA-Z][a-zA-Z])/[1-9][0-9][0-9][0-9]:[0-9][0-9]:[0-9][0-9]:[0-9][0-9] [\\+|\\-][0-9][0-9][0-9][0-9]"
+#define FIRSTLINE_REGEX ".*" /* hp/dissectors/HttpFirstLineDissector.java:56-57 */
+
+enum { TP_PLAIN, TP_FIXED, TP_NAMED, TP_PARAM };
+enum { CUSTOM_NONE = 0, CUSTOM_STRFTIME = 1 };
+
+typedef struct { char *type, *name; int casts; } ofield;
+
+typedef struct {
+    int kind;
+    char *tok;      /* literal token (PLAIN/FIXED) or pattern (NAMED/PARAM) */
+    char *regex;
+    int prio;
+    ofield outs[4];
+    int nouts;
+    int custom;
+    jre *pat;
+} tparser;
+
+typedef struct { tparser *v; int n, cap; } tplist;
+
+static tparser *tp_add(tplist *l, int kind, const char *tok, const char *regex, int prio) {
+    if (l->n == l->cap) { l->cap = l->cap ? l->cap * 2 : 64; l->v = (tparser *)realloc(l->v, sizeof(tparser) * (size_t)l->cap); }
+    tparser *t = &l->v[l->n++];
+    memset(t, 0, sizeof *t);
+    t->kind = kind;
+    t->tok = xstrdup(tok);
+    t->regex = xstrdup(regex);
+    t->prio = prio;
+    if (kind == TP_NAMED || kind == TP_PARAM) t->pat = must_compile(tok);
+    return t;
+}
+/* TokenOutputField lowercases the name (tokenformat/TokenOutputField.java:39-44) */
+static void tp_out(tparser *t, const char *type, const char *name, int casts) {
+    char *n = xstrdup(name);
+    ascii_lower(n);
+    t->outs[t->nouts].type = xstrdup(type);
+    t->outs[t->nouts].name = n;
+    t->outs[t->nouts].casts = casts;
+    t->nouts++;
+}
+
+/* ApacheHttpdLogFormatDissector.createFirstAndLastTokenParsers (:651-714) */
+static void first_last(tplist *l, const char *token, const char *name, const char *type, int casts, const char *regex, int prio) {
+    tparser *t = tp_add(l, TP_PLAIN, token, regex, prio);
+    const char *orig_tokens[] = {"%s", "%U", "%T", "%{us}T", "%{ms}T", "%{s}T", "%D", "%r", NULL};
+    int orig = 0;
+    for (int i = 0; orig_tokens[i]; i++) if (strcmp(orig_tokens[i], token) == 0) orig = 1;
+    char buf[256];
+    tp_out(t, type, name, casts);
+    snprintf(buf, sizeof buf, "%s%s", name, orig ? ".original" : ".last");
+    tp_out(t, type, buf, casts);
+    /* replaceFirst("%", "%<") */
+    char tk[128];
+    const char *pc = strchr(token, '%');
+    snprintf(tk, sizeof tk, "%.*s%%<%s", (int)(pc - token), token, pc + 1);
+    t = tp_add(l, TP_PLAIN, tk, regex, prio);
+    snprintf(buf, sizeof buf, "%s.original", name);
+    tp_out(t, type, buf, casts);
+    snprintf(tk, sizeof tk, "%.*s%%>%s", (int)(pc - token), token, pc + 1);
+    t = tp_add(l, TP_PLAIN, tk, regex, prio);
+    snprintf(buf, sizeof buf, "%s.last", name);
+    tp_out(t, type, buf, casts);
+}
+static void fl(tplist *l, const char *token, const char *name, const char *type, int casts, const char *regex) {
+    first_last(l, token, name, type, casts, regex, 0);
+}
+/* addExtraOutput (:640-649): first parser with exactly this token */
+static void extra_out(tplist *l, const char *token, const char *type, const char *name, int casts) {
+    for (int i = 0; i < l->n; i++)
+        if (strcmp(l->v[i].tok, token) == 0) { tp_out(&l->v[i], type, name, casts); return; }
+}
+
+/* ApacheHttpdLogFormatDissector.createAllTokenParsers (:199-638) */
+static void apache_token_parsers(tplist *l) {
+    tp_add(l, TP_FIXED, "%%", "%", 0);
+    fl(l, "%a", "connection.client.ip", "IP", STRING_ONLY, FORMAT_CLF_IP);
+    fl(l, "%{c}a", "connection.client.peerip", "IP", STRING_ONLY, FORMAT_CLF_IP);
+    fl(l, "%A", "connection.server.ip", "IP", STRING_ONLY, FORMAT_CLF_IP);
+    fl(l, "%B", "response.body.bytes", "BYTES", STRING_OR_LONG, FORMAT_NUMBER);
+    fl(l, "%b", "response.body.bytes", "BYTESCLF", STRING_OR_LONG, FORMAT_CLF_NUMBER);
+    extra_out(l, "%b", "BYTES", "response.body.bytesclf", STRING_OR_LONG);
+    tp_out(tp_add(l, TP_NAMED, "\\%\\{([a-z0-9\\-_]*)\\}C", FORMAT_STRING, 0), "HTTP.COOKIE", "request.cookies.", STRING_ONLY);
+    tp_out(tp_add(l, TP_NAMED, "\\%\\{([a-z0-9\\-_]*)\\}e", FORMAT_STRING, 0), "VARIABLE", "server.environment.", STRING_ONLY);
+    fl(l, "%f", "server.filename", "FILENAME", STRING_ONLY, FORMAT_STRING);
+    fl(l, "%h", "connection.client.host", "IP", STRING_ONLY, FORMAT_NO_SPACE_STRING);
+    fl(l, "%H", "request.protocol", "PROTOCOL", STRING_ONLY, FORMAT_NO_SPACE_STRING);
+    tp_out(tp_add(l, TP_NAMED, "\\%\\{([a-z0-9\\-_]*)\\}i", FORMAT_STRING, 0), "HTTP.HEADER", "request.header.", STRING_ONLY);
+    tp_out(tp_add(l, TP_NAMED, "\\%\\{([a-z0-9\\-_]*)\\}\\^ti", FORMAT_STRING, 0), "HTTP.TRAILER", "request.trailer.", STRING_ONLY);
+    fl(l, "%k", "connection.keepalivecount", "NUMBER", STRING_OR_LONG, FORMAT_NUMBER);
+    fl(l, "%l", "connection.client.logname", "NUMBER", STRING_OR_LONG, FORMAT_CLF_NUMBER);
+    fl(l, "%L", "request.errorlogid", "STRING", STRING_ONLY, FORMAT_NO_SPACE_STRING);
+    fl(l, "%m", "request.method", "HTTP.METHOD", STRING_ONLY, FORMAT_NO_SPACE_STRING);
+    tp_out(tp_add(l, TP_NAMED, "\\%\\{([a-z0-9\\-_]*)\\}n", FORMAT_STRING, 0), "STRING", "server.module_note.", STRING_ONLY);
+    tp_out(tp_add(l, TP_NAMED, "\\%\\{([a-z0-9\\-]*)\\}o", FORMAT_STRING, 0), "HTTP.HEADER", "response.header.", STRING_ONLY);
+    tp_out(tp_add(l, TP_NAMED, "\\%\\{([a-z0-9\\-_]*)\\}\\^to", FORMAT_STRING, 0), "HTTP.TRAILER", "response.trailer.", STRING_ONLY);
+    fl(l, "%p", "request.server.port.canonical", "PORT", STRING_OR_LONG, FORMAT_NUMBER);
+    fl(l, "%{canonical}p", "connection.server.port.canonical", "PORT", STRING_OR_LONG, FORMAT_NUMBER);
+    fl(l, "%{local}p", "connection.server.port", "PORT", STRING_OR_LONG, FORMAT_NUMBER);
+    fl(l, "%{remote}p", "connection.client.port", "PORT", STRING_OR_LONG, FORMAT_NUMBER);
+    fl(l, "%P", "connection.server.child.processid", "NUMBER", STRING_OR_LONG, FORMAT_NUMBER);
+    fl(l, "%{pid}P", "connection.server.child.processid", "NUMBER", STRING_OR_LONG, FORMAT_NUMBER);
+    fl(l, "%{tid}P", "connection.server.child.threadid", "NUMBER", STRING_OR_LONG, FORMAT_NUMBER);
+    fl(l, "%{hextid}P", "connection.server.child.hexthreadid", "NUMBER", STRING_OR_LONG, FORMAT_CLF_HEXNUMBER);
+    fl(l, "%q", "request.querystring", "HTTP.QUERYSTRING", STRING_ONLY, FORMAT_NO_SPACE_STRING);
+    fl(l, "%r", "request.firstline", "HTTP.FIRSTLINE", STRING_ONLY, FIRSTLINE_REGEX);
+    fl(l, "%R", "request.handler", "STRING", STRING_ONLY, FORMAT_STRING);
+    first_last(l, "%s", "request.status", "STRING", STRING_ONLY, FORMAT_NO_SPACE_STRING, 0);
+    fl(l, "%t", "request.receive.time", "TIME.STAMP", STRING_ONLY, FORMAT_STANDARD_TIME_US);
+    tparser *t;
+    t = tp_add(l, TP_PARAM, "\\%\\{([^\\}]*%[^\\}]*)\\}t", FORMAT_STRING, -1);
+    tp_out(t, "TIME.STRFTIME_", "request.receive.time", STRING_ONLY);
+    t->custom = CUSTOM_STRFTIME;
+    t = tp_add(l, TP_PARAM, "\\%\\{begin:([^\\}]*%[^\\}]*)\\}t", FORMAT_STRING, 0);
+    tp_out(t, "TIME.STRFTIME_", "request.receive.time.begin", STRING_ONLY);
+    t->custom = CUSTOM_STRFTIME;
+    t = tp_add(l, TP_PARAM, "\\%\\{end:([^\\}]*%[^\\}]*)\\}t", FORMAT_STRING, 0);
+    tp_out(t, "TIME.STRFTIME_", "request.receive.time.end", STRING_ONLY);
+    t->custom = CUSTOM_STRFTIME;
+    fl(l, "%{sec}t", "request.receive.time.sec", "TIME.SECONDS", STRING_OR_LONG, FORMAT_NUMBER);
+    fl(l, "%{begin:sec}t", "request.receive.time.begin.sec", "TIME.SECONDS", STRING_OR_LONG, FORMAT_NUMBER);
+    fl(l, "%{end:sec}t", "request.receive.time.end.sec", "TIME.SECONDS", STRING_OR_LONG, FORMAT_NUMBER);
+    fl(l, "%{msec}t", "request.receive.time.msec", "TIME.EPOCH", STRING_OR_LONG, FORMAT_NUMBER);
+    extra_out(l, "%{msec}t", "TIME.EPOCH", "request.receive.time.begin.msec", STRING_OR_LONG);
+    fl(l, "%{begin:msec}t", "request.receive.time.begin.msec", "TIME.EPOCH", STRING_OR_LONG, FORMAT_NUMBER);
+    fl(l, "%{end:msec}t", "request.receive.time.end.msec", "TIME.EPOCH", STRING_OR_LONG, FORMAT_NUMBER);
+    fl(l, "%{usec}t", "request.receive.time.usec", "TIME.EPOCH.USEC", STRING_OR_LONG, FORMAT_NUMBER);
+    extra_out(l, "%{usec}t", "TIME.EPOCH.USEC", "request.receive.time.begin.usec", STRING_OR_LONG);
+    fl(l, "%{begin:usec}t", "request.receive.time.begin.usec", "TIME.EPOCH.USEC", STRING_OR_LONG, FORMAT_NUMBER);
+    fl(l, "%{end:usec}t", "request.receive.time.end.usec", "TIME.EPOCH.USEC", STRING_OR_LONG, FORMAT_NUMBER);
+    fl(l, "%{msec_frac}t", "request.receive.time.msec_frac", "TIME.EPOCH", STRING_OR_LONG, FORMAT_NUMBER);
+    extra_out(l, "%{msec_frac}t", "TIME.EPOCH", "request.receive.time.begin.msec_frac", STRING_OR_LONG);
+    fl(l, "%{begin:msec_frac}t", "request.receive.time.begin.msec_frac", "TIME.EPOCH", STRING_OR_LONG, FORMAT_NUMBER);
+    fl(l, "%{end:msec_frac}t", "request.receive.time.end.msec_frac", "TIME.EPOCH", STRING_OR_LONG, FORMAT_NUMBER);
+    fl(l, "%{usec_frac}t", "request.receive.time.usec_frac", "TIME.EPOCH.USEC_FRAC", STRING_OR_LONG, FORMAT_NUMBER);
+    extra_out(l, "%{usec_frac}t", "TIME.EPOCH.USEC_FRAC", "request.receive.time.begin.usec_frac", STRING_OR_LONG);
+    fl(l, "%{begin:usec_frac}t", "request.receive.time.begin.usec_frac", "TIME.EPOCH.USEC_FRAC", STRING_OR_LONG, FORMAT_NUMBER);
+    fl(l, "%{end:usec_frac}t", "request.receive.time.end.usec_frac", "TIME.EPOCH.USEC_FRAC", STRING_OR_LONG, FORMAT_NUMBER);
+    fl(l, "%T", "response.server.processing.time", "SECONDS", STRING_OR_LONG, FORMAT_NUMBER);
+    fl(l, "%D", "response.server.processing.time", "MICROSECONDS", STRING_OR_LONG, FORMAT_NUMBER);
+    extra_out(l, "%D", "MICROSECONDS", "server.process.time", STRING_OR_LONG);
+    fl(l, "%{us}T", "response.server.processing.time", "MICROSECONDS", STRING_OR_LONG, FORMAT_NUMBER);
+    fl(l, "%{ms}T", "response.server.processing.time", "MILLISECONDS", STRING_OR_LONG, FORMAT_NUMBER);
+    fl(l, "%{s}T", "response.server.processing.time", "SECONDS", STRING_OR_LONG, FORMAT_NUMBER);
+    fl(l, "%u", "connection.client.user", "STRING", STRING_ONLY, FORMAT_NO_SPACE_STRING);
+    fl(l, "%U", "request.urlpath", "URI", STRING_ONLY, FORMAT_NO_SPACE_STRING);
+    fl(l, "%v", "connection.server.name.canonical", "STRING", STRING_ONLY, FORMAT_NO_SPACE_STRING);
+    fl(l, "%V", "connection.server.name", "STRING", STRING_ONLY, FORMAT_NO_SPACE_STRING);
+    fl(l, "%X", "response.connection.status", "HTTP.CONNECTSTATUS", STRING_ONLY, FORMAT_NO_SPACE_STRING);
+    fl(l, "%I", "request.bytes", "BYTES", STRING_OR_LONG, FORMAT_CLF_NUMBER);
+    fl(l, "%O", "response.bytes", "BYTES", STRING_OR_LONG, FORMAT_CLF_NUMBER);
+    fl(l, "%S", "total.bytes", "BYTES", STRING_OR_LONG, FORMAT_NON_ZERO_NUMBER);
+    first_last(l, "%{cookie}i", "request.cookies", "HTTP.COOKIES", STRING_ONLY, FORMAT_STRING, 1);
+    first_last(l, "%{set-cookie}o", "response.cookies", "HTTP.SETCOOKIES", STRING_ONLY, FORMAT_STRING, 1);
+    first_last(l, "%{user-agent}i", "request.user-agent", "HTTP.USERAGENT", STRING_ONLY, FORMAT_STRING, 1);
+    first_last(l, "%{referer}i", "request.referer", "HTTP.URI", STRING_ONLY, FORMAT_STRING, 1);
+}
+
+/* =============================================================== tokens */
+typedef struct {
+    int fixed;          /* FixedStringToken */
+    char *regex;        /* fixed: the literal text */
+    int start, len, prio;
+    ofield outs[4];
+    int nouts;
+    int custom;
+    char *custom_type, *custom_param;
+} token;
+
+typedef struct { token *v; int n, cap; } toklist;
+static token *tk_push(toklist *l) {
+    if (l->n == l->cap) { l->cap = l->cap ? l->cap * 2 : 32; l->v = (token *)realloc(l->v, sizeof(token) * (size_t)l->cap); }
+    token *t = &l->v[l->n++];
+    memset(t, 0, sizeof *t);
+    return t;
+}
+
+/* ParameterizedTokenParser.tokenParameterToTypeName (:99-105) */
+static char *param_type_name(const char *base_type, const char *param) {
+    char clean[512];
+    int k = 0;
+    for (const char *p = param; *p && k < 500; p++)
+        if ((*p >= 'A' && *p <= 'Z') || (*p >= 'a' && *p <= 'z') || (*p >= '0' && *p <= '9')) clean[k++] = *p;
+    clean[k] = 0;
+    char md5[33];
+    oracle_md5_hex((const unsigned char *)param, strlen(param), md5);
+    char *r = xfmt("%s%s_%s", base_type, clean, md5);
+    ascii_upper(r);
+    return r;
+}
+
+/* TokenParser/NamedTokenParser/ParameterizedTokenParser.getNextToken and
+ * TokenParser.getTokens (TokenParser.java:569-614, NamedTokenParser.java:43-77,
+ * ParameterizedTokenParser.java:58-95) */
+static void collect_tokens(const tparser *tp, const char *fmt, const int *fcp, int fn, toklist *out) {
+    /* StringUtils.isBlank */
+    int blank = 1;
+    for (const char *p = fmt; *p; p++) if (!(*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r' || *p == '\f' || *p == 0x0B)) blank = 0;
+    if (blank) return;
+    int offset = 0;
+    for (;;) {
+        int start, len;
+        char *fieldname = NULL;
+        if (tp->kind == TP_PLAIN || tp->kind == TP_FIXED) {
+            int tn;
+            int *tcp = cp_of(tp->tok, &tn);
+            int pos = -1;
+            for (int i = offset; i + tn <= fn; i++)
+                if (memcmp(fcp + i, tcp, sizeof(int) * (size_t)tn) == 0) { pos = i; break; }
+            free(tcp);
+            if (pos < 0) return;
+            start = pos;
+            len = tn;
+        } else {
+            int caps[2 * 8];
+            if (!jre_find(tp->pat, fcp, fn, offset, caps)) return;
+            start = caps[0];
+            len = caps[1] - caps[0];
+            if (jre_ngroups(tp->pat) > 0 && caps[2] >= 0) fieldname = utf8_of(fcp + caps[2], caps[3] - caps[2]);
+            else fieldname = xstrdup("");
+        }
+        token *t = tk_push(out);
+        t->fixed = tp->kind == TP_FIXED;
+        t->regex = xstrdup(tp->regex);
+        t->start = start;
+        t->len = len;
+        t->prio = tp->kind == TP_FIXED ? 0 : tp->prio;
+        for (int i = 0; i < tp->nouts; i++) {
+            ofield o = tp->outs[i];
+            if (tp->kind == TP_NAMED) {
+                char *nm = xfmt("%s%s", o.name, fieldname);
+                ascii_lower(nm); /* new TokenOutputField lowercases */
+                t->outs[i].type = xstrdup(o.type);
+                t->outs[i].name = nm;
+            } else if (tp->kind == TP_PARAM) {
+                t->outs[i].type = param_type_name(o.type, fieldname);
+                t->outs[i].name = xstrdup(o.name);
+            } else {
+                t->outs[i].type = xstrdup(o.type);
+                t->outs[i].name = xstrdup(o.name);
+            }
+            t->outs[i].casts = o.casts;
+        }
+        t->nouts = tp->nouts;
+        if (tp->custom) {
+            t->custom = tp->custom;
+            t->custom_type = xstrdup(t->outs[0].type);
+            t->custom_param = xstrdup(fieldname);
+        }
+        free(fieldname);
+        offset = start + len;
+    }
+}
+
+static int tok_cmp(const token *a, const token *b) { /* TokenSorterByStartPos */
+    if (a->start != b->start) return a->start < b->start ? -1 : 1;
+    if (a->len != b->len) return a->len < b->len ? -1 : 1;
+    if (a->prio != b->prio) return a->prio > b->prio ? -1 : 1;
+    return 0;
+}
+
+/* ============================================================= formats */
+enum { FMT_APACHE = 1, FMT_NGINX = 2 };
+
+typedef struct {
+    int kind;
+    char *logformat;      /* as registered (after alias mapping) */
+    char *cleaned;
+    token *tokens;        /* in order, incl. fixed strings */
+    int ntokens;
+    slist output_types;   /* "TYPE:name" */
+    slist requested;      /* requestedFields (output names) */
+    /* prepared */
+    char *regex;
+    jre *re;
+    int *used;            /* group -> token index */
+    int nused;
+    int unsupported;      /* reason flag */
+} fmtd;
+
+/* TokenFormatDissector.parseTokenLogFileDefinition (:294-379) */
+static void parse_token_def(fmtd *f, const tplist *tps) {
+    int fn;
+    int *fcp = cp_of(f->cleaned, &fn);
+    toklist all = {0};
+    for (int i = 0; i < tps->n; i++) collect_tokens(&tps->v[i], f->cleaned, fcp, fn, &all);
+    /* stable sort */
+    for (int i = 1; i < all.n; i++) {
+        token t = all.v[i];
+        int j = i - 1;
+        while (j >= 0 && tok_cmp(&all.v[j], &t) > 0) { all.v[j + 1] = all.v[j]; j--; }
+        all.v[j + 1] = t;
+    }
+    char *kick = (char *)xmalloc((size_t)all.n + 1);
+    int prev = -1;
+    for (int i = 0; i < all.n; i++) {
+        token *tk = &all.v[i];
+        if (prev < 0) { prev = i; continue; }
+        token *pv = &all.v[prev];
+        if (pv->start == tk->start) {
+            if (pv->len == tk->len) {
+                if (pv->prio < tk->prio) kick[prev] = 1; else kick[i] = 1;
+            } else {
+                if (pv->len < tk->len) kick[prev] = 1; else kick[i] = 1;
+            }
+        } else {
+            if (pv->start + pv->len > tk->start) { kick[i] = 1; continue; }
+        }
+        prev = i;
+    }
+    toklist res = {0};
+    int tend = 0;
+    for (int i = 0; i < all.n; i++) {
+        if (kick[i]) continue;
+        token *tk = &all.v[i];
+        if (tk->start - tend > 0) {
+            token *fx = tk_push(&res);
+            fx->fixed = 1;
+            fx->regex = utf8_of(fcp + tend, tk->start - tend);
+            fx->start = tk->start;
+            fx->len = tk->start - tend;
+        }
+        *tk_push(&res) = *tk;
+        tend = tk->start + tk->len;
+    }
+    if (tend < fn) {
+        token *fx = tk_push(&res);
+        fx->fixed = 1;
+        fx->regex = utf8_of(fcp + tend, fn - tend);
+        fx->start = tend;
+        fx->len = fn - tend;
+    }
+    free(kick);
+    free(all.v);
+    free(fcp);
+    f->tokens = res.v;
+    f->ntokens = res.n;
+    for (int i = 0; i < f->ntokens; i++) {
+        token *t = &f->tokens[i];
+        if (t->fixed) continue;
+        for (int k = 0; k < t->nouts; k++) {
+            char *s = xfmt("%s:%s", t->outs[k].type, t->outs[k].name);
+            sl_add(&f->output_types, s);
+            free(s);
+        }
+    }
+}
+
+/* ApacheHttpdLogFormatDissector.cleanupLogFormat (:121-167) */
+static char *apache_cleanup(const char *fmt) {
+    char *a = re_replace_all_s("%!?[0-9]{3}(?:,[0-9]{3})*", fmt, "%");
+    /* makeHeaderNamesLowercaseInLogFormat: %{X}c (c != 't') -> lowercase X */
+    arena ar = {0};
+    jre *re = must_compile("%\\{([^}]*)}([^t])");
+    js in = js_lit(&ar, a);
+    int caps[6];
+    int from = 0, last = 0;
+    int *ob = (int *)xmalloc(sizeof(int) * (size_t)(in.n * 2 + 8));
+    int on = 0;
+    while (from <= in.n && jre_find(re, in.c, in.n, from, caps)) {
+        for (int k = last; k < caps[0]; k++) ob[on++] = in.c[k];
+        ob[on++] = '%';
+        ob[on++] = '{';
+        for (int k = caps[2]; k < caps[3]; k++) {
+            int c = in.c[k];
+            ob[on++] = (c >= 'A' && c <= 'Z') ? c + 32 : c;
+        }
+        ob[on++] = '}';
+        ob[on++] = in.c[caps[4]];
+        last = caps[1];
+        from = caps[1] > caps[0] ? caps[1] : caps[1] + 1;
+    }
+    for (int k = last; k < in.n; k++) ob[on++] = in.c[k];
+    char *b = utf8_of(ob, on);
+    free(ob);
+    jre_free(re);
+    ar_free(&ar);
+    free(a);
+    char *c = re_replace_all_s("%t", b, "[%t]");
+    free(b);
+    return c;
+}
+
+static int ieq(const char *a, const char *b) {
+    for (; *a && *b; a++, b++) {
+        int x = *a, y = *b;
+        if (x >= 'A' && x <= 'Z') x += 32;
+        if (y >= 'A' && y <= 'Z') y += 32;
+        if (x != y) return 0;
+    }
+    return *a == *b;
+}
+
+/* ApacheHttpdLogFormatDissector.setLogFormat alias mapping (:73-101) */
+static const char *apache_alias(const char *f) {
+    if (ieq(f, "common")) return "%h %l %u %t \"%r\" %>s %b";
+    if (ieq(f, "combined")) return "%h %l %u %t \"%r\" %>s %b \"%{Referer}i\" \"%{User-Agent}i\"";
+    if (ieq(f, "combinedio")) return "%h %l %u %t \"%r\" %>s %b \"%{Referer}i\" \"%{User-Agent}i\" %I %O";
+    if (ieq(f, "referer")) return "%{Referer}i -> %U";
+    if (ieq(f, "agent")) return "%{User-agent}i";
+    return f;
+}
+static int looks_apache(const char *f) {
+    return strchr(f, '%') != NULL || ieq(f, "common") || ieq(f, "combined") || ieq(f, "combinedio") || ieq(f, "referer") || ieq(f, "agent");
+}
+static int looks_nginx(const char *f) { return strchr(f, '$') != NULL || ieq(f, "combined"); }
+
+static tplist g_apache_tps;
+static pthread_once_t g_tps_once = PTHREAD_ONCE_INIT;
+static void init_tps(void) { apache_token_parsers(&g_apache_tps); }
+
+static fmtd *fmt_new(int kind, const char *logformat) {
+    pthread_once(&g_tps_once, init_tps);
+    fmtd *f = (fmtd *)xmalloc(sizeof(fmtd));
+    f->kind = kind;
+    if (kind == FMT_APACHE) {
+        f->logformat = xstrdup(apache_alias(logformat));
+        f->cleaned = apache_cleanup(f->logformat);
+        parse_token_def(f, &g_apache_tps);
+    } else {
+        f->logformat = xstrdup(logformat);
+        f->cleaned = xstrdup(logformat);
+        f->unsupported = 1; /* NGINX: not restated in this oracle version */
+    }
+    return f;
+}
+
+static fmtd *fmt_clone(const fmtd *src) { return fmt_new(src->kind, src->logformat); }
+
+/* TokenFormatDissector.prepareForDissect (:162-174) */
+static int fmt_prepare_for_dissect(fmtd *f, const char *outname) {
+    sl_add_unique(&f->requested, outname);
+    for (int i = 0; i < f->ntokens; i++)
+        for (int k = 0; k < f->tokens[i].nouts; k++)
+            if (strcmp(outname, f->tokens[i].outs[k].name) == 0) return f->tokens[i].outs[k].casts;
+    return STRING_ONLY;
+}
+
+/* Pattern.quote */
+static void append_quote(char **dst, size_t *dn, size_t *dcap, const char *s) {
+#define APP(str) do { size_t l_ = strlen(str); while (*dn + l_ + 1 > *dcap) { *dcap *= 2; *dst = (char *)realloc(*dst, *dcap); } memcpy(*dst + *dn, str, l_); *dn += l_; (*dst)[*dn] = 0; } while (0)
+    const char *e = strstr(s, "\\E");
+    if (!e) { APP("\\Q"); APP(s); APP("\\E"); return; }
+    APP("\\Q");
+    const char *cur = s;
+    while ((e = strstr(cur, "\\E")) != NULL) {
+        char tmp[4096];
+        snprintf(tmp, sizeof tmp, "%.*s", (int)(e - cur), cur);
+        APP(tmp);
+        cur = e + 2;
+        APP("\\E\\\\E\\Q");
+    }
+    APP(cur);
+    APP("\\E");
+}
+
+/* TokenFormatDissector.prepareForRun (:178-213) */
+static void fmt_prepare_for_run(fmtd *f) {
+    size_t cap = 256, n = 0;
+    char *r = (char *)xmalloc(cap);
+    r[0] = 0;
+    f->used = (int *)xmalloc(sizeof(int) * (size_t)(f->ntokens + 1));
+    f->nused = 0;
+#define APPL(str) do { size_t l_ = strlen(str); while (n + l_ + 1 > cap) { cap *= 2; r = (char *)realloc(r, cap); } memcpy(r + n, str, l_); n += l_; r[n] = 0; } while (0)
+    APPL("^");
+    for (int i = 0; i < f->ntokens; i++) {
+        token *t = &f->tokens[i];
+        if (t->fixed) { append_quote(&r, &n, &cap, t->regex); continue; }
+        int wanted = 0;
+        for (int k = 0; k < t->nouts; k++) if (sl_has(&f->requested, t->outs[k].name)) wanted = 1;
+        if (wanted) {
+            f->used[f->nused++] = i;
+            APPL("("); APPL(t->regex); APPL(")");
+        } else {
+            APPL("(?:"); APPL(t->regex); APPL(")");
+        }
+    }
+    APPL("$");
+#undef APPL
+#undef APP
+    f->regex = r;
+    char err[256];
+    f->re = jre_compile(r, err, sizeof err);
+    if (!f->re) { fprintf(stderr, "oracle: format regex failed: %s\n%s\n", err, r); f->unsupported = 1; }
+    else if (jre_ngroups(f->re) != f->nused) f->unsupported = 1; /* capturing groups inside token regexes */
+}
+
+/* ========================================================= dissectors */
+enum {
+    D_ROOT, D_TIMESTAMP, D_TIMESTAMP_ISO, D_FIRSTLINE, D_PROTOCOL, D_URI, D_QUERY,
+    D_COOKIES, D_SETCOOKIES, D_SETCOOKIE, D_UNIQUEID, D_CLF2NUM, D_NUM2CLF,
+    D_STRFTIME, D_LOCALIZED
+};
+
+typedef struct {
+    int cls;
+    char *in_type;
+    slist outs;          /* "TYPE:name" */
+    char *out_type;      /* converters */
+    /* root */
+    fmtd **fmts;
+    int nfmts;
+} dissector;
+
+static const char *TS_OUTS[] = {
+    "TIME.DAY:day", "TIME.MONTHNAME:monthname", "TIME.MONTH:month", "TIME.WEEK:weekofweekyear",
+    "TIME.YEAR:weekyear", "TIME.YEAR:year", "TIME.HOUR:hour", "TIME.MINUTE:minute",
+    "TIME.SECOND:second", "TIME.MILLISECOND:millisecond", "TIME.MICROSECOND:microsecond",
+    "TIME.NANOSECOND:nanosecond", "TIME.DATE:date", "TIME.TIME:time", "TIME.ZONE:timezone",
+    "TIME.EPOCH:epoch", "TIME.DAY:day_utc", "TIME.MONTHNAME:monthname_utc", "TIME.MONTH:month_utc",
+    "TIME.WEEK:weekofweekyear_utc", "TIME.YEAR:weekyear_utc", "TIME.YEAR:year_utc",
+    "TIME.HOUR:hour_utc", "TIME.MINUTE:minute_utc", "TIME.SECOND:second_utc",
+    "TIME.MILLISECOND:millisecond_utc", "TIME.MICROSECOND:microsecond_utc",
+    "TIME.NANOSECOND:nanosecond_utc", "TIME.DATE:date_utc", "TIME.TIME:time_utc", NULL};
+
+static dissector *dis_new(int cls, const char *in_type) {
+    dissector *d = (dissector *)xmalloc(sizeof(dissector));
+    d->cls = cls;
+    d->in_type = xstrdup(in_type);
+    switch (cls) {
+    case D_TIMESTAMP: case D_TIMESTAMP_ISO: case D_STRFTIME:
+        for (int i = 0; TS_OUTS[i]; i++) sl_add(&d->outs, TS_OUTS[i]);
+        break;
+    case D_FIRSTLINE:
+        sl_add(&d->outs, "HTTP.METHOD:method"); sl_add(&d->outs, "HTTP.URI:uri"); sl_add(&d->outs, "HTTP.PROTOCOL_VERSION:protocol");
+        break;
+    case D_PROTOCOL:
+        sl_add(&d->outs, "HTTP.PROTOCOL:"); sl_add(&d->outs, "HTTP.PROTOCOL.VERSION:version");
+        break;
+    case D_URI: {
+        const char *o[] = {"HTTP.PROTOCOL:protocol", "HTTP.USERINFO:userinfo", "HTTP.HOST:host", "HTTP.PORT:port",
+                           "HTTP.PATH:path", "HTTP.QUERYSTRING:query", "HTTP.REF:ref", NULL};
+        for (int i = 0; o[i]; i++) sl_add(&d->outs, o[i]);
+        break;
+    }
+    case D_QUERY: sl_add(&d->outs, "STRING:*"); break;
+    case D_COOKIES: sl_add(&d->outs, "HTTP.COOKIE:*"); break;
+    case D_SETCOOKIES: sl_add(&d->outs, "HTTP.SETCOOKIE:*"); break;
+    case D_SETCOOKIE: {
+        const char *o[] = {"STRING:value", "STRING:expires", "TIME.EPOCH:expires", "STRING:path", "STRING:domain", "STRING:comment", NULL};
+        for (int i = 0; o[i]; i++) sl_add(&d->outs, o[i]);
+        break;
+    }
+    case D_UNIQUEID: {
+        const char *o[] = {"TIME.EPOCH:epoch", "IP:ip", "PROCESSID:processid", "COUNTER:counter", "THREAD_INDEX:threadindex", NULL};
+        for (int i = 0; o[i]; i++) sl_add(&d->outs, o[i]);
+        break;
+    }
+    case D_LOCALIZED: sl_add(&d->outs, "TIME.LOCALIZEDSTRING:"); break;
+    default: break;
+    }
+    return d;
+}
+
+/* ===================================================== planner state */
+typedef struct instance {
+    dissector *d;
+    slist requested;  /* extractFieldName(input, output) */
+    /* root: own formats (getNewInstance re-registers them) */
+    fmtd **fmts;
+    int nfmts;
+    int active;       /* sticky active format (HttpdLogFormatDissector.java:180-202) */
+    int want_all;     /* query */
+} instance;
+
+typedef struct { char *id; instance **ph; int n; } centry;
+
+struct orc_parser {
+    dissector **dis;
+    int ndis;
+    char *root_type;
+    slist needed;     /* cleaned targets */
+    centry *compiled;
+    int ncompiled;
+    slist useful;     /* usefulIntermediateFields (names) */
+    slist located;
+    int unsupported;
+    char unsupported_why[256];
+    /* for cloning */
+    char *logformat_arg;
+    slist field_args;
+    arena ar;
+};
+
+static centry *c_get(orc_parser *p, const char *id) {
+    for (int i = 0; i < p->ncompiled; i++) if (strcmp(p->compiled[i].id, id) == 0) return &p->compiled[i];
+    return NULL;
+}
+static centry *c_put(orc_parser *p, const char *id) {
+    p->compiled = (centry *)realloc(p->compiled, sizeof(centry) * (size_t)(p->ncompiled + 1));
+    centry *c = &p->compiled[p->ncompiled++];
+    c->id = xstrdup(id);
+    c->ph = NULL;
+    c->n = 0;
+    return c;
+}
+
+/* Dissector.extractFieldName (core/Dissector.java:147-157) */
+static char *extract_field_name(const char *in, const char *out) {
+    if (strcmp(in, out) == 0) return xstrdup("");
+    if (in[0]) return xstrdup(out + strlen(in) + 1);
+    return xstrdup(out);
+}
+
+static instance *inst_new(dissector *d) {
+    instance *in = (instance *)xmalloc(sizeof(instance));
+    in->d = d;
+    if (d->cls == D_ROOT) {
+        in->nfmts = d->nfmts;
+        in->fmts = (fmtd **)xmalloc(sizeof(fmtd *) * (size_t)(d->nfmts + 1));
+        for (int i = 0; i < d->nfmts; i++) in->fmts[i] = fmt_clone(d->fmts[i]);
+        in->active = -1;
+    }
+    return in;
+}
+
+static void inst_prepare(orc_parser *p, instance *in, const char *subroot, const char *check) {
+    char *name = extract_field_name(subroot, check);
+    sl_add_unique(&in->requested, name);
+    if (in->d->cls == D_ROOT)
+        for (int i = 0; i < in->nfmts; i++) fmt_prepare_for_dissect(in->fmts[i], check);
+    switch (in->d->cls) {
+    case D_TIMESTAMP_ISO: case D_STRFTIME: case D_LOCALIZED: case D_COOKIES: case D_SETCOOKIES:
+    case D_SETCOOKIE: case D_UNIQUEID:
+        if (!p->unsupported) {
+            p->unsupported = 1;
+            snprintf(p->unsupported_why, sizeof p->unsupported_why, "unsupported dissector for input type %s", in->d->in_type);
+        }
+        break;
+    default: break;
+    }
+    free(name);
+}
+
+/* Parser.findUsefulDissectorsFromField (core/Parser.java:360-458) */
+static void find_useful(orc_parser *p, slist *possible, const char *sr_type, const char *sr_name, int is_root) {
+    char *srid = xfmt("%s:%s", sr_type, sr_name);
+    if (sl_has(&p->located, srid)) { free(srid); return; }
+    sl_add(&p->located, srid);
+    for (int di = 0; di < p->ndis; di++) {
+        dissector *d = p->dis[di];
+        if (strcmp(d->in_type, sr_type) != 0) continue;
+        for (int oi = 0; oi < d->outs.n; oi++) {
+            const char *out = d->outs.v[oi];
+            const char *colon = strchr(out, ':');
+            char *otype = xfmt("%.*s", (int)(colon - out), out);
+            const char *oname = colon + 1;
+            slist checks = {0};
+            if (strcmp(oname, "*") == 0) {
+                char *pre = xfmt("%s.", sr_name);
+                for (int k = 0; k < possible->n; k++)
+                    if (strncmp(possible->v[k], pre, strlen(pre)) == 0) sl_add_unique(&checks, possible->v[k]);
+                free(pre);
+            } else if (is_root) {
+                sl_add(&checks, oname);
+            } else if (oname[0] == 0) {
+                sl_add(&checks, sr_name);
+            } else {
+                char *c = xfmt("%s.%s", sr_name, oname);
+                sl_add(&checks, c);
+                free(c);
+            }
+            for (int k = 0; k < checks.n; k++) {
+                const char *cf = checks.v[k];
+                char *cid = xfmt("%s:%s", otype, cf);
+                if (sl_has(possible, cf) && !c_get(p, cid)) {
+                    centry *ce = c_get(p, srid);
+                    if (!ce) { ce = c_put(p, srid); sl_add_unique(&p->useful, sr_name); }
+                    instance *in = NULL;
+                    for (int q = 0; q < ce->n; q++) if (ce->ph[q]->d->cls == d->cls) in = ce->ph[q];
+                    if (!in) {
+                        in = inst_new(d);
+                        ce = c_get(p, srid);
+                        ce->ph = (instance **)realloc(ce->ph, sizeof(instance *) * (size_t)(ce->n + 1));
+                        ce->ph[ce->n++] = in;
+                    }
+                    inst_prepare(p, in, sr_name, cf);
+                    find_useful(p, possible, otype, cf, 0);
+                }
+                free(cid);
+            }
+            sl_free(&checks);
+            free(otype);
+        }
+    }
+    free(srid);
+}
+
+/* Parser.cleanupFieldValue (core/Parser.java:681-691) */
+static char *cleanup_field(const char *f) {
+    const char *c = strchr(f, ':');
+    char *r = xstrdup(f);
+    if (!c) { ascii_lower(r); return r; }
+    size_t k = (size_t)(c - f);
+    for (size_t i = 0; i < k; i++) if (r[i] >= 'a' && r[i] <= 'z') r[i] -= 32;
+    ascii_lower(r + k + 1);
+    return r;
+}
+
+/* HttpdLoglineParser.setupDissectors + HttpdLogFormatDissector ctor */
+static int build_dissectors(orc_parser *p, const char *logformat, char *err, int errlen) {
+    dissector *root = dis_new(D_ROOT, "HTTPLOGLINE");
+    /* addMultipleLogFormats: split("\\r?\\n") */
+    char *copy = xstrdup(logformat);
+    slist formats = {0};
+    int jetty = 0;
+    char *s = copy;
+    for (;;) {
+        char *nl = strchr(s, '\n');
+        if (nl) { *nl = 0; if (nl > s && nl[-1] == '\r') nl[-1] = 0; }
+        /* addLogFormat (:110-140) */
+        int blank = 1;
+        for (char *q = s; *q; q++) if (!(*q == ' ' || *q == '\t' || *q == '\r' || *q == '\n' || *q == '\f' || *q == 0x0B)) blank = 0;
+        if (!blank) {
+            char *up = xstrdup(s);
+            ascii_upper(up);
+            char *t = up; while (*t == ' ' || *t == '\t') t++;
+            char *e = t + strlen(t); while (e > t && (e[-1] == ' ' || e[-1] == '\t')) *--e = 0;
+            if (strcmp(t, "ENABLE JETTY FIX") == 0) jetty = 1;
+            else if (!sl_has(&formats, s)) sl_add(&formats, s);
+            free(up);
+        }
+        if (!nl) break;
+        s = nl + 1;
+    }
+    free(copy);
+    if (jetty) {
+        snprintf(err, errlen, "unsupported: ENABLE JETTY FIX");
+        sl_free(&formats);
+        return -1;
+    }
+    root->fmts = (fmtd **)xmalloc(sizeof(fmtd *) * (size_t)(formats.n + 1));
+    for (int i = 0; i < formats.n; i++) {
+        int kind = looks_apache(formats.v[i]) ? FMT_APACHE : looks_nginx(formats.v[i]) ? FMT_NGINX : 0;
+        if (!kind) continue;
+        fmtd *f = fmt_new(kind, formats.v[i]);
+        root->fmts[root->nfmts++] = f;
+        for (int k = 0; k < f->output_types.n; k++) sl_add_unique(&root->outs, f->output_types.v[k]);
+    }
+    sl_free(&formats);
+    int nd = 0;
+    p->dis = (dissector **)xmalloc(sizeof(dissector *) * 64);
+    p->dis[nd++] = root;
+    p->dis[nd++] = dis_new(D_TIMESTAMP, "TIME.STAMP");
+    p->dis[nd++] = dis_new(D_TIMESTAMP_ISO, "TIME.ISO8601");
+    p->dis[nd++] = dis_new(D_FIRSTLINE, "HTTP.FIRSTLINE");
+    p->dis[nd++] = dis_new(D_PROTOCOL, "HTTP.PROTOCOL_VERSION");
+    p->dis[nd++] = dis_new(D_URI, "HTTP.URI");
+    p->dis[nd++] = dis_new(D_QUERY, "HTTP.QUERYSTRING");
+    p->dis[nd++] = dis_new(D_COOKIES, "HTTP.COOKIES");
+    p->dis[nd++] = dis_new(D_SETCOOKIES, "HTTP.SETCOOKIES");
+    p->dis[nd++] = dis_new(D_SETCOOKIE, "HTTP.SETCOOKIE");
+    p->dis[nd++] = dis_new(D_UNIQUEID, "MOD_UNIQUE_ID");
+    dissector *c2n = dis_new(D_CLF2NUM, "BYTESCLF");
+    c2n->out_type = xstrdup("BYTES");
+    sl_add(&c2n->outs, "BYTES:");
+    p->dis[nd++] = c2n;
+    dissector *n2c = dis_new(D_NUM2CLF, "BYTES");
+    n2c->out_type = xstrdup("BYTESCLF");
+    sl_add(&n2c->outs, "BYTESCLF:");
+    p->dis[nd++] = n2c;
+    /* createAdditionalDissectors (core/Parser.java:281-292): token custom
+     * dissectors (StrfTimeStampDissector) + LocalizedTimeDissector */
+    for (int i = 0; i < root->nfmts; i++) {
+        fmtd *f = root->fmts[i];
+        for (int k = 0; k < f->ntokens; k++) {
+            if (f->tokens[k].custom == CUSTOM_STRFTIME && nd < 60) {
+                p->dis[nd++] = dis_new(D_STRFTIME, f->tokens[k].custom_type);
+                p->dis[nd++] = dis_new(D_LOCALIZED, f->tokens[k].custom_type);
+            }
+        }
+    }
+    p->ndis = nd;
+    p->root_type = xstrdup("HTTPLOGLINE");
+    return 0;
+}
+
+/* ============================================================ runtime */
+enum { V_STRING = 0, V_LONG = 1 };
+typedef struct { int filled; js s; int64_t l; int lnull; } val;
+
+static val vstr(js s) { val v; memset(&v, 0, sizeof v); v.filled = V_STRING; v.s = s; return v; }
+static val vlong(int64_t l) { val v; memset(&v, 0, sizeof v); v.filled = V_LONG; v.l = l; return v; }
+
+/* Value.getString (core/Value.java:48-57) */
+static js v_getstring(arena *a, val v) {
+    if (v.filled == V_STRING) return v.s;
+    if (v.lnull) return js_null();
+    char b[32];
+    snprintf(b, sizeof b, "%lld", (long long)v.l);
+    return js_lit(a, b);
+}
+
+typedef struct { char *type; char *name; val v; } pfield;
+typedef struct { char *name; val v; int seq; } rentry;
+
+typedef struct {
+    orc_parser *p;
+    arena *a;
+    pfield *cache; int ncache, capcache;
+    pfield *todo; int ntodo, captodo;
+    rentry *rec; int nrec, caprec;
+    int failed;
+    int unsupported;
+} parsable;
+
+static void cache_put(parsable *ps, const char *type, const char *name, val v) {
+    for (int i = 0; i < ps->ncache; i++)
+        if (strcmp(ps->cache[i].type, type) == 0 && strcmp(ps->cache[i].name, name) == 0) { ps->cache[i].v = v; return; }
+    if (ps->ncache == ps->capcache) { ps->capcache = ps->capcache ? ps->capcache * 2 : 32; ps->cache = (pfield *)realloc(ps->cache, sizeof(pfield) * (size_t)ps->capcache); }
+    char *t = (char *)ar_alloc(ps->a, strlen(type) + 1); strcpy(t, type);
+    char *n = (char *)ar_alloc(ps->a, strlen(name) + 1); strcpy(n, name);
+    ps->cache[ps->ncache].type = t;
+    ps->cache[ps->ncache].name = n;
+    ps->cache[ps->ncache].v = v;
+    ps->ncache++;
+}
+static val *cache_get(parsable *ps, const char *type, const char *name) {
+    for (int i = 0; i < ps->ncache; i++)
+        if (strcmp(ps->cache[i].type, type) == 0 && strcmp(ps->cache[i].name, name) == 0) return &ps->cache[i].v;
+    return NULL;
+}
+static void todo_add(parsable *ps, const char *type, const char *name) {
+    if (ps->ntodo == ps->captodo) { ps->captodo = ps->captodo ? ps->captodo * 2 : 32; ps->todo = (pfield *)realloc(ps->todo, sizeof(pfield) * (size_t)ps->captodo); }
+    char *t = (char *)ar_alloc(ps->a, strlen(type) + 1); strcpy(t, type);
+    char *n = (char *)ar_alloc(ps->a, strlen(name) + 1); strcpy(n, name);
+    ps->todo[ps->ntodo].type = t;
+    ps->todo[ps->ntodo].name = n;
+    ps->ntodo++;
+}
+static void rec_add(parsable *ps, const char *name, val v) {
+    if (ps->nrec == ps->caprec) { ps->caprec = ps->caprec ? ps->caprec * 2 : 64; ps->rec = (rentry *)realloc(ps->rec, sizeof(rentry) * (size_t)ps->caprec); }
+    char *n = (char *)ar_alloc(ps->a, strlen(name) + 1); strcpy(n, name);
+    ps->rec[ps->nrec].name = n;
+    ps->rec[ps->nrec].v = v;
+    ps->rec[ps->nrec].seq = ps->nrec;
+    ps->nrec++;
+}
+
+/* Parsable.addDissection (core/Parsable.java:142-193), no type remappings */
+static void add_dissection(parsable *ps, const char *base, const char *type, const char *name, val v) {
+    char complete[1024], wild[1024], needed[1024];
+    if (base[0] == 0) {
+        snprintf(complete, sizeof complete, "%s", name);
+        snprintf(wild, sizeof wild, "%s:*", type);
+    } else {
+        if (name[0] == 0) snprintf(complete, sizeof complete, "%s", base);
+        else snprintf(complete, sizeof complete, "%s.%s", base, name);
+        snprintf(wild, sizeof wild, "%s:%s.*", type, base);
+    }
+    snprintf(needed, sizeof needed, "%s:%s", type, complete);
+    if (sl_has(&ps->p->useful, complete)) {
+        cache_put(ps, type, complete, v);
+        todo_add(ps, type, complete);
+    }
+    if (sl_has(&ps->p->needed, needed)) rec_add(ps, needed, v);
+    if (sl_has(&ps->p->needed, wild)) rec_add(ps, needed, v);
+}
+
+static void add_str(parsable *ps, const char *base, const char *type, const char *name, js s) {
+    add_dissection(ps, base, type, name, vstr(s));
+}
+static void add_long(parsable *ps, const char *base, const char *type, const char *name, int64_t l) {
+    add_dissection(ps, base, type, name, vlong(l));
+}
+static char *js_cstr(parsable *ps, js s) { return js_to_utf8(ps->a, s, NULL); }
+
+/* ------------------------------------------------------ root / format */
+/* ApacheHttpdLogFormatDissector.decodeExtractedValue (:169-196): note the
+ * condition tests the VALUE (not the token name), as the reference does. */
+static int apache_decode(parsable *ps, js value, js *out) {
+    if (value.null || value.n == 0) { *out = value; return 0; }
+    if (js_eq_lit(value, "-")) { *out = js_null(); return 0; }
+    if (js_eq_lit(value, "request.firstline") || js_starts_lit(value, "request.header.") || js_starts_lit(value, "response.header.")) {
+        if (js_index_of_char(value, '\\', 0) >= 0) { ps->unsupported = 1; return -1; }
+    }
+    *out = value;
+    return 0;
+}
+
+/* TokenFormatDissector.dissect (:243-275); returns 1 on match */
+static int fmt_dissect(parsable *ps, fmtd *f, js line, const char *inputname) {
+    if (f->unsupported) { ps->unsupported = 1; return 0; }
+    int caps[2 * 128];
+    if (f->nused >= 127) { ps->unsupported = 1; return 0; }
+    if (!jre_find(f->re, line.c, line.n, 0, caps)) return 0;
+    for (int g = 1; g <= f->nused; g++) {
+        token *t = &f->tokens[f->used[g - 1]];
+        js grp = caps[2 * g] < 0 ? js_null() : js_sub(line, caps[2 * g], caps[2 * g + 1]);
+        for (int k = 0; k < t->nouts; k++) {
+            js dec;
+            if (f->kind == FMT_APACHE) { if (apache_decode(ps, grp, &dec) < 0) return 1; }
+            else dec = js_eq_lit(grp, "-") ? js_null() : grp; /* NginxHttpdLogFormatDissector.java:107-119 */
+            add_str(ps, inputname, t->outs[k].type, t->outs[k].name, dec);
+        }
+    }
+    return 1;
+}
+
+/* HttpdLogFormatDissector.dissect (:173-204) */
+static void d_root(parsable *ps, instance *in, const char *inputname) {
+    val *v = cache_get(ps, "HTTPLOGLINE", inputname);
+    js line = v_getstring(ps->a, *v);
+    if (in->nfmts == 0) { ps->failed = 1; return; }
+    if (in->active < 0) in->active = 0;
+    if (fmt_dissect(ps, in->fmts[in->active], line, inputname)) return;
+    if (ps->unsupported) return;
+    if (in->nfmts > 1) {
+        for (int i = 0; i < in->nfmts; i++) {
+            if (fmt_dissect(ps, in->fmts[i], line, inputname)) { in->active = i; return; }
+            if (ps->unsupported) return;
+        }
+    }
+    ps->failed = 1;
+}
+
+/* ------------------------------------------------------------- time */
+static int64_t days_from_civil(int64_t y, int m, int d) {
+    y -= m <= 2;
+    const int64_t era = (y >= 0 ? y : y - 399) / 400;
+    const int64_t yoe = y - era * 400;
+    const int64_t doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+    const int64_t doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+    return era * 146097 + doe - 719468;
+}
+static void civil_from_days(int64_t z, int64_t *y, int *m, int *d) {
+    z += 719468;
+    const int64_t era = (z >= 0 ? z : z - 146096) / 146097;
+    const int64_t doe = z - era * 146097;
+    const int64_t yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+    const int64_t yy = yoe + era * 400;
+    const int64_t doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
+    const int64_t mp = (5 * doy + 2) / 153;
+    *d = (int)(doy - (153 * mp + 2) / 5 + 1);
+    *m = (int)(mp < 10 ? mp + 3 : mp - 9);
+    *y = yy + (*m <= 2);
+}
+static int is_leap(int64_t y) { return (y % 4 == 0 && y % 100 != 0) || y % 400 == 0; }
+static int month_len(int64_t y, int m) {
+    static const int ml[] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+    return m == 2 ? (is_leap(y) ? 29 : 28) : ml[m - 1];
+}
+/* ISO-8601 week fields (WeekFields.ISO == WeekFields.of(Locale.UK)) */
+static void iso_week(int64_t y, int m, int d, int64_t *wy, int *wk) {
+    int64_t days = days_from_civil(y, m, d);
+    int wd = (int)(((days % 7) + 7 + 3) % 7) + 1; /* 1970-01-01 = Thursday; Mon=1 */
+    int doy = (int)(days - days_from_civil(y, 1, 1)) + 1;
+    int w = (doy - wd + 10) / 7;
+    if (w < 1) {
+        int64_t py = y - 1;
+        int64_t jan1 = days_from_civil(py, 1, 1);
+        int jwd = (int)(((jan1 % 7) + 7 + 3) % 7) + 1;
+        int weeks = (jwd == 4 || (jwd == 3 && is_leap(py))) ? 53 : 52;
+        *wy = py; *wk = weeks;
+        return;
+    }
+    int64_t jan1 = days_from_civil(y, 1, 1);
+    int jwd = (int)(((jan1 % 7) + 7 + 3) % 7) + 1;
+    int weeks = (jwd == 4 || (jwd == 3 && is_leap(y))) ? 53 : 52;
+    if (w > weeks) { *wy = y + 1; *wk = 1; return; }
+    *wy = y; *wk = w;
+}
+
+static const char *MONTH_SHORT[] = {"Jan", "Feb", "Mar", "Apr", "May", "Jun", "Jul", "Aug", "Sep", "Oct", "Nov", "Dec"};
+static const char *MONTH_FULL[] = {"January", "February", "March", "April", "May", "June", "July", "August", "September", "October", "November", "December"};
+
+static int dig(int c) { return c >= '0' && c <= '9' ? c - '0' : -1; }
+
+/* DateTimeFormatter "dd/MMM/yyyy:HH:mm:ss ZZ" (parseCaseInsensitive,
+ * Locale.UK, SMART resolver) -- TimeStampDissector.java:46,100-109,418.
+ * Returns 0 ok, 1 DateTimeParseException. */
+static int parse_apache_time(js s, int64_t *ly, int *lm, int *ld, int *lh, int *lmi, int *ls, int *offset_secs) {
+    if (s.n != 26) return 1;
+    const int *c = s.c;
+    int d1 = dig(c[0]), d2 = dig(c[1]);
+    if (d1 < 0 || d2 < 0 || c[2] != '/') return 1;
+    int day = d1 * 10 + d2;
+    int month = -1;
+    for (int m = 0; m < 12; m++) {
+        int ok = 1;
+        for (int k = 0; k < 3; k++) {
+            int x = c[3 + k], y = MONTH_SHORT[m][k];
+            if (x >= 'a' && x <= 'z') x -= 32;
+            if (y >= 'a' && y <= 'z') y -= 32;
+            if (x != y) ok = 0;
+        }
+        if (ok) { month = m + 1; break; }
+    }
+    if (month < 0 || c[6] != '/') return 1;
+    int64_t year = 0;
+    for (int k = 0; k < 4; k++) { int v = dig(c[7 + k]); if (v < 0) return 1; year = year * 10 + v; }
+    if (c[11] != ':') return 1;
+    int hh = dig(c[12]) * 10 + dig(c[13]);
+    if (dig(c[12]) < 0 || dig(c[13]) < 0 || c[14] != ':') return 1;
+    int mi = dig(c[15]) * 10 + dig(c[16]);
+    if (dig(c[15]) < 0 || dig(c[16]) < 0 || c[17] != ':') return 1;
+    int ss = dig(c[18]) * 10 + dig(c[19]);
+    if (dig(c[18]) < 0 || dig(c[19]) < 0 || c[20] != ' ') return 1;
+    /* OffsetIdPrinterParser("+HHMM","+0000") */
+    int off;
+    if (c[21] == '+' && c[22] == '0' && c[23] == '0' && c[24] == '0' && c[25] == '0') off = 0;
+    else {
+        if (c[21] != '+' && c[21] != '-') return 1;
+        int oh1 = dig(c[22]), oh2 = dig(c[23]), om1 = dig(c[24]), om2 = dig(c[25]);
+        if (oh1 < 0 || oh2 < 0 || om1 < 0 || om2 < 0) return 1;
+        int oh = oh1 * 10 + oh2, om = om1 * 10 + om2;
+        if (oh > 59 || om > 59) return 1;
+        off = (c[21] == '-' ? -1 : 1) * (oh * 3600 + om * 60);
+    }
+    /* resolve: ZoneOffset.ofTotalSeconds range */
+    if (off > 18 * 3600 || off < -18 * 3600) return 1;
+    /* resolveDate: DAY_OF_MONTH 1..31, MONTH 1..12; SMART clamps to month length */
+    if (day < 1 || day > 31) return 1;
+    int ml = month_len(year, month);
+    if (day > ml) day = ml;
+    /* resolveTime: MINUTE 0..59, SMART 24:00:00 = end of day */
+    if (mi > 59) return 1;
+    int plus_day = 0;
+    if (hh == 24 && mi == 0 && ss == 0) { hh = 0; plus_day = 1; }
+    else {
+        if (hh > 23) return 1;
+        if (ss > 59) return 1;
+    }
+    if (plus_day) {
+        int64_t days = days_from_civil(year, month, day) + 1;
+        civil_from_days(days, &year, &month, &day);
+    }
+    *ly = year; *lm = month; *ld = day; *lh = hh; *lmi = mi; *ls = ss; *offset_secs = off;
+    return 0;
+}
+
+static int has_req(instance *in, const char *n) { return sl_has(&in->requested, n); }
+
+static js fmt2(parsable *ps, const char *f, int64_t a, int b, int c) {
+    char buf[64];
+    snprintf(buf, sizeof buf, f, (long long)a, b, c);
+    return js_lit(ps->a, buf);
+}
+
+/* TimeStampDissector.dissect (:404-564) */
+static void d_timestamp(parsable *ps, instance *in, const char *inputname) {
+    val *vp = cache_get(ps, in->d->in_type, inputname);
+    js s = v_getstring(ps->a, *vp);
+    if (s.null || s.n == 0) return;
+    int64_t y; int m, d, h, mi, sec, off;
+    if (parse_apache_time(s, &y, &m, &d, &h, &mi, &sec, &off)) { ps->failed = 1; return; }
+    int64_t epoch_s = days_from_civil(y, m, d) * 86400 + h * 3600 + mi * 60 + sec - off;
+    int any_tz = has_req(in, "timezone") || has_req(in, "epoch");
+    if (any_tz) {
+        /* timezone: emitted as TIME.TIMEZONE but advertised as TIME.ZONE ->
+         * never stored (:429); only epoch matters */
+        if (has_req(in, "epoch")) add_long(ps, inputname, "TIME.EPOCH", "epoch", epoch_s * 1000);
+    }
+    const char *asp[] = {"day", "monthname", "month", "weekofweekyear", "weekyear", "year", "hour", "minute", "second",
+                         "millisecond", "microsecond", "nanosecond", "date", "time", NULL};
+    int any_local = 0, any_utc = 0;
+    for (int i = 0; asp[i]; i++) {
+        char u[64];
+        snprintf(u, sizeof u, "%s_utc", asp[i]);
+        if (has_req(in, asp[i])) any_local = 1;
+        if (has_req(in, u)) any_utc = 1;
+    }
+    for (int pass = 0; pass < 2; pass++) {
+        if (pass == 0 && !any_local) continue;
+        if (pass == 1 && !any_utc) continue;
+        int64_t Y = y; int M = m, D = d, H = h, MI = mi, S = sec;
+        if (pass == 1) {
+            int64_t days = epoch_s >= 0 ? epoch_s / 86400 : -((-epoch_s + 86399) / 86400);
+            int64_t rem = epoch_s - days * 86400;
+            civil_from_days(days, &Y, &M, &D);
+            H = (int)(rem / 3600); MI = (int)(rem % 3600 / 60); S = (int)(rem % 60);
+        }
+        const char *sfx = pass == 1 ? "_utc" : "";
+        char nm[64];
+#define WANT(base) (snprintf(nm, sizeof nm, "%s%s", base, sfx), has_req(in, nm))
+        int64_t wy; int wk;
+        iso_week(Y, M, D, &wy, &wk);
+        if (WANT("day")) add_long(ps, inputname, "TIME.DAY", nm, D);
+        if (WANT("monthname")) add_str(ps, inputname, "TIME.MONTHNAME", nm, js_lit(ps->a, MONTH_FULL[M - 1]));
+        if (WANT("month")) add_long(ps, inputname, "TIME.MONTH", nm, M);
+        if (WANT("weekofweekyear")) add_long(ps, inputname, "TIME.WEEK", nm, wk);
+        if (WANT("weekyear")) add_long(ps, inputname, "TIME.YEAR", nm, wy);
+        if (WANT("year")) add_long(ps, inputname, "TIME.YEAR", nm, Y);
+        if (WANT("hour")) add_long(ps, inputname, "TIME.HOUR", nm, H);
+        if (WANT("minute")) add_long(ps, inputname, "TIME.MINUTE", nm, MI);
+        if (WANT("second")) add_long(ps, inputname, "TIME.SECOND", nm, S);
+        if (WANT("millisecond")) add_long(ps, inputname, "TIME.MILLISECOND", nm, 0);
+        if (WANT("microsecond")) add_long(ps, inputname, "TIME.MICROSECOND", nm, 0);
+        if (WANT("nanosecond")) add_long(ps, inputname, "TIME.NANOSECOND", nm, 0);
+        if (WANT("date")) add_str(ps, inputname, "TIME.DATE", nm, fmt2(ps, "%04lld-%02d-%02d", Y, M, D));
+        if (WANT("time")) add_str(ps, inputname, "TIME.TIME", nm, fmt2(ps, "%02lld:%02d:%02d", H, MI, S));
+#undef WANT
+    }
+}
+
+/* ------------------------------------------------------- first line */
+static jre *g_fl1, *g_fl2, *g_bad_escape, *g_almost_html, *g_eq_hash, *g_hash_amp, *g_double_hash;
+static jre *g_q_question, *g_q_amp, *g_valid_std, *g_chopped_std, *g_valid_nonstd, *g_chopped_nonstd;
+static pthread_once_t g_re_once = PTHREAD_ONCE_INIT;
+static void init_res(void) {
+    g_fl1 = must_compile("^([a-zA-Z-_]+) (.*) (HTTP/[0-9]+\\.[0-9]+)$");   /* HttpFirstLineDissector.java:59-60 */
+    g_fl2 = must_compile("^([a-zA-Z-_]+) (.*)$");                            /* :62-63 */
+    g_bad_escape = must_compile("%([^0-9a-fA-F]|[0-9a-fA-F][^0-9a-fA-F]|.$|$)"); /* HttpUriDissector.java:123 */
+    g_almost_html = must_compile("([^&])(#x[0-9a-fA-F][0-9a-fA-F];)");     /* :127 */
+    g_eq_hash = must_compile("=#");
+    g_hash_amp = must_compile("#&");
+    g_double_hash = must_compile("#(.*)#");
+    g_q_question = must_compile("\\?");
+    g_q_amp = must_compile("&");
+    g_valid_std = must_compile("%([0-9A-Fa-f]{2})");                        /* Utils.java:27-30 */
+    g_chopped_std = must_compile("%[0-9A-Fa-f]?$");
+    g_valid_nonstd = must_compile("%u([0-9A-Fa-f][0-9A-Fa-f])([0-9A-Fa-f][0-9A-Fa-f])");
+    g_chopped_nonstd = must_compile("%u[0-9A-Fa-f]{0,3}$");
+}
+
+/* HttpFirstLineDissector.dissect (:86-122) */
+static void d_firstline(parsable *ps, instance *in, const char *inputname) {
+    val *vp = cache_get(ps, "HTTP.FIRSTLINE", inputname);
+    js s = v_getstring(ps->a, *vp);
+    if (s.null || s.n == 0 || js_eq_lit(s, "-")) return;
+    int caps[8];
+    if (jre_find(g_fl1, s.c, s.n, 0, caps)) {
+        if (has_req(in, "method")) add_str(ps, inputname, "HTTP.METHOD", "method", js_sub(s, caps[2], caps[3]));
+        if (has_req(in, "uri")) add_str(ps, inputname, "HTTP.URI", "uri", js_sub(s, caps[4], caps[5]));
+        if (has_req(in, "protocol")) add_str(ps, inputname, "HTTP.PROTOCOL_VERSION", "protocol", js_sub(s, caps[6], caps[7]));
+        return;
+    }
+    if (jre_find(g_fl2, s.c, s.n, 0, caps)) {
+        if (has_req(in, "method")) add_str(ps, inputname, "HTTP.METHOD", "method", js_sub(s, caps[2], caps[3]));
+        if (has_req(in, "uri")) add_str(ps, inputname, "HTTP.URI", "uri", js_sub(s, caps[4], caps[5]));
+        add_str(ps, inputname, "HTTP.PROTOCOL_VERSION", "protocol", js_null());
+    }
+}
+
+/* HttpFirstLineProtocolDissector.dissect (:56-77) */
+static void d_protocol(parsable *ps, instance *in, const char *inputname) {
+    val *vp = cache_get(ps, "HTTP.PROTOCOL_VERSION", inputname);
+    js s = v_getstring(ps->a, *vp);
+    if (s.null || s.n == 0 || js_eq_lit(s, "-")) return;
+    js *parts;
+    int np = js_split_char_limit(ps->a, s, '/', 2, &parts);
+    if (np == 2) {
+        if (has_req(in, "")) add_str(ps, inputname, "HTTP.PROTOCOL", "", parts[0]);
+        if (has_req(in, "version")) add_str(ps, inputname, "HTTP.PROTOCOL.VERSION", "version", parts[1]);
+        return;
+    }
+    add_str(ps, inputname, "HTTP.PROTOCOL", "", js_null());
+    add_str(ps, inputname, "HTTP.PROTOCOL.VERSION", "version", js_null());
+}
+
+/* ------------------------------------------------------------- URI */
+/* commons-httpclient 3.1 URIUtil.encode(s, allowed, "UTF-8") with the
+ * HttpUriDissector badUriChars set (HttpUriDissector.java:111-120):
+ * allowed = 0..254 minus URI.unwise {}|\^[]` , space, control (0-0x1F,0x7F),
+ * and <>".  Bytes >= 0x80 stay raw and then decode as US-ASCII -> U+FFFD. */
+static int uri_allowed(int b) {
+    if (b == 255) return 0;
+    if (b <= 0x20 || b == 0x7F) return 0;
+    switch (b) {
+    case '{': case '}': case '|': case '\\': case '^': case '[': case ']': case '`':
+    case '<': case '>': case '"': return 0;
+    }
+    return 1;
+}
+static js uriutil_encode(parsable *ps, js s) {
+    int blen;
+    char *u8 = js_to_utf8(ps->a, s, &blen);
+    int *o = (int *)ar_alloc(ps->a, sizeof(int) * (size_t)(blen * 3 + 1));
+    int k = 0;
+    static const char *HX = "0123456789ABCDEF";
+    for (int i = 0; i < blen; i++) {
+        int b = (unsigned char)u8[i];
+        if (uri_allowed(b)) o[k++] = b >= 0x80 ? 0xFFFD : b;
+        else { o[k++] = '%'; o[k++] = HX[b >> 4]; o[k++] = HX[b & 15]; }
+    }
+    js r = {o, k, 0};
+    return r;
+}
+
+/* commons-lang3 3.8.1 StringEscapeUtils.unescapeHtml4 restated for the
+ * BASIC + ISO8859_1 tables and NumericEntityUnescaper(semiColonRequired).
+ * Any other '&name;' sequence -> UNSUPPORTED (HTML40 extended table not
+ * restated). */
+static const char *LAT1[] = {"nbsp", "iexcl", "cent", "pound", "curren", "yen", "brvbar", "sect", "uml", "copy", "ordf", "laquo", "not", "shy", "reg", "macr",
+                             "deg", "plusmn", "sup2", "sup3", "acute", "micro", "para", "middot", "cedil", "sup1", "ordm", "raquo", "frac14", "frac12", "frac34", "iquest",
+                             "Agrave", "Aacute", "Acirc", "Atilde", "Auml", "Aring", "AElig", "Ccedil", "Egrave", "Eacute", "Ecirc", "Euml", "Igrave", "Iacute", "Icirc", "Iuml",
+                             "ETH", "Ntilde", "Ograve", "Oacute", "Ocirc", "Otilde", "Ouml", "times", "Oslash", "Ugrave", "Uacute", "Ucirc", "Uuml", "Yacute", "THORN", "szlig",
+                             "agrave", "aacute", "acirc", "atilde", "auml", "aring", "aelig", "ccedil", "egrave", "eacute", "ecirc", "euml", "igrave", "iacute", "icirc", "iuml",
+                             "eth", "ntilde", "ograve", "oacute", "ocirc", "otilde", "ouml", "divide", "oslash", "ugrave", "uacute", "ucirc", "uuml", "yacute", "thorn", "yuml"};
+static int is_hexc(int c) { return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'f') || (c >= 'A' && c <= 'F'); }
+static int is_alnum(int c) { return (c >= '0' && c <= '9') || (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z'); }
+
+static js unescape_html4(parsable *ps, js s) {
+    int *o = (int *)ar_alloc(ps->a, sizeof(int) * (size_t)(s.n + 1));
+    int k = 0, changed = 0;
+    for (int i = 0; i < s.n;) {
+        int c = s.c[i];
+        if (c == '&') {
+            /* Lookup translators: longest key first; keys are &name; */
+            int j = i + 1;
+            while (j < s.n && is_alnum(s.c[j]) && j - i <= 10) j++;
+            if (j < s.n && s.c[j] == ';' && j > i + 1) {
+                char nm[16];
+                int L = j - i - 1;
+                for (int q = 0; q < L; q++) nm[q] = (char)s.c[i + 1 + q];
+                nm[L] = 0;
+                int val = -1;
+                if (!strcmp(nm, "quot")) val = '"';
+                else if (!strcmp(nm, "amp")) val = '&';
+                else if (!strcmp(nm, "lt")) val = '<';
+                else if (!strcmp(nm, "gt")) val = '>';
+                else for (int q = 0; q < 96; q++) if (!strcmp(nm, LAT1[q])) { val = 160 + q; break; }
+                if (val >= 0) { o[k++] = val; i = j + 1; changed = 1; continue; }
+                ps->unsupported = 1; /* possibly an HTML40-extended entity */
+                return s;
+            }
+            /* NumericEntityUnescaper */
+            if (i < s.n - 2 && s.c[i + 1] == '#') {
+                int start = i + 2, hex = 0;
+                if (s.c[start] == 'x' || s.c[start] == 'X') { start++; hex = 1; if (start == s.n) goto copy; }
+                int end = start;
+                while (end < s.n && is_hexc(s.c[end])) end++;
+                int semi = end != s.n && s.c[end] == ';';
+                if (!semi) goto copy;
+                if (end == start) goto copy; /* parseInt("") -> NFE -> 0 */
+                long long v = 0;
+                int bad = 0;
+                for (int q = start; q < end; q++) {
+                    int dv = s.c[q] <= '9' ? s.c[q] - '0' : (s.c[q] | 32) - 'a' + 10;
+                    if (!hex && dv > 9) { bad = 1; break; }
+                    v = v * (hex ? 16 : 10) + dv;
+                    if (v > 0x7FFFFFFF) { bad = 1; break; }
+                }
+                if (bad) goto copy;
+                if (v > 0x10FFFF || (v >= 0xD800 && v <= 0xDFFF)) { ps->unsupported = 1; return s; }
+                o[k++] = (int)v;
+                i = end + 1;
+                changed = 1;
+                continue;
+            }
+        }
+    copy:
+        o[k++] = c;
+        i++;
+    }
+    if (!changed) return s;
+    js r = {o, k, 0};
+    return r;
+}
+
+/* java.net.URI.decode (UTF-8 with REPLACE); invalid UTF-8 -> UNSUPPORTED */
+static js uri_decode(parsable *ps, js s) {
+    if (s.null || s.n == 0 || js_index_of_char(s, '%', 0) < 0) return s;
+    int *o = (int *)ar_alloc(ps->a, sizeof(int) * (size_t)(s.n + 1));
+    int k = 0, between = 0;
+    for (int i = 0; i < s.n;) {
+        int c = s.c[i];
+        if (c == '[') between = 1;
+        else if (between && c == ']') between = 0;
+        if (c != '%' || between) { o[k++] = c; i++; continue; }
+        unsigned char bytes[4096];
+        int nb = 0;
+        while (i < s.n && s.c[i] == '%') {
+            if (i + 2 >= s.n) { ps->unsupported = 1; return s; }
+            int h1 = s.c[i + 1], h2 = s.c[i + 2];
+            int v1 = h1 <= '9' ? h1 - '0' : (h1 | 32) - 'a' + 10;
+            int v2 = h2 <= '9' ? h2 - '0' : (h2 | 32) - 'a' + 10;
+            if (nb < 4096) bytes[nb++] = (unsigned char)(v1 * 16 + v2);
+            i += 3;
+        }
+        /* strict UTF-8 decode */
+        for (int q = 0; q < nb;) {
+            unsigned b = bytes[q];
+            int need, cp;
+            if (b < 0x80) { need = 0; cp = (int)b; }
+            else if (b >= 0xC2 && b <= 0xDF) { need = 1; cp = (int)(b & 0x1F); }
+            else if (b >= 0xE0 && b <= 0xEF) { need = 2; cp = (int)(b & 0x0F); }
+            else if (b >= 0xF0 && b <= 0xF4) { need = 3; cp = (int)(b & 0x07); }
+            else { ps->unsupported = 1; return s; }
+            if (need > 0 && q + need >= nb) { ps->unsupported = 1; return s; }
+            for (int r = 1; r <= need; r++) {
+                if ((bytes[q + r] & 0xC0) != 0x80) { ps->unsupported = 1; return s; }
+                cp = (cp << 6) | (bytes[q + r] & 0x3F);
+            }
+            if ((need == 2 && (cp < 0x800 || (cp >= 0xD800 && cp <= 0xDFFF))) || (need == 3 && (cp < 0x10000 || cp > 0x10FFFF))) {
+                ps->unsupported = 1;
+                return s;
+            }
+            o[k++] = cp;
+            q += need + 1;
+        }
+    }
+    js r = {o, k, 0};
+    return r;
+}
+
+/* java.net.URI parser (RFC 2396 as implemented by JDK 8 java.net.URI.Parser) */
+#define CL_ALPHA 1
+#define CL_DIGIT 2
+#define CL_MARK 4      /* -_.!~*'() */
+#define CL_RESERVED 8  /* ;/?:@&=+$,[] */
+static int ccls(int c) {
+    int r = 0;
+    if ((c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z')) r |= CL_ALPHA;
+    if (c >= '0' && c <= '9') r |= CL_DIGIT;
+    if (c && strchr("-_.!~*'()", c) && c < 128) r |= CL_MARK;
+    if (c && strchr(";/?:@&=+$,[]", c) && c < 128) r |= CL_RESERVED;
+    return r;
+}
+typedef struct {
+    js s;
+    js scheme, userinfo, host, path, query, fragment;
+    int port;
+    int fail;
+} urip;
+
+enum { K_URIC, K_PATH, K_SCHEME, K_USERINFO, K_SERVER, K_REGNAME };
+static int char_ok(int k, int c) {
+    int cl = ccls(c);
+    int unreserved = cl & (CL_ALPHA | CL_DIGIT | CL_MARK);
+    switch (k) {
+    case K_URIC: return unreserved || (cl & CL_RESERVED);
+    case K_PATH: return unreserved || (c && c < 128 && strchr(":@&=+$,;/", c));
+    case K_SCHEME: return (cl & (CL_ALPHA | CL_DIGIT)) || c == '+' || c == '-' || c == '.';
+    case K_USERINFO: return unreserved || (c && c < 128 && strchr(";:&=+$,", c));
+    case K_SERVER: return unreserved || (c && c < 128 && strchr(";:&=+$,", c)) || (cl & (CL_ALPHA | CL_DIGIT)) || c == '-' || (c && c < 128 && strchr(".:@[]", c));
+    case K_REGNAME: return unreserved || (c && c < 128 && strchr("$,;:@&=+", c));
+    }
+    return 0;
+}
+/* scan while chars match class k, allowing escapes (and non-ASCII "other") */
+static int u_scan_cls(urip *u, int p, int n, int k, int escapes) {
+    while (p < n) {
+        int c = u->s.c[p];
+        if (char_ok(k, c)) { p++; continue; }
+        if (escapes) {
+            if (c == '%') {
+                if (p + 3 <= n && is_hexc(u->s.c[p + 1]) && is_hexc(u->s.c[p + 2])) { p += 3; continue; }
+                u->fail = 1; /* Malformed escape pair */
+                return p;
+            }
+            if (c > 128) { u->fail = 2; return p; } /* "other" chars: not restated */
+        }
+        break;
+    }
+    return p;
+}
+static int u_scan_stop(urip *u, int p, int n, const char *err, const char *stop) {
+    while (p < n) {
+        int c = u->s.c[p];
+        if (c < 128 && c && strchr(err, c)) return -1;
+        if (c < 128 && c && strchr(stop, c)) break;
+        p++;
+    }
+    return p;
+}
+static int u_check(urip *u, int p, int q, int k) {
+    int r = u_scan_cls(u, p, q, k, 1);
+    if (u->fail) return 0;
+    if (r < q) { u->fail = 1; return 0; }
+    return 1;
+}
+static int u_at(urip *u, int p, int n, int c) { return p < n && u->s.c[p] == c; }
+
+static int u_scan_byte(urip *u, int p, int n) {
+    int q = p;
+    while (q < n && u->s.c[q] >= '0' && u->s.c[q] <= '9') q++;
+    if (q <= p) return q;
+    long long v = 0;
+    for (int i = p; i < q; i++) { v = v * 10 + (u->s.c[i] - '0'); if (v > 100000) break; }
+    if (v > 255) return p;
+    return q;
+}
+/* parseIPv4Address: returns end or -1 */
+static int u_ipv4(urip *u, int start, int n) {
+    int p = start, m = start;
+    while (m < n && ((u->s.c[m] >= '0' && u->s.c[m] <= '9') || u->s.c[m] == '.')) m++;
+    if (m <= p) return -1;
+    int q;
+    int ok = 0;
+    for (;;) {
+        if ((q = u_scan_byte(u, p, m)) <= p) break; p = q;
+        if (!u_at(u, p, m, '.')) break; p++;
+        if ((q = u_scan_byte(u, p, m)) <= p) break; p = q;
+        if (!u_at(u, p, m, '.')) break; p++;
+        if ((q = u_scan_byte(u, p, m)) <= p) break; p = q;
+        if (!u_at(u, p, m, '.')) break; p++;
+        if ((q = u_scan_byte(u, p, m)) <= p) break; p = q;
+        if (q < m) break;
+        ok = 1;
+        break;
+    }
+    if (!ok) return -1;
+    if (p > start && p < n && u->s.c[p] != ':') return -1;
+    if (p > start) u->host = js_sub(u->s, start, p);
+    return p;
+}
+static int u_hostname(urip *u, int start, int n) {
+    int p = start, q, l = -1;
+    do {
+        q = p;
+        while (q < n && (ccls(u->s.c[q]) & (CL_ALPHA | CL_DIGIT))) q++;
+        if (q <= p) break;
+        l = p;
+        p = q;
+        q = p;
+        while (q < n && ((ccls(u->s.c[q]) & (CL_ALPHA | CL_DIGIT)) || u->s.c[q] == '-')) q++;
+        if (q > p) {
+            if (u->s.c[q - 1] == '-') { u->fail = 1; return -1; }
+            p = q;
+        }
+        if (!u_at(u, p, n, '.')) break;
+        p++;
+    } while (p < n);
+    if (p < n && !u_at(u, p, n, ':')) { u->fail = 1; return -1; }
+    if (l < 0) { u->fail = 1; return -1; }
+    if (l > start && !(ccls(u->s.c[l]) & CL_ALPHA)) { u->fail = 1; return -1; }
+    u->host = js_sub(u->s, start, p);
+    return p;
+}
+static int u_server(urip *u, int start, int n) {
+    int p = start, q;
+    q = u_scan_stop(u, p, n, "/?#", "@");
+    if (q >= p && u_at(u, q, n, '@')) {
+        if (!u_check(u, p, q, K_USERINFO)) return -1;
+        u->userinfo = js_sub(u->s, p, q);
+        p = q + 1;
+    }
+    if (u_at(u, p, n, '[')) { u->fail = 2; return -1; } /* IPv6 literal: not restated */
+    q = u_ipv4(u, p, n);
+    if (q <= p) {
+        q = u_hostname(u, p, n);
+        if (u->fail) return -1;
+    }
+    p = q;
+    if (u_at(u, p, n, ':')) {
+        p++;
+        q = u_scan_stop(u, p, n, "", "/");
+        if (q > p) {
+            for (int i = p; i < q; i++) if (!(u->s.c[i] >= '0' && u->s.c[i] <= '9')) { u->fail = 1; return -1; }
+            long long v = 0;
+            for (int i = p; i < q; i++) { v = v * 10 + (u->s.c[i] - '0'); if (v > 0x7FFFFFFF) { u->fail = 1; return -1; } }
+            u->port = (int)v;
+            p = q;
+        }
+    }
+    if (p < n) { u->fail = 1; return -1; }
+    return p;
+}
+static int u_authority(urip *u, int p, int n) {
+    int server_chars, reg_chars;
+    int q = p;
+    for (q = p; q < n && char_ok(K_SERVER, u->s.c[q]); q++) {}
+    /* JDK: scan(p, n, "]") > p  ->  authority starts with ']' (never for our inputs) */
+    server_chars = (q == n);
+    int r = p;
+    while (r < n) {
+        int c = u->s.c[r];
+        if (char_ok(K_REGNAME, c)) { r++; continue; }
+        if (c == '%' && r + 3 <= n && is_hexc(u->s.c[r + 1]) && is_hexc(u->s.c[r + 2])) { r += 3; continue; }
+        if (c == '%') { u->fail = 1; return n; }
+        if (c > 128) { u->fail = 2; return n; }
+        break;
+    }
+    reg_chars = (r == n);
+    if (reg_chars && !server_chars) return n; /* registry-based */
+    int failed = 0;
+    q = p;
+    if (server_chars) {
+        urip save = *u;
+        int e = u_server(u, p, n);
+        if (u->fail == 2) return n;
+        if (u->fail || e < n) {
+            *u = save;
+            u->userinfo = js_null(); u->host = js_null(); u->port = -1;
+            u->fail = 0;
+            failed = 1;
+            q = p;
+        } else q = n;
+    }
+    if (q < n) {
+        if (reg_chars) return n;
+        (void)failed;
+        u->fail = 1;
+    }
+    return n;
+}
+static int u_hier(urip *u, int start, int n) {
+    int p = start;
+    if (u_at(u, p, n, '/') && u_at(u, p + 1, n, '/')) {
+        p += 2;
+        int q = u_scan_stop(u, p, n, "", "/?#");
+        if (q > p) p = u_authority(u, p, q);
+        else if (q < n) { /* empty authority allowed */ }
+        else { u->fail = 1; return n; }
+        if (u->fail) return n;
+    }
+    int q = u_scan_stop(u, p, n, "", "?#");
+    if (!u_check(u, p, q, K_PATH)) return n;
+    u->path = js_sub(u->s, p, q);
+    p = q;
+    if (u_at(u, p, n, '?')) {
+        p++;
+        q = u_scan_stop(u, p, n, "", "#");
+        if (!u_check(u, p, q, K_URIC)) return n;
+        u->query = js_sub(u->s, p, q);
+        p = q;
+    }
+    return p;
+}
+static void u_parse(urip *u) {
+    int n = u->s.n;
+    u->scheme = u->userinfo = u->host = u->path = u->query = u->fragment = js_null();
+    u->port = -1;
+    u->fail = 0;
+    int p = u_scan_stop(u, 0, n, "/?#", ":");
+    if (p >= 0 && u_at(u, p, n, ':')) {
+        if (p == 0) { u->fail = 1; return; }
+        if (!(ccls(u->s.c[0]) & CL_ALPHA)) { u->fail = 1; return; }
+        for (int i = 1; i < p; i++) if (!char_ok(K_SCHEME, u->s.c[i])) { u->fail = 1; return; }
+        u->scheme = js_sub(u->s, 0, p);
+        p++;
+        if (u_at(u, p, n, '/')) {
+            p = u_hier(u, p, n);
+            if (u->fail) return;
+        } else {
+            int q = u_scan_stop(u, p, n, "", "#");
+            if (q <= p) { u->fail = 1; return; }
+            if (!u_check(u, p, q, K_URIC)) return;
+            p = q; /* opaque: path/query stay null */
+        }
+    } else {
+        p = u_hier(u, 0, n);
+        if (u->fail) return;
+    }
+    if (u_at(u, p, n, '#')) {
+        if (!u_check(u, p + 1, n, K_URIC)) return;
+        u->fragment = js_sub(u->s, p + 1, n);
+        p = n;
+    }
+    if (p < n) u->fail = 1;
+}
+
+/* HttpUriDissector.dissect (:130-233) */
+static void d_uri(parsable *ps, instance *in, const char *inputname) {
+    val *vp = cache_get(ps, "HTTP.URI", inputname);
+    js s = v_getstring(ps->a, *vp);
+    if (s.null || s.n == 0) return;
+    for (int i = 0; i < s.n; i++) if (s.c[i] >= 0xD800 && s.c[i] <= 0xDFFF) { ps->unsupported = 1; return; }
+    s = uriutil_encode(ps, s);
+    int fq = js_index_of_char(s, '?', 0), fa = js_index_of_char(s, '&', 0);
+    if (fq != -1 || fa != -1) {
+        s = js_replace_all(ps->a, g_q_question, s, "&");
+        s = js_replace_first(ps->a, g_q_amp, s, "?&");
+    }
+    s = js_replace_all(ps->a, g_bad_escape, s, "%25$1");
+    s = js_replace_all(ps->a, g_bad_escape, s, "%25$1");
+    s = js_replace_all(ps->a, g_almost_html, s, "$1&$2");
+    s = unescape_html4(ps, s);
+    if (ps->unsupported) return;
+    s = js_replace_all(ps->a, g_eq_hash, s, "=");
+    s = js_replace_all(ps->a, g_hash_amp, s, "&");
+    for (;;) {
+        int caps[4];
+        if (!jre_find(g_double_hash, s.c, s.n, 0, caps)) break;
+        s = js_replace_all(ps->a, g_double_hash, s, "~$1#");
+    }
+    if (s.n == 0) { ps->unsupported = 1; return; } /* charAt(0) on "" -> StringIndexOutOfBounds */
+    int is_url = 1;
+    urip u;
+    memset(&u, 0, sizeof u);
+    if (s.c[0] == '/') {
+        u.s = js_cat(ps->a, js_lit(ps->a, "dummy-protocol://dummy.host.name"), s);
+        is_url = 0;
+    } else u.s = s;
+    for (int i = 0; i < u.s.n; i++) if (u.s.c[i] >= 0xD800 && u.s.c[i] <= 0xDFFF) { ps->unsupported = 1; return; }
+    u_parse(&u);
+    if (u.fail == 2) { ps->unsupported = 1; return; }
+    if (u.fail) { ps->failed = 1; return; }
+    if (has_req(in, "query") || has_req(in, "path") || has_req(in, "ref")) {
+        if (has_req(in, "query")) add_str(ps, inputname, "HTTP.QUERYSTRING", "query", u.query.null ? js_lit(ps->a, "") : u.query);
+        if (has_req(in, "path")) {
+            js d = uri_decode(ps, u.path);
+            if (ps->unsupported) return;
+            add_str(ps, inputname, "HTTP.PATH", "path", d);
+        }
+        if (has_req(in, "ref")) {
+            js d = uri_decode(ps, u.fragment);
+            if (ps->unsupported) return;
+            add_str(ps, inputname, "HTTP.REF", "ref", d);
+        }
+    }
+    if (is_url) {
+        if (has_req(in, "protocol")) add_str(ps, inputname, "HTTP.PROTOCOL", "protocol", u.scheme);
+        if (has_req(in, "userinfo")) {
+            js d = uri_decode(ps, u.userinfo);
+            if (ps->unsupported) return;
+            add_str(ps, inputname, "HTTP.USERINFO", "userinfo", d);
+        }
+        if (has_req(in, "host")) add_str(ps, inputname, "HTTP.HOST", "host", u.host);
+        if (has_req(in, "port") && u.port != -1) add_long(ps, inputname, "HTTP.PORT", "port", u.port);
+    }
+}
+
+/* ----------------------------------------------------------- query */
+/* URLDecoder.decode(s, "UTF-16") (JDK 8).  Returns 0, or 1 on
+ * IllegalArgumentException, 2 unsupported. */
+static int url_decode_utf16(parsable *ps, js s, js *out) {
+    int *o = (int *)ar_alloc(ps->a, sizeof(int) * (size_t)(s.n + 1));
+    int k = 0, changed = 0;
+    for (int i = 0; i < s.n;) {
+        int c = s.c[i];
+        if (c == '+') { o[k++] = ' '; i++; changed = 1; continue; }
+        if (c != '%') { o[k++] = c; i++; continue; }
+        unsigned char bytes[8192];
+        int nb = 0;
+        while (i + 2 < s.n && c == '%') {
+            int a = s.c[i + 1], b = s.c[i + 2];
+            /* Integer.parseInt(x, 16): optional sign then hex digits */
+            int sign = 1, v;
+            if (a == '+' || a == '-') {
+                if (!is_hexc(b)) return 1;
+                if (a == '-') sign = -1;
+                v = b <= '9' ? b - '0' : (b | 32) - 'a' + 10;
+            } else {
+                if (a >= 128 || b >= 128) return 2; /* Character.digit on non-ASCII: not restated */
+                if (!is_hexc(a) || !is_hexc(b)) return 1;
+                v = (a <= '9' ? a - '0' : (a | 32) - 'a' + 10) * 16 + (b <= '9' ? b - '0' : (b | 32) - 'a' + 10);
+            }
+            v *= sign;
+            if (v < 0) return 1;
+            if (nb < 8192) bytes[nb++] = (unsigned char)v;
+            i += 3;
+            if (i < s.n) c = s.c[i];
+        }
+        if (i < s.n && c == '%') return 1; /* Incomplete trailing escape */
+        /* new String(bytes, "UTF-16"): BOM sniffing, BE default */
+        int q = 0, le = 0;
+        if (nb >= 2 && bytes[0] == 0xFE && bytes[1] == 0xFF) q = 2;
+        else if (nb >= 2 && bytes[0] == 0xFF && bytes[1] == 0xFE) { q = 2; le = 1; }
+        while (q + 1 < nb) {
+            int unit = le ? (bytes[q] | (bytes[q + 1] << 8)) : ((bytes[q] << 8) | bytes[q + 1]);
+            q += 2;
+            if (unit >= 0xD800 && unit <= 0xDBFF) {
+                if (q + 1 < nb) {
+                    int u2 = le ? (bytes[q] | (bytes[q + 1] << 8)) : ((bytes[q] << 8) | bytes[q + 1]);
+                    if (u2 >= 0xDC00 && u2 <= 0xDFFF) {
+                        o[k++] = 0x10000 + ((unit - 0xD800) << 10) + (u2 - 0xDC00);
+                        q += 2;
+                        continue;
+                    }
+                }
+                return 2; /* malformed surrogate: replacement rules not restated */
+            }
+            if (unit >= 0xDC00 && unit <= 0xDFFF) return 2;
+            o[k++] = unit;
+        }
+        if (q < nb) return 2; /* odd trailing byte */
+        changed = 1;
+    }
+    (void)changed;
+    js r = {o, k, 0};
+    *out = r;
+    return 0;
+}
+
+/* Utils.resilientUrlDecode (Utils.java:38-65) */
+static int resilient_url_decode(parsable *ps, js in, js *out) {
+    js cooked = in;
+    if (js_index_of_char(cooked, '%', 0) > -1) {
+        cooked = js_replace_all(ps->a, g_valid_std, cooked, "%00%$1");
+        cooked = js_replace_all(ps->a, g_chopped_std, cooked, "");
+        js pu = js_lit(ps->a, "%u");
+        if (js_index_of(cooked, pu, 0) >= 0) {
+            cooked = js_replace_all(ps->a, g_valid_nonstd, cooked, "%$1%$2");
+            cooked = js_replace_all(ps->a, g_chopped_nonstd, cooked, "");
+        }
+    }
+    return url_decode_utf16(ps, cooked, out);
+}
+
+/* QueryStringFieldDissector.dissect (:76-108) */
+static void d_query(parsable *ps, instance *in, const char *inputname) {
+    val *vp = cache_get(ps, "HTTP.QUERYSTRING", inputname);
+    js s = v_getstring(ps->a, *vp);
+    if (s.null || s.n == 0) return;
+    int want_all = has_req(in, "*");
+    js *parts;
+    int np = js_split_char(ps->a, s, '&', &parts);
+    for (int i = 0; i < np; i++) {
+        js v = parts[i];
+        int eq = js_index_of_char(v, '=', 0);
+        if (eq == -1) {
+            if (v.n != 0) {
+                js name = js_lower(ps->a, v);
+                char *nm = js_cstr(ps, name);
+                if (want_all || has_req(in, nm)) add_str(ps, inputname, "STRING", nm, js_lit(ps->a, ""));
+            }
+        } else {
+            js name = js_lower(ps->a, js_sub(v, 0, eq));
+            char *nm = js_cstr(ps, name);
+            if (want_all || has_req(in, nm)) {
+                js dec;
+                int r = resilient_url_decode(ps, js_sub(v, eq + 1, v.n), &dec);
+                if (r == 1) { ps->failed = 1; return; }
+                if (r == 2) { ps->unsupported = 1; return; }
+                add_str(ps, inputname, "STRING", nm, dec);
+            }
+        }
+    }
+}
+
+/* ------------------------------------------------------ converters */
+/* ConvertCLFIntoNumber.dissect (translate/ConvertCLFIntoNumber.java:33-40) */
+static void d_clf2num(parsable *ps, instance *in, const char *inputname) {
+    val *vp = cache_get(ps, in->d->in_type, inputname);
+    js sv = v_getstring(ps->a, *vp);
+    if (sv.null || js_eq_lit(sv, "-")) add_long(ps, inputname, in->d->out_type, "", 0);
+    else add_dissection(ps, inputname, in->d->out_type, "", *vp);
+}
+/* ConvertNumberIntoCLF.dissect (translate/ConvertNumberIntoCLF.java:33-39) */
+static void d_num2clf(parsable *ps, instance *in, const char *inputname) {
+    val *vp = cache_get(ps, in->d->in_type, inputname);
+    js sv = v_getstring(ps->a, *vp);
+    if (js_eq_lit(sv, "0")) add_str(ps, inputname, in->d->out_type, "", js_null());
+    else add_dissection(ps, inputname, in->d->out_type, "", *vp);
+}
+
+static void run_instance(parsable *ps, instance *in, const char *name) {
+    switch (in->d->cls) {
+    case D_ROOT: d_root(ps, in, name); break;
+    case D_TIMESTAMP: d_timestamp(ps, in, name); break;
+    case D_FIRSTLINE: d_firstline(ps, in, name); break;
+    case D_PROTOCOL: d_protocol(ps, in, name); break;
+    case D_URI: d_uri(ps, in, name); break;
+    case D_QUERY: d_query(ps, in, name); break;
+    case D_CLF2NUM: d_clf2num(ps, in, name); break;
+    case D_NUM2CLF: d_num2clf(ps, in, name); break;
+    default: ps->unsupported = 1; break;
+    }
+}
+
+/* =================================================================== API */
+static orc_parser *build(const char *logformat, const char *const *fields, int nfields, char *err, int errlen, int for_paths) {
+    pthread_once(&g_re_once, init_res);
+    orc_parser *p = (orc_parser *)xmalloc(sizeof(orc_parser));
+    p->logformat_arg = xstrdup(logformat);
+    for (int i = 0; i < nfields; i++) sl_add(&p->field_args, fields[i]);
+    if (build_dissectors(p, logformat, err, errlen)) { return NULL; }
+    if (for_paths) return p;
+    for (int i = 0; i < nfields; i++) {
+        char *c = cleanup_field(fields[i]);
+        sl_add_unique(&p->needed, c);
+        free(c);
+    }
+    /* Parser.assembleDissectors (core/Parser.java:300-356) */
+    for (int i = 0; i < p->ndis; i++)
+        if (p->dis[i]->outs.n == 0) {
+            snprintf(err, errlen, "InvalidDissectorException: Dissector cannot create any outputs (%s)", p->dis[i]->in_type);
+            return NULL;
+        }
+    slist needed = {0};
+    for (int i = 0; i < p->needed.n; i++) sl_add(&needed, p->needed.v[i]);
+    char *rootneed = xfmt("%s:", p->root_type);
+    sl_add(&needed, rootneed);
+    free(rootneed);
+    slist possible = {0};
+    for (int i = 0; i < needed.n; i++) {
+        const char *nm = strchr(needed.v[i], ':') + 1;
+        char sb[1024];
+        sb[0] = 0;
+        size_t sbl = 0;
+        const char *s = nm;
+        for (;;) {
+            const char *dot = strchr(s, '.');
+            size_t pl = dot ? (size_t)(dot - s) : strlen(s);
+            if (sbl == 0 || pl == 0) { memcpy(sb + sbl, s, pl); sbl += pl; }
+            else { sb[sbl++] = '.'; memcpy(sb + sbl, s, pl); sbl += pl; }
+            sb[sbl] = 0;
+            sl_add_unique(&possible, sb);
+            if (!dot) break;
+            s = dot + 1;
+        }
+    }
+    find_useful(p, &possible, p->root_type, "", 1);
+    sl_free(&needed);
+    sl_free(&possible);
+    /* prepareForRun on every phase */
+    for (int i = 0; i < p->ncompiled; i++)
+        for (int k = 0; k < p->compiled[i].n; k++) {
+            instance *in = p->compiled[i].ph[k];
+            if (in->d->cls == D_ROOT) {
+                if (in->nfmts == 0) { snprintf(err, errlen, "InvalidDissectorException: Cannot run without logformats"); return NULL; }
+                for (int f = 0; f < in->nfmts; f++) {
+                    fmt_prepare_for_run(in->fmts[f]);
+                    if (in->fmts[f]->unsupported && !p->unsupported) {
+                        p->unsupported = 1;
+                        snprintf(p->unsupported_why, sizeof p->unsupported_why, "logformat not restated: %s", in->fmts[f]->logformat);
+                    }
+                }
+            }
+        }
+    if (p->ncompiled == 0) { snprintf(err, errlen, "MissingDissectorsException: There are no dissectors at all"); return NULL; }
+    /* getTheMissingFields (core/Parser.java:472-490) */
+    for (int i = 0; i < p->needed.n; i++) {
+        const char *t = p->needed.v[i];
+        if (sl_has(&p->located, t)) continue;
+        size_t L = strlen(t);
+        if (L && t[L - 1] == '*') {
+            if (L >= 2 && t[L - 2] == '.') {
+                char *pre = xfmt("%.*s", (int)(L - 2), t);
+                int ok = sl_has(&p->located, pre);
+                free(pre);
+                if (!ok) { snprintf(err, errlen, "MissingDissectorsException: %s", t); return NULL; }
+            }
+        } else { snprintf(err, errlen, "MissingDissectorsException: %s", t); return NULL; }
+    }
+    if (p->unsupported) { snprintf(err, errlen, "unsupported: %s", p->unsupported_why); return NULL; }
+    return p;
+}
+
+orc_parser *orc_new(const char *logformat, const char *const *fields, int nfields, char *err, int errlen) {
+    if (err && errlen) err[0] = 0;
+    return build(logformat, fields, nfields, err, errlen, 0);
+}
+
+void orc_free(orc_parser *p) {
+    /* the oracle is short-lived test code; formats/dissectors are leaked */
+    if (!p) return;
+    ar_free(&p->ar);
+    free(p);
+}
+
+int orc_format_regex(orc_parser *p, int i, char *out, int out_cap) {
+    centry *ce = c_get(p, "HTTPLOGLINE:");
+    if (!ce || ce->n == 0) return -1;
+    instance *in = ce->ph[0];
+    if (i < 0 || i >= in->nfmts || !in->fmts[i]->regex) return -1;
+    int L = (int)strlen(in->fmts[i]->regex);
+    if (L + 1 > out_cap) return -1;
+    memcpy(out, in->fmts[i]->regex, (size_t)L + 1);
+    return L;
+}
+
+/* JSON output helpers */
+typedef struct { char *b; int n, cap; int overflow; } ob;
+static void ob_put(ob *o, const char *s, int n) {
+    if (o->n + n + 1 > o->cap) { o->overflow = 1; return; }
+    memcpy(o->b + o->n, s, (size_t)n);
+    o->n += n;
+    o->b[o->n] = 0;
+}
+static void ob_s(ob *o, const char *s) { ob_put(o, s, (int)strlen(s)); }
+static void ob_json_str(ob *o, const char *s, int n) {
+    ob_put(o, "\"", 1);
+    for (int i = 0; i < n; i++) {
+        unsigned char c = (unsigned char)s[i];
+        char e[8];
+        if (c == '"') ob_put(o, "\\\"", 2);
+        else if (c == '\\') ob_put(o, "\\\\", 2);
+        else if (c < 0x20) { snprintf(e, sizeof e, "\\u%04x", c); ob_put(o, e, 6); }
+        else ob_put(o, (const char *)&c, 1);
+    }
+    ob_put(o, "\"", 1);
+}
+
+static int rcmp(const void *a, const void *b) {
+    const rentry *x = (const rentry *)a, *y = (const rentry *)b;
+    int c = strcmp(x->name, y->name);
+    if (c) return c;
+    return x->seq - y->seq;
+}
+
+int orc_parse(orc_parser *p, const char *line, int len, char *out, int out_cap) {
+    parsable ps;
+    memset(&ps, 0, sizeof ps);
+    ps.p = p;
+    ar_reset(&p->ar);
+    ps.a = &p->ar;
+    js l = js_from_utf8(ps.a, line, len);
+    /* reject invalid UTF-8 input (callers decode bytes with replacement;
+     * that decoding is outside the restated path) */
+    {
+        const unsigned char *u = (const unsigned char *)line;
+        for (int i = 0; i < len;) {
+            unsigned c = u[i];
+            int need = c < 0x80 ? 0 : (c >= 0xC2 && c <= 0xDF) ? 1 : (c >= 0xE0 && c <= 0xEF) ? 2 : (c >= 0xF0 && c <= 0xF4) ? 3 : -1;
+            if (need < 0) return ORC_UNSUPPORTED;
+            for (int k = 1; k <= need; k++) if (i + k >= len || (u[i + k] & 0xC0) != 0x80) return ORC_UNSUPPORTED;
+            i += need + 1;
+        }
+    }
+    cache_put(&ps, p->root_type, "", vstr(l));
+    todo_add(&ps, p->root_type, "");
+    /* Parser.parse(Parsable) worklist (core/Parser.java:726-756) */
+    int guard = 0;
+    while (ps.ntodo > 0 && !ps.failed && !ps.unsupported) {
+        int n = ps.ntodo;
+        pfield *batch = (pfield *)malloc(sizeof(pfield) * (size_t)n);
+        memcpy(batch, ps.todo, sizeof(pfield) * (size_t)n);
+        ps.ntodo = 0;
+        for (int i = 0; i < n && !ps.failed && !ps.unsupported; i++) {
+            char id[1024];
+            snprintf(id, sizeof id, "%s:%s", batch[i].type, batch[i].name);
+            centry *ce = c_get(p, id);
+            if (!ce) continue;
+            for (int k = 0; k < ce->n && !ps.failed && !ps.unsupported; k++) run_instance(&ps, ce->ph[k], batch[i].name);
+        }
+        free(batch);
+        if (++guard > 64) { ps.unsupported = 1; break; }
+    }
+    int status = ps.unsupported ? ORC_UNSUPPORTED : ps.failed ? ORC_BAD : ORC_OK;
+    if (status == ORC_OK && out) {
+        qsort(ps.rec, (size_t)ps.nrec, sizeof(rentry), rcmp);
+        ob o = {out, 0, out_cap, 0};
+        out[0] = 0;
+        ob_s(&o, "{");
+        for (int i = 0; i < ps.nrec;) {
+            if (i) ob_s(&o, ",");
+            ob_json_str(&o, ps.rec[i].name, (int)strlen(ps.rec[i].name));
+            ob_s(&o, ":[");
+            int j = i;
+            for (; j < ps.nrec && strcmp(ps.rec[j].name, ps.rec[i].name) == 0; j++) {
+                if (j > i) ob_s(&o, ",");
+                val v = ps.rec[j].v;
+                if (v.filled == V_LONG) {
+                    char b[48];
+                    if (v.lnull) snprintf(b, sizeof b, "{\"l\":null}");
+                    else snprintf(b, sizeof b, "{\"l\":%lld}", (long long)v.l);
+                    ob_s(&o, b);
+                } else if (v.s.null) ob_s(&o, "null");
+                else {
+                    int bl;
+                    char *u8 = js_to_utf8(ps.a, v.s, &bl);
+                    ob_json_str(&o, u8, bl);
+                }
+            }
+            ob_s(&o, "]");
+            i = j;
+        }
+        ob_s(&o, "}");
+        if (o.overflow) status = -1;
+    }
+    free(ps.cache);
+    free(ps.todo);
+    free(ps.rec);
+    return status;
+}
+
+/* Parser.getPossiblePaths (core/Parser.java:914-1012) */
+static void find_paths(orc_parser *p, slist *paths, const char *base, const char *btype, int depth) {
+    if (depth == 0) return;
+    for (int di = 0; di < p->ndis; di++) {
+        dissector *d = p->dis[di];
+        if (strcmp(d->in_type, btype) != 0) continue;
+        for (int oi = 0; oi < d->outs.n; oi++) {
+            const char *o = d->outs.v[oi];
+            const char *colon = strchr(o, ':');
+            char *ctype = xfmt("%.*s", (int)(colon - o), o);
+            const char *cname = colon + 1;
+            char *cbase;
+            if (base[0] == 0) cbase = xstrdup(cname);
+            else if (cname[0] == 0) cbase = xstrdup(base);
+            else cbase = xfmt("%s.%s", base, cname);
+            char *np = xfmt("%s:%s", ctype, cbase);
+            if (!sl_has(paths, np)) {
+                sl_add(paths, np);
+                find_paths(p, paths, cbase, ctype, depth - 1);
+            }
+            free(np);
+            free(cbase);
+            free(ctype);
+        }
+    }
+}
+
+static int scmp(const void *a, const void *b) { return strcmp(*(char *const *)a, *(char *const *)b); }
+
+int orc_possible_paths(const char *logformat, int max_depth, char *out, int out_cap) {
+    char err[256];
+    pthread_once(&g_re_once, init_res);
+    orc_parser *p = build(logformat, NULL, 0, err, sizeof err, 1);
+    if (!p) return -1;
+    slist paths = {0};
+    find_paths(p, &paths, "", p->root_type, max_depth);
+    qsort(paths.v, (size_t)paths.n, sizeof(char *), scmp);
+    int n = 0;
+    for (int i = 0; i < paths.n; i++) {
+        int L = (int)strlen(paths.v[i]);
+        if (n + L + 2 > out_cap) { sl_free(&paths); return -1; }
+        memcpy(out + n, paths.v[i], (size_t)L);
+        n += L;
+        out[n++] = '\n';
+    }
+    out[n] = 0;
+    sl_free(&paths);
+    return n;
+}
+
+int orc_resilient_url_decode(const char *in, int len, char *out, int out_cap) {
+    pthread_once(&g_re_once, init_res);
+    arena a = {0};
+    parsable ps;
+    memset(&ps, 0, sizeof ps);
+    ps.a = &a;
+    js s = js_from_utf8(&a, in, len);
+    js r;
+    int st = resilient_url_decode(&ps, s, &r);
+    int n = -1;
+    if (st == 0) {
+        int bl;
+        char *u8 = js_to_utf8(&a, r, &bl);
+        if (bl + 1 <= out_cap) { memcpy(out, u8, (size_t)bl + 1); n = bl; }
+    } else n = st == 1 ? -2 : -3;
+    ar_free(&a);
+    return n;
+}
+
+/* ------------------------------------------------------------- bench */
+typedef struct {
+    const char *logformat;
+    const char *const *fields;
+    int nfields;
+    const char *buf;
+    size_t from, to;
+    int64_t lines, ok, bad, unsup;
+} bench_job;
+
+static void *bench_thread(void *arg) {
+    bench_job *j = (bench_job *)arg;
+    char err[256];
+    orc_parser *p = orc_new(j->logformat, j->fields, j->nfields, err, sizeof err);
+    if (!p) return NULL;
+    static __thread char out[1 << 16];
+    size_t i = j->from;
+    while (i < j->to) {
+        const char *nl = (const char *)memchr(j->buf + i, '\n', j->to - i);
+        size_t e = nl ? (size_t)(nl - j->buf) : j->to;
+        int st = orc_parse(p, j->buf + i, (int)(e - i), out, sizeof out);
+        j->lines++;
+        if (st == ORC_OK) j->ok++; else if (st == ORC_BAD) j->bad++; else j->unsup++;
+        i = e + 1;
+    }
+    orc_free(p);
+    return NULL;
+}
+
+double orc_bench(const char *logformat, const char *const *fields, int nfields,
+                 const char *buf, size_t nbytes, int nthreads, int64_t *out4) {
+    if (nthreads < 1) nthreads = 1;
+    bench_job *jobs = (bench_job *)xmalloc(sizeof(bench_job) * (size_t)nthreads);
+    pthread_t *th = (pthread_t *)xmalloc(sizeof(pthread_t) * (size_t)nthreads);
+    /* newline-aligned contiguous ranges, one parser per thread */
+    size_t start = 0;
+    for (int t = 0; t < nthreads; t++) {
+        size_t end = t == nthreads - 1 ? nbytes : (nbytes * (size_t)(t + 1)) / (size_t)nthreads;
+        if (end < start) end = start;
+        while (end < nbytes && end > 0 && buf[end - 1] != '\n') end++;
+        jobs[t].logformat = logformat;
+        jobs[t].fields = fields;
+        jobs[t].nfields = nfields;
+        jobs[t].buf = buf;
+        jobs[t].from = start;
+        jobs[t].to = end;
+        start = end;
+    }
+    struct timespec a, b;
+    clock_gettime(CLOCK_MONOTONIC, &a);
+    for (int t = 0; t < nthreads; t++) pthread_create(&th[t], NULL, bench_thread, &jobs[t]);
+    for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    clock_gettime(CLOCK_MONOTONIC, &b);
+    int64_t tot[4] = {0, 0, 0, 0};
+    for (int t = 0; t < nthreads; t++) { tot[0] += jobs[t].lines; tot[1] += jobs[t].ok; tot[2] += jobs[t].bad; tot[3] += jobs[t].unsup; }
+    if (out4) memcpy(out4, tot, sizeof tot);
+    free(jobs);
+    free(th);
+    return (double)(b.tv_sec - a.tv_sec) + 1e-9 * (double)(b.tv_nsec - a.tv_nsec);
+}

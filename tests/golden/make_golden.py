@@ -1,0 +1,367 @@
+"""Writes tests/golden/reference_vectors.json.
+
+Every case below is TRANSCRIBED DATA (input line, logformat, requested fields,
+expected values) from the reference's own JUnit tests; each carries the
+reference file:line it comes from (paths relative to /root/reference,
+hpt/ = httpdlog/httpdlog-parser/src/test/java/nl/basjes/parse/httpdlog/).
+No reference source is copied: only the literal inputs/expectations.
+
+Expectation encoding (mirrors TestRecord's absent / null / value split,
+parser-core/src/test/java/nl/basjes/parse/core/test/TestRecord.java:47-114):
+  "expect":  {path: value}  value = "str" | null | {"l": n}; the value must be
+             among the values delivered for that path
+  "absent":  [path, ...]    the path must not be delivered at all
+  "bad":     true           the line must raise DissectionFailure
+Fields the reference test asserts through dissectors this build does not
+cover (cookies, GeoIP, type remappings, screen resolution) are left out and
+listed in "skipped".
+"""
+import json
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+CASES = []
+
+
+def case(source, logformat, line, fields, expect=None, absent=(), bad=False, skipped=(), note=""):
+    CASES.append({
+        "source": source,
+        "logformat": logformat,
+        "line": line,
+        "fields": list(fields),
+        "expect": expect or {},
+        "absent": list(absent),
+        "bad": bad,
+        "skipped": list(skipped),
+        "note": note,
+    })
+
+
+# --------------------------------------------------------------- Apache whole line
+FULLCOMBINED = ("%%%h %a %A %l %u %t \"%r\" %>s %b %p \"%q\" \"%!200,304,302{Referer}i\" %D "
+                "\"%200{User-agent}i\" \"%{Cookie}i\" \"%{Set-Cookie}o\" \"%{If-None-Match}i\" \"%{Etag}o\"")
+APACHE_TEST_FIELDS = [
+    "STRING:request.firstline.uri.query.*", "STRING:request.querystring.aap", "IP:connection.client.ip",
+    "NUMBER:connection.client.logname", "STRING:connection.client.user", "TIME.STAMP:request.receive.time",
+    "TIME.SECOND:request.receive.time.second", "HTTP.URI:request.firstline.uri", "STRING:request.status.last",
+    "BYTESCLF:response.body.bytes", "HTTP.URI:request.referer", "STRING:request.referer.query.mies",
+    "STRING:request.referer.query.wim", "HTTP.USERAGENT:request.user-agent", "TIME.DAY:request.receive.time.day",
+    "TIME.HOUR:request.receive.time.hour", "TIME.MONTHNAME:request.receive.time.monthname",
+    "TIME.EPOCH:request.receive.time.epoch", "TIME.WEEK:request.receive.time.weekofweekyear",
+    "TIME.YEAR:request.receive.time.weekyear", "TIME.YEAR:request.receive.time.year",
+    "HTTP.COOKIES:request.cookies", "HTTP.SETCOOKIES:response.cookies",
+    "MICROSECONDS:response.server.processing.time", "HTTP.HEADER:response.header.etag",
+]
+APACHE_SKIPPED = ["HTTP.COOKIE:request.cookies.jquery-ui-theme", "HTTP.SETCOOKIE:response.cookies.apache",
+                  "STRING:response.cookies.apache.domain", "SCREENWIDTH:request.firstline.uri.query.res.width",
+                  "SCREENHEIGHT:request.firstline.uri.query.res.height"]
+
+case("hpt/ApacheHttpdLogParserTest.java:104-163", FULLCOMBINED,
+     "%127.0.0.1 127.0.0.1 127.0.0.1 - - [31/Dec/2012:23:49:40 +0100] "
+     "\"GET /icons/powered_by_rh.png?aap=noot&res=1024x768 HTTP/1.1\" 200 1213 "
+     "80 \"\" \"http://localhost/index.php?mies=wim\" 351 "
+     "\"Mozilla/5.0 (X11; Linux i686 on x86_64; rv:11.0) Gecko/20100101 Firefox/11.0\" "
+     "\"jquery-ui-theme=Eggplant\" \"Apache=127.0.0.1.1344635380111339; path=/; domain=.basjes.nl\" \"-\" "
+     "\"\\\"3780ff-4bd-4c1ce3df91380\\\"\"",
+     APACHE_TEST_FIELDS,
+     expect={
+         "STRING:request.firstline.uri.query.aap": "noot",
+         "IP:connection.client.ip": "127.0.0.1",
+         "NUMBER:connection.client.logname": None,
+         "STRING:connection.client.user": None,
+         "TIME.STAMP:request.receive.time": "31/Dec/2012:23:49:40 +0100",
+         "TIME.EPOCH:request.receive.time.epoch": {"l": 1356994180000},
+         "TIME.WEEK:request.receive.time.weekofweekyear": {"l": 1},
+         "TIME.YEAR:request.receive.time.weekyear": {"l": 2013},
+         "TIME.YEAR:request.receive.time.year": {"l": 2012},
+         "TIME.SECOND:request.receive.time.second": {"l": 40},
+         "HTTP.URI:request.firstline.uri": "/icons/powered_by_rh.png?aap=noot&res=1024x768",
+         "STRING:request.status.last": "200",
+         "BYTESCLF:response.body.bytes": "1213",
+         "HTTP.URI:request.referer": "http://localhost/index.php?mies=wim",
+         "STRING:request.referer.query.mies": "wim",
+         "HTTP.USERAGENT:request.user-agent": "Mozilla/5.0 (X11; Linux i686 on x86_64; rv:11.0) Gecko/20100101 Firefox/11.0",
+         "TIME.DAY:request.receive.time.day": {"l": 31},
+         "TIME.HOUR:request.receive.time.hour": {"l": 23},
+         "TIME.MONTHNAME:request.receive.time.monthname": "December",
+         "MICROSECONDS:response.server.processing.time": "351",
+         "HTTP.SETCOOKIES:response.cookies": "Apache=127.0.0.1.1344635380111339; path=/; domain=.basjes.nl",
+         "HTTP.COOKIES:request.cookies": "jquery-ui-theme=Eggplant",
+         "HTTP.HEADER:response.header.etag": "\\\"3780ff-4bd-4c1ce3df91380\\\"",
+     },
+     absent=["STRING:request.firstline.uri.query.foo", "STRING:request.querystring.aap"],
+     skipped=APACHE_SKIPPED)
+
+case("hpt/ApacheHttpdLogParserTest.java:168-200", FULLCOMBINED,
+     "%127.0.0.1 127.0.0.1 127.0.0.1 - - [10/Aug/2012:23:55:11 +0200] \"GET /icons/powered_by_rh.png HTTP/1.1\" 200 1213 80"
+     " \"\" \"http://localhost/\" 1306 \"Mozilla/5.0 (X11; Linux i686 on x86_64; rv:11.0) Gecko/20100101 Firefox/11.0\""
+     " \"jquery-ui-theme=Eggplant; Apache=127.0.0.1.1344635667182858\" \"-\" \"-\" \"\\\"3780ff-4bd-4c1ce3df91380\\\"\"",
+     APACHE_TEST_FIELDS,
+     expect={
+         "IP:connection.client.ip": "127.0.0.1",
+         "NUMBER:connection.client.logname": None,
+         "STRING:connection.client.user": None,
+         "TIME.STAMP:request.receive.time": "10/Aug/2012:23:55:11 +0200",
+         "TIME.SECOND:request.receive.time.second": {"l": 11},
+         "HTTP.URI:request.firstline.uri": "/icons/powered_by_rh.png",
+         "STRING:request.status.last": "200",
+         "BYTESCLF:response.body.bytes": "1213",
+         "HTTP.URI:request.referer": "http://localhost/",
+         "HTTP.USERAGENT:request.user-agent": "Mozilla/5.0 (X11; Linux i686 on x86_64; rv:11.0) Gecko/20100101 Firefox/11.0",
+         "TIME.DAY:request.receive.time.day": {"l": 10},
+         "TIME.HOUR:request.receive.time.hour": {"l": 23},
+         "TIME.MONTHNAME:request.receive.time.monthname": "August",
+         "MICROSECONDS:response.server.processing.time": "1306",
+         "HTTP.SETCOOKIES:response.cookies": None,
+         "HTTP.COOKIES:request.cookies": "jquery-ui-theme=Eggplant; Apache=127.0.0.1.1344635667182858",
+         "HTTP.HEADER:response.header.etag": "\\\"3780ff-4bd-4c1ce3df91380\\\"",
+     },
+     absent=["HTTP.QUERYSTRING:request.firstline.uri.query.foo"])
+
+case("hpt/ApacheHttpdLogParserTest.java:205-239", FULLCOMBINED,
+     "%127.0.0.1 127.0.0.1 127.0.0.1 - - [10/Aug/2012:23:55:11 +0200] \"GET /ImagineAURLHereThatIsTooLong\" 414 1213 80"
+     " \"\" \"http://localhost/\" 1306 \"Mozilla/5.0 (X11; Linux i686 on x86_64; rv:11.0) Gecko/20100101 Firefox/11.0\""
+     " \"jquery-ui-theme=Eggplant; Apache=127.0.0.1.1344635667182858\" \"-\" \"-\" \"\\\"3780ff-4bd-4c1ce3df91380\\\"\"",
+     APACHE_TEST_FIELDS,
+     expect={
+         "IP:connection.client.ip": "127.0.0.1",
+         "TIME.STAMP:request.receive.time": "10/Aug/2012:23:55:11 +0200",
+         "TIME.SECOND:request.receive.time.second": {"l": 11},
+         "HTTP.URI:request.firstline.uri": "/ImagineAURLHereThatIsTooLong",
+         "STRING:request.status.last": "414",
+         "BYTESCLF:response.body.bytes": "1213",
+         "HTTP.URI:request.referer": "http://localhost/",
+         "TIME.MONTHNAME:request.receive.time.monthname": "August",
+         "MICROSECONDS:response.server.processing.time": "1306",
+         "HTTP.SETCOOKIES:response.cookies": None,
+         "HTTP.HEADER:response.header.etag": "\\\"3780ff-4bd-4c1ce3df91380\\\"",
+     })
+
+QS_FIELDS = ["STRING:request.firstline.uri.query.foo", "STRING:request.firstline.uri.query.bar",
+             "HTTP.PATH:request.firstline.uri.path", "HTTP.QUERYSTRING:request.firstline.uri.query",
+             "HTTP.REF:request.firstline.uri.ref"]
+for line, foo, bar, query, ref, ln in [
+    ("GET /index.html HTTP/1.1", "ABSENT", "ABSENT", "", "NULL", "349-354"),
+    ("GET /index.html?foo HTTP/1.1", "", "ABSENT", "&foo", "NULL", "357-362"),
+    ("GET /index.html&foo HTTP/1.1", "", "ABSENT", "&foo", "NULL", "365-370"),
+    ("GET /index.html?foo=foofoo# HTTP/1.1", "foofoo", "ABSENT", "&foo=foofoo", "", "373-378"),
+    ("GET /index.html&foo=foofoo HTTP/1.1", "foofoo", "ABSENT", "&foo=foofoo", "NULL", "381-386"),
+    ("GET /index.html?bar&foo=foofoo# HTTP/1.1", "foofoo", "", "&bar&foo=foofoo", "", "389-394"),
+    ("GET /index.html?bar&foo=foofoo#bookmark HTTP/1.1", "foofoo", "", "&bar&foo=foofoo", "bookmark", "397-402"),
+    ("GET /index.html?bar=barbar&foo=foofoo#bookmark HTTP/1.1", "foofoo", "barbar", "&bar=barbar&foo=foofoo", "bookmark", "405-410"),
+    ("GET /index.html&bar=barbar&foo=foofoo#bla HTTP/1.1", "foofoo", "barbar", "&bar=barbar&foo=foofoo", "bla", "413-418"),
+    ("GET /index.html&bar=barbar?foo=foofoo HTTP/1.1", "foofoo", "barbar", "&bar=barbar&foo=foofoo", "NULL", "421-426"),
+]:
+    exp = {"HTTP.PATH:request.firstline.uri.path": "/index.html", "HTTP.QUERYSTRING:request.firstline.uri.query": query}
+    absent = []
+    for k, v in (("STRING:request.firstline.uri.query.foo", foo), ("STRING:request.firstline.uri.query.bar", bar),
+                 ("HTTP.REF:request.firstline.uri.ref", ref)):
+        if v == "ABSENT":
+            absent.append(k)
+        elif v == "NULL":
+            exp[k] = None
+        else:
+            exp[k] = v
+    case("hpt/ApacheHttpdLogParserTest.java:" + ln, "%r", line, QS_FIELDS, expect=exp, absent=absent,
+         note="Map-based test record: a null assert may mean absent or null; both accepted as reference encodes")
+
+case("hpt/EdgeCasesTest.java:26-57",
+     "%a %{Host}i %u %t \"%r\" %>s %O \"%{Referer}i\" \"%{User-Agent}i\" %{Content-length}i %P %A",
+     "1.2.3.4 - - [03/Apr/2017:03:27:28 -0600] \"\\x16\\x03\\x01\" 404 419 \"-\" \"-\" - 115052 5.6.7.8",
+     ["IP:connection.client.ip", "IP:connection.server.ip", "TIME.EPOCH:request.receive.time.last.epoch",
+      "STRING:connection.client.user", "TIME.STAMP:request.receive.time.last", "TIME.DATE:request.receive.time.last.date",
+      "TIME.TIME:request.receive.time.last.time", "NUMBER:connection.server.child.processid", "BYTES:response.bytes",
+      "STRING:request.status.last", "HTTP.USERAGENT:request.user-agent", "HTTP.HEADER:request.header.host",
+      "HTTP.HEADER:request.header.content-length", "HTTP.URI:request.referer", "HTTP.FIRSTLINE:request.firstline",
+      "HTTP.METHOD:request.firstline.method", "HTTP.URI:request.firstline.uri", "HTTP.PROTOCOL:request.firstline.protocol"],
+     expect={
+         "IP:connection.client.ip": "1.2.3.4",
+         "IP:connection.server.ip": "5.6.7.8",
+         "TIME.EPOCH:request.receive.time.last.epoch": {"l": 1491211648000},
+         "STRING:connection.client.user": None,
+         "TIME.STAMP:request.receive.time.last": "03/Apr/2017:03:27:28 -0600",
+         "TIME.DATE:request.receive.time.last.date": "2017-04-03",
+         "TIME.TIME:request.receive.time.last.time": "03:27:28",
+         "NUMBER:connection.server.child.processid": "115052",
+         "BYTES:response.bytes": "419",
+         "STRING:request.status.last": "404",
+         "HTTP.USERAGENT:request.user-agent": None,
+         "HTTP.HEADER:request.header.host": None,
+         "HTTP.HEADER:request.header.content-length": None,
+         "HTTP.URI:request.referer": None,
+         "HTTP.FIRSTLINE:request.firstline": "\\x16\\x03\\x01",
+     },
+     absent=["HTTP.METHOD:request.firstline.method", "HTTP.URI:request.firstline.uri",
+             "HTTP.PROTOCOL:request.firstline.protocol"])
+
+# Multi-format sticky switching (hpt/MultiLineHttpdLogParserTest.java:64-124)
+ML_FMT = "%h %t \"%r\" %>s %b \"%{Referer}i\"\n\n%h %t \"%r\" %>s \"%{User-Agent}i\"\n\n"
+ML_FIELDS = ["IP:connection.client.host", "TIME.STAMP:request.receive.time", "TIME.SECOND:request.receive.time.second",
+             "STRING:request.status.last", "BYTESCLF:response.body.bytes", "HTTP.URI:request.firstline.uri",
+             "HTTP.URI:request.referer", "HTTP.USERAGENT:request.user-agent"]
+ML_L1 = ("127.0.0.1 [31/Dec/2012:23:49:41 +0100] \"GET /foo HTTP/1.1\" 200 1213 \"http://localhost/index.php?mies=wim\"")
+ML_L2 = ("127.0.0.2 [31/Dec/2012:23:49:42 +0100] \"GET /foo HTTP/1.1\" 404 "
+         "\"Mozilla/5.0 (X11; Linux i686 on x86_64; rv:11.0) Gecko/20100101 Firefox/11.0\"")
+ML_E1 = {"IP:connection.client.host": "127.0.0.1", "TIME.STAMP:request.receive.time": "31/Dec/2012:23:49:41 +0100",
+         "HTTP.URI:request.firstline.uri": "/foo", "STRING:request.status.last": "200",
+         "BYTESCLF:response.body.bytes": "1213", "HTTP.URI:request.referer": "http://localhost/index.php?mies=wim"}
+ML_E2 = {"IP:connection.client.host": "127.0.0.2", "TIME.STAMP:request.receive.time": "31/Dec/2012:23:49:42 +0100",
+         "HTTP.URI:request.firstline.uri": "/foo", "STRING:request.status.last": "404",
+         "HTTP.USERAGENT:request.user-agent": "Mozilla/5.0 (X11; Linux i686 on x86_64; rv:11.0) Gecko/20100101 Firefox/11.0"}
+for i, which in enumerate([1, 1, 2, 2, 1, 1, 2, 2, 1, 1, 2, 2]):
+    case("hpt/MultiLineHttpdLogParserTest.java:64-124 (sequence step %d)" % i, ML_FMT, ML_L1 if which == 1 else ML_L2,
+         ML_FIELDS, expect=ML_E1 if which == 1 else ML_E2,
+         absent=["HTTP.USERAGENT:request.user-agent"] if which == 1 else ["BYTESCLF:response.body.bytes", "HTTP.URI:request.referer"],
+         note="sequence: one parser for all 12 steps (sticky active format)")
+
+# ------------------------------------------------------- component-level (via one-token formats)
+# HttpUriDissector tests (hpt/dissectors/TestHttpUriDissector.java) through "%{referer}i": the line is the URI.
+URI_PFX = "request.referer."
+URI_F = ["HTTP.PROTOCOL:protocol", "HTTP.USERINFO:userinfo", "HTTP.HOST:host", "HTTP.PORT:port", "HTTP.PATH:path",
+         "HTTP.QUERYSTRING:query", "HTTP.REF:ref"]
+
+
+def uri_case(ln, uri, exp, absent=(), extra_fields=()):
+    def pfx(f):
+        t, n = f.split(":", 1)
+        return t + ":" + URI_PFX + n
+    fields = [pfx(f) for f in URI_F] + [pfx(f) for f in extra_fields]
+    case("hpt/dissectors/TestHttpUriDissector.java:" + ln, "%{referer}i", uri, fields,
+         expect={pfx(k): v for k, v in exp.items()}, absent=[pfx(a) for a in absent])
+
+
+uri_case("25-40", "http://www.example.com/some/thing/else/index.html?foofoo=bar%20bar",
+         {"HTTP.PROTOCOL:protocol": "http", "HTTP.USERINFO:userinfo": None, "HTTP.HOST:host": "www.example.com",
+          "HTTP.PATH:path": "/some/thing/else/index.html", "HTTP.QUERYSTRING:query": "&foofoo=bar%20bar",
+          "HTTP.REF:ref": None}, absent=["HTTP.PORT:port"])
+uri_case("42-57", "http://www.example.com/some/thing/else/index.html&aap=noot?foofoo=barbar&",
+         {"HTTP.PROTOCOL:protocol": "http", "HTTP.USERINFO:userinfo": None, "HTTP.HOST:host": "www.example.com",
+          "HTTP.PATH:path": "/some/thing/else/index.html", "HTTP.QUERYSTRING:query": "&aap=noot&foofoo=barbar&",
+          "HTTP.REF:ref": None}, absent=["HTTP.PORT:port"])
+uri_case("59-74", "http://www.example.com:8080/some/thing/else/index.html&aap=noot?foofoo=barbar&#blabla",
+         {"HTTP.PROTOCOL:protocol": "http", "HTTP.USERINFO:userinfo": None, "HTTP.HOST:host": "www.example.com",
+          "HTTP.PORT:port": {"l": 8080}, "HTTP.PATH:path": "/some/thing/else/index.html",
+          "HTTP.QUERYSTRING:query": "&aap=noot&foofoo=barbar&", "HTTP.REF:ref": "blabla"})
+uri_case("76-91", "/some/thing/else/index.html?foofoo=barbar#blabla",
+         {"HTTP.PATH:path": "/some/thing/else/index.html", "HTTP.QUERYSTRING:query": "&foofoo=barbar", "HTTP.REF:ref": "blabla"},
+         absent=["HTTP.PROTOCOL:protocol", "HTTP.USERINFO:userinfo", "HTTP.HOST:host", "HTTP.PORT:port"])
+uri_case("93-108", "/some/thing/else/index.html&aap=noot?foofoo=bar%20bar&#bla%20bla",
+         {"HTTP.PATH:path": "/some/thing/else/index.html", "HTTP.QUERYSTRING:query": "&aap=noot&foofoo=bar%20bar&",
+          "HTTP.REF:ref": "bla bla"},
+         absent=["HTTP.PROTOCOL:protocol", "HTTP.USERINFO:userinfo", "HTTP.HOST:host", "HTTP.PORT:port"])
+uri_case("110-125", "android-app://com.google.android.googlequicksearchbox",
+         {"HTTP.PROTOCOL:protocol": "android-app", "HTTP.USERINFO:userinfo": None,
+          "HTTP.HOST:host": "com.google.android.googlequicksearchbox", "HTTP.PATH:path": "",
+          "HTTP.QUERYSTRING:query": "", "HTTP.REF:ref": None}, absent=["HTTP.PORT:port"])
+uri_case("127-142", "android-app://com.google.android.googlequicksearchbox/https/www.google.com",
+         {"HTTP.PROTOCOL:protocol": "android-app", "HTTP.USERINFO:userinfo": None,
+          "HTTP.HOST:host": "com.google.android.googlequicksearchbox", "HTTP.PATH:path": "/https/www.google.com",
+          "HTTP.QUERYSTRING:query": "", "HTTP.REF:ref": None}, absent=["HTTP.PORT:port"])
+uri_case("144-160", "/some/thing/else/[index.html&aap=noot?foofoo=bar%20bar #bla%20bla ",
+         {"HTTP.PATH:path": "/some/thing/else/[index.html", "HTTP.QUERYSTRING:query": "&aap=noot&foofoo=bar%20bar%20",
+          "HTTP.REF:ref": "bla bla "},
+         absent=["HTTP.PROTOCOL:protocol", "HTTP.USERINFO:userinfo", "HTTP.HOST:host", "HTTP.PORT:port"])
+uri_case("162-179", "/index.html&promo=Give-50%-discount&promo=And-do-%Another-Wrong&last=also bad %#bla%20bla ",
+         {"HTTP.PATH:path": "/index.html",
+          "HTTP.QUERYSTRING:query": "&promo=Give-50%25-discount&promo=And-do-%25Another-Wrong&last=also%20bad%20%25",
+          "HTTP.REF:ref": "bla bla "},
+         absent=["HTTP.PROTOCOL:protocol", "HTTP.USERINFO:userinfo", "HTTP.HOST:host", "HTTP.PORT:port"])
+uri_case("181-198", "/index.html?Linkid=%%%3dv(%40Foo)%3d%%%&emcid=B%ar",
+         {"HTTP.PATH:path": "/index.html", "HTTP.QUERYSTRING:query": "&Linkid=%25%25%3dv(%40Foo)%3d%25%25%25&emcid=B%25ar",
+          "STRING:query.linkid": "%%=v(@Foo)=%%%", "HTTP.REF:ref": None},
+         absent=["HTTP.PROTOCOL:protocol", "HTTP.USERINFO:userinfo", "HTTP.HOST:host", "HTTP.PORT:port"],
+         extra_fields=["STRING:query.linkid"])
+for u in ["https://www.basjes.nl/#foo#bar#bazz#bla#bla#",
+          "https://www.basjes.nl/path/?s2a=&Referrer=ADV1234#product_title&f=API&subid=?s2a=#product_title&name=12341234",
+          "https://www.basjes.nl/path/?Referrer=ADV1234#&f=API&subid=#&name=12341234",
+          "https://www.basjes.nl/path?sort&#x3D;price&filter&#x3D;new&sortOrder&#x3D;asc",
+          "https://www.basjes.nl/login.html?redirectUrl=https%3A%2F%2Fwww.basjes.nl%2Faccount%2Findex.html"
+          "&_requestid=1234#x3D;12341234&Referrer&#x3D;ENTblablabla"]:
+    uri_case("200-213", u, {"HTTP.HOST:host": "www.basjes.nl"})
+
+# QueryStringFieldDissector (hpt/dissectors/TestQueryStringDissector.java:26-42)
+case("hpt/dissectors/TestQueryStringDissector.java:26-42", "%{referer}i",
+     "/some/thing/else/index.html&aap=1&noot=&mies&",
+     ["HTTP.PATH:request.referer.path", "HTTP.QUERYSTRING:request.referer.query",
+      "STRING:request.referer.query.aap", "STRING:request.referer.query.noot", "STRING:request.referer.query.mies",
+      "STRING:request.referer.query.wim"],
+     expect={"HTTP.PATH:request.referer.path": "/some/thing/else/index.html",
+             "HTTP.QUERYSTRING:request.referer.query": "&aap=1&noot=&mies&",
+             "STRING:request.referer.query.aap": "1", "STRING:request.referer.query.noot": "",
+             "STRING:request.referer.query.mies": ""},
+     absent=["STRING:request.referer.query.wim"])
+
+# HttpFirstLineDissector (hpt/dissectors/TestHttpFirstLineDissector.java) through "%r"
+FL_F = ["HTTP.METHOD:request.firstline.method", "HTTP.URI:request.firstline.uri",
+        "HTTP.PROTOCOL:request.firstline.protocol", "HTTP.PROTOCOL.VERSION:request.firstline.protocol.version"]
+case("hpt/dissectors/TestHttpFirstLineDissector.java:25-36", "%r", "GET /index.html HTTP/1.1", FL_F,
+     expect={"HTTP.METHOD:request.firstline.method": "GET", "HTTP.URI:request.firstline.uri": "/index.html",
+             "HTTP.PROTOCOL:request.firstline.protocol": "HTTP", "HTTP.PROTOCOL.VERSION:request.firstline.protocol.version": "1.1"})
+case("hpt/dissectors/TestHttpFirstLineDissector.java:38-48", "%r", "GET /index.html HTT", FL_F,
+     expect={"HTTP.METHOD:request.firstline.method": "GET", "HTTP.URI:request.firstline.uri": "/index.html HTT"},
+     absent=["HTTP.PROTOCOL:request.firstline.protocol", "HTTP.PROTOCOL.VERSION:request.firstline.protocol.version"])
+case("hpt/dissectors/TestHttpFirstLineDissector.java:50-58", "%r", "\\x16\\x03\\x01", FL_F,
+     absent=["HTTP.METHOD:request.firstline.method", "HTTP.URI:request.firstline.uri"])
+case("hpt/dissectors/TestHttpFirstLineDissector.java:60-71", "%r", "VERSION-CONTROL /index.html HTTP/1.1", FL_F,
+     expect={"HTTP.METHOD:request.firstline.method": "VERSION-CONTROL", "HTTP.URI:request.firstline.uri": "/index.html",
+             "HTTP.PROTOCOL:request.firstline.protocol": "HTTP", "HTTP.PROTOCOL.VERSION:request.firstline.protocol.version": "1.1"})
+
+# TimeStampDissector (hpt/dissectors/TestTimeStampDissector.java) through "%t" (line = "[ts]")
+TS = "request.receive.time."
+TS_F = ["TIME.EPOCH:epoch", "TIME.YEAR:year", "TIME.MONTH:month", "TIME.MONTHNAME:monthname", "TIME.DAY:day",
+        "TIME.HOUR:hour", "TIME.MINUTE:minute", "TIME.SECOND:second", "TIME.DATE:date", "TIME.TIME:time",
+        "TIME.YEAR:year_utc", "TIME.MONTH:month_utc", "TIME.MONTHNAME:monthname_utc", "TIME.DAY:day_utc",
+        "TIME.HOUR:hour_utc", "TIME.MINUTE:minute_utc", "TIME.SECOND:second_utc", "TIME.DATE:date_utc",
+        "TIME.TIME:time_utc"]
+
+
+def tsf(f):
+    t, n = f.split(":", 1)
+    return t + ":" + TS + n
+
+
+case("hpt/dissectors/TestTimeStampDissector.java:46-86", "%t", "[31/Dec/2012:23:00:44 -0700]", [tsf(f) for f in TS_F],
+     expect={tsf(k): v for k, v in {
+         "TIME.EPOCH:epoch": {"l": 1357020044000}, "TIME.YEAR:year": {"l": 2012}, "TIME.MONTH:month": {"l": 12},
+         "TIME.MONTHNAME:monthname": "December", "TIME.DAY:day": {"l": 31}, "TIME.HOUR:hour": {"l": 23},
+         "TIME.MINUTE:minute": {"l": 0}, "TIME.SECOND:second": {"l": 44}, "TIME.DATE:date": "2012-12-31",
+         "TIME.TIME:time": "23:00:44", "TIME.YEAR:year_utc": {"l": 2013}, "TIME.MONTH:month_utc": {"l": 1},
+         "TIME.MONTHNAME:monthname_utc": "January", "TIME.DAY:day_utc": {"l": 1}, "TIME.HOUR:hour_utc": {"l": 6},
+         "TIME.MINUTE:minute_utc": {"l": 0}, "TIME.SECOND:second_utc": {"l": 44}, "TIME.DATE:date_utc": "2013-01-01",
+         "TIME.TIME:time_utc": "06:00:44"}.items()})
+for m in ["sep", "Sep", "sEp", "SEp", "seP", "SeP", "sEP", "SEP"]:
+    case("hpt/dissectors/TestTimeStampDissector.java:150-169", "%t", "[30/%s/2016:00:00:06 +0000]" % m,
+         [tsf("TIME.YEAR:year_utc"), tsf("TIME.MONTH:month_utc"), tsf("TIME.DAY:day_utc")],
+         expect={tsf("TIME.YEAR:year_utc"): {"l": 2016}, tsf("TIME.MONTH:month_utc"): {"l": 9},
+                 tsf("TIME.DAY:day_utc"): {"l": 30}})
+
+# examples/apache-flink/.../TestCase.java:37-43,86-94 (IPv6 %h, long query string); GeoIP / remapped fields skipped.
+FLINK_LINE = open(os.path.join(HERE, "flink_testcase_line.txt"), encoding="utf-8").read().rstrip("\n") \
+    if os.path.exists(os.path.join(HERE, "flink_testcase_line.txt")) else None
+if FLINK_LINE:
+    case("examples/apache-flink/src/test/java/nl/basjes/parse/httpdlog/flink/TestCase.java:37-43,86-94",
+         "%h %l %u %t \"%r\" %>s %b \"%{Referer}i\" \"%{User-Agent}i\" \"%{Cookie}i\"", FLINK_LINE,
+         ["IP:connection.client.host", "TIME.STAMP:request.receive.time", "TIME.EPOCH:request.receive.time.epoch",
+          "HTTP.USERAGENT:request.user-agent", "STRING:request.firstline.uri.query.g", "STRING:request.firstline.uri.query.s"],
+         expect={"IP:connection.client.host": "2001:980:91c0:1:8d31:a232:25e5:85d",
+                 "TIME.STAMP:request.receive.time": "05/Sep/2010:11:27:50 +0200",
+                 "TIME.EPOCH:request.receive.time.epoch": {"l": 1283678870000},
+                 "STRING:request.firstline.uri.query.s": "1280x800",
+                 "HTTP.USERAGENT:request.user-agent": "Mozilla/5.0 (Macintosh; U; Intel Mac OS X 10_6_4; nl-nl) "
+                                                      "AppleWebKit/533.17.8 (KHTML, like Gecko) Version/5.0.1 Safari/533.17.8"},
+         skipped=["STRING:request.firstline.uri.query.g.query.promo (type remapping)", "GeoIP fields", "HTTP.COOKIE:request.cookies.bui"])
+
+# resilientUrlDecode (hpt/UtilsTest.java:27-49): unit vectors, not whole lines
+URLDECODE = [
+    ["  ", "  "], [" %20", "  "], ["%20 ", "  "], ["%20%20", "  "], ["%u0020%u0020", "  "], ["%20%u0020", "  "],
+    ["%u0020%20", "  "], ["x %2", "x "], ["x%20%2", "x "], ["x%u202", "x"], ["x%u20", "x"], ["x%u2", "x"],
+    ["x%u", "x"], ["x%", "x"], ["%20 %20%u0020%20 %20%2", "       "],
+]
+
+if __name__ == "__main__":
+    out = {"generated_by": "tests/golden/make_golden.py", "cases": CASES,
+           "url_decode": {"source": "hpt/UtilsTest.java:27-49", "vectors": URLDECODE}}
+    with open(os.path.join(HERE, "reference_vectors.json"), "w", encoding="utf-8") as f:
+        json.dump(out, f, indent=1, ensure_ascii=False)
+    print("wrote", len(CASES), "cases")

@@ -1,0 +1,119 @@
+"""ctypes binding of the CPU oracle (oracle/_build/liboracle.so).
+
+TEST INFRASTRUCTURE ONLY: the oracle is the checker, never the product.
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use it.
+"""
+import ctypes
+import json
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+
+OK, BAD, UNSUPPORTED = 0, 1, 2
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        L = ctypes.CDLL(LIB)
+        L.orc_new.restype = ctypes.c_void_p
+        L.orc_new.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int,
+                              ctypes.c_char_p, ctypes.c_int]
+        L.orc_free.argtypes = [ctypes.c_void_p]
+        L.orc_parse.restype = ctypes.c_int
+        L.orc_parse.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        L.orc_possible_paths.restype = ctypes.c_int
+        L.orc_possible_paths.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        L.orc_format_regex.restype = ctypes.c_int
+        L.orc_format_regex.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        L.orc_bench.restype = ctypes.c_double
+        L.orc_bench.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int,
+                                ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
+        L.orc_resilient_url_decode.restype = ctypes.c_int
+        L.orc_resilient_url_decode.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        _lib = L
+    return _lib
+
+
+def _fields(fields):
+    arr = (ctypes.c_char_p * max(1, len(fields)))()
+    for i, f in enumerate(fields):
+        arr[i] = f.encode()
+    return arr
+
+
+class OracleError(Exception):
+    pass
+
+
+class Oracle:
+    """One oracle parser (the reference's Parser is stateful: sticky format)."""
+
+    def __init__(self, logformat, fields):
+        L = lib()
+        err = ctypes.create_string_buffer(512)
+        self._fields = _fields(fields)
+        self.h = L.orc_new(logformat.encode(), self._fields, len(fields), err, 512)
+        if not self.h:
+            raise OracleError(err.value.decode())
+        self.buf = ctypes.create_string_buffer(1 << 20)
+
+    def parse_raw(self, line):
+        if isinstance(line, str):
+            line = line.encode("utf-8")
+        st = lib().orc_parse(self.h, line, len(line), self.buf, len(self.buf))
+        if st < 0:
+            raise OracleError("output buffer too small")
+        return st, (self.buf.value.decode("utf-8") if st == OK else None)
+
+    def parse(self, line):
+        st, js = self.parse_raw(line)
+        return st, (json.loads(js) if js is not None else None)
+
+    def regex(self, i=0):
+        out = ctypes.create_string_buffer(1 << 16)
+        n = lib().orc_format_regex(self.h, i, out, len(out))
+        return out.value.decode() if n >= 0 else None
+
+    def __del__(self):
+        try:
+            if self.h:
+                lib().orc_free(self.h)
+        except Exception:
+            pass
+
+
+def possible_paths(logformat, max_depth=15):
+    out = ctypes.create_string_buffer(1 << 20)
+    n = lib().orc_possible_paths(logformat.encode(), max_depth, out, len(out))
+    if n < 0:
+        raise OracleError("possible paths failed")
+    return [p for p in out.value.decode().split("\n") if p]
+
+
+def resilient_url_decode(s):
+    b = s.encode("utf-8")
+    out = ctypes.create_string_buffer(len(b) * 4 + 16)
+    n = lib().orc_resilient_url_decode(b, len(b), out, len(out))
+    if n == -2:
+        raise ValueError("IllegalArgumentException")
+    if n < 0:
+        raise OracleError("unsupported")
+    return out.raw[:n].decode("utf-8")
+
+
+def bench(logformat, fields, data, threads):
+    out = (ctypes.c_int64 * 4)()
+    f = _fields(fields)
+    secs = lib().orc_bench(logformat.encode(), f, len(fields), data, len(data), threads, out)
+    return secs, list(out)
