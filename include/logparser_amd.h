@@ -1,0 +1,127 @@
+/*
+ * logparser_amd -- MI355X (gfx950) batch engine for logparser's per-line hot
+ * path: match Apache HTTPD access-log lines against a LogFormat and extract
+ * typed fields (tokens, epoch-millisecond timestamps, request first line,
+ * URI parts, percent-decoded query parameters).
+ *
+ * Drop-in boundary.  Every entry point below replaces a piece of the
+ * reference's per-line Java path (paths relative to the reference repo,
+ * hp/ = httpdlog/httpdlog-parser/src/main/java/nl/basjes/parse/httpdlog/,
+ * core/ = parser-core/src/main/java/nl/basjes/parse/core/):
+ *
+ *   lp_compile        new HttpdLoglineParser<>(cls, logformat) + addParseTarget(...)
+ *                     + the lazy Parser.assembleDissectors on first parse
+ *                     (hp/HttpdLoglineParser.java:44-50,104-126;
+ *                      core/Parser.java:237-356, 581-635;
+ *                      hp/dissectors/tokenformat/TokenFormatDissector.java:127-213)
+ *   lp_possible_paths Parser.getPossiblePaths() (core/Parser.java:904-1012)
+ *   lp_parse_batch    a loop of Parser.parse(record, line) over a batch of
+ *                     '\n'-separated lines (core/Parser.java:716-756), i.e.
+ *                     HttpdLogFormatDissector.dissect + TokenFormatDissector.dissect
+ *                     (hp/HttpdLogFormatDissector.java:173-204,
+ *                      hp/dissectors/tokenformat/TokenFormatDissector.java:243-275)
+ *                     and the downstream TimeStamp / HttpFirstLine / HttpUri /
+ *                     QueryStringField / CLF converter dissectors -- run on the GPU.
+ *   lp_line_status    the per-line outcome the caller's loop sees
+ *                     (ApacheHttpdLogfileRecordReader.java:256-269): OK, BAD
+ *                     (= DissectionFailure), FALLBACK (= not proven on device:
+ *                     hand the line to the reference Java dissector).
+ *   lp_line_record_json  the values the reference would have delivered to the
+ *                     record's setters for that line (Parser.store,
+ *                     core/Parser.java:760-876), as a canonical JSON object.
+ *   lp_counters       the RecordReader counters "Lines read / Good lines /
+ *                     Bad lines" (ApacheHttpdLogfileRecordReader.java:118-120)
+ *                     plus the FALLBACK count.
+ *
+ * Threading: like the reference Parser (not thread-safe), one handle per
+ * host thread / GPU.  Ownership: the caller owns the input buffer; the
+ * handle owns device scratch and results until the next lp_parse_batch or
+ * lp_free.  No torch types cross this boundary.
+ */
+#ifndef LOGPARSER_AMD_H
+#define LOGPARSER_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* return codes */
+#define LP_OK 0
+#define LP_E_INVALID (-1)      /* bad arguments / logformat (InvalidDissectorException) */
+#define LP_E_MISSING (-2)      /* MissingDissectorsException */
+#define LP_E_UNSUPPORTED (-3)  /* compiled, but some requested path needs a dissector
+                                  not implemented on the device: every line -> FALLBACK */
+#define LP_E_DEVICE (-4)       /* HIP error / no device / extension not usable */
+#define LP_E_NOMEM (-5)
+#define LP_E_STATE (-6)        /* called in the wrong order */
+
+/* per-line status */
+#define LP_LINE_OK 0
+#define LP_LINE_BAD 1          /* the reference throws DissectionFailure */
+#define LP_LINE_FALLBACK 2     /* outside the device's proven subset */
+
+/* lp_parse_batch buffer flags */
+#define LP_BUF_HOST 0          /* host memory: copied H2D on the stream */
+#define LP_BUF_DEVICE 1        /* device pointer, already resident in HBM */
+
+typedef struct lp_handle lp_handle;
+
+/* Compile a LogFormat (one or more, '\n' separated; aliases common /
+ * combined / combinedio / referer / agent) and the requested "TYPE:path"
+ * targets.  device: HIP device ordinal.  Returns NULL on failure; *status
+ * receives LP_OK / LP_E_UNSUPPORTED (handle still usable) / error code. */
+lp_handle *lp_compile(const char *logformats, const char *const *paths, int n_paths,
+                      int device, int *status, char *err, size_t errlen);
+void lp_free(lp_handle *h);
+
+/* Parser.getPossiblePaths(max_depth) for a logformat: '\n'-separated, sorted.
+ * Returns the number of bytes written (excluding NUL) or a negative error. */
+int64_t lp_possible_paths(const char *logformats, int max_depth, char *out, size_t cap);
+
+/* Parse every '\n'-terminated line of buf[0, nbytes) (a final line without
+ * '\n' counts; Hadoop LineRecordReader semantics on '\n').  stream: a
+ * hipStream_t (NULL = default stream).  Enqueues all work on the stream and
+ * returns without synchronizing; call lp_sync before reading results. */
+int lp_parse_batch(lp_handle *h, const uint8_t *buf, uint64_t nbytes, int buf_flags, void *stream);
+int lp_sync(lp_handle *h);
+
+/* Results of the last batch (after lp_sync). */
+int64_t lp_num_lines(lp_handle *h);
+/* copies statuses of lines [first, first+count) to host memory */
+int lp_line_status(lp_handle *h, int64_t first, int64_t count, uint8_t *out);
+/* byte offset of line i in the batch (i <= num_lines) */
+int64_t lp_line_offset(lp_handle *h, int64_t i);
+/* canonical record of line i (status must be OK):
+ *   {"TYPE:path": [v, ...], ...}  keys sorted; v = "str" | null | {"l": n}
+ * returns bytes written (excluding NUL) or negative (LP_E_STATE if the line
+ * is not OK, -100 - needed if cap is too small). */
+int64_t lp_line_record_json(lp_handle *h, int64_t i, char *out, size_t cap);
+/* out[0..3] = lines, ok, bad, fallback of the last batch (device counters) */
+int lp_counters(lp_handle *h, uint64_t *out, int n);
+
+/* Device-side timing of the last batch, in milliseconds, measured with HIP
+ * events on the batch's stream: [0] whole batch, [1] line index kernels,
+ * [2] parse kernel.  Returns the number of values written. */
+int lp_last_timing(lp_handle *h, float *out_ms, int n);
+
+/* Algorithmic bytes of the last batch: [0] input bytes read, [1] bytes of
+ * SoA results + arena written (for roofline accounting). */
+int lp_last_bytes(lp_handle *h, uint64_t *out, int n);
+
+/* Description of the compiled device program (for logs/tests), NUL-terminated. */
+int64_t lp_describe(lp_handle *h, char *out, size_t cap);
+
+/* Synthetic 'combined' access-log generator (deterministic per seed), used
+ * by bench.py and tests to build BASELINE.json config-2 inputs.  Writes
+ * complete lines into out (cap bytes) starting at line index first_line;
+ * returns bytes written and sets *n_lines. */
+int64_t lp_synth_combined(uint64_t seed, int64_t first_line, int64_t max_lines,
+                          char *out, size_t cap, int64_t *n_lines);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,275 @@
+"""logparser_amd -- MI355X-native batch engine for logparser's per-line hot path.
+
+Host-side mirror of the reference's parser surface for this path
+(nl.basjes.parse.httpdlog.HttpdLoglineParser / nl.basjes.parse.core.Parser,
+reference: httpdlog/httpdlog-parser/src/main/java/nl/basjes/parse/httpdlog/
+HttpdLoglineParser.java:44-126 and parser-core/src/main/java/nl/basjes/parse/core/
+Parser.java:496-756, 904-1012) over the C ABI in include/logparser_amd.h.
+
+    parser = HttpdLoglineParser("combined", ["TIME.EPOCH:request.receive.time.epoch", ...])
+    batch  = parser.parse_batch(raw_bytes_or_cuda_uint8_tensor)   # all lines on the GPU
+    batch.status            # per line: OK / BAD (DissectionFailure) / FALLBACK
+    batch.record(i)         # {"TYPE:path": [values]} as the reference setters receive them
+    parser.parse(line)      # Parser.parse(line) for one line (raises DissectionFailure)
+
+The engine runs only on the GPU: there is no CPU implementation behind this
+module, and every call fails loudly when the HIP library or a device is
+missing.  FALLBACK lines are the lines the device could not prove it handles
+exactly; a deployment hands them to the reference Java dissector.
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "_lib", "liblogparser_amd.so")
+
+LP_OK, LP_E_INVALID, LP_E_MISSING, LP_E_UNSUPPORTED, LP_E_DEVICE, LP_E_NOMEM, LP_E_STATE = 0, -1, -2, -3, -4, -5, -6
+LINE_OK, LINE_BAD, LINE_FALLBACK = 0, 1, 2
+BUF_HOST, BUF_DEVICE = 0, 1
+
+
+class DissectionFailure(Exception):
+    """nl.basjes.parse.core.exceptions.DissectionFailure"""
+
+
+class FallbackRequired(Exception):
+    """The device could not prove the line; hand it to the reference parser."""
+
+
+class MissingDissectorsException(Exception):
+    """nl.basjes.parse.core.exceptions.MissingDissectorsException"""
+
+
+class InvalidDissectorException(Exception):
+    """nl.basjes.parse.core.exceptions.InvalidDissectorException"""
+
+
+class EngineUnavailable(RuntimeError):
+    """The HIP library or a GPU is missing."""
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise EngineUnavailable("logparser_amd: %s not built (run __graft_entry__.build())" % LIB_PATH)
+    L = ctypes.CDLL(LIB_PATH)
+    c_char_pp = ctypes.POINTER(ctypes.c_char_p)
+    L.lp_compile.restype = ctypes.c_void_p
+    L.lp_compile.argtypes = [ctypes.c_char_p, c_char_pp, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int),
+                             ctypes.c_char_p, ctypes.c_size_t]
+    L.lp_free.argtypes = [ctypes.c_void_p]
+    L.lp_possible_paths.restype = ctypes.c_int64
+    L.lp_possible_paths.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]
+    L.lp_parse_batch.restype = ctypes.c_int
+    L.lp_parse_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
+    L.lp_sync.argtypes = [ctypes.c_void_p]
+    L.lp_num_lines.restype = ctypes.c_int64
+    L.lp_num_lines.argtypes = [ctypes.c_void_p]
+    L.lp_line_status.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p]
+    L.lp_line_offset.restype = ctypes.c_int64
+    L.lp_line_offset.argtypes = [ctypes.c_void_p, ctypes.c_int64]
+    L.lp_line_record_json.restype = ctypes.c_int64
+    L.lp_line_record_json.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_char_p, ctypes.c_size_t]
+    L.lp_counters.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
+    L.lp_last_timing.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
+    L.lp_last_bytes.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
+    L.lp_describe.restype = ctypes.c_int64
+    L.lp_describe.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]
+    L.lp_synth_combined.restype = ctypes.c_int64
+    L.lp_synth_combined.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t,
+                                    ctypes.POINTER(ctypes.c_int64)]
+    _lib = L
+    return L
+
+
+def get_possible_paths(logformat, max_depth=15):
+    """Parser.getPossiblePaths(maxDepth) for a HttpdLoglineParser on logformat."""
+    cap = 1 << 20
+    out = ctypes.create_string_buffer(cap)
+    n = lib().lp_possible_paths(logformat.encode(), max_depth, out, cap)
+    if n < 0:
+        raise InvalidDissectorException("possible paths overflow")
+    return [p for p in out.value.decode().split("\n") if p]
+
+
+def synth_combined(seed, first_line, n_lines):
+    """Deterministic synthetic 'combined' lines (BASELINE config 2 shape) as bytes."""
+    cap = n_lines * 700 + 1024
+    buf = ctypes.create_string_buffer(cap)
+    got = ctypes.c_int64(0)
+    nb = lib().lp_synth_combined(seed, first_line, n_lines, buf, cap, ctypes.byref(got))
+    return buf.raw[:nb]
+
+
+class BatchResult:
+    """Results of one parse_batch call (valid until the parser's next batch)."""
+
+    def __init__(self, parser):
+        self._p = parser
+        L = lib()
+        L.lp_sync(parser._h)
+        self.n_lines = L.lp_num_lines(parser._h)
+        st = np.zeros(max(1, self.n_lines), dtype=np.uint8)
+        if self.n_lines:
+            rc = L.lp_line_status(parser._h, 0, self.n_lines, st.ctypes.data)
+            if rc != LP_OK:
+                raise EngineUnavailable("lp_line_status failed: %d" % rc)
+        self.status = st[: self.n_lines]
+        c = (ctypes.c_uint64 * 4)()
+        L.lp_counters(parser._h, c, 4)
+        self.counters = {"lines": c[0], "ok": c[1], "bad": c[2], "fallback": c[3]}
+        t = (ctypes.c_float * 3)()
+        L.lp_last_timing(parser._h, t, 3)
+        self.timing_ms = {"total": t[0], "index": t[1], "parse": t[2]}
+        b = (ctypes.c_uint64 * 2)()
+        L.lp_last_bytes(parser._h, b, 2)
+        self.bytes_in, self.bytes_out = b[0], b[1]
+
+    def record(self, i):
+        """Values the reference Parser would deliver for line i (status OK)."""
+        return json.loads(self.record_json(i))
+
+    def record_json(self, i):
+        cap = 1 << 16
+        while True:
+            out = ctypes.create_string_buffer(cap)
+            n = lib().lp_line_record_json(self._p._h, i, out, cap)
+            if n >= 0:
+                return out.value.decode("utf-8")
+            if n <= -100:
+                cap = int(-n - 100) + 16
+                continue
+            if n == LP_E_STATE:
+                raise ValueError("line %d has status %d" % (i, self.status[i]))
+            raise EngineUnavailable("lp_line_record_json failed: %d" % n)
+
+    def line_offset(self, i):
+        return lib().lp_line_offset(self._p._h, i)
+
+
+class HttpdLoglineParser:
+    """GPU-backed equivalent of new HttpdLoglineParser<>(RECORD.class, logformat)
+    with addParseTarget(...) for each requested "TYPE:path"."""
+
+    def __init__(self, logformat, fields=(), device=0):
+        self.logformat = logformat
+        self.fields = list(fields)
+        self.device = device
+        self._h = None
+        self.device_program_ok = None
+        self.unsupported_reason = ""
+
+    # Parser.addParseTarget (core/Parser.java:581-635)
+    def add_parse_target(self, *fields):
+        self.fields.extend(fields)
+        self._close()
+        return self
+
+    def get_possible_paths(self, max_depth=15):
+        return get_possible_paths(self.logformat, max_depth)
+
+    def _ensure(self):
+        if self._h:
+            return
+        L = lib()
+        arr = (ctypes.c_char_p * max(1, len(self.fields)))()
+        for i, f in enumerate(self.fields):
+            arr[i] = f.encode()
+        st = ctypes.c_int(0)
+        err = ctypes.create_string_buffer(1024)
+        h = L.lp_compile(self.logformat.encode(), arr, len(self.fields), self.device, ctypes.byref(st), err, 1024)
+        msg = err.value.decode(errors="replace")
+        if not h:
+            if st.value == LP_E_MISSING:
+                raise MissingDissectorsException(msg)
+            if st.value == LP_E_DEVICE:
+                raise EngineUnavailable(msg)
+            raise InvalidDissectorException(msg)
+        self._h = h
+        self.device_program_ok = st.value == LP_OK
+        self.unsupported_reason = msg if st.value == LP_E_UNSUPPORTED else ""
+
+    def parse_batch(self, data, stream=None):
+        """Parse every '\\n'-separated line.  data: bytes / bytearray / numpy
+        uint8 (host, copied to HBM) or a torch.uint8 CUDA tensor (in HBM)."""
+        self._ensure()
+        L = lib()
+        s = ctypes.c_void_p(stream) if stream is not None else None
+        if hasattr(data, "data_ptr") and getattr(data, "is_cuda", False):
+            rc = L.lp_parse_batch(self._h, ctypes.c_void_p(data.data_ptr()), data.numel() * data.element_size(),
+                                  BUF_DEVICE, s)
+        else:
+            if isinstance(data, np.ndarray):
+                buf = np.ascontiguousarray(data, dtype=np.uint8)
+                ptr, n = buf.ctypes.data, buf.nbytes
+            else:
+                buf = bytes(data)
+                ptr, n = ctypes.cast(ctypes.c_char_p(buf), ctypes.c_void_p).value, len(buf)
+            rc = L.lp_parse_batch(self._h, ctypes.c_void_p(ptr), n, BUF_HOST, s)
+            L.lp_sync(self._h)  # the host buffer must outlive the copy
+        if rc != LP_OK:
+            raise EngineUnavailable("lp_parse_batch failed: %d" % rc)
+        return BatchResult(self)
+
+    def run(self, data_ptr, nbytes, on_device=True, stream=None):
+        """Lean batch call for benchmarks/pipelines: parse nbytes at data_ptr
+        (a device pointer when on_device), wait, and return the device
+        counters, HIP-event timings and algorithmic byte counts (no per-line
+        copies to the host)."""
+        self._ensure()
+        L = lib()
+        rc = L.lp_parse_batch(self._h, ctypes.c_void_p(data_ptr), nbytes, BUF_DEVICE if on_device else BUF_HOST,
+                              ctypes.c_void_p(stream) if stream is not None else None)
+        if rc != LP_OK:
+            raise EngineUnavailable("lp_parse_batch failed: %d" % rc)
+        L.lp_sync(self._h)
+        c = (ctypes.c_uint64 * 4)()
+        L.lp_counters(self._h, c, 4)
+        t = (ctypes.c_float * 3)()
+        L.lp_last_timing(self._h, t, 3)
+        b = (ctypes.c_uint64 * 2)()
+        L.lp_last_bytes(self._h, b, 2)
+        return {"lines": c[0], "ok": c[1], "bad": c[2], "fallback": c[3],
+                "ms_total": t[0], "ms_index": t[1], "ms_parse": t[2], "bytes_in": b[0], "bytes_out": b[1]}
+
+    def parse(self, line):
+        """Parser.parse(line) (core/Parser.java:700-709): the record's values,
+        DissectionFailure for a bad line, FallbackRequired when the device
+        cannot prove the line."""
+        if isinstance(line, str):
+            line = line.encode("utf-8")
+        if b"\n" in line:
+            raise ValueError("one line without terminator expected")
+        r = self.parse_batch(line)
+        if r.n_lines != 1:
+            raise DissectionFailure("empty input")
+        if r.status[0] == LINE_BAD:
+            raise DissectionFailure("The input line does not match the specified log format.")
+        if r.status[0] == LINE_FALLBACK:
+            raise FallbackRequired(self.unsupported_reason or "line outside the device's proven subset")
+        return r.record(0)
+
+    def describe(self):
+        self._ensure()
+        out = ctypes.create_string_buffer(1 << 16)
+        lib().lp_describe(self._h, out, 1 << 16)
+        return out.value.decode()
+
+    def _close(self):
+        if self._h:
+            lib().lp_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self._close()
+        except Exception:
+            pass

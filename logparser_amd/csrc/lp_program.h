@@ -1,0 +1,184 @@
+// Compiled device program: the LogFormat turned into a flat element list
+// (literal separators + field classes) plus the downstream dissector stages
+// the requested paths need.  Plain-old-data; lives in __constant__ memory on
+// the GPU.  Built on the host by lp_compile (plan.cpp).
+//
+// Reference: TokenFormatDissector.parseTokenLogFileDefinition / prepareForRun
+// (hp/dissectors/tokenformat/TokenFormatDissector.java:179-213, 294-379)
+// produce "^" + \Q..\E literals + (token regex) + "$"; here each token regex
+// is mapped to an element kind with an exact leftmost-first candidate
+// enumerator (lp_device.h).
+#pragma once
+#include <stdint.h>
+
+#if !defined(__HIP__)
+// host-only translation units (plan.cpp, the test-only tests/emu build)
+#ifndef __host__
+#define __host__
+#endif
+#ifndef __device__
+#define __device__
+#endif
+#endif
+
+namespace lp {
+
+constexpr int MAX_ELEMS = 48;
+constexpr int MAX_LIT = 2048;
+constexpr int MAX_TOK = 16;      // captured tokens (bit k of the null/zero masks)
+constexpr int MAX_TIME = 4;
+constexpr int MAX_FL = 4;
+constexpr int MAX_URI = 8;
+constexpr int MAX_QUERY = 8;
+constexpr int MAX_QNAMES = 32;   // explicitly requested query parameter names
+constexpr int MAX_LINE = 8191;   // longer lines -> FALLBACK (13-bit offsets)
+constexpr int MAX_STACK = 16;    // DFS choice points
+
+// Element kinds = the token regexes of the Apache table
+// (hp/dissectors/tokenformat/TokenParser.java:35-59).
+enum ElemKind : uint8_t {
+    EK_LIT = 0,
+    EK_NOSPACE,      // [^\s]*
+    EK_NUMBER,       // [0-9]+
+    EK_CLFNUMBER,    // [0-9]+|-
+    EK_HEXNUMBER,    // [0-9a-fA-F]+
+    EK_CLFHEXNUMBER, // [0-9a-fA-F]+|-
+    EK_NONZERO,      // [1-9][0-9]*
+    EK_ANY_GREEDY,   // .*
+    EK_ANY_LAZY,     // .*?
+    EK_TIME_US,      // [0-3][0-9]/(?:[a-zA-Z]{3})/[1-9][0-9]{3}:[0-9]{2}:[0-9]{2}:[0-9]{2} [\+|\-][0-9]{4}
+    EK_CLF_IP,       // IPv4|IPv6|-  (IPv4 dotted quad or '-' on device, else FALLBACK)
+    EK_IP,           // IPv4|IPv6
+};
+
+struct Elem {
+    uint8_t kind;
+    uint8_t det;       // only the first candidate can lead to an overall match
+    int8_t cap;        // captured token slot, -1 = non-capturing (?:...)
+    uint8_t last;      // last element (followed by '$')
+    uint16_t lit_off;  // EK_LIT: own literal; tokens: following literal (if nlit)
+    uint16_t lit_len;
+    uint8_t nlit;      // token followed by a literal
+    uint8_t pad[3];
+};
+
+// TimeStampDissector on a TIME.STAMP token (dd/MMM/yyyy:HH:mm:ss ZZ,
+// hp/dissectors/TimeStampDissector.java:46, 404-564).
+struct TimeStage {
+    int8_t tok;
+    uint8_t pad[3];
+};
+
+// HttpFirstLineDissector on an HTTP.FIRSTLINE token
+// (hp/dissectors/HttpFirstLineDissector.java:56-134).
+struct FlStage {
+    int8_t tok;
+    uint8_t pad[3];
+};
+
+// HttpUriDissector (hp/dissectors/HttpUriDissector.java:130-233) on either a
+// token (e.g. request.referer) or the uri of a first-line stage.
+struct UriStage {
+    int8_t src_tok;     // >= 0: token slot
+    int8_t src_fl;      // >= 0: first-line stage (its uri)
+    uint8_t want_query; // rawQuery needed (delivered or dissected further)
+    uint8_t want_path;
+    uint8_t want_ref;
+    uint8_t want_userinfo;
+    int8_t query_stage; // QueryStringFieldDissector on its query, -1 none
+    uint8_t pad;
+};
+
+// QueryStringFieldDissector (hp/dissectors/QueryStringFieldDissector.java:56-108)
+struct QueryStage {
+    int8_t uri;
+    uint8_t want_all;       // "*" requested
+    uint8_t n_names;        // explicitly requested (lower-case) names
+    uint8_t pad;
+    uint16_t name_off[MAX_QNAMES];  // into lit pool
+    uint8_t name_len[MAX_QNAMES];
+};
+
+struct Program {
+    int32_t n_elems;
+    int32_t n_tok;        // captured token slots
+    int32_t n_time, n_fl, n_uri, n_query;
+    int32_t apache;       // 1 = Apache decodeExtractedValue rules, 0 = NGINX
+    int32_t tok_decode;   // bitmask: token slots whose value goes through decodeExtractedValue
+    Elem elems[MAX_ELEMS];
+    TimeStage time[MAX_TIME];
+    FlStage fl[MAX_FL];
+    UriStage uri[MAX_URI];
+    QueryStage query[MAX_QUERY];
+    uint8_t lit[MAX_LIT];
+};
+
+// Packed calendar fields (TimeStampDissector "as parsed" / "_utc" groups)
+//   bits  0..15 year, 16..19 month, 20..24 day, 25..29 hour, 30..35 minute,
+//   36..41 second, 42..57 week-based-year, 58..63 week-of-week-based-year
+__host__ __device__ inline uint64_t pack_cal(uint32_t y, uint32_t mo, uint32_t d, uint32_t h, uint32_t mi,
+                                             uint32_t s, uint32_t wy, uint32_t wk) {
+    return (uint64_t)y | ((uint64_t)mo << 16) | ((uint64_t)d << 20) | ((uint64_t)h << 25) | ((uint64_t)mi << 30) |
+           ((uint64_t)s << 36) | ((uint64_t)wy << 42) | ((uint64_t)wk << 58);
+}
+
+// A "ref" names a byte string: bits 0..31 offset, 32..62 length, bit 63 set
+// when the bytes live in the line's arena region (else: relative to the
+// line start).
+constexpr uint64_t REF_ARENA = 1ull << 63;
+__host__ __device__ inline uint64_t mkref(uint32_t off, uint32_t len, bool arena) {
+    return (uint64_t)off | ((uint64_t)len << 32) | (arena ? REF_ARENA : 0ull);
+}
+__host__ __device__ inline uint32_t ref_off(uint64_t r) { return (uint32_t)r; }
+__host__ __device__ inline uint32_t ref_len(uint64_t r) { return (uint32_t)((r >> 32) & 0x7FFFFFFFu); }
+__host__ __device__ inline bool ref_arena(uint64_t r) { return (r & REF_ARENA) != 0; }
+
+// Token span: start | end << 16 (line-relative)
+__host__ __device__ inline uint32_t mkspan(uint32_t a, uint32_t b) { return a | (b << 16); }
+
+// First-line stage info word
+enum : uint32_t { FL_NONE = 0, FL_FULL = 1, FL_CHOPPED = 2 };
+
+// URI stage flag bits
+enum : uint32_t {
+    UF_DONE = 1u << 0,       // dissected (input non-null, non-empty)
+    UF_IS_URL = 1u << 1,     // not the dummy-protocol relative form
+    UF_HOST = 1u << 2,       // host non-null
+    UF_PORT = 1u << 3,       // port != -1
+    UF_QUERY = 1u << 4,      // rawQuery non-null (else "")
+    UF_FRAG = 1u << 5,       // fragment non-null
+    UF_PATH = 1u << 6,       // path non-null
+    UF_SCHEME = 1u << 7,     // scheme non-null
+};
+
+// Output column set of one batch (device pointers).
+struct Columns {
+    uint8_t* status;          // [n]
+    const uint64_t* line_off; // [n+1]
+    uint32_t* tok_span[MAX_TOK];
+    uint32_t* tok_flags;      // bit k: value "-" (null); bit 16+k: value == "0"
+    int64_t* t_epoch[MAX_TIME];
+    uint64_t* t_local[MAX_TIME];
+    uint64_t* t_utc[MAX_TIME];
+    uint32_t* fl_kind[MAX_FL];
+    uint32_t* fl_method[MAX_FL];  // spans
+    uint32_t* fl_uri[MAX_FL];
+    uint32_t* fl_proto[MAX_FL];
+    uint32_t* u_flags[MAX_URI];
+    uint64_t* u_scheme[MAX_URI];
+    uint64_t* u_host[MAX_URI];
+    int32_t* u_port[MAX_URI];
+    uint64_t* u_path[MAX_URI];
+    uint64_t* u_query[MAX_URI];
+    uint64_t* u_frag[MAX_URI];
+    uint64_t* u_userinfo[MAX_URI];
+    uint32_t* q_count[MAX_QUERY]; // params are (name ref, value ref) pairs in the arena
+    uint64_t* q_params[MAX_QUERY];// ref to the param table in the arena
+    uint64_t* arena_base;         // [n]
+    uint8_t* arena;
+    uint64_t arena_cap;
+    unsigned long long* arena_top;  // bump pointer
+    unsigned long long* counters;   // [4] lines ok bad fallback
+};
+
+}  // namespace lp

@@ -1,0 +1,1171 @@
+// Host setup: LogFormat compilation, dissection-tree planning and device
+// Program construction, plus the per-line replay of device results.
+//
+// Restates (reference paths; hp/ = httpdlog/httpdlog-parser/src/main/java/nl/basjes/parse/httpdlog/,
+// core/ = parser-core/src/main/java/nl/basjes/parse/core/):
+//   ApacheHttpdLogFormatDissector.setLogFormat / cleanupLogFormat / createAllTokenParsers
+//                                         hp/ApacheHttpdLogFormatDissector.java:73-167, 199-714
+//   TokenParser / NamedTokenParser / ParameterizedTokenParser .getNextToken / getTokens
+//                                         hp/dissectors/tokenformat/*.java
+//   TokenFormatDissector.parseTokenLogFileDefinition (sort, kick, fixed-string gaps)
+//                                         hp/dissectors/tokenformat/TokenFormatDissector.java:294-379
+//   HttpdLogFormatDissector.addLogFormat  hp/HttpdLogFormatDissector.java:99-140
+//   HttpdLoglineParser.setupDissectors    hp/HttpdLoglineParser.java:104-126
+//   Parser.assembleDissectors / findUsefulDissectorsFromField / getTheMissingFields / getPossiblePaths
+//                                         core/Parser.java:237-490, 904-1012
+//   Parsable.addDissection                core/Parsable.java:142-193 (replay)
+#include "plan.h"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <functional>
+
+#include "../../include/logparser_amd.h"
+
+namespace lp {
+
+namespace {
+
+// --------------------------------------------------------------- regexes
+// hp/dissectors/tokenformat/TokenParser.java:35-59
+const std::string R_DIGIT = "[0-9]";
+const std::string R_NUMBER = R_DIGIT + "+";
+const std::string R_CLF_NUMBER = R_NUMBER + "|-";
+const std::string R_HEXDIGIT = "[0-9a-fA-F]";
+const std::string R_HEXNUMBER = R_HEXDIGIT + "+";
+const std::string R_CLF_HEXNUMBER = R_HEXNUMBER + "|-";
+const std::string R_NON_ZERO = "[1-9][0-9]*";
+const std::string R_8BIT = "(?:25[0-5]|2[0-4][0-9]|[01]?[0-9][0-9]?)";
+const std::string R_IPV4 = "(?:" + R_8BIT + "\\.){3}" + R_8BIT;
+const std::string R_IPV6 = ":?(?:" + R_HEXDIGIT + "{1,4}(?::|.)?){0,8}(?::|::)?(?:" + R_HEXDIGIT + "{1,4}(?::|.)?){0,8}";
+const std::string R_IP = R_IPV4 + "|" + R_IPV6;
+const std::string R_CLF_IP = R_IP + "|-";
+const std::string R_STRING = ".*?";
+const std::string R_NO_SPACE = "[^\\s]*";
+const std::string R_TIME_US =
+    "[0-3][0-9]/(?:[a-zA-Z][a-zA-Z][a-zA-Z])/[1-9][0-9][0-9][0-9]:[0-9][0-9]:[0-9][0-9]:[0-9][0-9] [\\+|\\-][0-9][0-9][0-9][0-9]";
+const std::string R_FIRSTLINE = ".*";  // hp/dissectors/HttpFirstLineDissector.java:56-57
+
+int elem_kind_of(const std::string& r) {
+    if (r == R_NO_SPACE) return EK_NOSPACE;
+    if (r == R_NUMBER) return EK_NUMBER;
+    if (r == R_CLF_NUMBER) return EK_CLFNUMBER;
+    if (r == R_HEXNUMBER) return EK_HEXNUMBER;
+    if (r == R_CLF_HEXNUMBER) return EK_CLFHEXNUMBER;
+    if (r == R_NON_ZERO) return EK_NONZERO;
+    if (r == R_FIRSTLINE) return EK_ANY_GREEDY;
+    if (r == R_STRING) return EK_ANY_LAZY;
+    if (r == R_TIME_US) return EK_TIME_US;
+    if (r == R_CLF_IP) return EK_CLF_IP;
+    if (r == R_IP) return EK_IP;
+    return -1;
+}
+
+// ----------------------------------------------------------- token table
+enum TpKind { TP_PLAIN, TP_FIXED, TP_NAMED, TP_PARAM };
+
+struct TParser {
+    TpKind kind;
+    std::string tok;   // PLAIN/FIXED literal token; NAMED/PARAM: id of the pattern
+    std::string regex;
+    int prio = 0;
+    std::vector<TokOut> outs;
+    bool strftime = false;
+    // NAMED pattern: "%{" NAMECLASS* "}" suffix ; PARAM: "%{" prefix [^}]*%[^}]* "}t"
+    std::string suffix;     // NAMED suffix after '}' (e.g. "i", "^ti")
+    bool underscore = true; // NAMED class includes '_'
+    std::string pprefix;    // PARAM prefix inside braces ("", "begin:", "end:")
+};
+
+std::string lower(std::string s) {
+    for (auto& c : s) if (c >= 'A' && c <= 'Z') c = char(c + 32);
+    return s;
+}
+std::string upper(std::string s) {
+    for (auto& c : s) if (c >= 'a' && c <= 'z') c = char(c - 32);
+    return s;
+}
+
+struct TokenTable {
+    std::vector<TParser> v;
+    TParser& add(TpKind k, const std::string& tok, const std::string& re, int prio) {
+        v.push_back(TParser{k, tok, re, prio, {}, false, "", true, ""});
+        return v.back();
+    }
+    static void out(TParser& t, const std::string& type, const std::string& name, int casts) {
+        t.outs.push_back(TokOut{type, lower(name), casts});  // TokenOutputField lowercases (TokenOutputField.java:39-44)
+    }
+    // createFirstAndLastTokenParsers (ApacheHttpdLogFormatDissector.java:651-714)
+    void fl(const std::string& token, const std::string& name, const std::string& type, int casts,
+            const std::string& re, int prio = 0) {
+        static const char* orig[] = {"%s", "%U", "%T", "%{us}T", "%{ms}T", "%{s}T", "%D", "%r"};
+        bool o = false;
+        for (auto* x : orig) if (token == x) o = true;
+        auto& a = add(TP_PLAIN, token, re, prio);
+        out(a, type, name, casts);
+        out(a, type, name + (o ? ".original" : ".last"), casts);
+        size_t pc = token.find('%');
+        auto& b = add(TP_PLAIN, token.substr(0, pc) + "%<" + token.substr(pc + 1), re, prio);
+        out(b, type, name + ".original", casts);
+        auto& c = add(TP_PLAIN, token.substr(0, pc) + "%>" + token.substr(pc + 1), re, prio);
+        out(c, type, name + ".last", casts);
+    }
+    void extra(const std::string& token, const std::string& type, const std::string& name, int casts) {
+        for (auto& t : v)
+            if (t.tok == token) { out(t, type, name, casts); return; }
+    }
+    void named(const std::string& suffix, bool underscore, const std::string& name, const std::string& type) {
+        auto& t = add(TP_NAMED, "named:" + suffix, R_STRING, 0);
+        t.suffix = suffix;
+        t.underscore = underscore;
+        out(t, type, name, CAST_S);
+    }
+    void param(const std::string& prefix, const std::string& name, int prio) {
+        auto& t = add(TP_PARAM, "param:" + prefix, R_STRING, prio);
+        t.pprefix = prefix;
+        t.strftime = true;
+        out(t, "TIME.STRFTIME_", name, CAST_S);
+    }
+};
+
+// ApacheHttpdLogFormatDissector.createAllTokenParsers (:199-638)
+const TokenTable& apache_table() {
+    static TokenTable T = [] {
+        TokenTable t;
+        const int S = CAST_S, SL = CAST_S | CAST_L;
+        t.add(TP_FIXED, "%%", "%", 0);
+        t.fl("%a", "connection.client.ip", "IP", S, R_CLF_IP);
+        t.fl("%{c}a", "connection.client.peerip", "IP", S, R_CLF_IP);
+        t.fl("%A", "connection.server.ip", "IP", S, R_CLF_IP);
+        t.fl("%B", "response.body.bytes", "BYTES", SL, R_NUMBER);
+        t.fl("%b", "response.body.bytes", "BYTESCLF", SL, R_CLF_NUMBER);
+        t.extra("%b", "BYTES", "response.body.bytesclf", SL);
+        t.named("C", true, "request.cookies.", "HTTP.COOKIE");
+        t.named("e", true, "server.environment.", "VARIABLE");
+        t.fl("%f", "server.filename", "FILENAME", S, R_STRING);
+        t.fl("%h", "connection.client.host", "IP", S, R_NO_SPACE);
+        t.fl("%H", "request.protocol", "PROTOCOL", S, R_NO_SPACE);
+        t.named("i", true, "request.header.", "HTTP.HEADER");
+        t.named("^ti", true, "request.trailer.", "HTTP.TRAILER");
+        t.fl("%k", "connection.keepalivecount", "NUMBER", SL, R_NUMBER);
+        t.fl("%l", "connection.client.logname", "NUMBER", SL, R_CLF_NUMBER);
+        t.fl("%L", "request.errorlogid", "STRING", S, R_NO_SPACE);
+        t.fl("%m", "request.method", "HTTP.METHOD", S, R_NO_SPACE);
+        t.named("n", true, "server.module_note.", "STRING");
+        t.named("o", false, "response.header.", "HTTP.HEADER");
+        t.named("^to", true, "response.trailer.", "HTTP.TRAILER");
+        t.fl("%p", "request.server.port.canonical", "PORT", SL, R_NUMBER);
+        t.fl("%{canonical}p", "connection.server.port.canonical", "PORT", SL, R_NUMBER);
+        t.fl("%{local}p", "connection.server.port", "PORT", SL, R_NUMBER);
+        t.fl("%{remote}p", "connection.client.port", "PORT", SL, R_NUMBER);
+        t.fl("%P", "connection.server.child.processid", "NUMBER", SL, R_NUMBER);
+        t.fl("%{pid}P", "connection.server.child.processid", "NUMBER", SL, R_NUMBER);
+        t.fl("%{tid}P", "connection.server.child.threadid", "NUMBER", SL, R_NUMBER);
+        t.fl("%{hextid}P", "connection.server.child.hexthreadid", "NUMBER", SL, R_CLF_HEXNUMBER);
+        t.fl("%q", "request.querystring", "HTTP.QUERYSTRING", S, R_NO_SPACE);
+        t.fl("%r", "request.firstline", "HTTP.FIRSTLINE", S, R_FIRSTLINE);
+        t.fl("%R", "request.handler", "STRING", S, R_STRING);
+        t.fl("%s", "request.status", "STRING", S, R_NO_SPACE, 0);
+        t.fl("%t", "request.receive.time", "TIME.STAMP", S, R_TIME_US);
+        t.param("", "request.receive.time", -1);
+        t.param("begin:", "request.receive.time.begin", 0);
+        t.param("end:", "request.receive.time.end", 0);
+        t.fl("%{sec}t", "request.receive.time.sec", "TIME.SECONDS", SL, R_NUMBER);
+        t.fl("%{begin:sec}t", "request.receive.time.begin.sec", "TIME.SECONDS", SL, R_NUMBER);
+        t.fl("%{end:sec}t", "request.receive.time.end.sec", "TIME.SECONDS", SL, R_NUMBER);
+        t.fl("%{msec}t", "request.receive.time.msec", "TIME.EPOCH", SL, R_NUMBER);
+        t.extra("%{msec}t", "TIME.EPOCH", "request.receive.time.begin.msec", SL);
+        t.fl("%{begin:msec}t", "request.receive.time.begin.msec", "TIME.EPOCH", SL, R_NUMBER);
+        t.fl("%{end:msec}t", "request.receive.time.end.msec", "TIME.EPOCH", SL, R_NUMBER);
+        t.fl("%{usec}t", "request.receive.time.usec", "TIME.EPOCH.USEC", SL, R_NUMBER);
+        t.extra("%{usec}t", "TIME.EPOCH.USEC", "request.receive.time.begin.usec", SL);
+        t.fl("%{begin:usec}t", "request.receive.time.begin.usec", "TIME.EPOCH.USEC", SL, R_NUMBER);
+        t.fl("%{end:usec}t", "request.receive.time.end.usec", "TIME.EPOCH.USEC", SL, R_NUMBER);
+        t.fl("%{msec_frac}t", "request.receive.time.msec_frac", "TIME.EPOCH", SL, R_NUMBER);
+        t.extra("%{msec_frac}t", "TIME.EPOCH", "request.receive.time.begin.msec_frac", SL);
+        t.fl("%{begin:msec_frac}t", "request.receive.time.begin.msec_frac", "TIME.EPOCH", SL, R_NUMBER);
+        t.fl("%{end:msec_frac}t", "request.receive.time.end.msec_frac", "TIME.EPOCH", SL, R_NUMBER);
+        t.fl("%{usec_frac}t", "request.receive.time.usec_frac", "TIME.EPOCH.USEC_FRAC", SL, R_NUMBER);
+        t.extra("%{usec_frac}t", "TIME.EPOCH.USEC_FRAC", "request.receive.time.begin.usec_frac", SL);
+        t.fl("%{begin:usec_frac}t", "request.receive.time.begin.usec_frac", "TIME.EPOCH.USEC_FRAC", SL, R_NUMBER);
+        t.fl("%{end:usec_frac}t", "request.receive.time.end.usec_frac", "TIME.EPOCH.USEC_FRAC", SL, R_NUMBER);
+        t.fl("%T", "response.server.processing.time", "SECONDS", SL, R_NUMBER);
+        t.fl("%D", "response.server.processing.time", "MICROSECONDS", SL, R_NUMBER);
+        t.extra("%D", "MICROSECONDS", "server.process.time", SL);
+        t.fl("%{us}T", "response.server.processing.time", "MICROSECONDS", SL, R_NUMBER);
+        t.fl("%{ms}T", "response.server.processing.time", "MILLISECONDS", SL, R_NUMBER);
+        t.fl("%{s}T", "response.server.processing.time", "SECONDS", SL, R_NUMBER);
+        t.fl("%u", "connection.client.user", "STRING", S, R_NO_SPACE);
+        t.fl("%U", "request.urlpath", "URI", S, R_NO_SPACE);
+        t.fl("%v", "connection.server.name.canonical", "STRING", S, R_NO_SPACE);
+        t.fl("%V", "connection.server.name", "STRING", S, R_NO_SPACE);
+        t.fl("%X", "response.connection.status", "HTTP.CONNECTSTATUS", S, R_NO_SPACE);
+        t.fl("%I", "request.bytes", "BYTES", SL, R_CLF_NUMBER);
+        t.fl("%O", "response.bytes", "BYTES", SL, R_CLF_NUMBER);
+        t.fl("%S", "total.bytes", "BYTES", SL, R_NON_ZERO);
+        t.fl("%{cookie}i", "request.cookies", "HTTP.COOKIES", S, R_STRING, 1);
+        t.fl("%{set-cookie}o", "response.cookies", "HTTP.SETCOOKIES", S, R_STRING, 1);
+        t.fl("%{user-agent}i", "request.user-agent", "HTTP.USERAGENT", S, R_STRING, 1);
+        t.fl("%{referer}i", "request.referer", "HTTP.URI", S, R_STRING, 1);
+        return t;
+    }();
+    return T;
+}
+
+// commons-codec Hex(MD5) for ParameterizedTokenParser.tokenParameterToTypeName
+std::string md5_hex(const std::string& msg) {
+    static const uint32_t K[64] = {
+        0xd76aa478, 0xe8c7b756, 0x242070db, 0xc1bdceee, 0xf57c0faf, 0x4787c62a, 0xa8304613, 0xfd469501, 0x698098d8,
+        0x8b44f7af, 0xffff5bb1, 0x895cd7be, 0x6b901122, 0xfd987193, 0xa679438e, 0x49b40821, 0xf61e2562, 0xc040b340,
+        0x265e5a51, 0xe9b6c7aa, 0xd62f105d, 0x02441453, 0xd8a1e681, 0xe7d3fbc8, 0x21e1cde6, 0xc33707d6, 0xf4d50d87,
+        0x455a14ed, 0xa9e3e905, 0xfcefa3f8, 0x676f02d9, 0x8d2a4c8a, 0xfffa3942, 0x8771f681, 0x6d9d6122, 0xfde5380c,
+        0xa4beea44, 0x4bdecfa9, 0xf6bb4b60, 0xbebfbc70, 0x289b7ec6, 0xeaa127fa, 0xd4ef3085, 0x04881d05, 0xd9d4d039,
+        0xe6db99e5, 0x1fa27cf8, 0xc4ac5665, 0xf4292244, 0x432aff97, 0xab9423a7, 0xfc93a039, 0x655b59c3, 0x8f0ccc92,
+        0xffeff47d, 0x85845dd1, 0x6fa87e4f, 0xfe2ce6e0, 0xa3014314, 0x4e0811a1, 0xf7537e82, 0xbd3af235, 0x2ad7d2bb,
+        0xeb86d391};
+    static const int R[64] = {7, 12, 17, 22, 7, 12, 17, 22, 7, 12, 17, 22, 7, 12, 17, 22, 5, 9, 14, 20, 5, 9,
+                              14, 20, 5, 9, 14, 20, 5, 9, 14, 20, 4, 11, 16, 23, 4, 11, 16, 23, 4, 11, 16, 23,
+                              4, 11, 16, 23, 6, 10, 15, 21, 6, 10, 15, 21, 6, 10, 15, 21, 6, 10, 15, 21};
+    std::vector<uint8_t> m(msg.begin(), msg.end());
+    uint64_t bits = (uint64_t)m.size() * 8;
+    m.push_back(0x80);
+    while (m.size() % 64 != 56) m.push_back(0);
+    for (int i = 0; i < 8; i++) m.push_back((uint8_t)(bits >> (8 * i)));
+    uint32_t h[4] = {0x67452301, 0xefcdab89, 0x98badcfe, 0x10325476};
+    for (size_t off = 0; off < m.size(); off += 64) {
+        uint32_t w[16];
+        for (int i = 0; i < 16; i++)
+            w[i] = m[off + 4 * i] | (m[off + 4 * i + 1] << 8) | (m[off + 4 * i + 2] << 16) | ((uint32_t)m[off + 4 * i + 3] << 24);
+        uint32_t a = h[0], b = h[1], c = h[2], d = h[3];
+        for (int i = 0; i < 64; i++) {
+            uint32_t f;
+            int g;
+            if (i < 16) { f = (b & c) | (~b & d); g = i; }
+            else if (i < 32) { f = (d & b) | (~d & c); g = (5 * i + 1) % 16; }
+            else if (i < 48) { f = b ^ c ^ d; g = (3 * i + 5) % 16; }
+            else { f = c ^ (b | ~d); g = (7 * i) % 16; }
+            uint32_t t = d;
+            d = c;
+            c = b;
+            uint32_t x = a + f + K[i] + w[g];
+            b = b + ((x << R[i]) | (x >> (32 - R[i])));
+            a = t;
+        }
+        h[0] += a; h[1] += b; h[2] += c; h[3] += d;
+    }
+    static const char* hx = "0123456789abcdef";
+    std::string out;
+    for (int i = 0; i < 4; i++)
+        for (int k = 0; k < 4; k++) {
+            unsigned byte = (h[i] >> (8 * k)) & 0xff;
+            out += hx[byte >> 4];
+            out += hx[byte & 15];
+        }
+    return out;
+}
+
+// Leftmost match of a NAMED / PARAM token pattern at or after 'from'
+// (NamedTokenParser.java:43-77; ParameterizedTokenParser.java:58-95 with
+// the patterns \%\{([a-z0-9\-_]*)\}X and \%\{PREFIX([^\}]*%[^\}]*)\}t).
+bool find_pattern(const TParser& tp, const std::string& s, size_t from, size_t& start, size_t& end,
+                  std::string& field) {
+    for (size_t p = from; p + 1 < s.size(); ++p) {
+        if (s[p] != '%' || s[p + 1] != '{') continue;
+        size_t q = p + 2;
+        if (tp.kind == TP_NAMED) {
+            while (q < s.size()) {
+                char c = s[q];
+                bool ok = (c >= 'a' && c <= 'z') || (c >= '0' && c <= '9') || c == '-' || (tp.underscore && c == '_');
+                if (!ok) break;
+                ++q;
+            }
+            if (q >= s.size() || s[q] != '}') continue;
+            if (s.compare(q + 1, tp.suffix.size(), tp.suffix) != 0) continue;
+            field = s.substr(p + 2, q - p - 2);
+            start = p;
+            end = q + 1 + tp.suffix.size();
+            return true;
+        }
+        // PARAM
+        if (s.compare(q, tp.pprefix.size(), tp.pprefix) != 0) continue;
+        q += tp.pprefix.size();
+        size_t close = s.find('}', q);
+        if (close == std::string::npos) continue;
+        std::string inner = s.substr(q, close - q);
+        if (inner.find('%') == std::string::npos) continue;
+        if (close + 1 >= s.size() || s[close + 1] != 't') continue;
+        field = inner;
+        start = p;
+        end = close + 2;
+        return true;
+    }
+    return false;
+}
+
+void collect_tokens(const TParser& tp, const std::string& fmt, std::vector<Token>& out) {
+    bool blank = true;  // StringUtils.isBlank
+    for (char c : fmt) if (!(c == ' ' || (c >= 9 && c <= 13))) blank = false;
+    if (blank) return;
+    size_t offset = 0;
+    for (;;) {
+        size_t start, end;
+        std::string field;
+        if (tp.kind == TP_PLAIN || tp.kind == TP_FIXED) {
+            size_t pos = fmt.find(tp.tok, offset);
+            if (pos == std::string::npos) return;
+            start = pos;
+            end = pos + tp.tok.size();
+        } else if (!find_pattern(tp, fmt, offset, start, end, field)) {
+            return;
+        }
+        Token t;
+        t.fixed = tp.kind == TP_FIXED;
+        t.regex = tp.regex;
+        t.start = (int)start;
+        t.len = (int)(end - start);
+        t.prio = t.fixed ? 0 : tp.prio;
+        for (const auto& o : tp.outs) {
+            TokOut x = o;
+            if (tp.kind == TP_NAMED) x.name = lower(o.name + field);
+            if (tp.kind == TP_PARAM) {
+                std::string clean;
+                for (char c : field) if (isalnum((unsigned char)c)) clean += c;
+                x.type = upper(o.type + clean + "_" + md5_hex(field));
+            }
+            t.outs.push_back(x);
+        }
+        if (tp.strftime) {
+            t.strftime = true;
+            t.custom_type = t.outs[0].type;
+            t.custom_param = field;
+        }
+        out.push_back(t);
+        offset = end;
+    }
+}
+
+// cleanupLogFormat (:121-167)
+std::string apache_cleanup(const std::string& in) {
+    // removeModifiersFromLogformat: "%!?[0-9]{3}(?:,[0-9]{3})*" -> "%"
+    std::string a;
+    for (size_t i = 0; i < in.size();) {
+        if (in[i] == '%') {
+            size_t j = i + 1;
+            if (j < in.size() && in[j] == '!') ++j;
+            auto three = [&](size_t k) {
+                return k + 3 <= in.size() && isdigit((unsigned char)in[k]) && isdigit((unsigned char)in[k + 1]) &&
+                       isdigit((unsigned char)in[k + 2]);
+            };
+            if (three(j)) {
+                j += 3;
+                while (j < in.size() && in[j] == ',' && three(j + 1)) j += 4;
+                a += '%';
+                i = j;
+                continue;
+            }
+        }
+        a += in[i++];
+    }
+    // makeHeaderNamesLowercaseInLogFormat: find loop of "%\{([^}]*)}([^t])"
+    // ([^}]* stops at the first '}'; [^t] is any char but 't', newline included)
+    std::string b;
+    size_t last = 0, from = 0;
+    for (;;) {
+        size_t p = a.find("%{", from);
+        if (p == std::string::npos) break;
+        size_t c = a.find('}', p + 2);
+        if (c == std::string::npos || c + 1 >= a.size() || a[c + 1] == 't') {
+            from = p + 1;
+            continue;
+        }
+        b += a.substr(last, p - last);
+        b += "%{" + lower(a.substr(p + 2, c - p - 2)) + "}" + a[c + 1];
+        last = c + 2;
+        from = c + 2;
+    }
+    b += a.substr(last);
+    // fixTimestampFormat: "%t" -> "[%t]"
+    std::string c;
+    for (size_t i = 0; i < b.size();) {
+        if (b.compare(i, 2, "%t") == 0) { c += "[%t]"; i += 2; }
+        else c += b[i++];
+    }
+    return c;
+}
+
+bool ieq(const std::string& a, const char* b) {
+    if (a.size() != strlen(b)) return false;
+    for (size_t i = 0; i < a.size(); ++i)
+        if (tolower((unsigned char)a[i]) != b[i]) return false;
+    return true;
+}
+
+std::string apache_alias(const std::string& f) {
+    if (ieq(f, "common")) return "%h %l %u %t \"%r\" %>s %b";
+    if (ieq(f, "combined")) return "%h %l %u %t \"%r\" %>s %b \"%{Referer}i\" \"%{User-Agent}i\"";
+    if (ieq(f, "combinedio")) return "%h %l %u %t \"%r\" %>s %b \"%{Referer}i\" \"%{User-Agent}i\" %I %O";
+    if (ieq(f, "referer")) return "%{Referer}i -> %U";
+    if (ieq(f, "agent")) return "%{User-agent}i";
+    return f;
+}
+bool looks_apache(const std::string& f) {
+    return f.find('%') != std::string::npos || ieq(f, "common") || ieq(f, "combined") || ieq(f, "combinedio") ||
+           ieq(f, "referer") || ieq(f, "agent");
+}
+bool looks_nginx(const std::string& f) { return f.find('$') != std::string::npos || ieq(f, "combined"); }
+
+// TokenFormatDissector.parseTokenLogFileDefinition (:294-379)
+void parse_token_def(Format& f, const TokenTable& T) {
+    std::vector<Token> all;
+    for (const auto& tp : T.v) collect_tokens(tp, f.cleaned, all);
+    std::stable_sort(all.begin(), all.end(), [](const Token& a, const Token& b) {
+        if (a.start != b.start) return a.start < b.start;
+        if (a.len != b.len) return a.len < b.len;
+        return a.prio > b.prio;
+    });
+    std::vector<char> kick(all.size(), 0);
+    int prev = -1;
+    for (int i = 0; i < (int)all.size(); ++i) {
+        if (prev < 0) { prev = i; continue; }
+        const Token& pv = all[prev];
+        const Token& tk = all[i];
+        if (pv.start == tk.start) {
+            if (pv.len == tk.len) { if (pv.prio < tk.prio) kick[prev] = 1; else kick[i] = 1; }
+            else { if (pv.len < tk.len) kick[prev] = 1; else kick[i] = 1; }
+        } else if (pv.start + pv.len > tk.start) {
+            kick[i] = 1;
+            continue;
+        }
+        prev = i;
+    }
+    int tend = 0;
+    for (size_t i = 0; i < all.size(); ++i) {
+        if (kick[i]) continue;
+        const Token& tk = all[i];
+        if (tk.start - tend > 0) {
+            Token fx;
+            fx.fixed = true;
+            fx.regex = f.cleaned.substr(tend, tk.start - tend);
+            fx.start = tk.start;
+            fx.len = tk.start - tend;
+            f.tokens.push_back(fx);
+        }
+        f.tokens.push_back(tk);
+        tend = tk.start + tk.len;
+    }
+    if (tend < (int)f.cleaned.size()) {
+        Token fx;
+        fx.fixed = true;
+        fx.regex = f.cleaned.substr(tend);
+        fx.start = tend;
+        fx.len = (int)f.cleaned.size() - tend;
+        f.tokens.push_back(fx);
+    }
+    for (const auto& t : f.tokens) {
+        if (t.fixed) continue;
+        for (const auto& o : t.outs) {
+            std::string s = o.type + ":" + o.name;
+            if (std::find(f.output_types.begin(), f.output_types.end(), s) == f.output_types.end())
+                f.output_types.push_back(s);
+        }
+    }
+}
+
+const char* TS_OUTS[] = {
+    "TIME.DAY:day", "TIME.MONTHNAME:monthname", "TIME.MONTH:month", "TIME.WEEK:weekofweekyear", "TIME.YEAR:weekyear",
+    "TIME.YEAR:year", "TIME.HOUR:hour", "TIME.MINUTE:minute", "TIME.SECOND:second", "TIME.MILLISECOND:millisecond",
+    "TIME.MICROSECOND:microsecond", "TIME.NANOSECOND:nanosecond", "TIME.DATE:date", "TIME.TIME:time",
+    "TIME.ZONE:timezone", "TIME.EPOCH:epoch", "TIME.DAY:day_utc", "TIME.MONTHNAME:monthname_utc",
+    "TIME.MONTH:month_utc", "TIME.WEEK:weekofweekyear_utc", "TIME.YEAR:weekyear_utc", "TIME.YEAR:year_utc",
+    "TIME.HOUR:hour_utc", "TIME.MINUTE:minute_utc", "TIME.SECOND:second_utc", "TIME.MILLISECOND:millisecond_utc",
+    "TIME.MICROSECOND:microsecond_utc", "TIME.NANOSECOND:nanosecond_utc", "TIME.DATE:date_utc", "TIME.TIME:time_utc"};
+
+std::unique_ptr<Dissector> mkdis(int cls, const std::string& in) {
+    auto d = std::make_unique<Dissector>();
+    d->cls = cls;
+    d->in_type = in;
+    switch (cls) {
+    case D_TIMESTAMP: case D_TIMESTAMP_ISO: case D_STRFTIME:
+        for (auto* s : TS_OUTS) d->outs.push_back(s);
+        break;
+    case D_FIRSTLINE: d->outs = {"HTTP.METHOD:method", "HTTP.URI:uri", "HTTP.PROTOCOL_VERSION:protocol"}; break;
+    case D_PROTOCOL: d->outs = {"HTTP.PROTOCOL:", "HTTP.PROTOCOL.VERSION:version"}; break;
+    case D_URI:
+        d->outs = {"HTTP.PROTOCOL:protocol", "HTTP.USERINFO:userinfo", "HTTP.HOST:host", "HTTP.PORT:port",
+                   "HTTP.PATH:path", "HTTP.QUERYSTRING:query", "HTTP.REF:ref"};
+        break;
+    case D_QUERY: d->outs = {"STRING:*"}; break;
+    case D_COOKIES: d->outs = {"HTTP.COOKIE:*"}; break;
+    case D_SETCOOKIES: d->outs = {"HTTP.SETCOOKIE:*"}; break;
+    case D_SETCOOKIE:
+        d->outs = {"STRING:value", "STRING:expires", "TIME.EPOCH:expires", "STRING:path", "STRING:domain", "STRING:comment"};
+        break;
+    case D_UNIQUEID:
+        d->outs = {"TIME.EPOCH:epoch", "IP:ip", "PROCESSID:processid", "COUNTER:counter", "THREAD_INDEX:threadindex"};
+        break;
+    case D_LOCALIZED: d->outs = {"TIME.LOCALIZEDSTRING:"}; break;
+    default: break;
+    }
+    return d;
+}
+
+std::string extract_field_name(const std::string& in, const std::string& out) {
+    if (in == out) return "";
+    if (!in.empty()) return out.substr(in.size() + 1);
+    return out;
+}
+
+std::string cleanup_field(const std::string& f) {  // Parser.cleanupFieldValue
+    size_t c = f.find(':');
+    if (c == std::string::npos) return lower(f);
+    return upper(f.substr(0, c)) + ":" + lower(f.substr(c + 1));
+}
+
+}  // namespace
+
+// ============================================================== planning
+int Plan::build_dissectors(const std::string& logformats, std::string& err) {
+    auto root = std::make_unique<Dissector>();
+    root->cls = D_ROOT;
+    root->in_type = root_type_;
+    std::vector<std::string> list;
+    bool jetty = false;
+    size_t s = 0;
+    for (;;) {  // split("\\r?\\n")
+        size_t nl = logformats.find('\n', s);
+        std::string line = logformats.substr(s, nl == std::string::npos ? std::string::npos : nl - s);
+        if (!line.empty() && line.back() == '\r' && nl != std::string::npos) line.pop_back();
+        bool blank = true;
+        for (char c : line) if (!(c == ' ' || (c >= 9 && c <= 13))) blank = false;
+        if (!blank) {
+            std::string up = upper(line);
+            size_t a = up.find_first_not_of(" \t"), b = up.find_last_not_of(" \t");
+            if (up.substr(a, b - a + 1) == "ENABLE JETTY FIX") jetty = true;
+            else if (std::find(list.begin(), list.end(), line) == list.end()) list.push_back(line);
+        }
+        if (nl == std::string::npos) break;
+        s = nl + 1;
+    }
+    if (jetty) { device_ok_ = false; why_ = "ENABLE JETTY FIX"; }
+    for (const auto& f : list) {
+        int kind = looks_apache(f) ? FMT_APACHE : looks_nginx(f) ? FMT_NGINX : 0;
+        if (!kind) continue;
+        auto fm = std::make_unique<Format>();
+        fm->kind = kind;
+        if (kind == FMT_APACHE) {
+            fm->logformat = apache_alias(f);
+            fm->cleaned = apache_cleanup(fm->logformat);
+            parse_token_def(*fm, apache_table());
+        } else {
+            fm->logformat = f;
+            fm->cleaned = f;
+            device_ok_ = false;
+            why_ = "NGINX log_format not yet compiled for the device";
+        }
+        for (const auto& o : fm->output_types)
+            if (std::find(root->outs.begin(), root->outs.end(), o) == root->outs.end()) root->outs.push_back(o);
+        formats_.push_back(std::move(fm));
+    }
+    dis_.push_back(std::move(root));
+    dis_.push_back(mkdis(D_TIMESTAMP, "TIME.STAMP"));
+    dis_.push_back(mkdis(D_TIMESTAMP_ISO, "TIME.ISO8601"));
+    dis_.push_back(mkdis(D_FIRSTLINE, "HTTP.FIRSTLINE"));
+    dis_.push_back(mkdis(D_PROTOCOL, "HTTP.PROTOCOL_VERSION"));
+    dis_.push_back(mkdis(D_URI, "HTTP.URI"));
+    dis_.push_back(mkdis(D_QUERY, "HTTP.QUERYSTRING"));
+    dis_.push_back(mkdis(D_COOKIES, "HTTP.COOKIES"));
+    dis_.push_back(mkdis(D_SETCOOKIES, "HTTP.SETCOOKIES"));
+    dis_.push_back(mkdis(D_SETCOOKIE, "HTTP.SETCOOKIE"));
+    dis_.push_back(mkdis(D_UNIQUEID, "MOD_UNIQUE_ID"));
+    auto c2n = mkdis(D_CLF2NUM, "BYTESCLF");
+    c2n->out_type = "BYTES";
+    c2n->outs = {"BYTES:"};
+    dis_.push_back(std::move(c2n));
+    auto n2c = mkdis(D_NUM2CLF, "BYTES");
+    n2c->out_type = "BYTESCLF";
+    n2c->outs = {"BYTESCLF:"};
+    dis_.push_back(std::move(n2c));
+    for (const auto& f : formats_)
+        for (const auto& t : f->tokens)
+            if (t.strftime) {
+                dis_.push_back(mkdis(D_STRFTIME, t.custom_type));
+                dis_.push_back(mkdis(D_LOCALIZED, t.custom_type));
+            }
+    (void)err;
+    return LP_OK;
+}
+
+void Plan::find_useful(const std::set<std::string>& possible, const std::string& type, const std::string& name,
+                       bool is_root) {
+    std::string srid = type + ":" + name;
+    if (located_.count(srid)) return;
+    located_.insert(srid);
+    for (const auto& dp : dis_) {
+        const Dissector& d = *dp;
+        if (d.in_type != type) continue;
+        for (const auto& out : d.outs) {
+            size_t colon = out.find(':');
+            std::string otype = out.substr(0, colon), oname = out.substr(colon + 1);
+            std::vector<std::string> checks;
+            if (oname == "*") {
+                std::string pre = name + ".";
+                for (const auto& p : possible)
+                    if (p.compare(0, pre.size(), pre) == 0) checks.push_back(p);
+            } else if (is_root) checks.push_back(oname);
+            else if (oname.empty()) checks.push_back(name);
+            else checks.push_back(name + "." + oname);
+            for (const auto& cf : checks) {
+                if (!possible.count(cf) || compiled_.count(otype + ":" + cf)) continue;
+                auto it = compiled_.find(srid);
+                if (it == compiled_.end()) {
+                    it = compiled_.emplace(srid, std::vector<Instance>{}).first;
+                    useful_.insert(name);
+                }
+                Instance* in = nullptr;
+                for (auto& x : it->second) if (x.cls == d.cls) in = &x;
+                if (!in) {
+                    it->second.push_back(Instance{d.cls, &d, {}});
+                    in = &it->second.back();
+                }
+                in->requested.insert(extract_field_name(name, cf));
+                if (d.cls == D_ROOT)
+                    for (auto& f : formats_) f->requested.insert(cf);  // TokenFormatDissector.prepareForDissect
+                find_useful(possible, otype, cf, false);
+            }
+        }
+    }
+}
+
+int Plan::build(const std::string& logformats, const std::vector<std::string>& fields, std::string& err) {
+    int r = build_dissectors(logformats, err);
+    if (r != LP_OK) return r;
+    for (const auto& f : fields) needed_.insert(cleanup_field(f));
+    for (const auto& d : dis_)
+        if (d->outs.empty()) {
+            err = "InvalidDissectorException: Dissector cannot create any outputs: " + d->in_type;
+            return LP_E_INVALID;
+        }
+    std::set<std::string> needed = needed_;
+    needed.insert(root_type_ + ":");
+    std::set<std::string> possible;
+    for (const auto& n : needed) {
+        std::string nm = n.substr(n.find(':') + 1);
+        std::string sb;
+        size_t s = 0;
+        for (;;) {
+            size_t dot = nm.find('.', s);
+            std::string part = nm.substr(s, dot == std::string::npos ? std::string::npos : dot - s);
+            if (sb.empty() || part.empty()) sb += part;
+            else sb += "." + part;
+            possible.insert(sb);
+            if (dot == std::string::npos) break;
+            s = dot + 1;
+        }
+    }
+    find_useful(possible, root_type_, "", true);
+    if (compiled_.empty()) {
+        err = "MissingDissectorsException: There are no dissectors at all which makes this a completely useless parser.";
+        return LP_E_MISSING;
+    }
+    if (formats_.empty()) {
+        err = "InvalidDissectorException: Cannot run without logformats";
+        return LP_E_INVALID;
+    }
+    for (const auto& t : needed_) {
+        if (located_.count(t)) continue;
+        if (!t.empty() && t.back() == '*') {
+            if (t.size() >= 2 && t[t.size() - 2] == '.' && !located_.count(t.substr(0, t.size() - 2))) {
+                err = "MissingDissectorsException: " + t;
+                return LP_E_MISSING;
+            }
+        } else {
+            err = "MissingDissectorsException: " + t;
+            return LP_E_MISSING;
+        }
+    }
+    compile_program();
+    return device_ok_ ? LP_OK : LP_E_UNSUPPORTED;
+}
+
+int Plan::possible_paths(const std::string& logformats, int max_depth, std::vector<std::string>& out,
+                         std::string& err) {
+    Plan p;
+    p.build_dissectors(logformats, err);
+    std::set<std::string> seen;
+    std::function<void(const std::string&, const std::string&, int)> rec = [&](const std::string& base,
+                                                                             const std::string& btype, int depth) {
+        if (depth == 0) return;
+        for (const auto& d : p.dis_) {
+            if (d->in_type != btype) continue;
+            for (const auto& o : d->outs) {
+                size_t colon = o.find(':');
+                std::string ctype = o.substr(0, colon), cname = o.substr(colon + 1);
+                std::string cbase = base.empty() ? cname : cname.empty() ? base : base + "." + cname;
+                std::string np = ctype + ":" + cbase;
+                if (seen.insert(np).second) rec(cbase, ctype, depth - 1);
+            }
+        }
+    };
+    rec("", p.root_type_, max_depth);
+    out.assign(seen.begin(), seen.end());
+    return LP_OK;
+}
+
+// ====================================================== device program
+namespace {
+enum Origin { O_NONE, O_TOKEN, O_FL_URI, O_FL_PROTO, O_FL_METHOD, O_URI_QUERY, O_URI_PART, O_CONV, O_TIME };
+}
+
+void Plan::compile_program() {
+    Program& P = prog_;
+    memset(&P, 0, sizeof P);
+    if (!device_ok_) return;
+    if (formats_.size() != 1) {
+        device_ok_ = false;
+        why_ = "multiple LogFormats (sticky multi-format routing) not yet on the device";
+        return;
+    }
+    const Format& f = *formats_[0];
+    P.apache = f.kind == FMT_APACHE;
+    int lit_used = 0;
+    auto add_lit = [&](const std::string& s) -> int {
+        if (lit_used + (int)s.size() > MAX_LIT) return -1;
+        memcpy(P.lit + lit_used, s.data(), s.size());
+        int off = lit_used;
+        lit_used += (int)s.size();
+        return off;
+    };
+    std::set<std::string> seen_names;
+    for (int i = 0; i < (int)f.tokens.size(); ++i) {
+        const Token& t = f.tokens[i];
+        if (P.n_elems == MAX_ELEMS) { device_ok_ = false; why_ = "too many LogFormat elements"; return; }
+        Elem& e = P.elems[P.n_elems++];
+        memset(&e, 0, sizeof e);
+        e.cap = -1;
+        if (t.fixed) {
+            e.kind = EK_LIT;
+            int off = add_lit(t.regex);
+            if (off < 0) { device_ok_ = false; why_ = "literal pool overflow"; return; }
+            e.lit_off = (uint16_t)off;
+            e.lit_len = (uint16_t)t.regex.size();
+            continue;
+        }
+        int k = elem_kind_of(t.regex);
+        if (k < 0) { device_ok_ = false; why_ = "token regex not on the device: " + t.regex; return; }
+        e.kind = (uint8_t)k;
+        bool wanted = false;
+        for (const auto& o : t.outs) if (f.requested.count(o.name)) wanted = true;
+        if (wanted) {
+            if (P.n_tok == MAX_TOK) { device_ok_ = false; why_ = "too many captured tokens"; return; }
+            for (const auto& o : t.outs)
+                if (!seen_names.insert(o.type + ":" + o.name).second) {
+                    device_ok_ = false;
+                    why_ = "the same output is produced by two tokens";
+                    return;
+                }
+            tok_slot_[i] = P.n_tok;
+            e.cap = (int8_t)P.n_tok++;
+        }
+    }
+    // anchoring literal / determinism of each token element
+    for (int i = 0; i < P.n_elems; ++i) {
+        Elem& e = P.elems[i];
+        if (e.kind == EK_LIT) continue;
+        e.last = i == P.n_elems - 1;
+        if (i + 1 < P.n_elems && P.elems[i + 1].kind == EK_LIT) {
+            e.nlit = 1;
+            e.lit_off = P.elems[i + 1].lit_off;
+            e.lit_len = P.elems[i + 1].lit_len;
+        }
+        uint8_t c0 = e.nlit ? P.lit[e.lit_off] : 0;
+        bool ws0 = c0 == ' ' || (c0 >= 9 && c0 <= 13);
+        bool dig0 = c0 >= '0' && c0 <= '9';
+        bool hex0 = dig0 || ((c0 | 32) >= 'a' && (c0 | 32) <= 'f');
+        switch (e.kind) {
+        case EK_NOSPACE: e.det = (e.nlit && ws0) || e.last; break;
+        case EK_NUMBER: case EK_CLFNUMBER: case EK_NONZERO: e.det = (e.nlit && !dig0) || e.last; break;
+        case EK_HEXNUMBER: case EK_CLFHEXNUMBER: e.det = (e.nlit && !hex0) || e.last; break;
+        case EK_ANY_GREEDY: case EK_ANY_LAZY: e.det = e.last; break;
+        case EK_TIME_US: e.det = 1; break;
+        default: e.det = 0; break;
+        }
+    }
+    // stages, walking the compiled tree from each captured token output
+    std::function<void(int, int, const std::string&, const std::string&)> walk =
+        [&](int ok, int oi, const std::string& type, const std::string& complete) {
+            if (!device_ok_) return;
+            if (!useful_.count(complete)) return;
+            auto it = compiled_.find(type + ":" + complete);
+            if (it == compiled_.end()) return;
+            for (const auto& in : it->second) {
+                switch (in.cls) {
+                case D_TIMESTAMP: {
+                    if (ok != O_TOKEN) { device_ok_ = false; why_ = "timestamp from a derived value"; return; }
+                    if (!time_of_tok_.count(oi)) {
+                        if (P.n_time == MAX_TIME) { device_ok_ = false; why_ = "too many timestamps"; return; }
+                        P.time[P.n_time].tok = (int8_t)oi;
+                        time_of_tok_[oi] = P.n_time++;
+                    }
+                    break;
+                }
+                case D_FIRSTLINE: {
+                    if (ok != O_TOKEN) { device_ok_ = false; why_ = "first line from a derived value"; return; }
+                    int fidx;
+                    if (!fl_of_tok_.count(oi)) {
+                        if (P.n_fl == MAX_FL) { device_ok_ = false; why_ = "too many first lines"; return; }
+                        P.fl[P.n_fl].tok = (int8_t)oi;
+                        fl_of_tok_[oi] = P.n_fl++;
+                    }
+                    fidx = fl_of_tok_[oi];
+                    walk(O_FL_URI, fidx, "HTTP.URI", complete + ".uri");
+                    walk(O_FL_PROTO, fidx, "HTTP.PROTOCOL_VERSION", complete + ".protocol");
+                    walk(O_FL_METHOD, fidx, "HTTP.METHOD", complete + ".method");
+                    break;
+                }
+                case D_PROTOCOL:
+                    if (ok != O_FL_PROTO) { device_ok_ = false; why_ = "protocol from a non first-line value"; return; }
+                    break;
+                case D_URI: {
+                    std::map<int, int>& m = ok == O_TOKEN ? uri_of_tok_ : uri_of_fl_;
+                    if (ok != O_TOKEN && ok != O_FL_URI) { device_ok_ = false; why_ = "URI from a derived value"; return; }
+                    if (!m.count(oi)) {
+                        if (P.n_uri == MAX_URI) { device_ok_ = false; why_ = "too many URIs"; return; }
+                        UriStage& U = P.uri[P.n_uri];
+                        memset(&U, 0, sizeof U);
+                        U.src_tok = ok == O_TOKEN ? (int8_t)oi : -1;
+                        U.src_fl = ok == O_FL_URI ? (int8_t)oi : -1;
+                        U.query_stage = -1;
+                        m[oi] = P.n_uri++;
+                    }
+                    int u = m[oi];
+                    UriStage& U = P.uri[u];
+                    if (in.requested.count("query")) U.want_query = 1;
+                    if (in.requested.count("path")) U.want_path = 1;
+                    if (in.requested.count("ref")) U.want_ref = 1;
+                    if (in.requested.count("userinfo")) U.want_userinfo = 1;
+                    walk(O_URI_QUERY, u, "HTTP.QUERYSTRING", complete + ".query");
+                    break;
+                }
+                case D_QUERY: {
+                    if (ok != O_URI_QUERY) { device_ok_ = false; why_ = "query string from a raw token"; return; }
+                    UriStage& U = P.uri[oi];
+                    U.want_query = 1;
+                    if (U.query_stage < 0) {
+                        if (P.n_query == MAX_QUERY) { device_ok_ = false; why_ = "too many query strings"; return; }
+                        memset(&P.query[P.n_query], 0, sizeof(QueryStage));
+                        P.query[P.n_query].uri = (int8_t)oi;
+                        U.query_stage = (int8_t)P.n_query;
+                        query_of_uri_[oi] = P.n_query++;
+                    }
+                    QueryStage& Q = P.query[U.query_stage];
+                    for (const auto& r : in.requested) {
+                        if (r == "*") { Q.want_all = 1; continue; }
+                        bool dup = false;
+                        for (int k = 0; k < Q.n_names; ++k)
+                            if (Q.name_len[k] == r.size() && !memcmp(P.lit + Q.name_off[k], r.data(), r.size())) dup = true;
+                        if (dup) continue;
+                        if (Q.n_names == MAX_QNAMES || r.size() > 255) { device_ok_ = false; why_ = "too many query names"; return; }
+                        int off = add_lit(r);
+                        if (off < 0) { device_ok_ = false; why_ = "literal pool overflow"; return; }
+                        Q.name_off[Q.n_names] = (uint16_t)off;
+                        Q.name_len[Q.n_names] = (uint8_t)r.size();
+                        Q.n_names++;
+                    }
+                    break;
+                }
+                case D_CLF2NUM: case D_NUM2CLF:
+                    if (ok != O_TOKEN && ok != O_CONV) { device_ok_ = false; why_ = "converter on a derived value"; return; }
+                    walk(O_CONV, oi, in.d->out_type, complete);
+                    break;
+                default:
+                    device_ok_ = false;
+                    why_ = "dissector for input type " + in.d->in_type + " not on the device";
+                    return;
+                }
+            }
+        };
+    for (int i = 0; i < (int)f.tokens.size(); ++i) {
+        auto it = tok_slot_.find(i);
+        if (it == tok_slot_.end()) continue;
+        for (const auto& o : f.tokens[i].outs) walk(O_TOKEN, it->second, o.type, o.name);
+    }
+}
+
+std::string Plan::describe() const {
+    std::string s;
+    char b[256];
+    snprintf(b, sizeof b, "device_ok=%d%s%s\n", (int)device_ok_, device_ok_ ? "" : " reason=", device_ok_ ? "" : why_.c_str());
+    s += b;
+    for (const auto& f : formats_) s += "format: " + f->cleaned + "\n";
+    static const char* kn[] = {"LIT", "NOSPACE", "NUMBER", "CLFNUMBER", "HEXNUMBER", "CLFHEXNUMBER", "NONZERO",
+                               "ANY_GREEDY", "ANY_LAZY", "TIME_US", "CLF_IP", "IP"};
+    for (int i = 0; i < prog_.n_elems; ++i) {
+        const Elem& e = prog_.elems[i];
+        std::string lit = e.kind == EK_LIT ? std::string((const char*)prog_.lit + e.lit_off, e.lit_len) : "";
+        snprintf(b, sizeof b, "  elem %2d %-12s cap=%2d det=%d last=%d nlit=%d %s\n", i, kn[e.kind], e.cap, e.det,
+                 e.last, e.nlit, e.kind == EK_LIT ? ("'" + lit + "'").c_str() : "");
+        s += b;
+    }
+    snprintf(b, sizeof b, "  tokens=%d time=%d firstline=%d uri=%d query=%d\n", prog_.n_tok, prog_.n_time, prog_.n_fl,
+             prog_.n_uri, prog_.n_query);
+    s += b;
+    return s;
+}
+
+// ================================================================ replay
+struct Plan::Ctx {
+    const HostResults& R;
+    int64_t i;
+    const uint8_t* line;
+    const uint8_t* arena;
+    std::vector<std::pair<std::string, MVal>> rec;
+    std::deque<std::string> pool;  // formatted date/time strings
+};
+
+namespace {
+MVal mstr(const uint8_t* p, uint32_t len) {
+    MVal v;
+    v.p = p;
+    v.len = len;
+    return v;
+}
+MVal mnull() {
+    MVal v;
+    v.null = true;
+    return v;
+}
+MVal mlong(int64_t l) {
+    MVal v;
+    v.is_long = true;
+    v.l = l;
+    return v;
+}
+const char* MONTH_FULL[] = {"January", "February", "March", "April", "May", "June", "July",
+                            "August", "September", "October", "November", "December"};
+}  // namespace
+
+static thread_local int t_origin_kind = 0, t_origin_idx = 0;
+
+void Plan::emit(Ctx& c, const std::string& base, const std::string& type, const std::string& name, const MVal& v) const {
+    std::string complete, wild;
+    if (base.empty()) {
+        complete = name;
+        wild = type + ":*";
+    } else {
+        complete = name.empty() ? base : base + "." + name;
+        wild = type + ":" + base + ".*";
+    }
+    std::string needed = type + ":" + complete;
+    int ok = t_origin_kind, oi = t_origin_idx;
+    if (useful_.count(complete)) {
+        auto it = compiled_.find(needed);
+        if (it != compiled_.end())
+            for (const auto& in : it->second) {
+                t_origin_kind = ok;
+                t_origin_idx = oi;
+                run_phase(c, in, complete, v);
+            }
+    }
+    if (needed_.count(needed)) c.rec.emplace_back(needed, v);
+    if (needed_.count(wild)) c.rec.emplace_back(needed, v);
+}
+
+void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const MVal& v) const {
+    const HostResults& R = c.R;
+    const int64_t i = c.i;
+    const int ok = t_origin_kind, oi = t_origin_idx;
+    auto has = [&](const char* n) { return in.requested.count(n) > 0; };
+    auto set_origin = [](int k, int x) { t_origin_kind = k; t_origin_idx = x; };
+    auto line_ref = [&](uint64_t r) { return mstr((ref_arena(r) ? c.arena : c.line) + ref_off(r), ref_len(r)); };
+    switch (in.cls) {
+    case D_TIMESTAMP: {
+        if (v.null || v.len == 0) return;
+        int t = time_of_tok_.at(oi);
+        int64_t epoch = R.t_epoch[t][i];
+        if (has("epoch")) { set_origin(O_TIME, t); emit(c, name, "TIME.EPOCH", "epoch", mlong(epoch)); }
+        for (int pass = 0; pass < 2; ++pass) {
+            uint64_t w = pass == 0 ? R.t_local[t][i] : R.t_utc[t][i];
+            const char* sfx = pass == 0 ? "" : "_utc";
+            int64_t Y = w & 0xFFFF, MO = (w >> 16) & 15, D = (w >> 20) & 31, H = (w >> 25) & 31, MI = (w >> 30) & 63,
+                    S = (w >> 36) & 63, WY = (w >> 42) & 0xFFFF, WK = (w >> 58) & 63;
+            auto nm = [&](const char* b) { return std::string(b) + sfx; };
+            set_origin(O_TIME, t);
+            if (has(nm("day").c_str())) emit(c, name, "TIME.DAY", nm("day"), mlong(D));
+            if (has(nm("monthname").c_str())) {
+                const char* mn = MONTH_FULL[MO - 1];
+                emit(c, name, "TIME.MONTHNAME", nm("monthname"), mstr((const uint8_t*)mn, (uint32_t)strlen(mn)));
+            }
+            if (has(nm("month").c_str())) emit(c, name, "TIME.MONTH", nm("month"), mlong(MO));
+            if (has(nm("weekofweekyear").c_str())) emit(c, name, "TIME.WEEK", nm("weekofweekyear"), mlong(WK));
+            if (has(nm("weekyear").c_str())) emit(c, name, "TIME.YEAR", nm("weekyear"), mlong(WY));
+            if (has(nm("year").c_str())) emit(c, name, "TIME.YEAR", nm("year"), mlong(Y));
+            if (has(nm("hour").c_str())) emit(c, name, "TIME.HOUR", nm("hour"), mlong(H));
+            if (has(nm("minute").c_str())) emit(c, name, "TIME.MINUTE", nm("minute"), mlong(MI));
+            if (has(nm("second").c_str())) emit(c, name, "TIME.SECOND", nm("second"), mlong(S));
+            if (has(nm("millisecond").c_str())) emit(c, name, "TIME.MILLISECOND", nm("millisecond"), mlong(0));
+            if (has(nm("microsecond").c_str())) emit(c, name, "TIME.MICROSECOND", nm("microsecond"), mlong(0));
+            if (has(nm("nanosecond").c_str())) emit(c, name, "TIME.NANOSECOND", nm("nanosecond"), mlong(0));
+            if (has(nm("date").c_str())) {
+                char b[32];
+                snprintf(b, sizeof b, "%04lld-%02lld-%02lld", (long long)Y, (long long)MO, (long long)D);
+                c.pool.emplace_back(b);
+                emit(c, name, "TIME.DATE", nm("date"), mstr((const uint8_t*)c.pool.back().data(), (uint32_t)c.pool.back().size()));
+            }
+            if (has(nm("time").c_str())) {
+                char b[32];
+                snprintf(b, sizeof b, "%02lld:%02lld:%02lld", (long long)H, (long long)MI, (long long)S);
+                c.pool.emplace_back(b);
+                emit(c, name, "TIME.TIME", nm("time"), mstr((const uint8_t*)c.pool.back().data(), (uint32_t)c.pool.back().size()));
+            }
+        }
+        return;
+    }
+    case D_FIRSTLINE: {
+        int f = fl_of_tok_.at(oi);
+        uint32_t kind = R.fl_kind[f][i];
+        if (kind == FL_NONE) return;
+        auto span = [&](uint32_t s) { return mstr(c.line + (s & 0xFFFF), (s >> 16) - (s & 0xFFFF)); };
+        if (has("method")) { set_origin(O_FL_METHOD, f); emit(c, name, "HTTP.METHOD", "method", span(R.fl_method[f][i])); }
+        if (has("uri")) { set_origin(O_FL_URI, f); emit(c, name, "HTTP.URI", "uri", span(R.fl_uri[f][i])); }
+        if (kind == FL_FULL) {
+            if (has("protocol")) { set_origin(O_FL_PROTO, f); emit(c, name, "HTTP.PROTOCOL_VERSION", "protocol", span(R.fl_proto[f][i])); }
+        } else {
+            set_origin(O_FL_PROTO, f);
+            emit(c, name, "HTTP.PROTOCOL_VERSION", "protocol", mnull());
+        }
+        return;
+    }
+    case D_PROTOCOL: {
+        if (v.null || v.len == 0 || (v.len == 1 && v.p[0] == '-')) return;
+        // "HTTP/x.y".split("/", 2)
+        uint32_t sl = 0;
+        while (sl < v.len && v.p[sl] != '/') ++sl;
+        set_origin(O_NONE, 0);
+        if (sl < v.len) {
+            if (has("")) emit(c, name, "HTTP.PROTOCOL", "", mstr(v.p, sl));
+            if (has("version")) emit(c, name, "HTTP.PROTOCOL.VERSION", "version", mstr(v.p + sl + 1, v.len - sl - 1));
+        } else {
+            emit(c, name, "HTTP.PROTOCOL", "", mnull());
+            emit(c, name, "HTTP.PROTOCOL.VERSION", "version", mnull());
+        }
+        return;
+    }
+    case D_URI: {
+        if (v.null || v.len == 0) return;
+        int u = ok == O_TOKEN ? uri_of_tok_.at(oi) : uri_of_fl_.at(oi);
+        uint32_t fl = R.u_flags[u][i];
+        if (!(fl & UF_DONE)) return;
+        if (has("query") || has("path") || has("ref")) {
+            if (has("query")) {
+                set_origin(O_URI_QUERY, u);
+                emit(c, name, "HTTP.QUERYSTRING", "query", line_ref(R.u_query[u][i]));
+            }
+            set_origin(O_URI_PART, u);
+            if (has("path")) emit(c, name, "HTTP.PATH", "path", line_ref(R.u_path[u][i]));
+            if (has("ref")) emit(c, name, "HTTP.REF", "ref", (fl & UF_FRAG) ? line_ref(R.u_frag[u][i]) : mnull());
+        }
+        if (fl & UF_IS_URL) {
+            set_origin(O_URI_PART, u);
+            if (has("protocol")) emit(c, name, "HTTP.PROTOCOL", "protocol", (fl & UF_SCHEME) ? line_ref(R.u_scheme[u][i]) : mnull());
+            if (has("userinfo")) emit(c, name, "HTTP.USERINFO", "userinfo", mnull());
+            if (has("host")) emit(c, name, "HTTP.HOST", "host", (fl & UF_HOST) ? line_ref(R.u_host[u][i]) : mnull());
+            if (has("port") && (fl & UF_PORT)) emit(c, name, "HTTP.PORT", "port", mlong(R.u_port[u][i]));
+        }
+        return;
+    }
+    case D_QUERY: {
+        if (v.null || v.len == 0) return;
+        int q = query_of_uri_.at(oi);
+        uint32_t cnt = R.q_count[q][i];
+        uint64_t tab = R.q_params[q][i];
+        const uint64_t* t = (const uint64_t*)(c.arena + ref_off(tab));
+        set_origin(O_NONE, 0);
+        for (uint32_t k = 0; k < cnt; ++k) {
+            MVal nm = line_ref(t[2 * k]);
+            MVal val = line_ref(t[2 * k + 1]);
+            emit(c, name, "STRING", std::string((const char*)nm.p, nm.len), val);
+        }
+        return;
+    }
+    case D_CLF2NUM: {
+        // ConvertCLFIntoNumber: null or "-" -> 0L, else the same value
+        bool dash = !v.null && !v.is_long && v.len == 1 && v.p[0] == '-';
+        set_origin(O_CONV, oi);
+        if (v.null || dash) emit(c, name, in.d->out_type, "", mlong(0));
+        else emit(c, name, in.d->out_type, "", v);
+        return;
+    }
+    case D_NUM2CLF: {
+        // ConvertNumberIntoCLF: "0" -> null, else the same value
+        bool zero = v.is_long ? v.l == 0 : (!v.null && v.len == 1 && v.p[0] == '0');
+        set_origin(O_CONV, oi);
+        if (zero) emit(c, name, in.d->out_type, "", mnull());
+        else emit(c, name, in.d->out_type, "", v);
+        return;
+    }
+    default:
+        return;
+    }
+}
+
+namespace {
+void json_str(std::string& o, const uint8_t* p, uint32_t n) {
+    o += '"';
+    for (uint32_t k = 0; k < n; ++k) {
+        uint8_t ch = p[k];
+        if (ch == '"') o += "\\\"";
+        else if (ch == '\\') o += "\\\\";
+        else if (ch < 0x20) {
+            char b[8];
+            snprintf(b, sizeof b, "\\u%04x", ch);
+            o += b;
+        } else o += (char)ch;
+    }
+    o += '"';
+}
+}  // namespace
+
+std::string Plan::record_json(const HostResults& R, int64_t i) const {
+    Ctx c{R, i, R.input.data() + R.line_off[i], R.arena.empty() ? nullptr : R.arena.data() + R.arena_base[i], {}};
+    const Format& f = *formats_[0];
+    for (const auto& kv : tok_slot_) {
+        int k = kv.second;
+        uint32_t sp = R.tok_span[k][i];
+        bool null = (R.tok_flags[i] >> k) & 1;
+        MVal v = null ? mnull() : mstr(c.line + (sp & 0xFFFF), (sp >> 16) - (sp & 0xFFFF));
+        for (const auto& o : f.tokens[kv.first].outs) {
+            t_origin_kind = O_TOKEN;
+            t_origin_idx = k;
+            emit(c, "", o.type, o.name, v);
+        }
+    }
+    std::stable_sort(c.rec.begin(), c.rec.end(),
+                     [](const std::pair<std::string, MVal>& a, const std::pair<std::string, MVal>& b) {
+                         return a.first < b.first;
+                     });
+    std::string o = "{";
+    for (size_t a = 0; a < c.rec.size();) {
+        if (a) o += ",";
+        json_str(o, (const uint8_t*)c.rec[a].first.data(), (uint32_t)c.rec[a].first.size());
+        o += ":[";
+        size_t b = a;
+        for (; b < c.rec.size() && c.rec[b].first == c.rec[a].first; ++b) {
+            if (b > a) o += ",";
+            const MVal& v = c.rec[b].second;
+            char buf[64];
+            if (v.is_long) {
+                snprintf(buf, sizeof buf, "{\"l\":%lld}", (long long)v.l);
+                o += buf;
+            } else if (v.null) o += "null";
+            else json_str(o, v.p, v.len);
+        }
+        o += "]";
+        a = b;
+    }
+    o += "}";
+    return o;
+}
+
+}  // namespace lp

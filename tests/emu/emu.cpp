@@ -1,0 +1,109 @@
+// TEST-ONLY CPU emulation of the device per-line logic.
+//
+// Compiles logparser_amd/csrc/lp_device.h (the exact source of the gfx950
+// kernel's per-line code) and plan.cpp with g++ so the planner, matcher and
+// stages can be diffed against the oracle in the CPU test suite.  It is never
+// part of the product: the product library (liblogparser_amd.so) only runs
+// this logic inside the HIP kernel and fails when no GPU is present.
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../logparser_amd/csrc/lp_device.h"
+#include "../../logparser_amd/csrc/plan.h"
+
+using namespace lp;
+
+struct Emu {
+    Plan plan;
+    int status;
+    std::string err;
+};
+
+extern "C" {
+
+void* emu_new(const char* fmt, const char* const* fields, int n, int* status, char* err, int errlen) {
+    Emu* e = new Emu();
+    std::vector<std::string> f(fields, fields + n);
+    e->status = e->plan.build(fmt, f, e->err);
+    *status = e->status;
+    if (err && errlen) snprintf(err, errlen, "%s%s", e->err.c_str(), e->plan.device_ok() ? "" : e->plan.unsupported_reason().c_str());
+    if (e->status != 0 && e->status != -3) { delete e; return nullptr; }
+    return e;
+}
+
+void emu_free(void* h) { delete (Emu*)h; }
+
+int emu_describe(void* h, char* out, int cap) {
+    std::string d = ((Emu*)h)->plan.describe();
+    snprintf(out, cap, "%s", d.c_str());
+    return (int)d.size();
+}
+
+// returns line status (0 OK, 1 BAD, 2 FALLBACK), fills out with the record JSON when OK
+int emu_parse(void* h, const char* line, int len, char* out, int cap) {
+    Emu* e = (Emu*)h;
+    if (!e->plan.device_ok()) return 2;
+    const Program& P = e->plan.program();
+    HostResults R;
+    R.n = 1;
+    R.input.assign(line, line + len);
+    R.input.push_back('\n');
+    R.line_off = {0, (uint64_t)len + 1};
+    R.status.assign(1, 0);
+    R.tok_span.assign(MAX_TOK, std::vector<uint32_t>(1));
+    R.tok_flags.assign(1, 0);
+    R.t_epoch.assign(MAX_TIME, std::vector<int64_t>(1));
+    R.t_local.assign(MAX_TIME, std::vector<uint64_t>(1));
+    R.t_utc.assign(MAX_TIME, std::vector<uint64_t>(1));
+    for (auto* v : {&R.fl_kind, &R.fl_method, &R.fl_uri, &R.fl_proto}) v->assign(MAX_FL, std::vector<uint32_t>(1));
+    R.u_flags.assign(MAX_URI, std::vector<uint32_t>(1));
+    for (auto* v : {&R.u_scheme, &R.u_host, &R.u_path, &R.u_query, &R.u_frag, &R.u_userinfo})
+        v->assign(MAX_URI, std::vector<uint64_t>(1));
+    R.u_port.assign(MAX_URI, std::vector<int32_t>(1));
+    R.q_count.assign(MAX_QUERY, std::vector<uint32_t>(1));
+    R.q_params.assign(MAX_QUERY, std::vector<uint64_t>(1));
+    R.arena_base.assign(1, 0);
+    Columns C;
+    memset(&C, 0, sizeof C);
+    C.status = R.status.data();
+    C.line_off = R.line_off.data();
+    for (int k = 0; k < MAX_TOK; ++k) C.tok_span[k] = R.tok_span[k].data();
+    C.tok_flags = R.tok_flags.data();
+    for (int t = 0; t < MAX_TIME; ++t) { C.t_epoch[t] = R.t_epoch[t].data(); C.t_local[t] = R.t_local[t].data(); C.t_utc[t] = R.t_utc[t].data(); }
+    for (int f = 0; f < MAX_FL; ++f) { C.fl_kind[f] = R.fl_kind[f].data(); C.fl_method[f] = R.fl_method[f].data(); C.fl_uri[f] = R.fl_uri[f].data(); C.fl_proto[f] = R.fl_proto[f].data(); }
+    for (int u = 0; u < MAX_URI; ++u) {
+        C.u_flags[u] = R.u_flags[u].data(); C.u_scheme[u] = R.u_scheme[u].data(); C.u_host[u] = R.u_host[u].data();
+        C.u_port[u] = R.u_port[u].data(); C.u_path[u] = R.u_path[u].data(); C.u_query[u] = R.u_query[u].data();
+        C.u_frag[u] = R.u_frag[u].data(); C.u_userinfo[u] = R.u_userinfo[u].data();
+    }
+    for (int q = 0; q < MAX_QUERY; ++q) { C.q_count[q] = R.q_count[q].data(); C.q_params[q] = R.q_params[q].data(); }
+    Line L{(const uint8_t*)R.input.data(), len};
+    LineOut o;
+    uint32_t stk[MAX_STACK];
+    phase1(P, L, o, stk, C, 0);
+    if (o.status == ST_OK && o.arena_need) {
+        R.arena.assign(o.arena_need + 64, 0);
+        Arena A{R.arena.data(), 0, o.arena_need};
+        phase2(P, L, o, A, C, 0);
+        if (A.used > o.arena_need) { snprintf(out, cap, "ARENA OVERFLOW %u > %u", A.used, o.arena_need); return 3; }
+    }
+    write_line(P, o, C, 0);
+    if (o.status != ST_OK) return o.status;
+    std::string js = e->plan.record_json(R, 0);
+    if ((int)js.size() + 1 > cap) return -1;
+    memcpy(out, js.c_str(), js.size() + 1);
+    return 0;
+}
+
+int emu_possible_paths(const char* fmt, int depth, char* out, int cap) {
+    std::vector<std::string> paths;
+    std::string err;
+    Plan::possible_paths(fmt, depth, paths, err);
+    std::string s;
+    for (auto& p : paths) s += p + "\n";
+    if ((int)s.size() + 1 > cap) return -1;
+    memcpy(out, s.c_str(), s.size() + 1);
+    return (int)s.size();
+}
+}

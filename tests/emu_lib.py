@@ -1,0 +1,85 @@
+"""TEST-ONLY ctypes binding of tests/emu (CPU emulation of the device per-line
+code, compiled from logparser_amd/csrc/lp_device.h with g++).  Lets the CPU
+test suite diff the device logic against the oracle; never used by the
+product or the benchmark."""
+import ctypes
+import json
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(ROOT, "tests", "emu", "_build", "libemu.so")
+SRCS = [os.path.join(ROOT, "tests", "emu", "emu.cpp"), os.path.join(ROOT, "logparser_amd", "csrc", "plan.cpp")]
+HDRS = [os.path.join(ROOT, "logparser_amd", "csrc", h) for h in ("lp_device.h", "lp_program.h", "plan.h")]
+
+_lib = None
+
+
+def build(force=False):
+    newest = max(os.path.getmtime(p) for p in SRCS + HDRS)
+    if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= newest:
+        return
+    os.makedirs(os.path.dirname(LIB), exist_ok=True)
+    subprocess.run(["g++", "-std=c++17", "-O2", "-g", "-fPIC", "-shared", "-o", LIB] + SRCS, check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(LIB)
+        L.emu_new.restype = ctypes.c_void_p
+        L.emu_new.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int,
+                              ctypes.POINTER(ctypes.c_int), ctypes.c_char_p, ctypes.c_int]
+        L.emu_free.argtypes = [ctypes.c_void_p]
+        L.emu_parse.restype = ctypes.c_int
+        L.emu_parse.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        L.emu_describe.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]
+        L.emu_possible_paths.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        _lib = L
+    return _lib
+
+
+class Emu:
+    def __init__(self, logformat, fields):
+        arr = (ctypes.c_char_p * max(1, len(fields)))()
+        for i, f in enumerate(fields):
+            arr[i] = f.encode()
+        self._arr = arr
+        st = ctypes.c_int(0)
+        err = ctypes.create_string_buffer(512)
+        self.h = lib().emu_new(logformat.encode(), arr, len(fields), ctypes.byref(st), err, 512)
+        self.status = st.value
+        self.err = err.value.decode()
+        if not self.h:
+            raise RuntimeError("emu compile failed %d: %s" % (self.status, self.err))
+        self.buf = ctypes.create_string_buffer(1 << 20)
+
+    def parse(self, line):
+        if isinstance(line, str):
+            line = line.encode("utf-8")
+        st = lib().emu_parse(self.h, line, len(line), self.buf, len(self.buf))
+        return st, (json.loads(self.buf.value.decode("utf-8")) if st == 0 else None)
+
+    def parse_raw(self, line):
+        if isinstance(line, str):
+            line = line.encode("utf-8")
+        st = lib().emu_parse(self.h, line, len(line), self.buf, len(self.buf))
+        return st, (self.buf.value.decode("utf-8") if st in (0, 3) else None)
+
+    def describe(self):
+        b = ctypes.create_string_buffer(1 << 16)
+        lib().emu_describe(self.h, b, len(b))
+        return b.value.decode()
+
+    def __del__(self):
+        try:
+            lib().emu_free(self.h)
+        except Exception:
+            pass
+
+
+def possible_paths(logformat, depth=15):
+    b = ctypes.create_string_buffer(1 << 20)
+    lib().emu_possible_paths(logformat.encode(), depth, b, len(b))
+    return [p for p in b.value.decode().split("\n") if p]

@@ -1,0 +1,120 @@
+"""CPU parity of the device per-line logic (lp_device.h compiled for the host
+by the test-only tests/emu build) against the oracle.  The same comparisons
+run on the real GPU path in test_gpu_parity.py."""
+import json
+import random
+
+import pytest
+
+import golden_check
+import logparser_amd as lpa
+
+ALL = None
+
+
+def all_paths(oracle):
+    global ALL
+    if ALL is None:
+        ALL = oracle.possible_paths("combined")
+    return ALL
+
+
+def compare(o, e, lines, allow_fallback=True):
+    stats = {"ok": 0, "bad": 0, "fallback": 0}
+    for l in lines:
+        s1, r1 = o.parse_raw(l)
+        s2, r2 = e.parse_raw(l)
+        assert s2 != 3, r2  # arena overflow would be a sizing bug
+        if s2 == 2:
+            stats["fallback"] += 1
+            assert allow_fallback, l
+            continue
+        if s1 == 2:
+            pytest.fail("device decided a line the oracle cannot restate: %r" % l)
+        assert s1 == s2, (l, s1, s2)
+        if s1 == 0:
+            assert r1 == r2, (l, json.dumps(json.loads(r1), indent=0)[:2000], r2[:2000])
+            stats["ok"] += 1
+        else:
+            stats["bad"] += 1
+    return stats
+
+
+def test_golden_vectors_emulated(oracle, emu, vectors):
+    n_checked = 0
+    for c in vectors["cases"]:
+        e = emu.Emu(c["logformat"], c["fields"])
+        if e.status != 0:  # not on the device: every line FALLBACK
+            assert e.parse(c["line"])[0] == 2
+            continue
+        st, rec = e.parse(c["line"])
+        if st == 2:
+            continue
+        assert golden_check.check_case(c, st, rec or {}) == [], c["source"]
+        n_checked += 1
+    assert n_checked >= 30
+
+
+def test_demolog_emulated(oracle, emu, demolog_lines):
+    o = oracle.Oracle("combined", all_paths(oracle))
+    e = emu.Emu("combined", all_paths(oracle))
+    s = compare(o, e, demolog_lines)
+    assert s["ok"] + s["fallback"] == 3456 and s["fallback"] < 30, s
+
+
+def test_synthetic_config2_emulated(oracle, emu):
+    data = lpa.synth_combined(20261015, 0, 5000)
+    lines = data.split(b"\n")[:-1]
+    o = oracle.Oracle("combined", all_paths(oracle))
+    e = emu.Emu("combined", all_paths(oracle))
+    s = compare(o, e, lines, allow_fallback=False)
+    assert s["ok"] == 5000
+
+
+def mutate(rng, line):
+    ops = [
+        lambda l: l[: rng.randrange(len(l))],                      # truncated
+        lambda l: l.replace(b'"', b"", 1),                          # missing quote
+        lambda l: l.replace(b"/Jan/", b"/Foo/").replace(b"/Feb/", b"/Foo/").replace(b"/Mar/", b"/Foo/"),
+        lambda l: l.replace(b"[0", b"[00", 1)[:-1] if b"[0" in l else l,
+        lambda l: l.replace(b" 200 ", b" 200 x", 1),
+        lambda l: l + b" extra",
+        lambda l: l.replace(b"GET /", b"GET /a b/", 1),             # space in URI
+        lambda l: l.replace(b"?", b"?x=%zz&", 1),                   # bad escape
+        lambda l: l.replace(b"/", b"/#frag", 1),
+        lambda l: l.replace(b"HTTP/1.1", b"HTTP/1", 1),
+        lambda l: l.replace(b"http://", b"http://user@", 1),
+        lambda l: l.replace(b"https://", b"ht tps://", 1),
+        lambda l: l.replace(b"=", b"=%u0041", 1),
+        lambda l: l.replace(b" - - ", b" 12 - ", 1),
+        lambda l: l.replace(b"+0", b"-1", 1),
+        lambda l: l.replace(b"&", b"&amp;", 1),
+        lambda l: l.replace(b"1", b"\t", 1),
+        lambda l: l.replace(b"a", b"\xc3\xa9", 1),
+    ]
+    return rng.choice(ops)(line)
+
+
+def test_mutated_lines_emulated(oracle, emu):
+    rng = random.Random(1234)
+    base = lpa.synth_combined(99, 0, 600).split(b"\n")[:-1]
+    lines = [mutate(rng, l) for l in base]
+    o = oracle.Oracle("combined", all_paths(oracle))
+    e = emu.Emu("combined", all_paths(oracle))
+    s = compare(o, e, lines)
+    assert s["bad"] > 50 and s["ok"] > 50, s
+
+
+@pytest.mark.parametrize("fmt", ["common", "combinedio", "%h %l %u %t \"%r\" %>s %b", "%a %A %{Host}i %u %t %r"])
+def test_other_formats_emulated(oracle, emu, fmt):
+    paths = oracle.possible_paths(fmt)
+    o = oracle.Oracle(fmt, paths)
+    e = emu.Emu(fmt, paths)
+    if e.status != 0:
+        pytest.skip("not on device: " + e.err)
+    rng = random.Random(5)
+    lines = []
+    for l in lpa.synth_combined(3, 0, 300).split(b"\n")[:-1]:
+        lines.append(l)
+        lines.append(mutate(rng, l))
+    compare(o, e, lines)

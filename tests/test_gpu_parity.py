@@ -1,0 +1,159 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle on the same
+inputs -- reference golden vectors, the reference demo log, synthetic
+config-2 lines, mutated/malformed lines, edge cases -- plus size-independent
+properties at a large batch size."""
+import json
+import random
+
+import numpy as np
+import pytest
+
+import golden_check
+import logparser_amd as lpa
+
+pytestmark = pytest.mark.gpu
+
+_PATHS = {}
+
+
+def paths(oracle, fmt="combined"):
+    if fmt not in _PATHS:
+        _PATHS[fmt] = oracle.possible_paths(fmt)
+    return _PATHS[fmt]
+
+
+def gpu_vs_oracle(oracle, fmt, fields, lines, allow_fallback=True):
+    p = lpa.HttpdLoglineParser(fmt, fields)
+    data = b"".join(l + b"\n" for l in lines)
+    r = p.parse_batch(data)
+    assert r.n_lines == len(lines)
+    o = oracle.Oracle(fmt, fields)
+    stats = {"ok": 0, "bad": 0, "fallback": 0}
+    for i, l in enumerate(lines):
+        s2 = int(r.status[i])
+        s1, r1 = o.parse_raw(l)
+        if s2 == lpa.LINE_FALLBACK:
+            stats["fallback"] += 1
+            assert allow_fallback, l
+            continue
+        assert s1 != oracle.UNSUPPORTED, l
+        assert s1 == s2, (i, l, s1, s2)
+        if s1 == oracle.OK:
+            r2 = r.record_json(i)
+            assert r1 == r2, (l, r1[:1500], r2[:1500])
+            stats["ok"] += 1
+        else:
+            stats["bad"] += 1
+    c = r.counters
+    assert c["lines"] == len(lines)
+    assert c["ok"] == stats["ok"] and c["bad"] == stats["bad"] and c["fallback"] == stats["fallback"]
+    return stats, r
+
+
+def test_golden_vectors_gpu(oracle, vectors):
+    groups = {}
+    for c in vectors["cases"]:
+        groups.setdefault((c["logformat"], tuple(c["fields"])), []).append(c)
+    checked = 0
+    for (fmt, fields), cases in groups.items():
+        p = lpa.HttpdLoglineParser(fmt, list(fields))
+        data = b"".join(c["line"].encode() + b"\n" for c in cases)
+        r = p.parse_batch(data)
+        assert r.n_lines == len(cases)
+        for i, c in enumerate(cases):
+            st = int(r.status[i])
+            if st == lpa.LINE_FALLBACK:
+                continue
+            rec = r.record(i) if st == lpa.LINE_OK else {}
+            assert golden_check.check_case(c, st, rec) == [], c["source"]
+            checked += 1
+    assert checked >= 30
+
+
+def test_demolog_gpu(oracle, demolog_lines):
+    s, _ = gpu_vs_oracle(oracle, "combined", paths(oracle), demolog_lines)
+    assert s["ok"] + s["fallback"] == 3456 and s["fallback"] < 30, s
+
+
+def test_synthetic_gpu(oracle):
+    lines = lpa.synth_combined(20261015, 0, 20000).split(b"\n")[:-1]
+    s, _ = gpu_vs_oracle(oracle, "combined", paths(oracle), lines, allow_fallback=False)
+    assert s["ok"] == 20000
+
+
+def test_mutated_gpu(oracle):
+    from test_emu_parity import mutate
+    rng = random.Random(77)
+    lines = [mutate(rng, l) for l in lpa.synth_combined(5, 0, 3000).split(b"\n")[:-1]]
+    s, _ = gpu_vs_oracle(oracle, "combined", paths(oracle), lines)
+    assert s["bad"] > 200 and s["ok"] > 200, s
+
+
+def test_edge_cases_gpu(oracle):
+    lines = [
+        b"",                                       # empty line
+        b"-",
+        b'1.2.3.4 - - [29/Feb/2016:23:59:59 +1800] "GET / HTTP/1.1" 200 - "-" "-"',
+        b'1.2.3.4 - - [29/Feb/2015:23:59:59 -1800] "GET / HTTP/1.1" 200 0 "-" "-"',   # clamp to 28 Feb
+        b'1.2.3.4 - - [31/Dec/2012:24:00:00 +0000] "GET / HTTP/1.1" 200 0 "-" "-"',   # end of day
+        b'1.2.3.4 - - [31/Dec/2012:24:00:01 +0000] "GET / HTTP/1.1" 200 0 "-" "-"',
+        b'1.2.3.4 - - [31/Dec/2012:23:00:00 +1801] "GET / HTTP/1.1" 200 0 "-" "-"',
+        b'1.2.3.4 - - [31/Dec/2012:23:00:00 |0100] "GET / HTTP/1.1" 200 0 "-" "-"',
+        b'1.2.3.4 - - [01/Jan/2021:00:00:00 +0000] "GET  HTTP/1.1" 200 0 "-" "-"',
+        b'1.2.3.4 - - [01/Jan/2021:00:00:00 +0000] "GET HTTP/1.1" 200 0 "-" "-"',
+        b'1.2.3.4 - - [01/Jan/2021:00:00:00 +0000] "" 200 0 "" ""',
+        b'1.2.3.4 - - [01/Jan/2021:00:00:00 +0000] "GET /x" y" 200 0 "a" "b" "c"',
+        b'1.2.3.4 - - [01/Jan/2021:00:00:00 +0000] "GET /?a=1&B=%41%C3%A9+x&=v&c HTTP/1.1" 200 0 "http://h:99/p?q=1#f" "u"',
+        b'1.2.3.4 - - [01/Jan/2021:00:00:00 +0000] "GET /%C3%A9 HTTP/1.1" 200 0 "http://under_score.example.com/" "u"',
+        b'1.2.3.4 - - [01/Jan/2021:00:00:00 +0000] "GET / HTTP/1.1" 200 0 "http://1.2.3.4.5/" "u"',
+        b'1.2.3.4 - - [01/Jan/2021:00:00:00 +0000] "GET / HTTP/1.1" 200 0 "http://h:99999999999/" "u"',
+        b'1.2.3.4 - - [01/Jan/2021:00:00:00 +0000] "GET / HTTP/1.1" 200 0 "foo bar:baz" "u"',
+        b'1.2.3.4 - - [01/Jan/2021:00:00:00 +0000] "GET / HTTP/1.1" 200 0 "relative/path?x" "u"',
+        b'1.2.3.4 - - [01/Jan/2021:00:00:00 +0000] "GET / HTTP/1.1" 200 0 "http:/abs?x" "u"',
+        b'1.2.3.4 - - [01/Jan/2021:00:00:00 +0000] "GET / HTTP/1.1" 200 0 "-" "u" trailing',
+        b"x" * 9000,                               # longer than the device window
+    ]
+    gpu_vs_oracle(oracle, "combined", paths(oracle), lines)
+
+
+def test_no_trailing_newline_and_batches(oracle):
+    p = lpa.HttpdLoglineParser("combined", ["IP:connection.client.host", "TIME.EPOCH:request.receive.time.epoch"])
+    lines = lpa.synth_combined(11, 0, 1000).split(b"\n")[:-1]
+    r1 = p.parse_batch(b"\n".join(lines))          # last line unterminated
+    assert r1.n_lines == 1000 and r1.counters["ok"] == 1000
+    last = r1.record(999)
+    r2 = p.parse_batch(lines[-1] + b"\n")
+    assert r2.n_lines == 1 and r2.record(0) == last
+    r3 = p.parse_batch(b"")
+    assert r3.n_lines == 0
+
+
+def test_device_tensor_input(oracle):
+    import torch
+    lines = lpa.synth_combined(12, 0, 2000)
+    t = torch.from_numpy(np.frombuffer(lines, dtype=np.uint8).copy()).cuda()
+    p = lpa.HttpdLoglineParser("combined", paths(oracle))
+    a = p.parse_batch(t)
+    recs = [a.record_json(i) for i in range(0, 2000, 97)]
+    b = p.parse_batch(lines)
+    assert [b.record_json(i) for i in range(0, 2000, 97)] == recs
+
+
+def test_large_batch_properties(oracle):
+    """2M synthetic lines: every line OK (no FALLBACK on config-2 data), the
+    line index matches the newline count, and a deterministic sample of
+    lines matches the oracle exactly."""
+    n = 2_000_000
+    data = lpa.synth_combined(20261015, 0, n)
+    p = lpa.HttpdLoglineParser("combined", paths(oracle))
+    r = p.parse_batch(data)
+    assert r.n_lines == n == data.count(b"\n")
+    assert r.counters == {"lines": n, "ok": n, "bad": 0, "fallback": 0}
+    o = oracle.Oracle("combined", paths(oracle))
+    rng = random.Random(3)
+    for i in sorted(rng.sample(range(n), 300)):
+        a = r.line_offset(i)
+        b = r.line_offset(i + 1) - 1
+        line = data[a:b]
+        s1, js = o.parse_raw(line)
+        assert s1 == 0 and js == r.record_json(i), i
