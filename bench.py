@@ -91,6 +91,19 @@ def cpu_baseline(lpa, fields, sample_lines, threads):
     }
 
 
+def pmc_traffic(path, n_lines, lib_path):
+    """HBM bytes per k_parse_lines launch measured by PMC counters, or None."""
+    try:
+        import hashlib
+        d = json.load(open(path))
+        sha = hashlib.sha256(open(lib_path, "rb").read()).hexdigest()
+        if d.get("lines") != n_lines or d.get("lib_sha256") != sha:
+            return None
+        return d["kernels"]["k_parse_lines"]["hbm_bytes"]
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -100,8 +113,9 @@ def main():
     ap.add_argument("--cpu-sample-lines", type=int, default=2_000_000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pmc-bytes", type=float, default=None,
-                    help="HBM bytes per parse launch from a separate rocprofv3 --pmc pass (fills roofline.traffic)")
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic_latest.json"),
+                    help="tools/pmc_traffic.py summary of separate rocprofv3 --pmc passes; fills roofline.traffic "
+                         "when it was taken on this workload with this exact engine build")
     args = ap.parse_args()
 
     import torch
@@ -191,7 +205,7 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": args.pmc_bytes,
+            "traffic": pmc_traffic(args.pmc_json, stats["lines"], lpa.LIB_PATH),
             "kernel": "k_parse_lines",
             "algorithmic_bytes_per_launch": int(algo_bytes),
             "bytes_per_line": round(algo_bytes / max(1, stats["lines"]), 1),

@@ -60,6 +60,14 @@ def lib():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise EngineUnavailable("logparser_amd: %s not built (run __graft_entry__.build())" % LIB_PATH)
+    # One HIP runtime per process: torch ships its own libamdhip64.so.7.  If it
+    # is loaded first, the engine binds to it (same SONAME) and device pointers
+    # and streams are shared; loaded the other way round, two runtimes fight
+    # over the device and torch sees no GPU.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     c_char_pp = ctypes.POINTER(ctypes.c_char_p)
     L.lp_compile.restype = ctypes.c_void_p
