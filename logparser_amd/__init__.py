@@ -24,7 +24,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "_lib", "liblogparser_amd.so")
+LIB_PATH = os.environ.get("LOGPARSER_AMD_LIB") or os.path.join(_HERE, "_lib", "liblogparser_amd.so")
 
 LP_OK, LP_E_INVALID, LP_E_MISSING, LP_E_UNSUPPORTED, LP_E_DEVICE, LP_E_NOMEM, LP_E_STATE = 0, -1, -2, -3, -4, -5, -6
 LINE_OK, LINE_BAD, LINE_FALLBACK = 0, 1, 2

@@ -42,7 +42,8 @@ struct lp_handle {
     int compile_status = LP_OK;
     int device = 0;
     hipStream_t stream = nullptr;
-    DevBuf input, chunk, line_off, cols, arena, misc;
+    DevBuf input, chunk, line_off, cols, arena, misc, waves, args;
+    lp::DeviceArgs host_args{};
     lp::Columns C{};
     int64_t n_lines = 0;
     uint64_t nbytes = 0;
@@ -52,7 +53,8 @@ struct lp_handle {
     bool pending = false;
     uint64_t row_bytes = 0;
     uint64_t counters[4]{};
-    uint64_t arena_used = 0;
+    uint64_t arena_used = 0;     // arena bytes allocated (bump pointer)
+    uint64_t arena_written = 0;  // arena bytes actually written
     float ms[3]{};
     bool host_valid = false;
     lp::HostResults host;
@@ -94,7 +96,6 @@ bool alloc_columns(lp_handle* h, int64_t n) {
         cols.push_back({(void**)&C.u_path[u], 8});
         cols.push_back({(void**)&C.u_query[u], 8});
         cols.push_back({(void**)&C.u_frag[u], 8});
-        cols.push_back({(void**)&C.u_userinfo[u], 8});
     }
     for (int q = 0; q < P.n_query; ++q) {
         cols.push_back({(void**)&C.q_count[q], 4});
@@ -152,7 +153,7 @@ bool fetch_host(lp_handle* h) {
         fetch(R.fl_uri[f], h->C.fl_uri[f], n);
         fetch(R.fl_proto[f], h->C.fl_proto[f], n);
     }
-    for (auto* v : {&R.u_scheme, &R.u_host, &R.u_path, &R.u_query, &R.u_frag, &R.u_userinfo}) v->resize(lp::MAX_URI);
+    for (auto* v : {&R.u_scheme, &R.u_host, &R.u_path, &R.u_query, &R.u_frag}) v->resize(lp::MAX_URI);
     R.u_flags.resize(lp::MAX_URI); R.u_port.resize(lp::MAX_URI);
     for (int u = 0; u < P.n_uri; ++u) {
         fetch(R.u_flags[u], h->C.u_flags[u], n);
@@ -162,7 +163,6 @@ bool fetch_host(lp_handle* h) {
         fetch(R.u_path[u], h->C.u_path[u], n);
         fetch(R.u_query[u], h->C.u_query[u], n);
         fetch(R.u_frag[u], h->C.u_frag[u], n);
-        fetch(R.u_userinfo[u], h->C.u_userinfo[u], n);
     }
     R.q_count.resize(lp::MAX_QUERY); R.q_params.resize(lp::MAX_QUERY);
     for (int q = 0; q < P.n_query; ++q) {
@@ -216,7 +216,7 @@ void lp_free(lp_handle* h) {
     if (!h) return;
     hipSetDevice(h->device);
     if (h->pending) hipStreamSynchronize(h->stream);
-    for (auto* b : {&h->input, &h->chunk, &h->line_off, &h->cols, &h->arena, &h->misc}) b->release();
+    for (auto* b : {&h->input, &h->chunk, &h->line_off, &h->cols, &h->arena, &h->misc, &h->waves, &h->args}) b->release();
     if (h->have_events)
         for (auto& ev : h->ev) hipEventDestroy(ev);
     delete h;
@@ -280,13 +280,20 @@ int lp_parse_batch(lp_handle* h, const uint8_t* buf, uint64_t nbytes, int buf_fl
     C.line_off = d_off;
     C.arena = h->arena.as<uint8_t>();
     C.arena_cap = h->arena.cap;
-    C.counters = h->misc.as<unsigned long long>();
+    if (!h->waves.ensure(4 * lp::WC_WORDS * (size_t)(lp::parse_waves(n) + 1))) return LP_E_NOMEM;
+    C.wave_counts = h->waves.as<uint32_t>();
     C.arena_top = h->misc.as<unsigned long long>(64);
     hipMemsetAsync(h->misc.p, 0, 128, s);
     if (h->plan.device_ok()) {
-        if (lp::set_program(P, s) != 0) return LP_E_DEVICE;
+        if (!h->args.ensure(sizeof(lp::DeviceArgs))) return LP_E_NOMEM;
+        h->host_args.prog = P;
+        h->host_args.cols = C;
+        if (hipMemcpyAsync(h->args.p, &h->host_args, sizeof(lp::DeviceArgs), hipMemcpyHostToDevice, s) != hipSuccess)
+            return LP_E_DEVICE;
         hipEventRecord(h->ev[2], s);
-        if (lp::launch_parse(h->d_buf, n, C, s) != 0) return LP_E_DEVICE;
+        if (lp::launch_parse(h->d_buf, nbytes, n, h->args.as<lp::DeviceArgs>(), C.wave_counts,
+                             h->misc.as<unsigned long long>(), s) != 0)
+            return LP_E_DEVICE;
     } else {
         // the requested paths need a dissector that is not on the device:
         // every line goes back to the reference (FALLBACK)
@@ -314,6 +321,7 @@ int lp_sync(lp_handle* h) {
         h->counters[3] = (uint64_t)h->n_lines;
     }
     h->arena_used = m[8];
+    h->arena_written = h->plan.device_ok() ? m[4] : 0;
     float a = 0, b = 0, c = 0;
     hipEventElapsedTime(&a, h->ev[0], h->ev[3]);
     hipEventElapsedTime(&b, h->ev[0], h->ev[1]);
@@ -343,6 +351,12 @@ int64_t lp_line_record_json(lp_handle* h, int64_t i, char* out, size_t cap) {
     if (!h || i < 0 || i >= h->n_lines) return LP_E_INVALID;
     if (!fetch_host(h)) return LP_E_DEVICE;
     if (h->host.status[(size_t)i] != LP_LINE_OK) return LP_E_STATE;
+#ifdef LP_DEBUG_HOST
+    for (int u = 0; u < h->plan.program().n_uri; ++u)
+        fprintf(stderr, "host i=%lld u=%d flags=%x query=%llx path=%llx line_off=%llu\n", (long long)i, u,
+                h->host.u_flags[u][i], (unsigned long long)h->host.u_query[u][i], (unsigned long long)h->host.u_path[u][i],
+                (unsigned long long)h->host.line_off[i]);
+#endif
     std::string js = h->plan.record_json(h->host, i);
     if (!out || js.size() + 1 > cap) return -100 - (int64_t)(js.size() + 1);
     memcpy(out, js.c_str(), js.size() + 1);
@@ -366,7 +380,7 @@ int lp_last_timing(lp_handle* h, float* out, int n) {
 int lp_last_bytes(lp_handle* h, uint64_t* out, int n) {
     if (!h || !out) return LP_E_INVALID;
     if (h->pending) lp_sync(h);
-    uint64_t v[2] = {h->nbytes, (uint64_t)h->n_lines * (h->row_bytes + 8) + h->arena_used};
+    uint64_t v[2] = {h->nbytes, (uint64_t)h->n_lines * (h->row_bytes + 8) + h->arena_written};
     for (int k = 0; k < n && k < 2; ++k) out[k] = v[k];
     return n < 2 ? n : 2;
 }

@@ -6,13 +6,24 @@
 
 namespace lp {
 
-int set_program(const Program& p, hipStream_t s);
+// Everything the parse kernel reads besides the input: copied to the device
+// per batch (stream-ordered), so concurrent handles never share state.
+struct DeviceArgs {
+    Program prog;
+    Columns cols;
+};
+
 int64_t count_chunks(uint64_t nbytes);
 // index pass 1: per-chunk '\n' counts, exclusively scanned in place;
 // d_chunk needs count_chunks()+1 entries, d_chunk[nc] = total '\n' count
 int launch_count(const uint8_t* d_buf, uint64_t nbytes, uint64_t* d_chunk, hipStream_t s);
 // index pass 2: d_line_off[k] = start of line k for k >= 1 (caller sets [0])
 int launch_offsets(const uint8_t* d_buf, uint64_t nbytes, const uint64_t* d_chunk, uint64_t* d_line_off, hipStream_t s);
-int launch_parse(const uint8_t* d_buf, int64_t n_lines, const Columns& C, hipStream_t s);
+// parse kernels: number of waves (C.wave_counts needs WC_WORDS u32 per wave)
+constexpr int WC_WORDS = 8;
+int64_t parse_waves(int64_t n_lines);
+// parse every line, then counters[0..4] += lines, ok, bad, fallback, arena bytes written
+int launch_parse(const uint8_t* d_buf, uint64_t nbytes, int64_t n_lines, const DeviceArgs* d_args,
+                 const uint32_t* d_wave_counts, unsigned long long* counters, hipStream_t s);
 
 }  // namespace lp

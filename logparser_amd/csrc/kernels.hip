@@ -3,9 +3,11 @@
 //   k_count_newlines  per-chunk '\n' count (16-byte loads, SWAR byte compare)
 //   k_scan_counts     exclusive scan of the chunk counts (single workgroup)
 //   k_line_offsets    line start offsets (Hadoop LineRecordReader '\n' semantics)
-//   k_parse_lines     one thread per line: LogFormat match + token / time /
-//                     first-line stages (phase 1), wave-aggregated arena
-//                     allocation, URI + query-string stages (phase 2)
+//   k_parse_lines     one wave per 64 lines, one lane per line: the lines'
+//                     byte window staged in LDS, LogFormat match + token /
+//                     time / first-line stages (phase 1), wave-aggregated
+//                     arena allocation, URI + query-string stages (phase 2)
+//   k_reduce_counts   per-wave status counts -> the batch counters
 //
 // The per-line logic is lp_device.h; this file only adds the data-parallel
 // scaffolding around it.
@@ -15,8 +17,6 @@
 #include "lp_device.h"
 
 namespace lp {
-
-__constant__ Program c_prog;
 
 namespace {
 
@@ -113,67 +113,145 @@ __global__ __launch_bounds__(NL_THREADS) void k_line_offsets(const uint8_t* __re
     }
 }
 
-// per-thread DFS stack interleaved in LDS (conflict-free: lane-contiguous)
-struct LdsStack {
+// ---------------------------------------------------------------- parse
+// One workgroup = one wave = 64 consecutive lines.  The wave copies the byte
+// window holding its lines into LDS with coalesced 16-byte loads, then every
+// lane runs the per-line stages of lp_device.h on its own line out of LDS.
+// Windows larger than the LDS budget (very long lines) read HBM directly.
+constexpr int PW = 64;
+constexpr int STK_WORDS = MAX_STACK * PW;
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+struct WaveStack {  // per-lane DFS stack, lane-interleaved (conflict-free)
     uint32_t* base;
-    __device__ uint32_t& operator[](int k) const { return base[k * 256]; }
+    __device__ uint32_t& operator[](int k) const { return base[k * PW]; }
 };
 
-__global__ __launch_bounds__(256) void k_parse_lines(const uint8_t* __restrict__ buf, int64_t n_lines, Columns C) {
-    __shared__ uint32_t stk[MAX_STACK * 256];
-    __shared__ unsigned long long cnt[4];
-    if (threadIdx.x < 4) cnt[threadIdx.x] = 0;
-    __syncthreads();
-    const int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool active = li < n_lines;
-    const Program& P = c_prog;
+template <typename Ptr>
+__device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, const Columns& C, Ptr base, uint32_t off,
+                                           int n, bool active, int64_t li, WaveStack stk) {
+    LineT<Ptr> L{base, off, n};
     LineOut o;
     o.status = ST_OK;
     o.arena_need = 0;
-    Line L{buf, 0};
-    if (active) {
-        const uint64_t s = C.line_off[li], e = C.line_off[li + 1] - 1;  // exclude '\n'
-        L.s = buf + s;
-        L.n = (int)((e - s) > (uint64_t)0x7FFFFFFF ? 0x7FFFFFFF : (e - s));
-        phase1(P, L, o, LdsStack{stk + threadIdx.x}, C, li);
-    }
+    if (active) phase1(P, elems, L, o, stk, C, li);
     // wave-aggregated arena allocation (every lane reaches this point)
-    uint32_t need = (active && o.status == ST_OK) ? o.arena_need : 0u;
-    const int lane = threadIdx.x & 63;
+    const uint32_t need = (active && o.status == ST_OK) ? o.arena_need : 0u;
+    const int lane = threadIdx.x;
     uint32_t x = need;
     for (int d = 1; d < 64; d <<= 1) {
         uint32_t y = __shfl_up(x, d);
         if (lane >= d) x += y;
     }
-    uint32_t total = __shfl(x, 63);
+    const uint32_t total = __shfl(x, 63);
     unsigned long long wbase = 0;
     if (lane == 63 && total) wbase = atomicAdd(C.arena_top, (unsigned long long)total);
     wbase = __shfl(wbase, 63);
+    uint32_t written = 0;
     if (active) {
         if (o.status == ST_OK && need) {
-            unsigned long long mine = wbase + x - need;
+            const unsigned long long mine = wbase + x - need;
             if (mine + need > C.arena_cap) o.status = ST_FALLBACK;
             else {
                 C.arena_base[li] = mine;
                 Arena A{C.arena + mine, 0, need};
                 phase2(P, L, o, A, C, li);
+                written = A.used;
             }
         } else if (o.status == ST_OK) {
             C.arena_base[li] = 0;
         }
         write_line(P, o, C, li);
-        atomicAdd(&cnt[0], 1ull);
-        atomicAdd(&cnt[1 + o.status], 1ull);
+    }
+    for (int d = 32; d > 0; d >>= 1) written += __shfl_xor(written, d);
+    const uint64_t m_act = __ballot(active);
+    const uint64_t m_ok = __ballot(active && o.status == ST_OK);
+    const uint64_t m_bad = __ballot(active && o.status == ST_BAD);
+    if (lane == 0) {
+        uint4 c, d;
+        c.x = (uint32_t)__popcll(m_act);
+        c.y = (uint32_t)__popcll(m_ok);
+        c.z = (uint32_t)__popcll(m_bad);
+        c.w = c.x - c.y - c.z;
+        d.x = written;
+        d.y = d.z = d.w = 0;
+        uint4* wc = reinterpret_cast<uint4*>(C.wave_counts + WC_WORDS * (size_t)blockIdx.x);
+        wc[0] = c;
+        wc[1] = d;
+    }
+}
+
+__global__ __launch_bounds__(PW) void k_parse_lines(const uint8_t* __restrict__ buf, uint64_t nbytes, int64_t n_lines,
+                                                    const DeviceArgs* __restrict__ args, uint32_t win_cap, int stage) {
+    const Program& P = args->prog;
+    const Columns& C = args->cols;
+    __shared__ Elem s_elems[MAX_ELEMS];
+    if ((int)threadIdx.x < P.n_elems) s_elems[threadIdx.x] = P.elems[threadIdx.x];
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    WaveStack stk{reinterpret_cast<uint32_t*>(smem) + threadIdx.x};
+    uint8_t* win = smem + STK_WORDS * 4;
+    const int lane = threadIdx.x;
+    const int64_t li0 = (int64_t)blockIdx.x * PW;
+    const int64_t li = li0 + lane;
+    const bool active = li < n_lines;
+    const int64_t lend = li0 + PW < n_lines ? li0 + PW : n_lines;
+    uint64_t s = 0, e = 0;
+    if (active) {
+        s = C.line_off[li];
+        e = C.line_off[li + 1] - 1;  // exclude '\n' (or the end sentinel)
+    }
+    const int n = (int)((e - s) > (uint64_t)0x7FFFFFFF ? 0x7FFFFFFF : (e - s));
+    const uint64_t w0 = C.line_off[li0] & ~15ull;
+    uint64_t w1 = C.line_off[lend];
+    if (w1 > nbytes) w1 = nbytes;
+    if (stage && w1 - w0 <= win_cap) {
+        const int nv = (int)((w1 - w0 + 15) >> 4);
+        for (int k = lane; k < nv; k += PW) {
+            const uint64_t p = w0 + 16ull * k;
+            u32x4 v;
+            if (p + 16 <= nbytes) {
+                v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(buf + p));
+            } else {
+                v = u32x4{0, 0, 0, 0};
+                for (int j = 0; j < 16 && p + j < nbytes; ++j) v[j >> 2] |= (uint32_t)buf[p + j] << (8 * (j & 3));
+            }
+            *reinterpret_cast<u32x4*>(win + 16 * k) = v;
+        }
+        __syncthreads();
+        parse_wave(P, s_elems, C, (lds_bytes)win, (uint32_t)(s - w0), n, active, li, stk);
+    } else {
+        __syncthreads();
+        // aligned-down base: word reads never cross the 4-byte word of a valid byte
+        const uintptr_t mis = (uintptr_t)buf & 3;
+        parse_wave(P, s_elems, C, buf - mis, (uint32_t)(s + mis), n, active, li, stk);
+    }
+}
+
+// counters[0..4] += sum of the per-wave counts (lines ok bad fallback arena-bytes)
+__global__ __launch_bounds__(256) void k_reduce_counts(const uint32_t* __restrict__ wc, int64_t n_waves,
+                                                       unsigned long long* __restrict__ counters) {
+    unsigned long long a[5] = {0, 0, 0, 0, 0};
+    for (int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x; w < n_waves; w += (int64_t)gridDim.x * 256) {
+        const uint4 c = reinterpret_cast<const uint4*>(wc + WC_WORDS * w)[0];
+        const uint4 d = reinterpret_cast<const uint4*>(wc + WC_WORDS * w)[1];
+        a[0] += c.x; a[1] += c.y; a[2] += c.z; a[3] += c.w; a[4] += d.x;
+    }
+    __shared__ unsigned long long red[5][4];
+    for (int k = 0; k < 5; ++k) {
+        unsigned long long v = a[k];
+        for (int d = 32; d > 0; d >>= 1) v += __shfl_down(v, d);
+        if ((threadIdx.x & 63) == 0) red[k][threadIdx.x >> 6] = v;
     }
     __syncthreads();
-    if (threadIdx.x < 4 && cnt[threadIdx.x]) atomicAdd(&C.counters[threadIdx.x], cnt[threadIdx.x]);
+    if (threadIdx.x < 5) {
+        unsigned long long v = red[threadIdx.x][0] + red[threadIdx.x][1] + red[threadIdx.x][2] + red[threadIdx.x][3];
+        if (v) atomicAdd(&counters[threadIdx.x], v);
+    }
 }
 
 }  // namespace
 
-int set_program(const Program& p, hipStream_t s) {
-    return hipMemcpyToSymbolAsync(HIP_SYMBOL(c_prog), &p, sizeof(Program), 0, hipMemcpyHostToDevice, s) == hipSuccess ? 0 : -1;
-}
 
 int64_t count_chunks(uint64_t nbytes) { return (int64_t)((nbytes + CHUNK - 1) / CHUNK); }
 
@@ -192,10 +270,26 @@ int launch_offsets(const uint8_t* d_buf, uint64_t nbytes, const uint64_t* d_chun
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_parse(const uint8_t* d_buf, int64_t n_lines, const Columns& C, hipStream_t s) {
+int64_t parse_waves(int64_t n_lines) { return (n_lines + PW - 1) / PW; }
+
+int launch_parse(const uint8_t* d_buf, uint64_t nbytes, int64_t n_lines, const DeviceArgs* d_args,
+                 const uint32_t* d_wave_counts, unsigned long long* counters, hipStream_t s) {
     if (n_lines == 0) return 0;
-    unsigned blocks = (unsigned)((n_lines + 255) / 256);
-    hipLaunchKernelGGL(k_parse_lines, dim3(blocks), dim3(256), 0, s, d_buf, n_lines, C);
+    const int64_t waves = parse_waves(n_lines);
+    // LDS window per wave: ~1.3x the mean bytes of 64 lines (+1 KiB), so
+    // nearly every wave stages; at most 60 KiB.  A window that does not fit
+    // reads HBM directly.
+    const uint64_t mean = (nbytes + n_lines - 1) / n_lines;
+    uint64_t cap = (PW * mean * 13) / 10 + 1024;
+    if (cap > 60 * 1024) cap = 60 * 1024;
+    cap = (cap + 15) & ~15ull;
+    const int stage = ((uintptr_t)d_buf & 15) == 0;
+    const size_t lds = STK_WORDS * 4 + cap;
+    hipLaunchKernelGGL(k_parse_lines, dim3((unsigned)waves), dim3(PW), lds, s, d_buf, nbytes, n_lines, d_args,
+                       (uint32_t)cap, stage);
+    int64_t rb = (waves + 255) / 256;
+    if (rb > 1024) rb = 1024;
+    hipLaunchKernelGGL(k_reduce_counts, dim3((unsigned)rb), dim3(256), 0, s, d_wave_counts, waves, counters);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

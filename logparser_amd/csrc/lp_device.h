@@ -10,6 +10,8 @@
 // Any input the device cannot prove it handles exactly returns FALLBACK
 // (status 2): the caller hands that line to the reference Java dissector.
 #pragma once
+#include <utility>
+
 #include "lp_program.h"
 
 namespace lp {
@@ -17,16 +19,16 @@ namespace lp {
 enum : int { ST_OK = 0, ST_BAD = 1, ST_FALLBACK = 2 };
 
 // ----------------------------------------------------------- byte classes
-__host__ __device__ inline bool is_ws(uint32_t c) { return c == ' ' || (c >= 9 && c <= 13); }      // \s
-__host__ __device__ inline bool is_digit(uint32_t c) { return c - '0' < 10u; }
-__host__ __device__ inline bool is_hex(uint32_t c) { return is_digit(c) || ((c | 32u) - 'a') < 6u; }
-__host__ __device__ inline bool is_alpha(uint32_t c) { return ((c | 32u) - 'a') < 26u; }
-__host__ __device__ inline bool is_alnum(uint32_t c) { return is_alpha(c) || is_digit(c); }
-__host__ __device__ inline uint32_t hexv(uint32_t c) { return c <= '9' ? c - '0' : (c | 32u) - 'a' + 10; }
+__host__ __device__ LP_INLINE bool is_ws(uint32_t c) { return c == ' ' || (c >= 9 && c <= 13); }      // \s
+__host__ __device__ LP_INLINE bool is_digit(uint32_t c) { return c - '0' < 10u; }
+__host__ __device__ LP_INLINE bool is_hex(uint32_t c) { return is_digit(c) || ((c | 32u) - 'a') < 6u; }
+__host__ __device__ LP_INLINE bool is_alpha(uint32_t c) { return ((c | 32u) - 'a') < 26u; }
+__host__ __device__ LP_INLINE bool is_alnum(uint32_t c) { return is_alpha(c) || is_digit(c); }
+__host__ __device__ LP_INLINE uint32_t hexv(uint32_t c) { return c <= '9' ? c - '0' : (c | 32u) - 'a' + 10; }
 // chars commons-httpclient URIUtil.encode escapes with the HttpUriDissector
 // "badUriChars" set (HttpUriDissector.java:111-120): control, space, unwise
 // {}|\^[]` and <>"  (ASCII only; non-ASCII lines never reach this point)
-__host__ __device__ inline bool uri_needs_encode(uint32_t c) {
+__host__ __device__ LP_INLINE bool uri_needs_encode(uint32_t c) {
     if (c <= 0x20 || c == 0x7F) return true;
     switch (c) {
     case '{': case '}': case '|': case '\\': case '^': case '[': case ']': case '`': case '<': case '>': case '"':
@@ -36,26 +38,176 @@ __host__ __device__ inline bool uri_needs_encode(uint32_t c) {
 }
 
 // -------------------------------------------------------------- matcher
-struct Line {
-    const uint8_t* s;
+// A line's bytes: b is a 4-byte aligned base (the wave's LDS window in the
+// kernel, or the input buffer), the line starts at byte o of it.  Byte reads
+// and aligned word reads (for the 4-bytes-at-a-time scanners below) go
+// through the same base, so one source serves LDS and HBM.
+// aligned 32-bit loads (global/plain pointer, and LDS in the kernel)
+__host__ __device__ LP_INLINE uint32_t load_word(const uint8_t* p) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return *reinterpret_cast<const uint32_t*>(__builtin_assume_aligned(p, 4));
+#else
+    uint32_t v;
+    __builtin_memcpy(&v, p, 4);
+    return v;
+#endif
+}
+#if defined(__HIP__)
+typedef const __attribute__((address_space(3))) uint8_t* lds_bytes;
+typedef const __attribute__((address_space(3))) uint32_t* lds_words;
+__device__ LP_INLINE uint32_t load_word(lds_bytes p) { return *(lds_words)p; }
+#endif
+
+template <typename Ptr>
+struct LineT {
+    Ptr b;
+    uint32_t o;
     int n;
-    __host__ __device__ uint32_t operator[](int i) const { return s[i]; }
+    __host__ __device__ LP_INLINE uint32_t operator[](int i) const { return b[o + i]; }
+    // aligned 32-bit word w of the base (little-endian: byte k at bits 8k..8k+7)
+    __host__ __device__ LP_INLINE uint32_t word(uint32_t w) const { return load_word(b + 4 * w); }
+};
+using Line = LineT<const uint8_t*>;
+
+// ---- SWAR byte classes on a 32-bit word: bit 8k+7 set when byte k is in
+// the class (exact, no false positives from carries).
+namespace swar {
+constexpr uint32_t ONES = 0x01010101u, HI = 0x80808080u, LO7 = 0x7F7F7F7Fu;
+__host__ __device__ LP_INLINE uint32_t eq(uint32_t w, uint32_t c) {
+    const uint32_t x = w ^ (c * ONES);
+    return ~(((x & LO7) + LO7) | x | LO7);
+}
+// bytes >= n / < n (1 <= n <= 0x80; bytes >= 0x80 count as >= n)
+__host__ __device__ LP_INLINE uint32_t ge(uint32_t w, uint32_t n) { return (((w & LO7) + (0x80u - n) * ONES) | w) & HI; }
+__host__ __device__ LP_INLINE uint32_t lt(uint32_t w, uint32_t n) { return ~ge(w, n) & HI; }
+__host__ __device__ LP_INLINE uint32_t ws(uint32_t w) { return eq(w, ' ') | (ge(w, 9) & lt(w, 14)); }  // \s
+__host__ __device__ LP_INLINE uint32_t digit(uint32_t w) { return ge(w, '0') & lt(w, '9' + 1); }
+__host__ __device__ LP_INLINE uint32_t hex(uint32_t w) {
+    const uint32_t l = w | 0x20202020u;
+    return digit(w) | (ge(l, 'a') & lt(l, 'g') & ~(w & HI));
+}
+__host__ __device__ LP_INLINE uint32_t upper(uint32_t w) { return ge(w, 'A') & lt(w, 'Z' + 1); }
+// not printable ASCII and not TAB: the fast-path guard
+__host__ __device__ LP_INLINE uint32_t guard_bad(uint32_t w) { return (lt(w, 0x20) & ~eq(w, '\t')) | ge(w, 0x7F); }
+// URIUtil "badUriChars" (see uri_needs_encode below), ASCII part
+__host__ __device__ LP_INLINE uint32_t needs_encode(uint32_t w) {
+    return lt(w, 0x21) | ge(w, 0x7F) | (ge(w, '{') & lt(w, '~')) | (ge(w, '[') & lt(w, '_')) | eq(w, '`') |
+           eq(w, '<') | eq(w, '>') | eq(w, '"');
+}
+__host__ __device__ LP_INLINE int first(uint32_t m) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (int)(__builtin_ctz(m) >> 3);
+#else
+    return (int)(__builtin_ctz(m) >> 3);
+#endif
+}
+__host__ __device__ LP_INLINE int last(uint32_t m) { return (int)((31 - __builtin_clz(m)) >> 3); }
+__host__ __device__ LP_INLINE int count(uint32_t m) { return __builtin_popcount(m); }
+}  // namespace swar
+
+// First position in [from, to) whose byte is in class F, else `to`.
+template <typename LN, typename F>
+__host__ __device__ LP_INLINE int find_fwd(const LN& L, int from, int to, F cls) {
+    if (from >= to) return to;
+    const uint32_t A = L.o + (uint32_t)from, E = L.o + (uint32_t)to;
+    uint32_t W = A >> 2;
+    uint32_t m = cls(L.word(W)) & (swar::HI << (8 * (A & 3)));
+    for (;;) {
+        if (m) {
+            const uint32_t p = (W << 2) + (uint32_t)swar::first(m);
+            return p < E ? (int)(p - L.o) : to;
+        }
+        ++W;
+        if ((W << 2) >= E) return to;
+        m = cls(L.word(W));
+    }
+}
+// Last position in [lo, hi] whose byte is in class F, else -1.
+template <typename LN, typename F>
+__host__ __device__ LP_INLINE int find_bwd(const LN& L, int hi, int lo, F cls) {
+    if (hi < lo) return -1;
+    const uint32_t A = L.o + (uint32_t)hi, S = L.o + (uint32_t)lo;
+    uint32_t W = A >> 2;
+    uint32_t m = cls(L.word(W)) & (swar::HI >> (8 * (3 - (A & 3))));
+    for (;;) {
+        if (m) {
+            const uint32_t p = (W << 2) + (uint32_t)swar::last(m);
+            return p >= S ? (int)(p - L.o) : -1;
+        }
+        if ((W << 2) <= S) return -1;
+        --W;
+        m = cls(L.word(W));
+    }
+}
+// Number of bytes in [a, b) in class F.
+template <typename LN, typename F>
+__host__ __device__ LP_INLINE uint32_t count_in(const LN& L, int a, int b, F cls) {
+    if (a >= b) return 0;
+    const uint32_t A = L.o + (uint32_t)a, E = L.o + (uint32_t)b;
+    const uint32_t W0 = A >> 2, W1 = (E - 1) >> 2;
+    uint32_t c = 0;
+    for (uint32_t W = W0; W <= W1; ++W) {
+        uint32_t m = cls(L.word(W));
+        if (W == W0) m &= swar::HI << (8 * (A & 3));
+        if (W == W1) m &= swar::HI >> (8 * (3 - ((E - 1) & 3)));
+        c += (uint32_t)swar::count(m);
+    }
+    return c;
+}
+
+// Small per-line array kept in registers: every element access in the source
+// uses a compile-time index (fold expressions), and a data-dependent index is
+// a compare-and-select chain, so the array is promoted to registers before
+// any pass could turn it into a dynamically indexed scratch-memory array.
+template <int N>
+struct RegArr {
+    uint32_t v[N];
+    template <size_t... J>
+    __host__ __device__ LP_INLINE uint32_t get_(int k, std::index_sequence<J...>) const {
+        uint32_t r = 0;
+        ((r = ((int)J == k) ? v[J] : r), ...);
+        return r;
+    }
+    template <size_t... J>
+    __host__ __device__ LP_INLINE void set_(int k, uint32_t x, std::index_sequence<J...>) {
+        ((v[J] = ((int)J == k) ? x : v[J]), ...);
+    }
+    template <typename F, size_t... J>
+    __host__ __device__ LP_INLINE void each_(F&& f, std::index_sequence<J...>) const {
+        (f((int)J, v[J]), ...);
+    }
+    __host__ __device__ LP_INLINE uint32_t get(int k) const { return get_(k, std::make_index_sequence<N>{}); }
+    __host__ __device__ LP_INLINE void set(int k, uint32_t x) { set_(k, x, std::make_index_sequence<N>{}); }
+    __host__ __device__ LP_INLINE void fill(uint32_t x) { set_all(x, std::make_index_sequence<N>{}); }
+    template <size_t... J>
+    __host__ __device__ LP_INLINE void set_all(uint32_t x, std::index_sequence<J...>) { ((v[J] = x), ...); }
+    // f(index, value) for every element, in index order
+    template <typename F>
+    __host__ __device__ LP_INLINE void each(F&& f) const { each_(f, std::make_index_sequence<N>{}); }
 };
 
-__host__ __device__ inline bool lit_at(const Program& P, const Line& L, int pos, int off, int len) {
+// Literal of element e (its own for EK_LIT, the following one for tokens)
+// at pos.  Literals of up to 4 bytes compare against e.lit4 (no Program
+// memory reads inside the scanners).
+template <typename LN>
+__host__ __device__ LP_INLINE bool lit_at(const Program& P, const LN& L, int pos, const Elem& e) {
+    const int len = e.lit_len;
     if (pos + len > L.n) return false;
+    if (len <= 4) {
+        for (int k = 0; k < len; ++k)
+            if (L[pos + k] != ((e.lit4 >> (8 * k)) & 0xFFu)) return false;
+        return true;
+    }
     for (int k = 0; k < len; ++k)
-        if (L[pos + k] != P.lit[off + k]) return false;
+        if (L[pos + k] != P.lit[e.lit_off + k]) return false;
     return true;
 }
 
-// Java Pattern.Dot: everything except line terminators.  The fast-path guard
-// already rejected \n \r and non-ASCII, so '.' runs to end of line.
-__host__ __device__ inline int dot_end(const Line& L, int p) { return L.n; }
-
-__host__ __device__ inline bool time_us_ok(const Line& L, int p) {
+template <typename LN>
+__host__ __device__ LP_INLINE bool time_us_ok(const LN& L, int p) {
     if (p + 26 > L.n) return false;
-    const uint8_t* c = L.s + p;
+    uint32_t c[26];
+    LP_UNROLL for (int k = 0; k < 26; ++k) c[k] = L[p + k];
     if (!(c[0] >= '0' && c[0] <= '3') || !is_digit(c[1]) || c[2] != '/') return false;
     if (!is_alpha(c[3]) || !is_alpha(c[4]) || !is_alpha(c[5]) || c[6] != '/') return false;
     if (!(c[7] >= '1' && c[7] <= '9') || !is_digit(c[8]) || !is_digit(c[9]) || !is_digit(c[10]) || c[11] != ':') return false;
@@ -67,7 +219,8 @@ __host__ __device__ inline bool time_us_ok(const Line& L, int p) {
 
 // The highest-priority IPv4 alternative of FORMAT_IPV4
 // (TokenParser.java:43-46) when every octet is taken whole: returns end or -1.
-__host__ __device__ inline int ipv4_first(const Line& L, int p) {
+template <typename LN>
+__host__ __device__ LP_INLINE int ipv4_first(const LN& L, int p) {
     int q = p;
     for (int o = 0; o < 4; ++o) {
         int a = q;
@@ -88,40 +241,61 @@ __host__ __device__ inline int ipv4_first(const Line& L, int p) {
     return q;
 }
 
+// Occurrence of e's following literal: the last one starting in [lo, hi]
+// (greedy order) or the first one starting in [lo, hi] (lazy order); -1 none.
+template <typename LN>
+__host__ __device__ LP_INLINE int lit_last(const Program& P, const LN& L, const Elem& e, int hi, int lo) {
+    const uint32_t c0 = e.lit4 & 0xFFu;
+    for (int q = hi;;) {
+        q = find_bwd(L, q, lo, [c0](uint32_t w) { return swar::eq(w, c0); });
+        if (q < 0) return -1;
+        if (lit_at(P, L, q, e)) return q;
+        --q;
+    }
+}
+template <typename LN>
+__host__ __device__ LP_INLINE int lit_first(const Program& P, const LN& L, const Elem& e, int lo, int hi) {
+    const uint32_t c0 = e.lit4 & 0xFFu;
+    for (int q = lo;;) {
+        q = find_fwd(L, q, hi + 1, [c0](uint32_t w) { return swar::eq(w, c0); });
+        if (q > hi) return -1;
+        if (lit_at(P, L, q, e)) return q;
+        ++q;
+    }
+}
+
 // First candidate end of element e at position p (exact leftmost-first
-// order), -1 = none, -2 = FALLBACK.
-__host__ __device__ inline int cand_first(const Program& P, const Elem& e, const Line& L, int p) {
+// order), -1 = none, -2 = FALLBACK.  '.' runs to the end of the line: the
+// fast-path guard already rejected every line terminator.
+template <typename LN>
+__host__ __device__ LP_INLINE int cand_first(const Program& P, const Elem& e, const LN& L, int p) {
     switch (e.kind) {
-    case EK_NOSPACE: { int q = p; while (q < L.n && !is_ws(L[q])) ++q; return q; }
-    case EK_NUMBER: { int q = p; while (q < L.n && is_digit(L[q])) ++q; return q > p ? q : -1; }
+    case EK_NOSPACE: return find_fwd(L, p, L.n, [](uint32_t w) { return swar::ws(w); });
+    case EK_NUMBER: { int q = find_fwd(L, p, L.n, [](uint32_t w) { return ~swar::digit(w) & swar::HI; }); return q > p ? q : -1; }
     case EK_CLFNUMBER: {
-        int q = p; while (q < L.n && is_digit(L[q])) ++q;
+        int q = find_fwd(L, p, L.n, [](uint32_t w) { return ~swar::digit(w) & swar::HI; });
         if (q > p) return q;
         return (p < L.n && L[p] == '-') ? p + 1 : -1;
     }
-    case EK_HEXNUMBER: { int q = p; while (q < L.n && is_hex(L[q])) ++q; return q > p ? q : -1; }
+    case EK_HEXNUMBER: { int q = find_fwd(L, p, L.n, [](uint32_t w) { return ~swar::hex(w) & swar::HI; }); return q > p ? q : -1; }
     case EK_CLFHEXNUMBER: {
-        int q = p; while (q < L.n && is_hex(L[q])) ++q;
+        int q = find_fwd(L, p, L.n, [](uint32_t w) { return ~swar::hex(w) & swar::HI; });
         if (q > p) return q;
         return (p < L.n && L[p] == '-') ? p + 1 : -1;
     }
     case EK_NONZERO: {
         if (p >= L.n || !(L[p] >= '1' && L[p] <= '9')) return -1;
-        int q = p + 1; while (q < L.n && is_digit(L[q])) ++q; return q;
+        return find_fwd(L, p + 1, L.n, [](uint32_t w) { return ~swar::digit(w) & swar::HI; });
     }
     case EK_ANY_GREEDY: {
-        int m = dot_end(L, p);
-        if (e.last) return m == L.n ? m : -1;
-        if (!e.nlit) return m;
-        for (int q = m; q >= p; --q) if (lit_at(P, L, q, e.lit_off, e.lit_len)) return q;
-        return -1;
+        if (e.last) return L.n;
+        if (!e.nlit) return L.n;
+        return lit_last(P, L, e, L.n - 1, p);
     }
     case EK_ANY_LAZY: {
-        int m = dot_end(L, p);
-        if (e.last) return m == L.n ? m : -1;
+        if (e.last) return L.n;
         if (!e.nlit) return p;
-        for (int q = p; q <= m; ++q) if (lit_at(P, L, q, e.lit_off, e.lit_len)) return q;
-        return -1;
+        return lit_first(P, L, e, p, L.n - 1);
     }
     case EK_TIME_US: return time_us_ok(L, p) ? p + 26 : -1;
     case EK_CLF_IP:
@@ -130,7 +304,7 @@ __host__ __device__ inline int cand_first(const Program& P, const Elem& e, const
         if (q >= 0) return q;
         // IPv6 alternative can only match empty at '-' (no hex/':'), so '-'
         // is exact when the following literal cannot start at p.
-        if (e.kind == EK_CLF_IP && p < L.n && L[p] == '-' && e.nlit && P.lit[e.lit_off] != '-') return p + 1;
+        if (e.kind == EK_CLF_IP && p < L.n && L[p] == '-' && e.nlit && (e.lit4 & 0xFFu) != '-') return p + 1;
         return -2;
     }
     }
@@ -138,7 +312,8 @@ __host__ __device__ inline int cand_first(const Program& P, const Elem& e, const
 }
 
 // Next candidate after 'cur' (same priority order).
-__host__ __device__ inline int cand_next(const Program& P, const Elem& e, const Line& L, int p, int cur) {
+template <typename LN>
+__host__ __device__ LP_INLINE int cand_next(const Program& P, const Elem& e, const LN& L, int p, int cur) {
     switch (e.kind) {
     case EK_NOSPACE: return cur - 1 >= p ? cur - 1 : -1;
     case EK_NUMBER: case EK_HEXNUMBER: case EK_NONZERO: return cur - 1 >= p + 1 ? cur - 1 : -1;
@@ -148,14 +323,11 @@ __host__ __device__ inline int cand_next(const Program& P, const Elem& e, const 
     case EK_ANY_GREEDY:
         if (e.last) return -1;
         if (!e.nlit) return cur - 1 >= p ? cur - 1 : -1;
-        for (int q = cur - 1; q >= p; --q) if (lit_at(P, L, q, e.lit_off, e.lit_len)) return q;
-        return -1;
+        return lit_last(P, L, e, cur - 1, p);
     case EK_ANY_LAZY: {
         if (e.last) return -1;
-        int m = dot_end(L, p);
-        if (!e.nlit) return cur + 1 <= m ? cur + 1 : -1;
-        for (int q = cur + 1; q <= m; ++q) if (lit_at(P, L, q, e.lit_off, e.lit_len)) return q;
-        return -1;
+        if (!e.nlit) return cur + 1 <= L.n ? cur + 1 : -1;
+        return lit_first(P, L, e, cur + 1, L.n - 1);
     }
     case EK_TIME_US: return -1;
     case EK_CLF_IP: case EK_IP:
@@ -165,29 +337,31 @@ __host__ __device__ inline int cand_next(const Program& P, const Elem& e, const 
 }
 
 // Backtracking match of "^" elems "$" with java.util.regex priority
-// semantics.  caps[k] = span of captured token k.  stk: MAX_STACK scratch.
-template <typename Stk>
-__host__ __device__ inline int match_line(const Program& P, const Line& L, uint32_t* caps, Stk stk) {
+// semantics.  caps = spans of the captured tokens.  stk: MAX_STACK scratch.
+// elems: the program's element table (the kernel passes an LDS copy).
+template <typename LN, typename EL, typename Caps, typename Stk>
+__host__ __device__ LP_INLINE int match_line(const Program& P, const EL& elems, const LN& L, Caps& caps, Stk stk) {
     int i = 0, pos = 0, sp = 0;
     int steps = 0;
     const int budget = 16 * L.n + 256;
+    const int ne = P.n_elems;
     for (;;) {
         if (++steps > budget) return ST_FALLBACK;
         bool ok;
-        if (i == P.n_elems) {
+        if (i == ne) {
             if (pos == L.n) return ST_OK;
             ok = false;
         } else {
-            const Elem& e = P.elems[i];
+            const Elem e = elems[i];
             if (e.kind == EK_LIT) {
-                ok = lit_at(P, L, pos, e.lit_off, e.lit_len);
+                ok = lit_at(P, L, pos, e);
                 if (ok) { pos += e.lit_len; ++i; continue; }
             } else {
                 int c = cand_first(P, e, L, pos);
                 if (c == -2) return ST_FALLBACK;
                 ok = c >= 0;
                 if (ok) {
-                    if (e.cap >= 0) caps[e.cap] = mkspan(pos, c);
+                    if (e.cap >= 0) caps.set(e.cap, mkspan(pos, c));
                     if (!e.det) {
                         if (sp == MAX_STACK) return ST_FALLBACK;
                         stk[sp++] = (uint32_t)i | ((uint32_t)pos << 6) | ((uint32_t)c << 19);
@@ -203,12 +377,12 @@ __host__ __device__ inline int match_line(const Program& P, const Line& L, uint3
             if (sp == 0) return ST_BAD;
             uint32_t top = stk[sp - 1];
             int j = top & 63, p = (top >> 6) & 8191, cur = (top >> 19) & 8191;
-            const Elem& e = P.elems[j];
+            const Elem e = elems[j];
             int c = cand_next(P, e, L, p, cur);
             if (c == -2) return ST_FALLBACK;
             if (c >= 0) {
                 stk[sp - 1] = (uint32_t)j | ((uint32_t)p << 6) | ((uint32_t)c << 19);
-                if (e.cap >= 0) caps[e.cap] = mkspan(p, c);
+                if (e.cap >= 0) caps.set(e.cap, mkspan(p, c));
                 pos = c;
                 i = j + 1;
                 break;
@@ -219,7 +393,7 @@ __host__ __device__ inline int match_line(const Program& P, const Line& L, uint3
 }
 
 // ------------------------------------------------------------- calendar
-__host__ __device__ inline int64_t days_from_civil(int64_t y, int m, int d) {
+__host__ __device__ LP_INLINE int64_t days_from_civil(int64_t y, int m, int d) {
     y -= m <= 2;
     const int64_t era = (y >= 0 ? y : y - 399) / 400;
     const int64_t yoe = y - era * 400;
@@ -227,7 +401,7 @@ __host__ __device__ inline int64_t days_from_civil(int64_t y, int m, int d) {
     const int64_t doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
     return era * 146097 + doe - 719468;
 }
-__host__ __device__ inline void civil_from_days(int64_t z, int64_t& y, int& m, int& d) {
+__host__ __device__ LP_INLINE void civil_from_days(int64_t z, int64_t& y, int& m, int& d) {
     z += 719468;
     const int64_t era = (z >= 0 ? z : z - 146096) / 146097;
     const int64_t doe = z - era * 146097;
@@ -238,14 +412,14 @@ __host__ __device__ inline void civil_from_days(int64_t z, int64_t& y, int& m, i
     m = (int)(mp < 10 ? mp + 3 : mp - 9);
     y = yoe + era * 400 + (m <= 2);
 }
-__host__ __device__ inline bool leap(int64_t y) { return (y % 4 == 0 && y % 100 != 0) || y % 400 == 0; }
-__host__ __device__ inline int month_len(int64_t y, int m) {
+__host__ __device__ LP_INLINE bool leap(int64_t y) { return (y % 4 == 0 && y % 100 != 0) || y % 400 == 0; }
+__host__ __device__ LP_INLINE int month_len(int64_t y, int m) {
     if (m == 2) return leap(y) ? 29 : 28;
     return (m == 4 || m == 6 || m == 9 || m == 11) ? 30 : 31;
 }
-__host__ __device__ inline int iso_dow(int64_t days) { return (int)(((days % 7) + 7 + 3) % 7) + 1; }  // Mon=1
+__host__ __device__ LP_INLINE int iso_dow(int64_t days) { return (int)(((days % 7) + 7 + 3) % 7) + 1; }  // Mon=1
 // WeekFields.ISO (== WeekFields.of(Locale.UK)): week-based-year and week
-__host__ __device__ inline void iso_week(int64_t y, int m, int d, int64_t& wy, int& wk) {
+__host__ __device__ LP_INLINE void iso_week(int64_t y, int m, int d, int64_t& wy, int& wk) {
     int64_t days = days_from_civil(y, m, d);
     int wd = iso_dow(days);
     int doy = (int)(days - days_from_civil(y, 1, 1)) + 1;
@@ -268,7 +442,10 @@ __host__ __device__ inline void iso_week(int64_t y, int m, int d, int64_t& wy, i
 // Locale.UK, ResolverStyle.SMART (TimeStampDissector.java:46,100-109,418):
 // day 1..31 clamped to the month length, 24:00:00 = next day 00:00:00,
 // offset sign+HHMM (each <= 59) with |offset| <= 18:00.
-__host__ __device__ inline bool parse_apache_time(const uint8_t* c, int64_t& epoch_s, uint64_t& local, uint64_t& utc) {
+template <typename LN>
+__host__ __device__ LP_INLINE bool parse_apache_time(const LN& L, int a, int64_t& epoch_s, uint64_t& local, uint64_t& utc) {
+    uint32_t c[26];
+    LP_UNROLL for (int k = 0; k < 26; ++k) c[k] = L[a + k];
     int day = (c[0] - '0') * 10 + (c[1] - '0');
     // month name: case-insensitive against the 12 UK short names
     uint32_t m3 = ((uint32_t)(c[3] | 32) << 16) | ((uint32_t)(c[4] | 32) << 8) | (uint32_t)(c[5] | 32);
@@ -320,33 +497,35 @@ __host__ __device__ inline bool parse_apache_time(const uint8_t* c, int64_t& epo
 // ----------------------------------------------------------- per-line state
 struct LineOut {
     int status;
-    uint32_t caps[MAX_TOK];
+    RegArr<MAX_TOK> caps;
     uint32_t tok_flags;
-    uint32_t fl_kind[MAX_FL], fl_method[MAX_FL], fl_uri[MAX_FL], fl_proto[MAX_FL];
+    RegArr<MAX_FL> fl_kind, fl_method, fl_uri, fl_proto;
     uint32_t arena_need;
 };
 
-__host__ __device__ inline bool prefix_at(const Line& L, int a, int b, const char* lit) {
+template <typename LN>
+__host__ __device__ LP_INLINE bool prefix_at(const LN& L, int a, int b, const char* lit) {
     int k = 0;
     for (; lit[k]; ++k)
         if (a + k >= b || L[a + k] != (uint8_t)lit[k]) return false;
     return true;
 }
-__host__ __device__ inline bool value_is_header_name(const Line& L, int a, int b) {
+template <typename LN>
+__host__ __device__ LP_INLINE bool value_is_header_name(const LN& L, int a, int b) {
     return (b - a == 17 && prefix_at(L, a, b, "request.firstline")) || prefix_at(L, a, b, "request.header.") ||
            prefix_at(L, a, b, "response.header.");
 }
 
 // Source span of URI stage u; returns false when the value is null/absent/empty
-__host__ __device__ inline bool uri_source(const Program& P, const LineOut& o, int u, int& a, int& b) {
+__host__ __device__ LP_INLINE bool uri_source(const Program& P, const LineOut& o, int u, int& a, int& b) {
     const UriStage& U = P.uri[u];
     uint32_t sp;
     if (U.src_tok >= 0) {
         if (o.tok_flags & (1u << U.src_tok)) return false;  // "-" -> null
-        sp = o.caps[U.src_tok];
+        sp = o.caps.get(U.src_tok);
     } else {
-        if (o.fl_kind[U.src_fl] == FL_NONE) return false;
-        sp = o.fl_uri[U.src_fl];
+        if (o.fl_kind.get(U.src_fl) == FL_NONE) return false;
+        sp = o.fl_uri.get(U.src_fl);
     }
     a = sp & 0xFFFF;
     b = sp >> 16;
@@ -354,40 +533,43 @@ __host__ __device__ inline bool uri_source(const Program& P, const LineOut& o, i
 }
 
 // Phase 1: guard, match, tokens, time, first line; arena need for phase 2.
-template <typename Stk, typename Cols>
-__host__ __device__ inline void phase1(const Program& P, const Line& L, LineOut& o, Stk stk, Cols& C, int64_t li) {
+template <typename LN, typename EL, typename Stk, typename Cols>
+__host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, const LN& L, LineOut& o, Stk stk, Cols& C,
+                                          int64_t li) {
     o.status = ST_OK;
     o.tok_flags = 0;
     o.arena_need = 0;
-    for (int k = 0; k < MAX_FL; ++k) o.fl_kind[k] = FL_NONE;
+    o.caps.fill(0);
+    o.fl_kind.fill(FL_NONE);
+    o.fl_method.fill(0);
+    o.fl_uri.fill(0);
+    o.fl_proto.fill(0);
     if (L.n > MAX_LINE) { o.status = ST_FALLBACK; return; }
     // fast-path guard: printable ASCII + TAB only (no \r, no line
     // terminators, no bytes that need UTF-8 decoding or URIUtil UTF-8 bytes)
-    for (int k = 0; k < L.n; ++k) {
-        uint32_t c = L[k];
-        if ((c < 0x20 && c != '\t') || c >= 0x7F) { o.status = ST_FALLBACK; return; }
-    }
-    int st = match_line(P, L, o.caps, stk);
+    if (find_fwd(L, 0, L.n, [](uint32_t w) { return swar::guard_bad(w); }) < L.n) { o.status = ST_FALLBACK; return; }
+    int st = match_line(P, elems, L, o.caps, stk);
     if (st != ST_OK) { o.status = st; return; }
     // decodeExtractedValue: "-" -> null (Apache: ApacheHttpdLogFormatDissector.java:169-196,
     // NGINX: NginxHttpdLogFormatDissector.java:107-119)
     for (int k = 0; k < P.n_tok; ++k) {
-        int a = o.caps[k] & 0xFFFF, b = o.caps[k] >> 16;
+        const uint32_t sp = o.caps.get(k);
+        int a = sp & 0xFFFF, b = sp >> 16;
         if (b - a == 1 && L[a] == '-') o.tok_flags |= 1u << k;
         if (b - a == 1 && L[a] == '0') o.tok_flags |= 1u << (16 + k);
         if (P.apache && b - a >= 15 && value_is_header_name(L, a, b)) {
             // the reference tests the VALUE (not the token name) against
             // "request.firstline" / "request.header." / "response.header." and
             // then unescapes \xhh sequences (ApacheHttpdLogFormatDissector.java:189-193)
-            for (int q = a; q < b; ++q) if (L[q] == '\\') { o.status = ST_FALLBACK; return; }
+            if (find_fwd(L, a, b, [](uint32_t w) { return swar::eq(w, '\\'); }) < b) { o.status = ST_FALLBACK; return; }
         }
     }
     // TimeStampDissector
     for (int t = 0; t < P.n_time; ++t) {
         int k = P.time[t].tok;
-        int a = o.caps[k] & 0xFFFF;
+        int a = o.caps.get(k) & 0xFFFF;
         int64_t ep; uint64_t lo, ut;
-        if (!parse_apache_time(L.s + a, ep, lo, ut)) { o.status = ST_BAD; return; }
+        if (!parse_apache_time(L, a, ep, lo, ut)) { o.status = ST_BAD; return; }
         C.t_epoch[t][li] = ep * 1000;
         C.t_local[t][li] = lo;
         C.t_utc[t][li] = ut;
@@ -395,18 +577,18 @@ __host__ __device__ inline void phase1(const Program& P, const Line& L, LineOut&
     // HttpFirstLineDissector: ^([a-zA-Z-_]+) (.*) (HTTP/[0-9]+\.[0-9]+)$ else ^([a-zA-Z-_]+) (.*)$
     for (int f = 0; f < P.n_fl; ++f) {
         int k = P.fl[f].tok;
-        o.fl_kind[f] = FL_NONE;
         if (o.tok_flags & (1u << k)) continue;                // null
-        int a = o.caps[k] & 0xFFFF, b = o.caps[k] >> 16;
+        const uint32_t sp0 = o.caps.get(k);
+        int a = sp0 & 0xFFFF, b = sp0 >> 16;
         if (b <= a) continue;                                 // empty
         int q = a;
         while (q < b && (is_alpha(L[q]) || L[q] == '-' || L[q] == '_')) ++q;
         if (q == a || q >= b || L[q] != ' ') continue;        // neither regex matches
-        o.fl_method[f] = mkspan(a, q);
+        o.fl_method.set(f, mkspan(a, q));
         int us = q + 1;
         // protocol: the last ' ' must be followed by HTTP/d+.d+ up to the end
-        int sp = b - 1;
-        while (sp >= us && L[sp] != ' ') --sp;
+        int sp = find_bwd(L, b - 1, us, [](uint32_t w) { return swar::eq(w, ' '); });
+        if (sp < 0) sp = us - 1;
         bool full = false;
         if (sp >= us && b - sp >= 9 && L[sp + 1] == 'H' && L[sp + 2] == 'T' && L[sp + 3] == 'T' && L[sp + 4] == 'P' &&
             L[sp + 5] == '/') {
@@ -419,13 +601,13 @@ __host__ __device__ inline void phase1(const Program& P, const Line& L, LineOut&
             }
         }
         if (full) {
-            o.fl_kind[f] = FL_FULL;
-            o.fl_uri[f] = mkspan(us, sp);
-            o.fl_proto[f] = mkspan(sp + 1, b);
+            o.fl_kind.set(f, FL_FULL);
+            o.fl_uri.set(f, mkspan(us, sp));
+            o.fl_proto.set(f, mkspan(sp + 1, b));
         } else {
-            o.fl_kind[f] = FL_CHOPPED;
-            o.fl_uri[f] = mkspan(us, b);
-            o.fl_proto[f] = 0;
+            o.fl_kind.set(f, FL_CHOPPED);
+            o.fl_uri.set(f, mkspan(us, b));
+            o.fl_proto.set(f, 0);
         }
     }
     // arena need of the URI / query stages (upper bound of phase-2 writes)
@@ -433,12 +615,8 @@ __host__ __device__ inline void phase1(const Program& P, const Line& L, LineOut&
     for (int u = 0; u < P.n_uri; ++u) {
         int a, b;
         if (!uri_source(P, o, u, a, b)) continue;
-        uint32_t enc = 0, sep = 0;
-        for (int q = a; q < b; ++q) {
-            uint32_t c = L[q];
-            enc += uri_needs_encode(c);
-            sep += (c == '&' || c == '?');
-        }
+        const uint32_t enc = count_in(L, a, b, [](uint32_t w) { return swar::needs_encode(w); });
+        const uint32_t sep = count_in(L, a, b, [](uint32_t w) { return swar::eq(w, '&') | swar::eq(w, '?'); });
         const UriStage& U = P.uri[u];
         uint32_t ulen = (uint32_t)(b - a), tl = ulen + 2 * enc + 2;
         uint32_t n = 16;
@@ -461,7 +639,8 @@ struct Arena {
 
 // java.net.URI.Parser.parseIPv4Address/scanIPv4Address on [a,b) of the
 // authority (JDK 8); returns end or -1.
-__host__ __device__ inline int jdk_ipv4(const Line& L, int a, int b) {
+template <typename LN>
+__host__ __device__ LP_INLINE int jdk_ipv4(const LN& L, int a, int b) {
     int m = a;
     while (m < b && (is_digit(L[m]) || L[m] == '.')) ++m;
     if (m <= a) return -1;
@@ -486,7 +665,8 @@ __host__ __device__ inline int jdk_ipv4(const Line& L, int a, int b) {
 }
 
 // java.net.URI.Parser.parseHostname on [a,b); returns end or -1 (fail)
-__host__ __device__ inline int jdk_hostname(const Line& L, int a, int b) {
+template <typename LN>
+__host__ __device__ LP_INLINE int jdk_hostname(const LN& L, int a, int b) {
     int p = a, l = -1;
     do {
         int q = p;
@@ -510,7 +690,7 @@ __host__ __device__ inline int jdk_hostname(const Line& L, int a, int b) {
 }
 
 // strict UTF-8 validation of a decoded byte string
-__host__ __device__ inline bool utf8_ok(const uint8_t* b, uint32_t n) {
+__host__ __device__ LP_INLINE bool utf8_ok(const uint8_t* b, uint32_t n) {
     for (uint32_t i = 0; i < n;) {
         uint32_t c = b[i];
         if (c < 0x80) { ++i; continue; }
@@ -534,10 +714,9 @@ __host__ __device__ inline bool utf8_ok(const uint8_t* b, uint32_t n) {
 
 // java.net.URI.decode of [a,b) of the line (escapes proven valid):
 // returns a ref (line span when nothing to decode), or ~0 on FALLBACK.
-__host__ __device__ inline uint64_t decode_span(const Line& L, int a, int b, Arena& A) {
-    bool pct = false;
-    for (int q = a; q < b; ++q) pct |= L[q] == '%';
-    if (!pct) return mkref(a, b - a, false);
+template <typename LN>
+__host__ __device__ LP_INLINE uint64_t decode_span(const LN& L, int a, int b, Arena& A) {
+    if (find_fwd(L, a, b, [](uint32_t w) { return swar::eq(w, '%'); }) >= b) return mkref(a, b - a, false);
     uint32_t start = A.used;
     for (int q = a; q < b;) {
         uint32_t c = L[q];
@@ -548,70 +727,83 @@ __host__ __device__ inline uint64_t decode_span(const Line& L, int a, int b, Are
     return mkref(start, A.used - start, true);
 }
 
-__host__ __device__ inline void put_encoded(Arena& A, uint32_t c) {
+__host__ __device__ LP_INLINE void put_encoded(Arena& A, uint32_t c) {
     const char* HX = "0123456789ABCDEF";
     A.put('%');
     A.put(HX[c >> 4]);
     A.put(HX[c & 15]);
 }
 
-// QueryStringFieldDissector on the rawQuery (arena bytes [qa, qb)).
-template <typename Cols>
-__host__ __device__ inline void query_stage(const Program& P, int qs, Arena& A, uint32_t qa, uint32_t qb, Cols& C, int64_t li) {
+// QueryStringFieldDissector (QueryStringFieldDissector.java:56-108) on the
+// rawQuery of a URI stage, read straight from the line bytes [qa, qb) (the
+// text after the first '?', up to '#').  The rawQuery is "&" + that text
+// with '?' -> '&' and URIUtil escapes, so its '&'-pieces are the pieces of
+// the line text split at '&' and '?'.  Names are the pieces' (escaped,
+// lower-cased) text before '='; values go through resilientUrlDecode.  A
+// name or value equal to line bytes is delivered as a line ref; only
+// rewritten strings are written to the arena.
+template <typename LN, typename Cols>
+__host__ __device__ LP_INLINE void query_stage(const Program& P, int qs, const LN& L, int qa, int qb, Arena& A, Cols& C,
+                                            int64_t li) {
     const QueryStage& Q = P.query[qs];
-    // count pieces for the table
-    uint32_t npieces = 1;
-    for (uint32_t q = qa; q < qb; ++q) npieces += A.p[q] == '&';
+    const uint32_t npieces = 1 + count_in(L, qa, qb, [](uint32_t w) { return swar::eq(w, '&') | swar::eq(w, '?'); });
     uint32_t tab = (A.used + 7) & ~7u;
     A.used = tab + 16 * npieces;
     uint32_t count = 0;
-    uint32_t s = qa;
+    int s = qa;
     while (s <= qb) {
-        uint32_t e = s;
-        while (e < qb && A.p[e] != '&') ++e;
+        const int e = find_fwd(L, s, qb, [](uint32_t w) { return swar::eq(w, '&') | swar::eq(w, '?'); });
         if (e > s) {
-            uint32_t eq = s;
-            while (eq < e && A.p[eq] != '=') ++eq;
-            uint32_t ne = eq;  // name [s, ne)
-            bool upper = false;
-            for (uint32_t q = s; q < ne; ++q) upper |= (A.p[q] - 'A') < 26u;
+            const int eq = find_fwd(L, s, e, [](uint32_t w) { return swar::eq(w, '='); });
+            // name [s, eq): URIUtil-escaped and lower-cased as in the rawQuery
+            const bool rewrite =
+                find_fwd(L, s, eq, [](uint32_t w) { return swar::upper(w) | swar::needs_encode(w); }) < eq;
+            const uint32_t mark = A.used;
+            uint64_t nref;
+            if (rewrite) {
+                const char* HX = "0123456789abcdef";  // URIUtil's %XX, lower-cased with the name
+                for (int q = s; q < eq; ++q) {
+                    uint32_t c = L[q];
+                    if (uri_needs_encode(c)) { A.put('%'); A.put(HX[c >> 4]); A.put(HX[c & 15]); }
+                    else A.put((c - 'A') < 26u ? (c | 32) : c);
+                }
+                nref = mkref(mark, A.used - mark, true);
+            } else {
+                nref = mkref(s, eq - s, false);
+            }
             // requested?  (wantAllFields || requestedParameters.contains(name))
             bool want = Q.want_all;
+            const uint32_t nlen = ref_len(nref);
             for (int k = 0; k < Q.n_names && !want; ++k) {
-                if (Q.name_len[k] != ne - s) continue;
+                if (Q.name_len[k] != nlen) continue;
                 bool same = true;
-                for (uint32_t q = 0; q < ne - s; ++q) {
-                    uint32_t c = A.p[s + q];
-                    if ((c - 'A') < 26u) c |= 32;
-                    if (c != P.lit[Q.name_off[k] + q]) { same = false; break; }
+                for (uint32_t q = 0; q < nlen && same; ++q) {
+                    uint32_t c = rewrite ? (uint32_t)A.p[mark + q] : L[s + (int)q];
+                    same = c == P.lit[Q.name_off[k] + q];
                 }
                 want = same;
             }
-            if (want) {
-                uint64_t nref;
-                if (upper) {
-                    uint32_t st = A.used;
-                    for (uint32_t q = s; q < ne; ++q) { uint32_t c = A.p[q]; A.put((c - 'A') < 26u ? (c | 32) : c); }
-                    nref = mkref(st, ne - s, true);
-                } else nref = mkref(s, ne - s, true);
+            if (!want) {
+                A.used = mark;
+            } else {
                 uint64_t vref;
-                if (eq == e) vref = mkref(0, 0, true);  // no '=' -> ""
+                if (eq == e) vref = mkref(0, 0, false);  // no '=' -> ""
                 else {
-                    uint32_t vs = eq + 1;
-                    bool plain = true;
-                    for (uint32_t q = vs; q < e; ++q) plain &= (A.p[q] != '%' && A.p[q] != '+');
-                    if (plain) vref = mkref(vs, e - vs, true);
+                    const int vs = eq + 1;
+                    const bool plain = find_fwd(L, vs, e, [](uint32_t w) { return swar::eq(w, '%') | swar::eq(w, '+'); }) >= e;
+                    if (plain) vref = mkref(vs, e - vs, false);
                     else {
                         // Utils.resilientUrlDecode: every '%' here is followed by two
                         // hex digits (URI stage guard), so each %XX is the Latin-1
-                        // char U+00XX (VALID_STANDARD -> %00%XX, UTF-16 decode) and
-                        // '+' is a space.  Output UTF-8.
+                        // char U+00XX (VALID_STANDARD -> %00%XX, UTF-16 decode), '+'
+                        // is a space, and URIUtil escapes decode back to their byte.
+                        // Output UTF-8.
                         uint32_t st = A.used;
-                        for (uint32_t q = vs; q < e;) {
-                            uint32_t c = A.p[q];
+                        for (int q = vs; q < e;) {
+                            uint32_t c = L[q];
                             if (c == '+') { A.put(' '); ++q; }
                             else if (c == '%') {
-                                uint32_t v = hexv(A.p[q + 1]) * 16 + hexv(A.p[q + 2]);
+                                uint32_t v = hexv(L[q + 1]) * 16 + hexv(L[q + 2]);
                                 if (v < 0x80) A.put(v);
                                 else { A.put(0xC0 | (v >> 6)); A.put(0x80 | (v & 0x3F)); }
                                 q += 3;
@@ -633,12 +825,18 @@ __host__ __device__ inline void query_stage(const Program& P, int qs, Arena& A, 
 }
 
 // HttpUriDissector fast path on the line bytes [a,b).  Returns status.
-template <typename Cols>
-__host__ __device__ inline int uri_stage(const Program& P, int u, const Line& L, int a, int b, Arena& A, Cols& C, int64_t li) {
+template <typename LN, typename Cols>
+__host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L, int a, int b, Arena& A, Cols& C, int64_t li) {
     const UriStage& U = P.uri[u];
     // ---- guards (FALLBACK when a cleanup step of the reference would change the string)
     int fa = -1, h = -1, nh = 0;
-    for (int q = a; q < b; ++q) {
+    // an unescapeHtml4 entity candidate needs a ';' somewhere in the URI
+    const bool semi = find_fwd(L, a, b, [](uint32_t w) { return swar::eq(w, ';'); }) < b;
+    for (int q = a;; ++q) {
+        q = find_fwd(L, q, b, [](uint32_t w) {
+            return swar::eq(w, '%') | swar::eq(w, '#') | swar::eq(w, '&') | swar::eq(w, '?');
+        });
+        if (q >= b) break;
         uint32_t c = L[q];
         if (c == '%') {
             if (q + 2 >= b || !is_hex(L[q + 1]) || !is_hex(L[q + 2])) return ST_FALLBACK;  // BAD_EXCAPE_PATTERN
@@ -650,9 +848,11 @@ __host__ __device__ inline int uri_stage(const Program& P, int u, const Line& L,
             if (q > a && L[q - 1] == '=') return ST_FALLBACK;                              // EQUALS_HASH
         } else if (c == '&' || c == '?') {
             if (fa < 0) fa = q;
-            int r = q + 1;                                                                // unescapeHtml4 candidates
-            while (r < b && (is_alnum(L[r]) || L[r] == '#')) ++r;
-            if (r < b && L[r] == ';') return ST_FALLBACK;
+            if (semi) {                                                                   // unescapeHtml4 candidates
+                int r = q + 1;
+                while (r < b && (is_alnum(L[r]) || L[r] == '#')) ++r;
+                if (r < b && L[r] == ';') return ST_FALLBACK;
+            }
         }
     }
     if (nh > 1) return ST_FALLBACK;                                                       // DOUBLE_HASH
@@ -741,17 +941,27 @@ __host__ __device__ inline int uri_stage(const Program& P, int u, const Line& L,
         if (fa >= 0 && (h < 0 || fa < h)) {
             // rawQuery = "&" + normalized text up to '#': '?'->'&', URIUtil escapes
             flags |= UF_QUERY;
-            uint32_t st = A.used;
-            A.put('&');
-            int qe = h >= 0 ? h : b;
-            for (int q = fa + 1; q < qe; ++q) {
-                uint32_t c = L[q];
-                if (c == '?') A.put('&');
-                else if (uri_needs_encode(c)) put_encoded(A, c);
-                else A.put(c);
+            const int qs0 = fa + 1, qe = h >= 0 ? h : b;
+            // the ref is formed before the scan below: with it formed after,
+            // the gfx950 build (ROCm 7.2, -O3) delivered a wrong offset on
+            // lanes whose scan ran an extra word (parity tests caught it)
+            const uint64_t amp_ref = mkref(qs0, qe - qs0, false) | REF_AMP;
+            const bool plain =
+                find_fwd(L, qs0, qe, [](uint32_t w) { return swar::eq(w, '?') | swar::needs_encode(w); }) >= qe;
+            if (plain) {
+                C.u_query[u][li] = amp_ref;
+            } else {
+                uint32_t st = A.used;
+                A.put('&');
+                for (int q = fa + 1; q < qe; ++q) {
+                    uint32_t c = L[q];
+                    if (c == '?') A.put('&');
+                    else if (uri_needs_encode(c)) put_encoded(A, c);
+                    else A.put(c);
+                }
+                C.u_query[u][li] = mkref(st, A.used - st, true);
             }
-            C.u_query[u][li] = mkref(st, A.used - st, true);
-            if (U.query_stage >= 0) query_stage(P, U.query_stage, A, st, A.used, C, li);
+            if (U.query_stage >= 0) query_stage(P, U.query_stage, L, fa + 1, qe, A, C, li);
         } else {
             C.u_query[u][li] = mkref(0, 0, true);
             if (U.query_stage >= 0) { C.q_count[U.query_stage][li] = 0; C.q_params[U.query_stage][li] = 0; }
@@ -781,8 +991,8 @@ __host__ __device__ inline int uri_stage(const Program& P, int u, const Line& L,
 }
 
 // Phase 2: URI + query stages into the line's arena region.
-template <typename Cols>
-__host__ __device__ inline void phase2(const Program& P, const Line& L, LineOut& o, Arena& A, Cols& C, int64_t li) {
+template <typename LN, typename Cols>
+__host__ __device__ LP_INLINE void phase2(const Program& P, const LN& L, LineOut& o, Arena& A, Cols& C, int64_t li) {
     for (int u = 0; u < P.n_uri && o.status == ST_OK; ++u) {
         int a, b;
         if (!uri_source(P, o, u, a, b)) {
@@ -797,17 +1007,15 @@ __host__ __device__ inline void phase2(const Program& P, const Line& L, LineOut&
 
 // Final per-line column writes (status, tokens, first line).
 template <typename Cols>
-__host__ __device__ inline void write_line(const Program& P, const LineOut& o, Cols& C, int64_t li) {
+__host__ __device__ LP_INLINE void write_line(const Program& P, const LineOut& o, Cols& C, int64_t li) {
     C.status[li] = (uint8_t)o.status;
     if (o.status != ST_OK) return;
-    for (int k = 0; k < P.n_tok; ++k) C.tok_span[k][li] = o.caps[k];
+    o.caps.each([&](int k, uint32_t v) { if (k < P.n_tok) C.tok_span[k][li] = v; });
     C.tok_flags[li] = o.tok_flags;
-    for (int f = 0; f < P.n_fl; ++f) {
-        C.fl_kind[f][li] = o.fl_kind[f];
-        C.fl_method[f][li] = o.fl_method[f];
-        C.fl_uri[f][li] = o.fl_uri[f];
-        C.fl_proto[f][li] = o.fl_proto[f];
-    }
+    o.fl_kind.each([&](int f, uint32_t v) { if (f < P.n_fl) C.fl_kind[f][li] = v; });
+    o.fl_method.each([&](int f, uint32_t v) { if (f < P.n_fl) C.fl_method[f][li] = v; });
+    o.fl_uri.each([&](int f, uint32_t v) { if (f < P.n_fl) C.fl_uri[f][li] = v; });
+    o.fl_proto.each([&](int f, uint32_t v) { if (f < P.n_fl) C.fl_proto[f][li] = v; });
 }
 
 }  // namespace lp

@@ -21,6 +21,14 @@
 #endif
 #endif
 
+#if defined(__HIP__)
+#define LP_UNROLL _Pragma("unroll")
+#define LP_INLINE __attribute__((always_inline)) inline
+#else
+#define LP_UNROLL
+#define LP_INLINE inline
+#endif
+
 namespace lp {
 
 constexpr int MAX_ELEMS = 48;
@@ -60,6 +68,7 @@ struct Elem {
     uint16_t lit_len;
     uint8_t nlit;      // token followed by a literal
     uint8_t pad[3];
+    uint32_t lit4;     // first (up to) 4 bytes of that literal, little-endian
 };
 
 // TimeStampDissector on a TIME.STAMP token (dd/MMM/yyyy:HH:mm:ss ZZ,
@@ -122,16 +131,20 @@ __host__ __device__ inline uint64_t pack_cal(uint32_t y, uint32_t mo, uint32_t d
            ((uint64_t)s << 36) | ((uint64_t)wy << 42) | ((uint64_t)wk << 58);
 }
 
-// A "ref" names a byte string: bits 0..31 offset, 32..62 length, bit 63 set
+// A "ref" names a byte string: bits 0..31 offset, 32..61 length, bit 63 set
 // when the bytes live in the line's arena region (else: relative to the
-// line start).
+// line start).  Bit 62 (REF_AMP, line refs only): the string is '&'
+// followed by the line bytes -- the HttpUriDissector rawQuery of a query
+// that needs no other rewriting, delivered without copying it.
 constexpr uint64_t REF_ARENA = 1ull << 63;
+constexpr uint64_t REF_AMP = 1ull << 62;
 __host__ __device__ inline uint64_t mkref(uint32_t off, uint32_t len, bool arena) {
     return (uint64_t)off | ((uint64_t)len << 32) | (arena ? REF_ARENA : 0ull);
 }
 __host__ __device__ inline uint32_t ref_off(uint64_t r) { return (uint32_t)r; }
-__host__ __device__ inline uint32_t ref_len(uint64_t r) { return (uint32_t)((r >> 32) & 0x7FFFFFFFu); }
+__host__ __device__ inline uint32_t ref_len(uint64_t r) { return (uint32_t)((r >> 32) & 0x3FFFFFFFu); }
 __host__ __device__ inline bool ref_arena(uint64_t r) { return (r & REF_ARENA) != 0; }
+__host__ __device__ inline bool ref_amp(uint64_t r) { return (r & REF_AMP) != 0; }
 
 // Token span: start | end << 16 (line-relative)
 __host__ __device__ inline uint32_t mkspan(uint32_t a, uint32_t b) { return a | (b << 16); }
@@ -171,14 +184,13 @@ struct Columns {
     uint64_t* u_path[MAX_URI];
     uint64_t* u_query[MAX_URI];
     uint64_t* u_frag[MAX_URI];
-    uint64_t* u_userinfo[MAX_URI];
     uint32_t* q_count[MAX_QUERY]; // params are (name ref, value ref) pairs in the arena
     uint64_t* q_params[MAX_QUERY];// ref to the param table in the arena
     uint64_t* arena_base;         // [n]
     uint8_t* arena;
     uint64_t arena_cap;
     unsigned long long* arena_top;  // bump pointer
-    unsigned long long* counters;   // [4] lines ok bad fallback
+    uint32_t* wave_counts;          // [n_waves][4] lines ok bad fallback (reduced after the launch)
 };
 
 }  // namespace lp

@@ -750,6 +750,7 @@ void Plan::compile_program() {
             if (off < 0) { device_ok_ = false; why_ = "literal pool overflow"; return; }
             e.lit_off = (uint16_t)off;
             e.lit_len = (uint16_t)t.regex.size();
+            for (int k = 0; k < 4 && k < (int)t.regex.size(); ++k) e.lit4 |= (uint32_t)(uint8_t)t.regex[k] << (8 * k);
             continue;
         }
         int k = elem_kind_of(t.regex);
@@ -780,6 +781,7 @@ void Plan::compile_program() {
             e.lit_len = P.elems[i + 1].lit_len;
         }
         uint8_t c0 = e.nlit ? P.lit[e.lit_off] : 0;
+        if (e.nlit) e.lit4 = P.elems[i + 1].lit4;
         bool ws0 = c0 == ' ' || (c0 >= 9 && c0 <= 13);
         bool dig0 = c0 >= '0' && c0 <= '9';
         bool hex0 = dig0 || ((c0 | 32) >= 'a' && (c0 | 32) <= 'f');
@@ -978,7 +980,13 @@ void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const 
     const int ok = t_origin_kind, oi = t_origin_idx;
     auto has = [&](const char* n) { return in.requested.count(n) > 0; };
     auto set_origin = [](int k, int x) { t_origin_kind = k; t_origin_idx = x; };
-    auto line_ref = [&](uint64_t r) { return mstr((ref_arena(r) ? c.arena : c.line) + ref_off(r), ref_len(r)); };
+    auto line_ref = [&](uint64_t r) {
+        if (ref_amp(r)) {  // '&' + line bytes (rawQuery delivered without a copy)
+            c.pool.emplace_back("&" + std::string((const char*)c.line + ref_off(r), ref_len(r)));
+            return mstr((const uint8_t*)c.pool.back().data(), (uint32_t)c.pool.back().size());
+        }
+        return mstr((ref_arena(r) ? c.arena : c.line) + ref_off(r), ref_len(r));
+    };
     switch (in.cls) {
     case D_TIMESTAMP: {
         if (v.null || v.len == 0) return;

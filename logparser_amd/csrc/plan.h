@@ -81,7 +81,7 @@ struct HostResults {
     std::vector<std::vector<uint64_t>> t_local, t_utc;
     std::vector<std::vector<uint32_t>> fl_kind, fl_method, fl_uri, fl_proto;
     std::vector<std::vector<uint32_t>> u_flags;
-    std::vector<std::vector<uint64_t>> u_scheme, u_host, u_path, u_query, u_frag, u_userinfo;
+    std::vector<std::vector<uint64_t>> u_scheme, u_host, u_path, u_query, u_frag;
     std::vector<std::vector<int32_t>> u_port;
     std::vector<std::vector<uint32_t>> q_count;
     std::vector<std::vector<uint64_t>> q_params;

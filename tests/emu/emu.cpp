@@ -40,9 +40,28 @@ int emu_describe(void* h, char* out, int cap) {
     return (int)d.size();
 }
 
+static int parse_impl(Emu* e, const char* line, int len, const uint8_t* base, uint32_t base_off, char* out, int cap);
+
 // returns line status (0 OK, 1 BAD, 2 FALLBACK), fills out with the record JSON when OK
 int emu_parse(void* h, const char* line, int len, char* out, int cap) {
-    Emu* e = (Emu*)h;
+    // the line at a varying offset of a 4-byte aligned base, as inside the
+    // kernel's LDS window (exercises the word-at-a-time scanners' edges)
+    const uint32_t off = (uint32_t)(len * 7 + (len > 0 ? (uint8_t)line[0] : 0)) & 3u;
+    std::vector<uint8_t> padded(off, 0xFF);
+    padded.insert(padded.end(), line, line + len);
+    padded.push_back('\n');
+    padded.resize(padded.size() + 8, 0xFF);  // word reads of the last bytes
+    return parse_impl((Emu*)h, line, len, padded.data(), off, out, cap);
+}
+
+// the line is buf[start, start+len) of a whole batch buffer (as the kernel
+// sees it: neighbouring lines around it); buf must be 4-byte aligned and
+// readable up to the next multiple of 4 after the line
+int emu_parse_in(void* h, const char* buf, int64_t start, int len, char* out, int cap) {
+    return parse_impl((Emu*)h, buf + start, len, (const uint8_t*)buf, (uint32_t)start, out, cap);
+}
+
+static int parse_impl(Emu* e, const char* line, int len, const uint8_t* base, uint32_t base_off, char* out, int cap) {
     if (!e->plan.device_ok()) return 2;
     const Program& P = e->plan.program();
     HostResults R;
@@ -58,7 +77,7 @@ int emu_parse(void* h, const char* line, int len, char* out, int cap) {
     R.t_utc.assign(MAX_TIME, std::vector<uint64_t>(1));
     for (auto* v : {&R.fl_kind, &R.fl_method, &R.fl_uri, &R.fl_proto}) v->assign(MAX_FL, std::vector<uint32_t>(1));
     R.u_flags.assign(MAX_URI, std::vector<uint32_t>(1));
-    for (auto* v : {&R.u_scheme, &R.u_host, &R.u_path, &R.u_query, &R.u_frag, &R.u_userinfo})
+    for (auto* v : {&R.u_scheme, &R.u_host, &R.u_path, &R.u_query, &R.u_frag})
         v->assign(MAX_URI, std::vector<uint64_t>(1));
     R.u_port.assign(MAX_URI, std::vector<int32_t>(1));
     R.q_count.assign(MAX_QUERY, std::vector<uint32_t>(1));
@@ -75,13 +94,13 @@ int emu_parse(void* h, const char* line, int len, char* out, int cap) {
     for (int u = 0; u < MAX_URI; ++u) {
         C.u_flags[u] = R.u_flags[u].data(); C.u_scheme[u] = R.u_scheme[u].data(); C.u_host[u] = R.u_host[u].data();
         C.u_port[u] = R.u_port[u].data(); C.u_path[u] = R.u_path[u].data(); C.u_query[u] = R.u_query[u].data();
-        C.u_frag[u] = R.u_frag[u].data(); C.u_userinfo[u] = R.u_userinfo[u].data();
+        C.u_frag[u] = R.u_frag[u].data();
     }
     for (int q = 0; q < MAX_QUERY; ++q) { C.q_count[q] = R.q_count[q].data(); C.q_params[q] = R.q_params[q].data(); }
-    Line L{(const uint8_t*)R.input.data(), len};
+    Line L{base, base_off, len};
     LineOut o;
     uint32_t stk[MAX_STACK];
-    phase1(P, L, o, stk, C, 0);
+    phase1(P, P.elems, L, o, stk, C, 0);
     if (o.status == ST_OK && o.arena_need) {
         R.arena.assign(o.arena_need + 64, 0);
         Arena A{R.arena.data(), 0, o.arena_need};

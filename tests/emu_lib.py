@@ -34,6 +34,9 @@ def lib():
         L.emu_free.argtypes = [ctypes.c_void_p]
         L.emu_parse.restype = ctypes.c_int
         L.emu_parse.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        L.emu_parse_in.restype = ctypes.c_int
+        L.emu_parse_in.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_char_p,
+                                   ctypes.c_int]
         L.emu_describe.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]
         L.emu_possible_paths.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
         _lib = L
@@ -66,6 +69,23 @@ class Emu:
             line = line.encode("utf-8")
         st = lib().emu_parse(self.h, line, len(line), self.buf, len(self.buf))
         return st, (self.buf.value.decode("utf-8") if st in (0, 3) else None)
+
+    def parse_batch_raw(self, data):
+        """Every '\\n'-terminated line of data, each parsed in place inside the
+        whole buffer (neighbouring bytes around it, as in the kernel's LDS
+        window).  Returns [(status, json or None)]."""
+        n = len(data)
+        buf = ctypes.create_string_buffer(data + b"\0" * 16, n + 16)
+        assert ctypes.addressof(buf) % 4 == 0
+        out, start = [], 0
+        while start < n:
+            end = data.find(b"\n", start)
+            if end < 0:
+                end = n
+            st = lib().emu_parse_in(self.h, ctypes.addressof(buf), start, end - start, self.buf, len(self.buf))
+            out.append((st, self.buf.value.decode("utf-8") if st in (0, 3) else None))
+            start = end + 1
+        return out
 
     def describe(self):
         b = ctypes.create_string_buffer(1 << 16)

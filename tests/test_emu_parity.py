@@ -118,3 +118,23 @@ def test_other_formats_emulated(oracle, emu, fmt):
         lines.append(l)
         lines.append(mutate(rng, l))
     compare(o, e, lines)
+
+
+def test_lines_in_batch_context_emulated(oracle, emu, vectors, demolog_lines):
+    """Lines parsed in place inside a whole batch buffer (arbitrary 4-byte
+    phase, neighbouring lines' bytes in the scanned words) give the same
+    records as lines parsed alone."""
+    groups = {}
+    for c in vectors["cases"]:
+        groups.setdefault((c["logformat"], tuple(c["fields"])), []).append(c["line"].encode())
+    groups[("combined", tuple(all_paths(oracle)))] = demolog_lines[:400] + lpa.synth_combined(8, 0, 400).split(b"\n")[:-1]
+    for (fmt, fields), lines in groups.items():
+        e = emu.Emu(fmt, list(fields))
+        if e.status != 0:
+            continue
+        for pad in range(4):
+            data = b"x" * pad + b"\n" + b"\n".join(lines) + b"\n"
+            got = e.parse_batch_raw(data)[1:]
+            assert len(got) == len(lines)
+            for l, (st, js) in zip(lines, got):
+                assert (st, js) == e.parse_raw(l), (fmt, l)
