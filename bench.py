@@ -113,6 +113,8 @@ def main():
     ap.add_argument("--cpu-sample-lines", type=int, default=2_000_000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--fields", default="all",
+                    help="all (the config-2 workload) | comma list of TYPE:path (profiling experiments only)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic_latest.json"),
                     help="tools/pmc_traffic.py summary of separate rocprofv3 --pmc passes; fills roofline.traffic "
                          "when it was taken on this workload with this exact engine build")
@@ -131,7 +133,7 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
 
-    fields = lpa.get_possible_paths("combined")
+    fields = lpa.get_possible_paths("combined") if args.fields == "all" else args.fields.split(",")
     log("rank %d/%d: generating %d lines (seed %d) on %s" % (rank, world, args.lines, SEED, device))
     buf, nbytes = generate_to_device(lpa, torch, rank * args.lines, args.lines, device)
     log("input resident in HBM: %.2f GB" % (nbytes / 1e9))

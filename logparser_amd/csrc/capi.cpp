@@ -291,7 +291,7 @@ int lp_parse_batch(lp_handle* h, const uint8_t* buf, uint64_t nbytes, int buf_fl
         if (hipMemcpyAsync(h->args.p, &h->host_args, sizeof(lp::DeviceArgs), hipMemcpyHostToDevice, s) != hipSuccess)
             return LP_E_DEVICE;
         hipEventRecord(h->ev[2], s);
-        if (lp::launch_parse(h->d_buf, nbytes, n, h->args.as<lp::DeviceArgs>(), C.wave_counts,
+        if (lp::launch_parse(h->d_buf, nbytes, n, h->args.as<lp::DeviceArgs>(), P.max_stack, C.wave_counts,
                              h->misc.as<unsigned long long>(), s) != 0)
             return LP_E_DEVICE;
     } else {

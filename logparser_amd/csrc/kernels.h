@@ -23,7 +23,7 @@ int launch_offsets(const uint8_t* d_buf, uint64_t nbytes, const uint64_t* d_chun
 constexpr int WC_WORDS = 8;
 int64_t parse_waves(int64_t n_lines);
 // parse every line, then counters[0..4] += lines, ok, bad, fallback, arena bytes written
-int launch_parse(const uint8_t* d_buf, uint64_t nbytes, int64_t n_lines, const DeviceArgs* d_args,
+int launch_parse(const uint8_t* d_buf, uint64_t nbytes, int64_t n_lines, const DeviceArgs* d_args, int stack_depth,
                  const uint32_t* d_wave_counts, unsigned long long* counters, hipStream_t s);
 
 }  // namespace lp

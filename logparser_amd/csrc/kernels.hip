@@ -13,6 +13,8 @@
 // scaffolding around it.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "kernels.h"
 #include "lp_device.h"
 
@@ -119,7 +121,6 @@ __global__ __launch_bounds__(NL_THREADS) void k_line_offsets(const uint8_t* __re
 // lane runs the per-line stages of lp_device.h on its own line out of LDS.
 // Windows larger than the LDS budget (very long lines) read HBM directly.
 constexpr int PW = 64;
-constexpr int STK_WORDS = MAX_STACK * PW;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
@@ -183,14 +184,15 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
 }
 
 __global__ __launch_bounds__(PW) void k_parse_lines(const uint8_t* __restrict__ buf, uint64_t nbytes, int64_t n_lines,
-                                                    const DeviceArgs* __restrict__ args, uint32_t win_cap, int stage) {
+                                                    const DeviceArgs* __restrict__ args, uint32_t win_cap, int stage,
+                                                    uint32_t stk_words) {
     const Program& P = args->prog;
     const Columns& C = args->cols;
     __shared__ Elem s_elems[MAX_ELEMS];
     if ((int)threadIdx.x < P.n_elems) s_elems[threadIdx.x] = P.elems[threadIdx.x];
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     WaveStack stk{reinterpret_cast<uint32_t*>(smem) + threadIdx.x};
-    uint8_t* win = smem + STK_WORDS * 4;
+    uint8_t* win = smem + stk_words * 4;
     const int lane = threadIdx.x;
     const int64_t li0 = (int64_t)blockIdx.x * PW;
     const int64_t li = li0 + lane;
@@ -222,9 +224,11 @@ __global__ __launch_bounds__(PW) void k_parse_lines(const uint8_t* __restrict__ 
         parse_wave(P, s_elems, C, (lds_bytes)win, (uint32_t)(s - w0), n, active, li, stk);
     } else {
         __syncthreads();
-        // aligned-down base: word reads never cross the 4-byte word of a valid byte
-        const uintptr_t mis = (uintptr_t)buf & 3;
-        parse_wave(P, s_elems, C, buf - mis, (uint32_t)(s + mis), n, active, li, stk);
+        // base = the line start aligned down to 4 bytes: word reads never
+        // leave the 4-byte words holding the line's bytes
+        const uint8_t* ls = buf + s;
+        const uint32_t mis = (uint32_t)((uintptr_t)ls & 3);
+        parse_wave(P, s_elems, C, ls - mis, mis, n, active, li, stk);
     }
 }
 
@@ -272,7 +276,7 @@ int launch_offsets(const uint8_t* d_buf, uint64_t nbytes, const uint64_t* d_chun
 
 int64_t parse_waves(int64_t n_lines) { return (n_lines + PW - 1) / PW; }
 
-int launch_parse(const uint8_t* d_buf, uint64_t nbytes, int64_t n_lines, const DeviceArgs* d_args,
+int launch_parse(const uint8_t* d_buf, uint64_t nbytes, int64_t n_lines, const DeviceArgs* d_args, int stack_depth,
                  const uint32_t* d_wave_counts, unsigned long long* counters, hipStream_t s) {
     if (n_lines == 0) return 0;
     const int64_t waves = parse_waves(n_lines);
@@ -280,13 +284,19 @@ int launch_parse(const uint8_t* d_buf, uint64_t nbytes, int64_t n_lines, const D
     // nearly every wave stages; at most 60 KiB.  A window that does not fit
     // reads HBM directly.
     const uint64_t mean = (nbytes + n_lines - 1) / n_lines;
-    uint64_t cap = (PW * mean * 13) / 10 + 1024;
+    // tuning knobs for profiling experiments (defaults are the product setting)
+    const char* e1 = getenv("LP_WIN_PCT");
+    const char* e2 = getenv("LP_NO_STAGE");
+    const int win_pct = e1 ? atoi(e1) : 110;
+    const int force_global = e2 ? atoi(e2) : 0;
+    uint64_t cap = (PW * mean * (uint64_t)win_pct) / 100 + 512;
     if (cap > 60 * 1024) cap = 60 * 1024;
     cap = (cap + 15) & ~15ull;
-    const int stage = ((uintptr_t)d_buf & 15) == 0;
-    const size_t lds = STK_WORDS * 4 + cap;
+    const int stage = ((uintptr_t)d_buf & 15) == 0 && !force_global;
+    const uint32_t stk_words = (uint32_t)(stack_depth > 0 ? stack_depth : 1) * PW;
+    const size_t lds = stk_words * 4 + cap;
     hipLaunchKernelGGL(k_parse_lines, dim3((unsigned)waves), dim3(PW), lds, s, d_buf, nbytes, n_lines, d_args,
-                       (uint32_t)cap, stage);
+                       (uint32_t)cap, stage, stk_words);
     int64_t rb = (waves + 255) / 256;
     if (rb > 1024) rb = 1024;
     hipLaunchKernelGGL(k_reduce_counts, dim3((unsigned)rb), dim3(256), 0, s, d_wave_counts, waves, counters);

@@ -241,6 +241,18 @@ __host__ __device__ LP_INLINE int ipv4_first(const LN& L, int p) {
     return q;
 }
 
+// Position of the k-th byte c (k >= 1) counted from the end of the line
+// within [lo, n), or -1.
+template <typename LN>
+__host__ __device__ LP_INLINE int kth_from_end(const LN& L, uint32_t c, int k, int lo) {
+    int q = L.n - 1;
+    for (;;) {
+        q = find_bwd(L, q, lo, [c](uint32_t w) { return swar::eq(w, c); });
+        if (q < 0 || --k == 0) return q;
+        --q;
+    }
+}
+
 // Occurrence of e's following literal: the last one starting in [lo, hi]
 // (greedy order) or the first one starting in [lo, hi] (lazy order); -1 none.
 template <typename LN>
@@ -290,7 +302,10 @@ __host__ __device__ LP_INLINE int cand_first(const Program& P, const Elem& e, co
     case EK_ANY_GREEDY: {
         if (e.last) return L.n;
         if (!e.nlit) return L.n;
-        return lit_last(P, L, e, L.n - 1, p);
+        // candidates past the need-th copy of the literal's first byte from
+        // the end cannot be followed by the rest of the format
+        const int hi = e.need > 1 ? kth_from_end(L, e.lit4 & 0xFFu, e.need, p) : L.n - 1;
+        return hi < 0 ? -1 : lit_last(P, L, e, hi, p);
     }
     case EK_ANY_LAZY: {
         if (e.last) return L.n;
@@ -337,7 +352,7 @@ __host__ __device__ LP_INLINE int cand_next(const Program& P, const Elem& e, con
 }
 
 // Backtracking match of "^" elems "$" with java.util.regex priority
-// semantics.  caps = spans of the captured tokens.  stk: MAX_STACK scratch.
+// semantics.  caps = spans of the captured tokens.  stk: P.max_stack entries.
 // elems: the program's element table (the kernel passes an LDS copy).
 template <typename LN, typename EL, typename Caps, typename Stk>
 __host__ __device__ LP_INLINE int match_line(const Program& P, const EL& elems, const LN& L, Caps& caps, Stk stk) {
@@ -363,7 +378,7 @@ __host__ __device__ LP_INLINE int match_line(const Program& P, const EL& elems, 
                 if (ok) {
                     if (e.cap >= 0) caps.set(e.cap, mkspan(pos, c));
                     if (!e.det) {
-                        if (sp == MAX_STACK) return ST_FALLBACK;
+                        if (sp >= P.max_stack) return ST_FALLBACK;  // cannot happen: one entry per non-det element
                         stk[sp++] = (uint32_t)i | ((uint32_t)pos << 6) | ((uint32_t)c << 19);
                     }
                     pos = c;

@@ -67,7 +67,8 @@ struct Elem {
     uint16_t lit_off;  // EK_LIT: own literal; tokens: following literal (if nlit)
     uint16_t lit_len;
     uint8_t nlit;      // token followed by a literal
-    uint8_t pad[3];
+    uint8_t need;      // ANY_GREEDY: occurrences of the literal's first byte in the literals from here to '$'
+    uint8_t pad[2];
     uint32_t lit4;     // first (up to) 4 bytes of that literal, little-endian
 };
 
@@ -114,6 +115,7 @@ struct Program {
     int32_t n_time, n_fl, n_uri, n_query;
     int32_t apache;       // 1 = Apache decodeExtractedValue rules, 0 = NGINX
     int32_t tok_decode;   // bitmask: token slots whose value goes through decodeExtractedValue
+    int32_t max_stack;    // DFS depth bound = number of non-deterministic elements (<= MAX_STACK)
     Elem elems[MAX_ELEMS];
     TimeStage time[MAX_TIME];
     FlStage fl[MAX_FL];

@@ -794,6 +794,23 @@ void Plan::compile_program() {
         default: e.det = 0; break;
         }
     }
+    // greedy '.*' candidates are occurrences of the following literal; one
+    // can only lead to a match if the rest of the line still holds every
+    // later literal's copy of that literal's first byte (pruning, exact)
+    for (int i = 0; i < P.n_elems; ++i) {
+        Elem& e = P.elems[i];
+        if (e.kind != EK_ANY_GREEDY || !e.nlit) continue;
+        const uint8_t c0 = P.lit[e.lit_off];
+        int need = 0;
+        for (int j = i + 1; j < P.n_elems; ++j)
+            if (P.elems[j].kind == EK_LIT)
+                for (int k = 0; k < P.elems[j].lit_len; ++k) need += P.lit[P.elems[j].lit_off + k] == c0;
+        e.need = (uint8_t)(need > 255 ? 255 : need);
+    }
+    P.max_stack = 0;
+    for (int i = 0; i < P.n_elems; ++i)
+        if (P.elems[i].kind != EK_LIT && !P.elems[i].det) ++P.max_stack;
+    if (P.max_stack > MAX_STACK) { device_ok_ = false; why_ = "too many backtracking elements"; return; }
     // stages, walking the compiled tree from each captured token output
     std::function<void(int, int, const std::string&, const std::string&)> walk =
         [&](int ok, int oi, const std::string& type, const std::string& complete) {

@@ -157,3 +157,31 @@ def test_large_batch_properties(oracle):
         line = data[a:b]
         s1, js = o.parse_raw(line)
         assert s1 == 0 and js == r.record_json(i), i
+
+
+@pytest.mark.parametrize("staged", [True, False])
+def test_offsets_beyond_4gb(oracle, staged, monkeypatch):
+    """A 4.4 GB batch (a 1 MB block of synthetic lines repeated on the device):
+    every line OK, and lines stored past the 4 GiB mark match the oracle --
+    with the LDS-window path and with the direct-HBM path (LP_NO_STAGE=1)."""
+    import torch
+    if not staged:
+        monkeypatch.setenv("LP_NO_STAGE", "1")
+    block = lpa.synth_combined(31, 0, 4096)
+    reps = 4_400_000_000 // len(block) + 1
+    dev = torch.frombuffer(bytearray(block), dtype=torch.uint8).cuda().repeat(reps)
+    p = lpa.HttpdLoglineParser("combined", paths(oracle))
+    r = p.parse_batch(dev)
+    n = 4096 * reps
+    assert r.n_lines == n
+    assert r.counters == {"lines": n, "ok": n, "bad": 0, "fallback": 0}
+    lines = block.split(b"\n")[:-1]
+    o = oracle.Oracle("combined", paths(oracle))
+    rng = random.Random(9)
+    first_past = (2 ** 32 // len(block) + 1) * 4096
+    for i in sorted(rng.sample(range(first_past, n), 40)):
+        assert r.line_offset(i) >= 2 ** 32
+        s1, js = o.parse_raw(lines[i % 4096])
+        assert s1 == 0 and js == r.record_json(i), i
+    del dev
+    torch.cuda.empty_cache()
