@@ -131,12 +131,14 @@ struct WaveStack {  // per-lane DFS stack, lane-interleaved (conflict-free)
 
 template <typename Ptr>
 __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, const Columns& C, Ptr base, uint32_t off,
-                                           int n, bool active, int64_t li, WaveStack stk) {
+                                           int n, bool active, int64_t li, WaveStack stk, bool clean) {
     LineT<Ptr> L{base, off, n};
     LineOut o;
     o.status = ST_OK;
     o.arena_need = 0;
-    if (active) phase1(P, elems, L, o, stk, C, li);
+    LP_PROF(1);
+    if (active) phase1(P, elems, L, o, stk, C, li, clean);
+    LP_PROF(9);
     // wave-aggregated arena allocation (every lane reaches this point)
     const uint32_t need = (active && o.status == ST_OK) ? o.arena_need : 0u;
     const int lane = threadIdx.x;
@@ -163,8 +165,10 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
         } else if (o.status == ST_OK) {
             C.arena_base[li] = 0;
         }
+        LP_PROF(20);
         write_line(P, o, C, li);
     }
+    LP_PROF(21);
     for (int d = 32; d > 0; d >>= 1) written += __shfl_xor(written, d);
     const uint64_t m_act = __ballot(active);
     const uint64_t m_ok = __ballot(active && o.status == ST_OK);
@@ -207,8 +211,10 @@ __global__ __launch_bounds__(PW) void k_parse_lines(const uint8_t* __restrict__ 
     const uint64_t w0 = C.line_off[li0] & ~15ull;
     uint64_t w1 = C.line_off[lend];
     if (w1 > nbytes) w1 = nbytes;
+    LP_PROF(0);
     if (stage && w1 - w0 <= win_cap) {
         const int nv = (int)((w1 - w0 + 15) >> 4);
+        uint32_t bad = 0;  // guard-failing bytes other than '\n' anywhere in the window
         for (int k = lane; k < nv; k += PW) {
             const uint64_t p = w0 + 16ull * k;
             u32x4 v;
@@ -219,16 +225,18 @@ __global__ __launch_bounds__(PW) void k_parse_lines(const uint8_t* __restrict__ 
                 for (int j = 0; j < 16 && p + j < nbytes; ++j) v[j >> 2] |= (uint32_t)buf[p + j] << (8 * (j & 3));
             }
             *reinterpret_cast<u32x4*>(win + 16 * k) = v;
+            for (int j = 0; j < 4; ++j) bad |= swar::guard_bad(v[j]) & ~swar::eq(v[j], '\n');
         }
+        const bool clean = !__any(bad != 0);
         __syncthreads();
-        parse_wave(P, s_elems, C, (lds_bytes)win, (uint32_t)(s - w0), n, active, li, stk);
+        parse_wave(P, s_elems, C, (lds_bytes)win, (uint32_t)(s - w0), n, active, li, stk, clean);
     } else {
         __syncthreads();
         // base = the line start aligned down to 4 bytes: word reads never
         // leave the 4-byte words holding the line's bytes
         const uint8_t* ls = buf + s;
         const uint32_t mis = (uint32_t)((uintptr_t)ls & 3);
-        parse_wave(P, s_elems, C, ls - mis, mis, n, active, li, stk);
+        parse_wave(P, s_elems, C, ls - mis, mis, n, active, li, stk, false);
     }
 }
 
@@ -275,6 +283,19 @@ int launch_offsets(const uint8_t* d_buf, uint64_t nbytes, const uint64_t* d_chun
 }
 
 int64_t parse_waves(int64_t n_lines) { return (n_lines + PW - 1) / PW; }
+
+#if defined(LP_PROFILE)
+// profiling build: copy out (and clear) the per-point timestamp sums
+extern "C" int lp_profile_read(unsigned long long* out, int n) {
+    unsigned long long h[64 * 16];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_prof), sizeof h) != hipSuccess) return -1;
+    for (int k = 0; k < n && k < 64; ++k) { out[2 * k] = h[k * 16]; out[2 * k + 1] = h[k * 16 + 1]; }
+    hipMemset(nullptr, 0, 0);
+    unsigned long long z[64 * 16] = {};
+    hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof z);
+    return 0;
+}
+#endif
 
 int launch_parse(const uint8_t* d_buf, uint64_t nbytes, int64_t n_lines, const DeviceArgs* d_args, int stack_depth,
                  const uint32_t* d_wave_counts, unsigned long long* counters, hipStream_t s) {

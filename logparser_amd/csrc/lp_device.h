@@ -18,6 +18,23 @@ namespace lp {
 
 enum : int { ST_OK = 0, ST_BAD = 1, ST_FALLBACK = 2 };
 
+// Profiling build only (-DLP_PROFILE): wave timestamps at fixed points,
+// summed per point; differences of the sums = cycles spent between points.
+#if defined(LP_PROFILE) && defined(__HIP__)
+__device__ unsigned long long g_prof[64 * 16];
+#endif
+#if defined(LP_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
+__device__ __forceinline__ void lp_prof_mark(int k) {
+    const unsigned long long t = clock64();
+    const uint64_t act = __ballot(1);
+    if ((int)threadIdx.x % 64 == (int)__builtin_ctzll(act)) atomicAdd(&g_prof[k * 16], t);
+    if ((int)threadIdx.x % 64 == (int)__builtin_ctzll(act)) atomicAdd(&g_prof[k * 16 + 1], 1ull);
+}
+#define LP_PROF(k) lp_prof_mark(k)
+#else
+#define LP_PROF(k)
+#endif
+
 // ----------------------------------------------------------- byte classes
 __host__ __device__ LP_INLINE bool is_ws(uint32_t c) { return c == ' ' || (c >= 9 && c <= 13); }      // \s
 __host__ __device__ LP_INLINE bool is_digit(uint32_t c) { return c - '0' < 10u; }
@@ -66,6 +83,11 @@ struct LineT {
     __host__ __device__ LP_INLINE uint32_t operator[](int i) const { return b[o + i]; }
     // aligned 32-bit word w of the base (little-endian: byte k at bits 8k..8k+7)
     __host__ __device__ LP_INLINE uint32_t word(uint32_t w) const { return load_word(b + 4 * w); }
+    // word w if it still holds bytes of the line, else 0 (look-ahead reads
+    // never leave the line's words)
+    __host__ __device__ LP_INLINE uint32_t word_or0(uint32_t w) const {
+        return 4 * w < o + (uint32_t)n ? load_word(b + 4 * w) : 0u;
+    }
 };
 using Line = LineT<const uint8_t*>;
 
@@ -153,6 +175,23 @@ __host__ __device__ LP_INLINE uint32_t count_in(const LN& L, int a, int b, F cls
         c += (uint32_t)swar::count(m);
     }
     return c;
+}
+
+// URIUtil-escaped bytes and '&'/'?' separators in [a, b), one pass.
+template <typename LN>
+__host__ __device__ LP_INLINE void count2_in(const LN& L, int a, int b, uint32_t& enc, uint32_t& sep) {
+    enc = sep = 0;
+    if (a >= b) return;
+    const uint32_t A = L.o + (uint32_t)a, E = L.o + (uint32_t)b;
+    const uint32_t W0 = A >> 2, W1 = (E - 1) >> 2;
+    for (uint32_t W = W0; W <= W1; ++W) {
+        const uint32_t w = L.word(W);
+        uint32_t keep = swar::HI;
+        if (W == W0) keep &= swar::HI << (8 * (A & 3));
+        if (W == W1) keep &= swar::HI >> (8 * (3 - ((E - 1) & 3)));
+        enc += (uint32_t)swar::count(swar::needs_encode(w) & keep);
+        sep += (uint32_t)swar::count((swar::eq(w, '&') | swar::eq(w, '?')) & keep);
+    }
 }
 
 // Small per-line array kept in registers: every element access in the source
@@ -515,6 +554,7 @@ struct LineOut {
     RegArr<MAX_TOK> caps;
     uint32_t tok_flags;
     RegArr<MAX_FL> fl_kind, fl_method, fl_uri, fl_proto;
+    RegArr<MAX_URI> usep;  // '&' + '?' count of each URI source (query table bound)
     uint32_t arena_need;
 };
 
@@ -548,9 +588,11 @@ __host__ __device__ LP_INLINE bool uri_source(const Program& P, const LineOut& o
 }
 
 // Phase 1: guard, match, tokens, time, first line; arena need for phase 2.
+// clean: the caller already proved every byte of the line passes the
+// fast-path guard (the kernel checks the whole staged window at once).
 template <typename LN, typename EL, typename Stk, typename Cols>
 __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, const LN& L, LineOut& o, Stk stk, Cols& C,
-                                          int64_t li) {
+                                          int64_t li, bool clean = false) {
     o.status = ST_OK;
     o.tok_flags = 0;
     o.arena_need = 0;
@@ -559,11 +601,18 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
     o.fl_method.fill(0);
     o.fl_uri.fill(0);
     o.fl_proto.fill(0);
+    o.usep.fill(0);
     if (L.n > MAX_LINE) { o.status = ST_FALLBACK; return; }
     // fast-path guard: printable ASCII + TAB only (no \r, no line
     // terminators, no bytes that need UTF-8 decoding or URIUtil UTF-8 bytes)
-    if (find_fwd(L, 0, L.n, [](uint32_t w) { return swar::guard_bad(w); }) < L.n) { o.status = ST_FALLBACK; return; }
+    LP_PROF(2);
+    if (!clean && find_fwd(L, 0, L.n, [](uint32_t w) { return swar::guard_bad(w); }) < L.n) {
+        o.status = ST_FALLBACK;
+        return;
+    }
+    LP_PROF(3);
     int st = match_line(P, elems, L, o.caps, stk);
+    LP_PROF(4);
     if (st != ST_OK) { o.status = st; return; }
     // decodeExtractedValue: "-" -> null (Apache: ApacheHttpdLogFormatDissector.java:169-196,
     // NGINX: NginxHttpdLogFormatDissector.java:107-119)
@@ -579,6 +628,7 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
             if (find_fwd(L, a, b, [](uint32_t w) { return swar::eq(w, '\\'); }) < b) { o.status = ST_FALLBACK; return; }
         }
     }
+    LP_PROF(5);
     // TimeStampDissector
     for (int t = 0; t < P.n_time; ++t) {
         int k = P.time[t].tok;
@@ -589,6 +639,7 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
         C.t_local[t][li] = lo;
         C.t_utc[t][li] = ut;
     }
+    LP_PROF(6);
     // HttpFirstLineDissector: ^([a-zA-Z-_]+) (.*) (HTTP/[0-9]+\.[0-9]+)$ else ^([a-zA-Z-_]+) (.*)$
     for (int f = 0; f < P.n_fl; ++f) {
         int k = P.fl[f].tok;
@@ -625,13 +676,15 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
             o.fl_proto.set(f, 0);
         }
     }
+    LP_PROF(7);
     // arena need of the URI / query stages (upper bound of phase-2 writes)
     uint32_t need = 0;
     for (int u = 0; u < P.n_uri; ++u) {
         int a, b;
         if (!uri_source(P, o, u, a, b)) continue;
-        const uint32_t enc = count_in(L, a, b, [](uint32_t w) { return swar::needs_encode(w); });
-        const uint32_t sep = count_in(L, a, b, [](uint32_t w) { return swar::eq(w, '&') | swar::eq(w, '?'); });
+        uint32_t enc = 0, sep = 0;
+        count2_in(L, a, b, enc, sep);
+        o.usep.set(u, sep);
         const UriStage& U = P.uri[u];
         uint32_t ulen = (uint32_t)(b - a), tl = ulen + 2 * enc + 2;
         uint32_t n = 16;
@@ -642,6 +695,7 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
         need += n;
     }
     o.arena_need = (need + 15) & ~15u;
+    LP_PROF(8);
 }
 
 // ------------------------------------------------------------ URI stage
@@ -749,127 +803,223 @@ __host__ __device__ LP_INLINE void put_encoded(Arena& A, uint32_t c) {
     A.put(HX[c & 15]);
 }
 
-// QueryStringFieldDissector (QueryStringFieldDissector.java:56-108) on the
-// rawQuery of a URI stage, read straight from the line bytes [qa, qb) (the
-// text after the first '?', up to '#').  The rawQuery is "&" + that text
-// with '?' -> '&' and URIUtil escapes, so its '&'-pieces are the pieces of
-// the line text split at '&' and '?'.  Names are the pieces' (escaped,
-// lower-cased) text before '='; values go through resilientUrlDecode.  A
-// name or value equal to line bytes is delivered as a line ref; only
-// rewritten strings are written to the arena.
+// Utils.resilientUrlDecode of line bytes [vs, e) into the arena: every '%'
+// here is followed by two hex digits (URI stage guard), so each %XX is the
+// Latin-1 char U+00XX (VALID_STANDARD -> %00%XX, UTF-16 decode), '+' is a
+// space, and URIUtil escapes decode back to their byte.  Output UTF-8.
+// Bytes come from a two-word register window (one LDS read per 4 bytes).
+template <typename LN>
+__host__ __device__ LP_INLINE uint64_t url_decode_value(const LN& L, int vs, int e, Arena& A) {
+    const uint32_t st = A.used;
+    uint32_t W = (L.o + (uint32_t)vs) >> 2;
+    uint64_t ww = (uint64_t)L.word(W) | ((uint64_t)L.word_or0(W + 1) << 32);
+    for (int q = vs; q < e;) {
+        const uint32_t k = L.o + (uint32_t)q - 4 * W;  // 0..3
+        const uint32_t c = (uint32_t)(ww >> (8 * k)) & 0xFFu;
+        if (c == '%') {
+            const uint32_t v = hexv((uint32_t)(ww >> (8 * k + 8)) & 0xFFu) * 16 + hexv((uint32_t)(ww >> (8 * k + 16)) & 0xFFu);
+            if (v < 0x80) A.put(v);
+            else { A.put(0xC0 | (v >> 6)); A.put(0x80 | (v & 0x3F)); }
+            q += 3;
+        } else {
+            A.put(c == '+' ? ' ' : c);
+            ++q;
+        }
+        if (L.o + (uint32_t)q >= 4 * (W + 1)) {
+            ++W;
+            ww = (ww >> 32) | ((uint64_t)L.word_or0(W + 1) << 32);
+        }
+    }
+    return mkref(st, A.used - st, true);
+}
+
+// Values whose decoding is deferred until the query scan is done, so the
+// byte loops of all lanes run side by side instead of one lane at a time.
+struct DeferredDecodes {
+    RegArr<8> span;  // value start | end << 16
+    RegArr<8> slot;  // index of the (name, value) table entry
+    uint32_t n;
+};
+
+// One '&'-piece of the rawQuery (line bytes [s, e), '=' at eq or -1):
+// QueryStringFieldDissector.java:75-104.  rw: the name holds upper-case or
+// URIUtil-escaped bytes; pv: the value holds '%' or '+'.
+template <typename LN>
+__host__ __device__ LP_INLINE void query_piece(const Program& P, const QueryStage& Q, const LN& L, int s, int e, int eq,
+                                               bool rw, bool pv, Arena& A, uint32_t tab, uint32_t& count,
+                                               DeferredDecodes& dd) {
+    const int ne = eq >= 0 ? eq : e;
+    // name [s, ne): URIUtil-escaped and lower-cased as in the rawQuery
+    const uint32_t mark = A.used;
+    uint64_t nref;
+    if (rw) {
+        const char* HX = "0123456789abcdef";  // URIUtil's %XX, lower-cased with the name
+        for (int q = s; q < ne; ++q) {
+            uint32_t c = L[q];
+            if (uri_needs_encode(c)) { A.put('%'); A.put(HX[c >> 4]); A.put(HX[c & 15]); }
+            else A.put((c - 'A') < 26u ? (c | 32) : c);
+        }
+        nref = mkref(mark, A.used - mark, true);
+    } else {
+        nref = mkref(s, ne - s, false);
+    }
+    // requested?  (wantAllFields || requestedParameters.contains(name))
+    bool want = Q.want_all;
+    const uint32_t nlen = ref_len(nref);
+    for (int k = 0; k < Q.n_names && !want; ++k) {
+        if (Q.name_len[k] != nlen) continue;
+        bool same = true;
+        for (uint32_t q = 0; q < nlen && same; ++q) {
+            uint32_t c = rw ? (uint32_t)A.p[mark + q] : L[s + (int)q];
+            same = c == P.lit[Q.name_off[k] + q];
+        }
+        want = same;
+    }
+    if (!want) {
+        A.used = mark;
+        return;
+    }
+    uint64_t vref;
+    if (eq < 0) vref = mkref(0, 0, false);  // no '=' -> ""
+    else if (!pv) vref = mkref(eq + 1, e - eq - 1, false);
+    else if (dd.n < 8) {
+        dd.span.set((int)dd.n, (uint32_t)(eq + 1) | ((uint32_t)e << 16));
+        dd.slot.set((int)dd.n, count);
+        ++dd.n;
+        vref = 0;  // filled in by query_pass
+    } else {
+        vref = url_decode_value(L, eq + 1, e, A);
+    }
+    uint64_t* t = (uint64_t*)(A.p + tab);
+    t[2 * count] = nref;
+    t[2 * count + 1] = vref;
+    ++count;
+}
+
+// The query part [qa, qb) of a URI, one word-at-a-time pass.  Returns
+// whether the rawQuery is "&" + these bytes unchanged (no further '?', no
+// URIUtil-escaped byte).  With qs >= 0 it also runs the
+// QueryStringFieldDissector (QueryStringFieldDissector.java:56-108): the
+// rawQuery's '&'-pieces are the pieces of [qa, qb) split at '&' and '?'.
 template <typename LN, typename Cols>
-__host__ __device__ LP_INLINE void query_stage(const Program& P, int qs, const LN& L, int qa, int qb, Arena& A, Cols& C,
-                                            int64_t li) {
-    const QueryStage& Q = P.query[qs];
-    const uint32_t npieces = 1 + count_in(L, qa, qb, [](uint32_t w) { return swar::eq(w, '&') | swar::eq(w, '?'); });
-    uint32_t tab = (A.used + 7) & ~7u;
-    A.used = tab + 16 * npieces;
-    uint32_t count = 0;
-    int s = qa;
-    while (s <= qb) {
-        const int e = find_fwd(L, s, qb, [](uint32_t w) { return swar::eq(w, '&') | swar::eq(w, '?'); });
-        if (e > s) {
-            const int eq = find_fwd(L, s, e, [](uint32_t w) { return swar::eq(w, '='); });
-            // name [s, eq): URIUtil-escaped and lower-cased as in the rawQuery
-            const bool rewrite =
-                find_fwd(L, s, eq, [](uint32_t w) { return swar::upper(w) | swar::needs_encode(w); }) < eq;
-            const uint32_t mark = A.used;
-            uint64_t nref;
-            if (rewrite) {
-                const char* HX = "0123456789abcdef";  // URIUtil's %XX, lower-cased with the name
-                for (int q = s; q < eq; ++q) {
-                    uint32_t c = L[q];
-                    if (uri_needs_encode(c)) { A.put('%'); A.put(HX[c >> 4]); A.put(HX[c & 15]); }
-                    else A.put((c - 'A') < 26u ? (c | 32) : c);
-                }
-                nref = mkref(mark, A.used - mark, true);
-            } else {
-                nref = mkref(s, eq - s, false);
+__host__ __device__ LP_INLINE bool query_pass(const Program& P, int qs, const LN& L, int qa, int qb, uint32_t max_pieces,
+                                              Arena& A, Cols& C, int64_t li) {
+    bool plain = true;
+    uint32_t tab = 0, count = 0;
+    if (qs >= 0) {
+        tab = (A.used + 7) & ~7u;
+        A.used = tab + 16 * max_pieces;
+    }
+    DeferredDecodes dd;
+    dd.n = 0;
+    dd.span.fill(0);
+    dd.slot.fill(0);
+    if (qa < qb) {
+        int s = qa, eqp = -1;
+        bool rw = false, pv = false;
+        const uint32_t AA = L.o + (uint32_t)qa, E = L.o + (uint32_t)qb;
+        const uint32_t W0 = AA >> 2, W1 = (E - 1) >> 2;
+        for (uint32_t W = W0; W <= W1; ++W) {
+            const uint32_t w = L.word(W);
+            uint32_t keep = swar::HI;
+            if (W == W0) keep &= swar::HI << (8 * (AA & 3));
+            if (W == W1) keep &= swar::HI >> (8 * (3 - ((E - 1) & 3)));
+            const uint32_t qm = swar::eq(w, '?') & keep;
+            const uint32_t sep = (swar::eq(w, '&') & keep) | qm;
+            const uint32_t enc = swar::needs_encode(w) & keep;
+            if (qs < 0) {
+                if (qm | enc) { plain = false; break; }
+                continue;
             }
-            // requested?  (wantAllFields || requestedParameters.contains(name))
-            bool want = Q.want_all;
-            const uint32_t nlen = ref_len(nref);
-            for (int k = 0; k < Q.n_names && !want; ++k) {
-                if (Q.name_len[k] != nlen) continue;
-                bool same = true;
-                for (uint32_t q = 0; q < nlen && same; ++q) {
-                    uint32_t c = rewrite ? (uint32_t)A.p[mark + q] : L[s + (int)q];
-                    same = c == P.lit[Q.name_off[k] + q];
+            const uint32_t eqm = swar::eq(w, '=') & keep;
+            const uint32_t rwm = (swar::upper(w) & keep) | enc;
+            const uint32_t pvm = (swar::eq(w, '%') | swar::eq(w, '+')) & keep;
+            if (qm | enc) plain = false;
+            uint32_t ev = sep | eqm | rwm | pvm;
+            while (ev) {
+                const int k = swar::first(ev);
+                const uint32_t bit = 0x80u << (8 * k);
+                const int pos = (int)((W << 2) + (uint32_t)k - L.o);
+                if (sep & bit) {
+                    if (pos > s) query_piece(P, P.query[qs], L, s, pos, eqp, rw, pv, A, tab, count, dd);
+                    s = pos + 1;
+                    eqp = -1;
+                    rw = pv = false;
+                } else if (eqm & bit) {
+                    if (eqp < 0) eqp = pos;
+                } else if (rwm & bit) {
+                    if (eqp < 0) rw = true;
+                } else if (eqp >= 0) {
+                    pv = true;
                 }
-                want = same;
-            }
-            if (!want) {
-                A.used = mark;
-            } else {
-                uint64_t vref;
-                if (eq == e) vref = mkref(0, 0, false);  // no '=' -> ""
-                else {
-                    const int vs = eq + 1;
-                    const bool plain = find_fwd(L, vs, e, [](uint32_t w) { return swar::eq(w, '%') | swar::eq(w, '+'); }) >= e;
-                    if (plain) vref = mkref(vs, e - vs, false);
-                    else {
-                        // Utils.resilientUrlDecode: every '%' here is followed by two
-                        // hex digits (URI stage guard), so each %XX is the Latin-1
-                        // char U+00XX (VALID_STANDARD -> %00%XX, UTF-16 decode), '+'
-                        // is a space, and URIUtil escapes decode back to their byte.
-                        // Output UTF-8.
-                        uint32_t st = A.used;
-                        for (int q = vs; q < e;) {
-                            uint32_t c = L[q];
-                            if (c == '+') { A.put(' '); ++q; }
-                            else if (c == '%') {
-                                uint32_t v = hexv(L[q + 1]) * 16 + hexv(L[q + 2]);
-                                if (v < 0x80) A.put(v);
-                                else { A.put(0xC0 | (v >> 6)); A.put(0x80 | (v & 0x3F)); }
-                                q += 3;
-                            } else { A.put(c); ++q; }
-                        }
-                        vref = mkref(st, A.used - st, true);
-                    }
-                }
-                uint64_t* t = (uint64_t*)(A.p + tab);
-                t[2 * count] = nref;
-                t[2 * count + 1] = vref;
-                ++count;
+                ev &= ~bit;
             }
         }
-        s = e + 1;
+        if (qs >= 0 && qb > s) query_piece(P, P.query[qs], L, s, qb, eqp, rw, pv, A, tab, count, dd);
     }
-    C.q_count[qs][li] = count;
-    C.q_params[qs][li] = mkref(tab, 16 * count, true);
+    for (uint32_t j = 0; j < dd.n; ++j) {
+        const uint32_t sp = dd.span.get((int)j);
+        const uint64_t vref = url_decode_value(L, (int)(sp & 0xFFFF), (int)(sp >> 16), A);
+        ((uint64_t*)(A.p + tab))[2 * dd.slot.get((int)j) + 1] = vref;
+    }
+    if (qs >= 0) {
+        C.q_count[qs][li] = count;
+        C.q_params[qs][li] = mkref(tab, 16 * count, true);
+    }
+    return plain;
 }
 
 // HttpUriDissector fast path on the line bytes [a,b).  Returns status.
 template <typename LN, typename Cols>
-__host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L, int a, int b, Arena& A, Cols& C, int64_t li) {
+__host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L, int a, int b, uint32_t usep, Arena& A,
+                                            Cols& C, int64_t li) {
     const UriStage& U = P.uri[u];
-    // ---- guards (FALLBACK when a cleanup step of the reference would change the string)
-    int fa = -1, h = -1, nh = 0;
-    // an unescapeHtml4 entity candidate needs a ';' somewhere in the URI
-    const bool semi = find_fwd(L, a, b, [](uint32_t w) { return swar::eq(w, ';'); }) < b;
-    for (int q = a;; ++q) {
-        q = find_fwd(L, q, b, [](uint32_t w) {
-            return swar::eq(w, '%') | swar::eq(w, '#') | swar::eq(w, '&') | swar::eq(w, '?');
-        });
-        if (q >= b) break;
-        uint32_t c = L[q];
-        if (c == '%') {
-            if (q + 2 >= b || !is_hex(L[q + 1]) || !is_hex(L[q + 2])) return ST_FALLBACK;  // BAD_EXCAPE_PATTERN
-        } else if (c == '#') {
-            ++nh;
-            if (h < 0) h = q;
-            if (q + 1 < b && (L[q + 1] == '&' || L[q + 1] == '?')) return ST_FALLBACK;     // HASH_AMP
-            if (q + 1 < b && L[q + 1] == 'x') return ST_FALLBACK;                          // ALMOST_HTML_ENCODED
-            if (q > a && L[q - 1] == '=') return ST_FALLBACK;                              // EQUALS_HASH
-        } else if (c == '&' || c == '?') {
-            if (fa < 0) fa = q;
-            if (semi) {                                                                   // unescapeHtml4 candidates
-                int r = q + 1;
-                while (r < b && (is_alnum(L[r]) || L[r] == '#')) ++r;
-                if (r < b && L[r] == ';') return ST_FALLBACK;
+    // ---- guards (FALLBACK when a cleanup step of the reference would change
+    // the string), one pass over the special bytes % # & ? ;
+    int fa = -1, h = -1, nh = 0, first_pct = -1;
+    bool frag_plain = true;  // no '%' '?' '&' after the '#'
+    {
+        const uint32_t AA = L.o + (uint32_t)a, E = L.o + (uint32_t)b;
+        const uint32_t W0 = AA >> 2, W1 = (E - 1) >> 2;
+        uint32_t wn = L.word(W0);
+        for (uint32_t W = W0; W <= W1; ++W) {
+            const uint32_t w = wn;
+            wn = L.word_or0(W + 1);  // look-ahead: '%' checks and the next iteration
+            uint32_t keep = swar::HI;
+            if (W == W0) keep &= swar::HI << (8 * (AA & 3));
+            if (W == W1) keep &= swar::HI >> (8 * (3 - ((E - 1) & 3)));
+            uint32_t ev = (swar::eq(w, '%') | swar::eq(w, '#') | swar::eq(w, '&') | swar::eq(w, '?') | swar::eq(w, ';')) & keep;
+            while (ev) {
+                const int k = swar::first(ev);
+                ev &= ~(0x80u << (8 * k));
+                const int q = (int)((W << 2) + (uint32_t)k - L.o);
+                const uint32_t c = (w >> (8 * k)) & 0xFFu;
+                if (c == '%') {
+                    const uint64_t ww = (uint64_t)w | ((uint64_t)wn << 32);
+                    if (q + 2 >= b || !is_hex((uint32_t)(ww >> (8 * k + 8)) & 0xFFu) ||
+                        !is_hex((uint32_t)(ww >> (8 * k + 16)) & 0xFFu))
+                        return ST_FALLBACK;  // BAD_EXCAPE_PATTERN
+                    if (first_pct < 0) first_pct = q;
+                    if (h >= 0) frag_plain = false;
+                } else if (c == '#') {
+                    ++nh;
+                    if (h < 0) h = q;
+                    if (q + 1 < b && (L[q + 1] == '&' || L[q + 1] == '?')) return ST_FALLBACK;     // HASH_AMP
+                    if (q + 1 < b && L[q + 1] == 'x') return ST_FALLBACK;                          // ALMOST_HTML_ENCODED
+                    if (q > a && L[q - 1] == '=') return ST_FALLBACK;                              // EQUALS_HASH
+                } else if (c == ';') {
+                    // unescapeHtml4 candidate: [&?][a-zA-Z0-9#]*;
+                    int r = q - 1;
+                    while (r >= a && (is_alnum(L[r]) || L[r] == '#')) --r;
+                    if (r >= a && (L[r] == '&' || L[r] == '?')) return ST_FALLBACK;
+                } else {  // '&' '?'
+                    if (fa < 0) fa = q;
+                    if (h >= 0) frag_plain = false;
+                }
             }
         }
     }
+    LP_PROF(30 + 8 * u);
     if (nh > 1) return ST_FALLBACK;                                                       // DOUBLE_HASH
     int pend = b;                              // end of path: first '?'(=fa) or '#'
     if (fa >= 0 && fa < pend) pend = fa;
@@ -943,15 +1093,17 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
         }
     }
     if (pend < ps) pend = ps;
+    LP_PROF(31 + 8 * u);
     // ---- outputs
     C.u_scheme[u][li] = (uint64_t)scheme_ref;
     C.u_host[u][li] = (uint64_t)host_ref;
     C.u_port[u][li] = port;
     if (U.want_path) {
-        uint64_t r = decode_span(L, ps, pend, A);
+        uint64_t r = (first_pct >= 0 && first_pct < pend) ? decode_span(L, ps, pend, A) : mkref(ps, pend - ps, false);
         if (r == ~0ull) return ST_FALLBACK;
         C.u_path[u][li] = r;
     }
+    LP_PROF(32 + 8 * u);
     if (U.want_query) {
         if (fa >= 0 && (h < 0 || fa < h)) {
             // rawQuery = "&" + normalized text up to '#': '?'->'&', URIUtil escapes
@@ -961,8 +1113,7 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
             // the gfx950 build (ROCm 7.2, -O3) delivered a wrong offset on
             // lanes whose scan ran an extra word (parity tests caught it)
             const uint64_t amp_ref = mkref(qs0, qe - qs0, false) | REF_AMP;
-            const bool plain =
-                find_fwd(L, qs0, qe, [](uint32_t w) { return swar::eq(w, '?') | swar::needs_encode(w); }) >= qe;
+            const bool plain = query_pass(P, U.query_stage, L, qs0, qe, usep + 1, A, C, li);
             if (plain) {
                 C.u_query[u][li] = amp_ref;
             } else {
@@ -976,18 +1127,16 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
                 }
                 C.u_query[u][li] = mkref(st, A.used - st, true);
             }
-            if (U.query_stage >= 0) query_stage(P, U.query_stage, L, fa + 1, qe, A, C, li);
         } else {
             C.u_query[u][li] = mkref(0, 0, true);
             if (U.query_stage >= 0) { C.q_count[U.query_stage][li] = 0; C.q_params[U.query_stage][li] = 0; }
         }
     }
+    LP_PROF(33 + 8 * u);
     if (U.want_ref && h >= 0) {
         flags |= UF_FRAG;
         // fragment = decode(normalized text after '#')
-        bool plain = true;
-        for (int q = h + 1; q < b; ++q) plain &= !(L[q] == '%' || L[q] == '?' || L[q] == '&');
-        if (plain) C.u_frag[u][li] = mkref(h + 1, b - h - 1, false);
+        if (frag_plain) C.u_frag[u][li] = mkref(h + 1, b - h - 1, false);
         else {
             uint32_t st = A.used;
             for (int q = h + 1; q < b;) {
@@ -1001,6 +1150,7 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
             C.u_frag[u][li] = mkref(st, A.used - st, true);
         }
     }
+    LP_PROF(34 + 8 * u);
     C.u_flags[u][li] = flags;
     return ST_OK;
 }
@@ -1015,7 +1165,9 @@ __host__ __device__ LP_INLINE void phase2(const Program& P, const LN& L, LineOut
             if (P.uri[u].query_stage >= 0) { C.q_count[P.uri[u].query_stage][li] = 0; C.q_params[P.uri[u].query_stage][li] = 0; }
             continue;
         }
-        int st = uri_stage(P, u, L, a, b, A, C, li);
+        LP_PROF(10 + 2 * u);
+        int st = uri_stage(P, u, L, a, b, o.usep.get(u), A, C, li);
+        LP_PROF(11 + 2 * u);
         if (st != ST_OK) o.status = st;
     }
 }

@@ -91,14 +91,33 @@ def mutate(rng, line):
         lambda l: l.replace(b"&", b"&amp;", 1),
         lambda l: l.replace(b"1", b"\t", 1),
         lambda l: l.replace(b"a", b"\xc3\xa9", 1),
+        # URI / query corner cases
+        lambda l: l.replace(b"?", b"?Upper=X&", 1),
+        lambda l: l.replace(b"?", b"?a b=c d&", 1),
+        lambda l: l.replace(b"=", b"=x+y%41%e9", 1),
+        lambda l: l.replace(b"&", b"?", 1),
+        lambda l: l.replace(b"?", b"?x=1&amp;y=2&", 1),
+        lambda l: l.replace(b"?", b"?q=a;b&", 1),
+        lambda l: l.replace(b"?", b"?&&=&", 1),
+        lambda l: l.replace(b" HTTP/", b"#frag%41?x&y HTTP/", 1),
+        lambda l: l.replace(b" HTTP/", b"#a HTTP/", 1),
+        lambda l: l.replace(b"GET /", b"GET /%7Epath%2Fx/", 1),
+        lambda l: l.replace(b"GET /", b"GET /a{b}|c^/", 1),
+        lambda l: l.replace(b"GET /", b"GET /p\"q/", 1),
+        lambda l: l.replace(b"?", b"?N%41ME=1&", 1),
+        lambda l: l.replace(b"http://", b"http://Host-Name.EXAMPLE:8080", 1),
+        lambda l: l.replace(b"://", b"://1.2.3.4:0", 1),
+        lambda l: l.replace(b"://", b"://[::1]", 1),
+        lambda l: l.replace(b"?", b"?=v&k&", 1),
+        lambda l: l.replace(b"GET /", b"GET //double/", 1),
     ]
     return rng.choice(ops)(line)
 
 
 def test_mutated_lines_emulated(oracle, emu):
     rng = random.Random(1234)
-    base = lpa.synth_combined(99, 0, 600).split(b"\n")[:-1]
-    lines = [mutate(rng, l) for l in base]
+    base = lpa.synth_combined(99, 0, 3000).split(b"\n")[:-1]
+    lines = [mutate(rng, l) for l in base] + [mutate(rng, mutate(rng, l)) for l in base]
     o = oracle.Oracle("combined", all_paths(oracle))
     e = emu.Emu("combined", all_paths(oracle))
     s = compare(o, e, lines)
