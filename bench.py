@@ -124,6 +124,7 @@ def main():
     import torch.distributed as dist
 
     import logparser_amd as lpa
+    from logparser_amd.shard import max_over_ranks, reduce_counters
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -145,7 +146,7 @@ def main():
         st = parser.run(buf.data_ptr(), nbytes, on_device=True)
         if world > 1:
             counters.copy_(torch.tensor([st["lines"], st["ok"], st["bad"], st["fallback"]], dtype=torch.int64))
-            dist.all_reduce(counters)
+            reduce_counters(counters)  # RCCL all-reduce: the only cross-GPU traffic
         return st
 
     for _ in range(args.warmup):
@@ -164,11 +165,7 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    t = torch.tensor([elapsed], dtype=torch.float64, device=device)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = max_over_ranks(time.perf_counter() - t0, device=device)
 
     total_bytes = nbytes * world * args.steps
     total_lines = stats["lines"] * world * args.steps
