@@ -274,7 +274,7 @@ int lp_parse_batch(lp_handle* h, const uint8_t* buf, uint64_t nbytes, int buf_fl
     if (!alloc_columns(h, n)) return LP_E_NOMEM;
     const lp::Program& P = h->plan.program();
     // arena: generous bound (only written bytes cost bandwidth)
-    uint64_t acap = h->plan.device_ok() && P.n_uri > 0 ? 2 * nbytes + 64 * (uint64_t)n + 4096 : 4096;
+    uint64_t acap = h->plan.device_ok() && P.n_uri > 0 ? 3 * nbytes + 64 * (uint64_t)n + 4096 : 4096;
     if (!h->arena.ensure(acap)) return LP_E_NOMEM;
     lp::Columns& C = h->C;
     C.line_off = d_off;

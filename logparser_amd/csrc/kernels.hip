@@ -129,10 +129,20 @@ struct WaveStack {  // per-lane DFS stack, lane-interleaved (conflict-free)
     __device__ uint32_t& operator[](int k) const { return base[k * PW]; }
 };
 
-template <typename Ptr>
-__device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, const Columns& C, Ptr base, uint32_t off,
-                                           int n, bool active, int64_t li, WaveStack stk, bool clean) {
-    LineT<Ptr> L{base, off, n};
+// The line of lane `own` of this wave (for work on another lane's line).
+template <typename LN>
+__device__ __forceinline__ LN owner_line(const LN& L, int own) {
+    LN R = L;
+    R.o = (uint32_t)__shfl((int)L.o, own);
+    R.n = __shfl(L.n, own);
+    if constexpr (!LN::has_masks)  // HBM path: every lane has its own base
+        R.b = reinterpret_cast<decltype(L.b)>(__shfl((unsigned long long)(uintptr_t)L.b, own));
+    return R;
+}
+
+template <typename LN>
+__device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, const Columns& C, const LN& L,
+                                           bool active, int64_t li, WaveStack stk, bool clean) {
     LineOut o;
     o.status = ST_OK;
     o.arena_need = 0;
@@ -160,7 +170,7 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
                 C.arena_base[li] = mine;
                 Arena A{C.arena + mine, 0, need};
                 phase2(P, L, o, A, C, li);
-                written = A.used;
+                written = A.used - A.slack;
             }
         } else if (o.status == ST_OK) {
             C.arena_base[li] = 0;
@@ -169,6 +179,41 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
         write_line(P, o, C, li);
     }
     LP_PROF(21);
+    // QueryStringFieldDissector pieces of all lines of the wave, spread evenly
+    // over the lanes (a line's pieces vary from 0 to dozens; one lane per line
+    // would leave most lanes idle while the longest query finishes)
+    if (P.n_query > 0) {
+        __syncthreads();  // the table slots written in phase 2 are visible to every lane
+        const bool has = active && o.status == ST_OK && need != 0;
+        const unsigned long long my_ab = has ? C.arena_base[li] : 0ull;
+        for (int qs = 0; qs < P.n_query; ++qs) {
+            const uint32_t np = has ? C.q_count[qs][li] : 0u;
+            const uint32_t my_tab = np ? ref_off(C.q_params[qs][li]) : 0u;
+            uint32_t incl = np;
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(incl, d);
+                if (lane >= d) incl += y;
+            }
+            const uint32_t base = incl - np, total = __shfl(incl, 63);
+            for (uint32_t g0 = 0; g0 < total; g0 += PW) {
+                const uint32_t g = g0 + (uint32_t)lane;
+                int own = 0;  // last lane whose first piece index is <= g
+                for (int st = 32; st; st >>= 1)
+                    if (__shfl(base, own + st) <= g) own += st;
+                const uint32_t ob = __shfl(base, own), otab = __shfl(my_tab, own);
+                const unsigned long long oab = __shfl(my_ab, own);
+                const auto OL = owner_line(L, own);
+                if (g < total) {
+                    uint8_t* region = C.arena + oab;
+                    uint64_t* slot = reinterpret_cast<uint64_t*>(region + otab) + 2 * (g - ob);
+                    const uint32_t reserved = 3u * (uint32_t)((slot[0] >> 32) - (uint32_t)slot[0]);
+                    const uint32_t used = query_piece(P, P.query[qs], OL, region, slot);
+                    written += used - reserved;  // modulo 2^32: the wave sum is exact
+                }
+            }
+        }
+    }
+    LP_PROF(22);
     for (int d = 32; d > 0; d >>= 1) written += __shfl_xor(written, d);
     const uint64_t m_act = __ballot(active);
     const uint64_t m_ok = __ballot(active && o.status == ST_OK);
@@ -194,9 +239,12 @@ __global__ __launch_bounds__(PW) void k_parse_lines(const uint8_t* __restrict__ 
     const Columns& C = args->cols;
     __shared__ Elem s_elems[MAX_ELEMS];
     if ((int)threadIdx.x < P.n_elems) s_elems[threadIdx.x] = P.elems[threadIdx.x];
+    // LDS: [DFS stack][byte window (win_cap, a multiple of 64)][MC_N class masks]
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     WaveStack stk{reinterpret_cast<uint32_t*>(smem) + threadIdx.x};
     uint8_t* win = smem + stk_words * 4;
+    const uint32_t mwords = win_cap >> 6;
+    uint16_t* msk16 = reinterpret_cast<uint16_t*>(win + win_cap);
     const int lane = threadIdx.x;
     const int64_t li0 = (int64_t)blockIdx.x * PW;
     const int64_t li = li0 + lane;
@@ -213,30 +261,41 @@ __global__ __launch_bounds__(PW) void k_parse_lines(const uint8_t* __restrict__ 
     if (w1 > nbytes) w1 = nbytes;
     LP_PROF(0);
     if (stage && w1 - w0 <= win_cap) {
+        // stage the window with coalesced 16-byte loads and classify every
+        // byte once (nibble-LUT classes -> 16 bits per class per 16 bytes)
         const int nv = (int)((w1 - w0 + 15) >> 4);
+        const int nv4 = (nv + 3) & ~3;  // whole 64-bit mask words
         uint32_t bad = 0;  // guard-failing bytes other than '\n' anywhere in the window
-        for (int k = lane; k < nv; k += PW) {
+        for (int k = lane; k < nv4; k += PW) {
             const uint64_t p = w0 + 16ull * k;
-            u32x4 v;
-            if (p + 16 <= nbytes) {
-                v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(buf + p));
-            } else {
-                v = u32x4{0, 0, 0, 0};
-                for (int j = 0; j < 16 && p + j < nbytes; ++j) v[j >> 2] |= (uint32_t)buf[p + j] << (8 * (j & 3));
+            u32x4 v = u32x4{0, 0, 0, 0};
+            if (k < nv) {
+                if (p + 16 <= nbytes) {
+                    v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(buf + p));
+                } else {
+                    for (int j = 0; j < 16 && p + j < nbytes; ++j) v[j >> 2] |= (uint32_t)buf[p + j] << (8 * (j & 3));
+                }
+                for (int j = 0; j < 4; ++j) bad |= swar::guard_bad(v[j]) & ~swar::eq(v[j], '\n');
             }
             *reinterpret_cast<u32x4*>(win + 16 * k) = v;
-            for (int j = 0; j < 4; ++j) bad |= swar::guard_bad(v[j]) & ~swar::eq(v[j], '\n');
+            uint32_t m0, m1;
+            bcls::classify16(v[0], v[1], v[2], v[3], m0, m1);
+            msk16[4 * mwords * MC_QUOTE + k] = (uint16_t)m0;
+            msk16[4 * mwords * MC_UEV + k] = (uint16_t)m1;
         }
         const bool clean = !__any(bad != 0);
         __syncthreads();
-        parse_wave(P, s_elems, C, (lds_bytes)win, (uint32_t)(s - w0), n, active, li, stk, clean);
+        const LineT<lds_bytes, lds_u64> L{(lds_bytes)win, (uint32_t)(s - w0), n,
+                                          (lds_u64)reinterpret_cast<uint64_t*>(msk16), mwords};
+        parse_wave(P, s_elems, C, L, active, li, stk, clean);
     } else {
         __syncthreads();
         // base = the line start aligned down to 4 bytes: word reads never
         // leave the 4-byte words holding the line's bytes
         const uint8_t* ls = buf + s;
         const uint32_t mis = (uint32_t)((uintptr_t)ls & 3);
-        parse_wave(P, s_elems, C, ls - mis, mis, n, active, li, stk, false);
+        const LineT<const uint8_t*> L{ls - mis, mis, n};
+        parse_wave(P, s_elems, C, L, active, li, stk, false);
     }
 }
 
@@ -301,8 +360,8 @@ int launch_parse(const uint8_t* d_buf, uint64_t nbytes, int64_t n_lines, const D
                  const uint32_t* d_wave_counts, unsigned long long* counters, hipStream_t s) {
     if (n_lines == 0) return 0;
     const int64_t waves = parse_waves(n_lines);
-    // LDS window per wave: ~1.3x the mean bytes of 64 lines (+1 KiB), so
-    // nearly every wave stages; at most 60 KiB.  A window that does not fit
+    // LDS window per wave: ~1.1x the mean bytes of 64 lines (+512 B), so
+    // nearly every wave stages; at most 48 KiB (+ 18 KiB of class masks).  A window that does not fit
     // reads HBM directly.
     const uint64_t mean = (nbytes + n_lines - 1) / n_lines;
     // tuning knobs for profiling experiments (defaults are the product setting)
@@ -311,11 +370,11 @@ int launch_parse(const uint8_t* d_buf, uint64_t nbytes, int64_t n_lines, const D
     const int win_pct = e1 ? atoi(e1) : 110;
     const int force_global = e2 ? atoi(e2) : 0;
     uint64_t cap = (PW * mean * (uint64_t)win_pct) / 100 + 512;
-    if (cap > 60 * 1024) cap = 60 * 1024;
-    cap = (cap + 15) & ~15ull;
+    if (cap > 48 * 1024) cap = 48 * 1024;
+    cap = (cap + 63) & ~63ull;
     const int stage = ((uintptr_t)d_buf & 15) == 0 && !force_global;
     const uint32_t stk_words = (uint32_t)(stack_depth > 0 ? stack_depth : 1) * PW;
-    const size_t lds = stk_words * 4 + cap;
+    const size_t lds = stk_words * 4 + cap + MC_N * (cap / 8);  // + class masks, 1 bit per window byte
     hipLaunchKernelGGL(k_parse_lines, dim3((unsigned)waves), dim3(PW), lds, s, d_buf, nbytes, n_lines, d_args,
                        (uint32_t)cap, stage, stk_words);
     int64_t rb = (waves + 255) / 256;

@@ -10,6 +10,8 @@
 // Any input the device cannot prove it handles exactly returns FALLBACK
 // (status 2): the caller hands that line to the reference Java dissector.
 #pragma once
+#include <cstddef>
+#include <type_traits>
 #include <utility>
 
 #include "lp_program.h"
@@ -46,12 +48,10 @@ __host__ __device__ LP_INLINE uint32_t hexv(uint32_t c) { return c <= '9' ? c - 
 // "badUriChars" set (HttpUriDissector.java:111-120): control, space, unwise
 // {}|\^[]` and <>"  (ASCII only; non-ASCII lines never reach this point)
 __host__ __device__ LP_INLINE bool uri_needs_encode(uint32_t c) {
-    if (c <= 0x20 || c == 0x7F) return true;
-    switch (c) {
-    case '{': case '}': case '|': case '\\': case '^': case '[': case ']': case '`': case '<': case '>': case '"':
-        return true;
-    }
-    return false;
+    // bit c of the 128-bit set {0x00-0x20, " < > [ \ ] ^ ` { | } 0x7F}
+    constexpr uint64_t LO = 0x5000000500000000ull | 0x1FFFFFFFFull;  // 0x00-0x20, '"' (0x22), '<' (0x3C), '>' (0x3E)
+    constexpr uint64_t HI = 0xB800000178000000ull;                   // [ \ ] ^ (0x5B-0x5E), ` (0x60), { | } (0x7B-0x7D), 0x7F
+    return c >= 0x80 || (((c < 64 ? LO : HI) >> (c & 63)) & 1u);
 }
 
 // -------------------------------------------------------------- matcher
@@ -75,11 +75,31 @@ typedef const __attribute__((address_space(3))) uint32_t* lds_words;
 __device__ LP_INLINE uint32_t load_word(lds_bytes p) { return *(lds_words)p; }
 #endif
 
-template <typename Ptr>
+// ---- byte-class bitmasks (1 bit per byte, one 64-bit word per 64 bytes),
+// built once per LDS window by the staging pass of the parse kernel, so the
+// per-line scanners walk 64 bytes per step instead of 4.  Exact for TAB and
+// printable ASCII (every other byte sends its line to FALLBACK before any
+// scanner runs).
+enum : int {
+    MC_QUOTE = 0,  // '"'
+    MC_UEV = 1,    // URI events: % # & ? ; = + A-Z and the bytes URIUtil.encode escapes
+    MC_N = 2
+};
+__host__ __device__ LP_INLINE uint64_t mask_load(const uint64_t* p) { return *p; }
+#if defined(__HIP__)
+typedef const __attribute__((address_space(3))) uint64_t* lds_u64;
+__device__ LP_INLINE uint64_t mask_load(lds_u64 p) { return *p; }
+#endif
+struct NoMasks {};
+
+template <typename Ptr, typename MPtr = NoMasks>
 struct LineT {
     Ptr b;
     uint32_t o;
     int n;
+    MPtr m = MPtr{};       // class c, 64-byte block w of b: m[c * ms + w]
+    uint32_t ms = 0;
+    static constexpr bool has_masks = !std::is_same<MPtr, NoMasks>::value;
     __host__ __device__ LP_INLINE uint32_t operator[](int i) const { return b[o + i]; }
     // aligned 32-bit word w of the base (little-endian: byte k at bits 8k..8k+7)
     __host__ __device__ LP_INLINE uint32_t word(uint32_t w) const { return load_word(b + 4 * w); }
@@ -88,8 +108,10 @@ struct LineT {
     __host__ __device__ LP_INLINE uint32_t word_or0(uint32_t w) const {
         return 4 * w < o + (uint32_t)n ? load_word(b + 4 * w) : 0u;
     }
+    __host__ __device__ LP_INLINE uint64_t mask(int c, uint32_t w) const { return mask_load(m + (c * ms + w)); }
 };
 using Line = LineT<const uint8_t*>;
+using MLine = LineT<const uint8_t*, const uint64_t*>;
 
 // ---- SWAR byte classes on a 32-bit word: bit 8k+7 set when byte k is in
 // the class (exact, no false positives from carries).
@@ -126,6 +148,70 @@ __host__ __device__ LP_INLINE int first(uint32_t m) {
 __host__ __device__ LP_INLINE int last(uint32_t m) { return (int)((31 - __builtin_clz(m)) >> 3); }
 __host__ __device__ LP_INLINE int count(uint32_t m) { return __builtin_popcount(m); }
 }  // namespace swar
+
+// ---- byte classes through two nibble look-up tables (the SIMD "shuffle"
+// classifier): class bits(b) = LO[b & 15] & HI[b >> 4], one v_perm_b32 per
+// 8-entry table half.  Bits: 0 ' ', 1 TAB, 2 '"', 3 hi 2 x lo {3,5,6,B}
+// (# % & +), 4 hi 3 x lo {B..F} (; < = > ?), 5 hi {4,7} x lo {B,C,D,F}
+// (K L M O { | }), 6 hi {4,5} x lo {1..E} (A-N Q-Z [ \ ] ^), 7 hi {5,6} x
+// lo 0 (P `).  WS = bits 0|1, QUOTE = bit 2, UEV = any bit.
+namespace bcls {
+constexpr uint32_t LO0 = 0x48444081u, LO1 = 0x40484840u;  // LO[0..3], LO[4..7]
+constexpr uint32_t LO2 = 0x78404240u, LO3 = 0x30507070u;  // LO[8..11], LO[12..15]
+constexpr uint32_t HI0 = 0x100D0002u, HI1 = 0x2080C060u;  // HI[0..3], HI[4..7]
+// v_perm_b32: byte i of the result = byte sel_i (0..7) of (s0:s1), s1 low
+__host__ __device__ LP_INLINE uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_perm(s0, s1, sel);
+#else
+    const uint64_t v = ((uint64_t)s0 << 32) | s1;
+    uint32_t r = 0;
+    for (int i = 0; i < 4; ++i) r |= (uint32_t)((v >> (8 * ((sel >> (8 * i)) & 7))) & 0xFFu) << (8 * i);
+    return r;
+#endif
+}
+// class bits of the 4 bytes of w (bytes >= 0x80: unspecified)
+__host__ __device__ LP_INLINE uint32_t bits(uint32_t w) {
+    const uint32_t s = w & 0x07070707u;
+    const uint32_t p1 = perm(LO1, LO0, s), p2 = perm(LO3, LO2, s);
+    const uint32_t m8 = ((w >> 3) & 0x01010101u) * 0xFFu;
+    const uint32_t rl = (p2 & m8) | (p1 & ~m8);
+    return rl & perm(HI1, HI0, (w >> 4) & 0x07070707u);
+}
+// bytes with bit 7 set -> 4-bit mask (byte k -> bit k)
+__host__ __device__ LP_INLINE uint32_t nib(uint32_t hb) { return (((hb >> 7) * 0x204081u) >> 21) & 15u; }
+__host__ __device__ LP_INLINE uint32_t quote_hb(uint32_t r) { return (r << 5) & swar::HI; }
+__host__ __device__ LP_INLINE uint32_t uev_hb(uint32_t r) { return (((r & swar::LO7) + swar::LO7) | r) & swar::HI; }
+// 16 bytes (4 little-endian words) -> the 16-bit QUOTE and UEV masks
+__host__ __device__ LP_INLINE void classify16(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t& qt,
+                                              uint32_t& uev) {
+    const uint32_t r0 = bits(w0), r1 = bits(w1), r2 = bits(w2), r3 = bits(w3);
+    qt = nib(quote_hb(r0)) | (nib(quote_hb(r1)) << 4) | (nib(quote_hb(r2)) << 8) | (nib(quote_hb(r3)) << 12);
+    uev = nib(uev_hb(r0)) | (nib(uev_hb(r1)) << 4) | (nib(uev_hb(r2)) << 8) | (nib(uev_hb(r3)) << 12);
+}
+// mask class whose members are exactly the byte c, -1 none
+__host__ __device__ LP_INLINE int class_of(uint32_t c) { return c == '"' ? MC_QUOTE : -1; }
+}  // namespace bcls
+
+// Host builder of the class masks of buf[0, n) (n a multiple of 16), the same
+// computation the kernel's staging pass does; used by the test-only CPU
+// emulation.  masks: MC_N arrays of ms 64-bit words.
+inline void build_masks(const uint8_t* buf, uint32_t n, uint64_t* masks, uint32_t ms) {
+    for (uint32_t i = 0; i < MC_N * ms; ++i) masks[i] = 0;
+    for (uint32_t k = 0; 16 * k < n; ++k) {
+        uint32_t w[4];
+        for (int j = 0; j < 4; ++j) __builtin_memcpy(&w[j], buf + 16 * k + 4 * j, 4);
+        uint32_t a, b;
+        bcls::classify16(w[0], w[1], w[2], w[3], a, b);
+        const int sh = 16 * (k & 3);
+        masks[MC_QUOTE * ms + (k >> 2)] |= (uint64_t)a << sh;
+        masks[MC_UEV * ms + (k >> 2)] |= (uint64_t)b << sh;
+    }
+}
+
+__host__ __device__ LP_INLINE int ctz64(uint64_t m) { return __builtin_ctzll(m); }
+__host__ __device__ LP_INLINE int msb64(uint64_t m) { return 63 - __builtin_clzll(m); }
+__host__ __device__ LP_INLINE int popc64(uint64_t m) { return __builtin_popcountll(m); }
 
 // First position in [from, to) whose byte is in class F, else `to`.
 template <typename LN, typename F>
@@ -177,21 +263,162 @@ __host__ __device__ LP_INLINE uint32_t count_in(const LN& L, int a, int b, F cls
     return c;
 }
 
-// URIUtil-escaped bytes and '&'/'?' separators in [a, b), one pass.
+// ---- scanners over the class masks (lines staged with masks)
+// First position in [from, to) in mask class c, else `to`.
 template <typename LN>
-__host__ __device__ LP_INLINE void count2_in(const LN& L, int a, int b, uint32_t& enc, uint32_t& sep) {
-    enc = sep = 0;
-    if (a >= b) return;
-    const uint32_t A = L.o + (uint32_t)a, E = L.o + (uint32_t)b;
-    const uint32_t W0 = A >> 2, W1 = (E - 1) >> 2;
-    for (uint32_t W = W0; W <= W1; ++W) {
-        const uint32_t w = L.word(W);
-        uint32_t keep = swar::HI;
-        if (W == W0) keep &= swar::HI << (8 * (A & 3));
-        if (W == W1) keep &= swar::HI >> (8 * (3 - ((E - 1) & 3)));
-        enc += (uint32_t)swar::count(swar::needs_encode(w) & keep);
-        sep += (uint32_t)swar::count((swar::eq(w, '&') | swar::eq(w, '?')) & keep);
+__host__ __device__ LP_INLINE int mfind_fwd(const LN& L, int c, int from, int to) {
+    if (from >= to) return to;
+    const uint32_t A = L.o + (uint32_t)from, E = L.o + (uint32_t)to;
+    uint32_t W = A >> 6;
+    uint64_t m = L.mask(c, W) & (~0ull << (A & 63));
+    for (;;) {
+        if (m) {
+            const uint32_t p = (W << 6) + (uint32_t)ctz64(m);
+            return p < E ? (int)(p - L.o) : to;
+        }
+        ++W;
+        if ((W << 6) >= E) return to;
+        m = L.mask(c, W);
     }
+}
+// Last position in [lo, hi] in mask class c, else -1.
+template <typename LN>
+__host__ __device__ LP_INLINE int mfind_bwd(const LN& L, int c, int hi, int lo) {
+    if (hi < lo) return -1;
+    const uint32_t A = L.o + (uint32_t)hi, S = L.o + (uint32_t)lo;
+    uint32_t W = A >> 6;
+    uint64_t m = L.mask(c, W) & (~0ull >> (63 - (A & 63)));
+    for (;;) {
+        if (m) {
+            const uint32_t p = (W << 6) + (uint32_t)msb64(m);
+            return p >= S ? (int)(p - L.o) : -1;
+        }
+        if ((W << 6) <= S) return -1;
+        --W;
+        m = L.mask(c, W);
+    }
+}
+
+// Calls f(q, c) for every position q in [a, b) whose byte c is a URI event
+// byte (MC_UEV: % # & ? ; = + A-Z and the URIUtil-escaped bytes), in order,
+// until f returns false.  Returns false when f stopped the walk.  Lines with
+// masks walk 64 bytes per step and read the next event's byte before f runs
+// on the current one (its LDS latency overlaps f); others classify 4 bytes
+// per step with the same nibble tables.
+template <typename LN, typename F>
+__host__ __device__ LP_INLINE bool for_uev(const LN& L, int a, int b, F&& f) {
+    if (a >= b) return true;
+    const uint32_t A = L.o + (uint32_t)a, E = L.o + (uint32_t)b;
+    if constexpr (LN::has_masks) {
+        const uint32_t W1 = (E - 1) >> 6;
+        const uint64_t last = ~0ull >> (63 - ((E - 1) & 63));
+        uint32_t W = A >> 6;
+        uint64_t m = L.mask(MC_UEV, W) & (~0ull << (A & 63));
+        if (W == W1) m &= last;
+        auto next = [&](int& q) {
+            while (!m) {
+                if (++W > W1) return false;
+                m = L.mask(MC_UEV, W);
+                if (W == W1) m &= last;
+            }
+            q = (int)((W << 6) + (uint32_t)ctz64(m) - L.o);
+            m &= m - 1;
+            return true;
+        };
+        int q;
+        if (!next(q)) return true;
+        uint32_t c = L[q];
+        for (;;) {
+            int q2 = 0;
+            const bool more = next(q2);
+            const uint32_t c2 = more ? L[q2] : 0u;
+            if (!f(q, c)) return false;
+            if (!more) return true;
+            q = q2;
+            c = c2;
+        }
+    } else {
+        const uint32_t W0 = A >> 2, W1 = (E - 1) >> 2;
+        for (uint32_t W = W0; W <= W1; ++W) {
+            const uint32_t w = L.word(W);
+            uint32_t m = bcls::uev_hb(bcls::bits(w));
+            if (W == W0) m &= swar::HI << (8 * (A & 3));
+            if (W == W1) m &= swar::HI >> (8 * (3 - ((E - 1) & 3)));
+            while (m) {
+                const int k = swar::first(m);
+                m &= m - 1;
+                if (!f((int)((W << 2) + (uint32_t)k - L.o), (w >> (8 * k)) & 0xFFu)) return false;
+            }
+        }
+    }
+    return true;
+}
+
+// Number of URI event bytes in [a, b).
+template <typename LN>
+__host__ __device__ LP_INLINE uint32_t count_uev(const LN& L, int a, int b) {
+    if (a >= b) return 0;
+    const uint32_t A = L.o + (uint32_t)a, E = L.o + (uint32_t)b;
+    uint32_t c = 0;
+    if constexpr (LN::has_masks) {
+        const uint32_t W0 = A >> 6, W1 = (E - 1) >> 6;
+        for (uint32_t W = W0; W <= W1; ++W) {
+            uint64_t m = L.mask(MC_UEV, W);
+            if (W == W0) m &= ~0ull << (A & 63);
+            if (W == W1) m &= ~0ull >> (63 - ((E - 1) & 63));
+            c += (uint32_t)popc64(m);
+        }
+    } else {
+        const uint32_t W0 = A >> 2, W1 = (E - 1) >> 2;
+        for (uint32_t W = W0; W <= W1; ++W) {
+            uint32_t m = bcls::uev_hb(bcls::bits(L.word(W)));
+            if (W == W0) m &= swar::HI << (8 * (A & 3));
+            if (W == W1) m &= swar::HI >> (8 * (3 - ((E - 1) & 3)));
+            c += (uint32_t)swar::count(m);
+        }
+    }
+    return c;
+}
+
+// First \s in [from, to), else `to`.
+template <typename LN>
+__host__ __device__ LP_INLINE int find_ws(const LN& L, int from, int to) {
+    return find_fwd(L, from, to, [](uint32_t w) { return swar::ws(w); });
+}
+
+// The 4 bytes at line position p as one little-endian word (bytes past the
+// line's last word read as 0).
+template <typename LN>
+__host__ __device__ LP_INLINE uint32_t load_u32_at(const LN& L, int p) {
+    const uint32_t A = L.o + (uint32_t)p;
+    const uint32_t w0 = L.word(A >> 2), w1 = L.word_or0((A >> 2) + 1);
+#if defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_alignbyte(w1, w0, A & 3);
+#else
+    return (uint32_t)((((uint64_t)w1 << 32) | w0) >> (8 * (A & 3)));
+#endif
+}
+
+// 28 bytes from line position p (p + 26 <= n) in 7 little-endian words.
+struct Bytes28 {
+    uint32_t v[7];
+    __host__ __device__ LP_INLINE uint32_t operator[](int k) const { return (v[k >> 2] >> (8 * (k & 3))) & 0xFFu; }
+};
+template <typename LN>
+__host__ __device__ LP_INLINE Bytes28 load28(const LN& L, int p) {
+    const uint32_t A = L.o + (uint32_t)p, W = A >> 2, s = A & 3;
+    uint32_t w[8];
+    LP_UNROLL for (int j = 0; j < 7; ++j) w[j] = L.word(W + j);
+    w[7] = L.word_or0(W + 7);
+    Bytes28 r;
+    LP_UNROLL for (int j = 0; j < 7; ++j) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        r.v[j] = __builtin_amdgcn_alignbyte(w[j + 1], w[j], s);
+#else
+        r.v[j] = (uint32_t)((((uint64_t)w[j + 1] << 32) | w[j]) >> (8 * s));
+#endif
+    }
+    return r;
 }
 
 // Small per-line array kept in registers: every element access in the source
@@ -233,9 +460,8 @@ __host__ __device__ LP_INLINE bool lit_at(const Program& P, const LN& L, int pos
     const int len = e.lit_len;
     if (pos + len > L.n) return false;
     if (len <= 4) {
-        for (int k = 0; k < len; ++k)
-            if (L[pos + k] != ((e.lit4 >> (8 * k)) & 0xFFu)) return false;
-        return true;
+        const uint32_t keep = len == 4 ? 0xFFFFFFFFu : ((1u << (8 * len)) - 1u);
+        return ((load_u32_at(L, pos) ^ e.lit4) & keep) == 0;
     }
     for (int k = 0; k < len; ++k)
         if (L[pos + k] != P.lit[e.lit_off + k]) return false;
@@ -245,8 +471,7 @@ __host__ __device__ LP_INLINE bool lit_at(const Program& P, const LN& L, int pos
 template <typename LN>
 __host__ __device__ LP_INLINE bool time_us_ok(const LN& L, int p) {
     if (p + 26 > L.n) return false;
-    uint32_t c[26];
-    LP_UNROLL for (int k = 0; k < 26; ++k) c[k] = L[p + k];
+    const Bytes28 c = load28(L, p);
     if (!(c[0] >= '0' && c[0] <= '3') || !is_digit(c[1]) || c[2] != '/') return false;
     if (!is_alpha(c[3]) || !is_alpha(c[4]) || !is_alpha(c[5]) || c[6] != '/') return false;
     if (!(c[7] >= '1' && c[7] <= '9') || !is_digit(c[8]) || !is_digit(c[9]) || !is_digit(c[10]) || c[11] != ':') return false;
@@ -284,6 +509,26 @@ __host__ __device__ LP_INLINE int ipv4_first(const LN& L, int p) {
 // within [lo, n), or -1.
 template <typename LN>
 __host__ __device__ LP_INLINE int kth_from_end(const LN& L, uint32_t c, int k, int lo) {
+    if constexpr (LN::has_masks) {
+        if (c == '"') {  // exact class: count set bits of the QUOTE mask backwards
+            if (L.n - 1 < lo) return -1;
+            const uint32_t A = L.o + (uint32_t)L.n - 1, S = L.o + (uint32_t)lo;
+            uint32_t W = A >> 6;
+            uint64_t m = L.mask(MC_QUOTE, W) & (~0ull >> (63 - (A & 63)));
+            for (;;) {
+                if (W == (S >> 6)) m &= ~0ull << (S & 63);
+                const int pc = popc64(m);
+                if (pc >= k) {
+                    for (int j = 1; j < k; ++j) m ^= 1ull << msb64(m);
+                    return (int)((W << 6) + (uint32_t)msb64(m) - L.o);
+                }
+                k -= pc;
+                if ((W << 6) <= S) return -1;
+                --W;
+                m = L.mask(MC_QUOTE, W);
+            }
+        }
+    }
     int q = L.n - 1;
     for (;;) {
         q = find_bwd(L, q, lo, [c](uint32_t w) { return swar::eq(w, c); });
@@ -292,13 +537,35 @@ __host__ __device__ LP_INLINE int kth_from_end(const LN& L, uint32_t c, int k, i
     }
 }
 
+// Candidate starts of e's following literal: positions of its first byte,
+// through the mask class holding that byte (e.acls) when the line has masks.
+template <typename LN>
+__host__ __device__ LP_INLINE int anchor_bwd(const LN& L, const Elem& e, int hi, int lo) {
+    const uint32_t c0 = e.lit4 & 0xFFu;
+    if constexpr (LN::has_masks) {
+        if (e.acls >= 0) {
+            return mfind_bwd(L, e.acls, hi, lo);  // exact class
+        }
+    }
+    return find_bwd(L, hi, lo, [c0](uint32_t w) { return swar::eq(w, c0); });
+}
+template <typename LN>
+__host__ __device__ LP_INLINE int anchor_fwd(const LN& L, const Elem& e, int lo, int to) {
+    const uint32_t c0 = e.lit4 & 0xFFu;
+    if constexpr (LN::has_masks) {
+        if (e.acls >= 0) {
+            return mfind_fwd(L, e.acls, lo, to);  // exact class
+        }
+    }
+    return find_fwd(L, lo, to, [c0](uint32_t w) { return swar::eq(w, c0); });
+}
+
 // Occurrence of e's following literal: the last one starting in [lo, hi]
 // (greedy order) or the first one starting in [lo, hi] (lazy order); -1 none.
 template <typename LN>
 __host__ __device__ LP_INLINE int lit_last(const Program& P, const LN& L, const Elem& e, int hi, int lo) {
-    const uint32_t c0 = e.lit4 & 0xFFu;
     for (int q = hi;;) {
-        q = find_bwd(L, q, lo, [c0](uint32_t w) { return swar::eq(w, c0); });
+        q = anchor_bwd(L, e, q, lo);
         if (q < 0) return -1;
         if (lit_at(P, L, q, e)) return q;
         --q;
@@ -306,9 +573,8 @@ __host__ __device__ LP_INLINE int lit_last(const Program& P, const LN& L, const 
 }
 template <typename LN>
 __host__ __device__ LP_INLINE int lit_first(const Program& P, const LN& L, const Elem& e, int lo, int hi) {
-    const uint32_t c0 = e.lit4 & 0xFFu;
     for (int q = lo;;) {
-        q = find_fwd(L, q, hi + 1, [c0](uint32_t w) { return swar::eq(w, c0); });
+        q = anchor_fwd(L, e, q, hi + 1);
         if (q > hi) return -1;
         if (lit_at(P, L, q, e)) return q;
         ++q;
@@ -321,7 +587,7 @@ __host__ __device__ LP_INLINE int lit_first(const Program& P, const LN& L, const
 template <typename LN>
 __host__ __device__ LP_INLINE int cand_first(const Program& P, const Elem& e, const LN& L, int p) {
     switch (e.kind) {
-    case EK_NOSPACE: return find_fwd(L, p, L.n, [](uint32_t w) { return swar::ws(w); });
+    case EK_NOSPACE: return find_ws(L, p, L.n);
     case EK_NUMBER: { int q = find_fwd(L, p, L.n, [](uint32_t w) { return ~swar::digit(w) & swar::HI; }); return q > p ? q : -1; }
     case EK_CLFNUMBER: {
         int q = find_fwd(L, p, L.n, [](uint32_t w) { return ~swar::digit(w) & swar::HI; });
@@ -447,46 +713,51 @@ __host__ __device__ LP_INLINE int match_line(const Program& P, const EL& elems, 
 }
 
 // ------------------------------------------------------------- calendar
-__host__ __device__ LP_INLINE int64_t days_from_civil(int64_t y, int m, int d) {
+// Proleptic Gregorian, 32-bit arithmetic: every year the formats admit is
+// in [0, 10000) ([1-9][0-9]{3}, plus/minus one day), so day numbers fit in
+// int32 and the divisions are unsigned divisions by constants.
+__host__ __device__ LP_INLINE int32_t days_from_civil(int32_t y, int m, int d) {
     y -= m <= 2;
-    const int64_t era = (y >= 0 ? y : y - 399) / 400;
-    const int64_t yoe = y - era * 400;
-    const int64_t doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
-    const int64_t doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
-    return era * 146097 + doe - 719468;
+    const uint32_t era = (uint32_t)y / 400u;
+    const uint32_t yoe = (uint32_t)y - era * 400u;
+    const uint32_t doy = (153u * (uint32_t)(m + (m > 2 ? -3 : 9)) + 2u) / 5u + (uint32_t)d - 1u;
+    const uint32_t doe = yoe * 365u + yoe / 4u - yoe / 100u + doy;
+    return (int32_t)(era * 146097u + doe) - 719468;
 }
-__host__ __device__ LP_INLINE void civil_from_days(int64_t z, int64_t& y, int& m, int& d) {
-    z += 719468;
-    const int64_t era = (z >= 0 ? z : z - 146096) / 146097;
-    const int64_t doe = z - era * 146097;
-    const int64_t yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
-    const int64_t doy = doe - (365 * yoe + yoe / 4 - yoe / 100);
-    const int64_t mp = (5 * doy + 2) / 153;
-    d = (int)(doy - (153 * mp + 2) / 5 + 1);
-    m = (int)(mp < 10 ? mp + 3 : mp - 9);
-    y = yoe + era * 400 + (m <= 2);
+__host__ __device__ LP_INLINE void civil_from_days(int32_t days, int32_t& y, int& m, int& d) {
+    const uint32_t z = (uint32_t)(days + 719468);
+    const uint32_t era = z / 146097u;
+    const uint32_t doe = z - era * 146097u;
+    const uint32_t yoe = (doe - doe / 1460u + doe / 36524u - doe / 146096u) / 365u;
+    const uint32_t doy = doe - (365u * yoe + yoe / 4u - yoe / 100u);
+    const uint32_t mp = (5u * doy + 2u) / 153u;
+    d = (int)(doy - (153u * mp + 2u) / 5u + 1u);
+    m = (int)(mp < 10u ? mp + 3u : mp - 9u);
+    y = (int32_t)(yoe + era * 400u) + (m <= 2);
 }
-__host__ __device__ LP_INLINE bool leap(int64_t y) { return (y % 4 == 0 && y % 100 != 0) || y % 400 == 0; }
-__host__ __device__ LP_INLINE int month_len(int64_t y, int m) {
+__host__ __device__ LP_INLINE bool leap(int32_t y) { return (y % 4 == 0 && y % 100 != 0) || y % 400 == 0; }
+__host__ __device__ LP_INLINE int month_len(int32_t y, int m) {
     if (m == 2) return leap(y) ? 29 : 28;
     return (m == 4 || m == 6 || m == 9 || m == 11) ? 30 : 31;
 }
-__host__ __device__ LP_INLINE int iso_dow(int64_t days) { return (int)(((days % 7) + 7 + 3) % 7) + 1; }  // Mon=1
-// WeekFields.ISO (== WeekFields.of(Locale.UK)): week-based-year and week
-__host__ __device__ LP_INLINE void iso_week(int64_t y, int m, int d, int64_t& wy, int& wk) {
-    int64_t days = days_from_civil(y, m, d);
-    int wd = iso_dow(days);
-    int doy = (int)(days - days_from_civil(y, 1, 1)) + 1;
-    int w = (doy - wd + 10) / 7;
+// ISO day of week, Mon = 1 (day 0 = 1970-01-01 is a Thursday)
+__host__ __device__ LP_INLINE int iso_dow(int32_t days) { return (int)((uint32_t)(days + 719468 + 2) % 7u) + 1; }
+// WeekFields.ISO (== WeekFields.of(Locale.UK)): week-based-year and week of
+// the date with day number `days` in year y
+__host__ __device__ LP_INLINE void iso_week(int32_t y, int32_t days, int32_t& wy, int& wk) {
+    const int32_t jan1 = days_from_civil(y, 1, 1);
+    const int wd = iso_dow(days);
+    const int doy = (int)(days - jan1) + 1;
+    const int w = (doy - wd + 10) / 7;
+    const int jwd = iso_dow(jan1);
     if (w < 1) {
-        int64_t py = y - 1;
-        int jwd = iso_dow(days_from_civil(py, 1, 1));
+        const int32_t py = y - 1;
+        const int pjwd = iso_dow(jan1 - (leap(py) ? 366 : 365));
         wy = py;
-        wk = (jwd == 4 || (jwd == 3 && leap(py))) ? 53 : 52;
+        wk = (pjwd == 4 || (pjwd == 3 && leap(py))) ? 53 : 52;
         return;
     }
-    int jwd = iso_dow(days_from_civil(y, 1, 1));
-    int weeks = (jwd == 4 || (jwd == 3 && leap(y))) ? 53 : 52;
+    const int weeks = (jwd == 4 || (jwd == 3 && leap(y))) ? 53 : 52;
     if (w > weeks) { wy = y + 1; wk = 1; return; }
     wy = y;
     wk = w;
@@ -498,8 +769,7 @@ __host__ __device__ LP_INLINE void iso_week(int64_t y, int m, int d, int64_t& wy
 // offset sign+HHMM (each <= 59) with |offset| <= 18:00.
 template <typename LN>
 __host__ __device__ LP_INLINE bool parse_apache_time(const LN& L, int a, int64_t& epoch_s, uint64_t& local, uint64_t& utc) {
-    uint32_t c[26];
-    LP_UNROLL for (int k = 0; k < 26; ++k) c[k] = L[a + k];
+    const Bytes28 c = load28(L, a);
     int day = (c[0] - '0') * 10 + (c[1] - '0');
     // month name: case-insensitive against the 12 UK short names
     uint32_t m3 = ((uint32_t)(c[3] | 32) << 16) | ((uint32_t)(c[4] | 32) << 8) | (uint32_t)(c[5] | 32);
@@ -508,7 +778,6 @@ __host__ __device__ LP_INLINE bool parse_apache_time(const LN& L, int a, int64_t
                                 0x6a756c, 0x617567, 0x736570, 0x6f6374, 0x6e6f76, 0x646563};
     for (int k = 0; k < 12; ++k) if (names[k] == m3) month = k + 1;
     if (!month) return false;
-    int64_t year = (c[7] - '0') * 1000 + (c[8] - '0') * 100 + (c[9] - '0') * 10 + (c[10] - '0');
     int hh = (c[12] - '0') * 10 + (c[13] - '0');
     int mi = (c[15] - '0') * 10 + (c[16] - '0');
     int ss = (c[18] - '0') * 10 + (c[19] - '0');
@@ -522,28 +791,36 @@ __host__ __device__ LP_INLINE bool parse_apache_time(const LN& L, int a, int64_t
     }
     if (off > 64800 || off < -64800) return false;
     if (day < 1 || day > 31) return false;
+    const int32_t year = (int32_t)((c[7] - '0') * 1000 + (c[8] - '0') * 100 + (c[9] - '0') * 10 + (c[10] - '0'));
     int ml = month_len(year, month);
     if (day > ml) day = ml;
     if (mi > 59) return false;
     int d = day, m = month;
-    int64_t y = year;
+    int32_t y = year;
+    int32_t days = days_from_civil(y, m, d);
     if (hh == 24 && mi == 0 && ss == 0) {
         hh = 0;
-        civil_from_days(days_from_civil(y, m, d) + 1, y, m, d);
+        ++days;
+        civil_from_days(days, y, m, d);
     } else if (hh > 23 || ss > 59) {
         return false;
     }
-    int64_t days = days_from_civil(y, m, d);
-    epoch_s = days * 86400 + hh * 3600 + mi * 60 + ss - off;
-    int64_t wy; int wk;
-    iso_week(y, m, d, wy, wk);
+    const int sod = hh * 3600 + mi * 60 + ss;
+    epoch_s = (int64_t)days * 86400 + sod - off;
+    int32_t wy;
+    int wk;
+    iso_week(y, days, wy, wk);
     local = pack_cal((uint32_t)y, m, d, hh, mi, ss, (uint32_t)wy, wk);
-    int64_t ud = epoch_s >= 0 ? epoch_s / 86400 : -((-epoch_s + 86399) / 86400);
-    int64_t rem = epoch_s - ud * 86400;
-    int64_t uy; int um, udd;
-    civil_from_days(ud, uy, um, udd);
-    iso_week(uy, um, udd, wy, wk);
-    utc = pack_cal((uint32_t)uy, um, udd, (uint32_t)(rem / 3600), (uint32_t)(rem % 3600 / 60), (uint32_t)(rem % 60),
+    // UTC: the same date unless the offset moves the time across midnight
+    int t = sod - off;
+    int32_t ud = days;
+    if (t < 0) { t += 86400; --ud; }
+    else if (t >= 86400) { t -= 86400; ++ud; }
+    if (ud != days) {
+        civil_from_days(ud, y, m, d);
+        iso_week(y, ud, wy, wk);
+    }
+    utc = pack_cal((uint32_t)y, m, d, (uint32_t)(t / 3600), (uint32_t)(t % 3600 / 60), (uint32_t)(t % 60),
                    (uint32_t)wy, wk);
     return true;
 }
@@ -557,6 +834,12 @@ struct LineOut {
     RegArr<MAX_URI> usep;  // '&' + '?' count of each URI source (query table bound)
     uint32_t arena_need;
 };
+
+// Last ' ' in [lo, hi], else -1.
+template <typename LN>
+__host__ __device__ LP_INLINE int find_space_bwd(const LN& L, int hi, int lo) {
+    return find_bwd(L, hi, lo, [](uint32_t w) { return swar::eq(w, ' '); });
+}
 
 template <typename LN>
 __host__ __device__ LP_INLINE bool prefix_at(const LN& L, int a, int b, const char* lit) {
@@ -653,7 +936,7 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
         o.fl_method.set(f, mkspan(a, q));
         int us = q + 1;
         // protocol: the last ' ' must be followed by HTTP/d+.d+ up to the end
-        int sp = find_bwd(L, b - 1, us, [](uint32_t w) { return swar::eq(w, ' '); });
+        int sp = find_space_bwd(L, b - 1, us);
         if (sp < 0) sp = us - 1;
         bool full = false;
         if (sp >= us && b - sp >= 9 && L[sp + 1] == 'H' && L[sp + 2] == 'T' && L[sp + 3] == 'T' && L[sp + 4] == 'P' &&
@@ -682,8 +965,10 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
     for (int u = 0; u < P.n_uri; ++u) {
         int a, b;
         if (!uri_source(P, o, u, a, b)) continue;
-        uint32_t enc = 0, sep = 0;
-        count2_in(L, a, b, enc, sep);
+        // URIUtil-escaped bytes and '&'/'?' separators are both URI event
+        // bytes: their count bounds both
+        const uint32_t ev = count_uev(L, a, b);
+        const uint32_t enc = ev, sep = ev;
         o.usep.set(u, sep);
         const UriStage& U = P.uri[u];
         uint32_t ulen = (uint32_t)(b - a), tl = ulen + 2 * enc + 2;
@@ -691,7 +976,7 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
         if (U.want_query) n += tl;
         if (U.want_path) n += ulen;
         if (U.want_ref) n += tl;
-        if (U.query_stage >= 0) n += 8 + 16 * (sep + 1) + 2 * tl;
+        if (U.query_stage >= 0) n += 8 + 16 * (sep + 1) + 3 * ulen;
         need += n;
     }
     o.arena_need = (need + 15) & ~15u;
@@ -703,6 +988,7 @@ struct Arena {
     uint8_t* p;     // this line's region
     uint32_t used;
     uint32_t cap;
+    uint32_t slack = 0;  // reserved, never written
     __host__ __device__ uint32_t put(uint32_t c) { p[used] = (uint8_t)c; return used++; }
 };
 
@@ -781,11 +1067,10 @@ __host__ __device__ LP_INLINE bool utf8_ok(const uint8_t* b, uint32_t n) {
     return true;
 }
 
-// java.net.URI.decode of [a,b) of the line (escapes proven valid):
-// returns a ref (line span when nothing to decode), or ~0 on FALLBACK.
+// java.net.URI.decode of [a,b) of the line (holds a '%'; escapes proven
+// valid): returns an arena ref, or ~0 on FALLBACK.
 template <typename LN>
 __host__ __device__ LP_INLINE uint64_t decode_span(const LN& L, int a, int b, Arena& A) {
-    if (find_fwd(L, a, b, [](uint32_t w) { return swar::eq(w, '%'); }) >= b) return mkref(a, b - a, false);
     uint32_t start = A.used;
     for (int q = a; q < b;) {
         uint32_t c = L[q];
@@ -833,29 +1118,79 @@ __host__ __device__ LP_INLINE uint64_t url_decode_value(const LN& L, int vs, int
     return mkref(st, A.used - st, true);
 }
 
-// Values whose decoding is deferred until the query scan is done, so the
-// byte loops of all lanes run side by side instead of one lane at a time.
-struct DeferredDecodes {
-    RegArr<8> span;  // value start | end << 16
-    RegArr<8> slot;  // index of the (name, value) table entry
-    uint32_t n;
-};
+// ---- QueryStringFieldDissector (QueryStringFieldDissector.java:56-108) in
+// two steps.  query_enum (per line, inside the URI stage) splits the rawQuery
+// at '&' / '?' and writes one table slot per non-empty piece:
+//     slot[0] = start | end << 32 (line positions), slot[1] = region offset
+// (3 bytes of the line's arena region per piece byte, enough for a rewritten
+// name plus a decoded value).  query_piece then turns a slot into the
+// (name ref, value ref) pair the replay delivers, or (REF_SKIP, 0) for a name
+// that was not requested.  The kernel runs query_piece on the pieces of all
+// 64 lines of a wave spread evenly over its lanes.
+constexpr uint64_t REF_SKIP = ~0ull;
 
-// One '&'-piece of the rawQuery (line bytes [s, e), '=' at eq or -1):
-// QueryStringFieldDissector.java:75-104.  rw: the name holds upper-case or
-// URIUtil-escaped bytes; pv: the value holds '%' or '+'.
+template <typename LN, typename Cols>
+__host__ __device__ LP_INLINE void query_enum(int qs, const LN& L, int qa, int qb, uint32_t max_pieces, Arena& A,
+                                              Cols& C, int64_t li) {
+    const uint32_t tab = (A.used + 7) & ~7u;
+    uint64_t* t = (uint64_t*)(A.p + tab);
+    uint32_t reg = tab + 16 * max_pieces;
+    uint32_t count = 0;
+    int s = qa;
+    auto piece = [&](int e) {
+        if (e > s) {
+            t[2 * count] = (uint32_t)s | ((uint64_t)(uint32_t)e << 32);
+            t[2 * count + 1] = reg;
+            reg += 3 * (uint32_t)(e - s);
+            ++count;
+        }
+    };
+    for_uev(L, qa, qb, [&](int q, uint32_t c) {
+        if (c == '&' || c == '?') {
+            piece(q);
+            s = q + 1;
+        }
+        return true;
+    });
+    piece(qb);
+    A.used = reg;
+    A.slack += 16 * (max_pieces - count);
+    C.q_count[qs][li] = count;
+    C.q_params[qs][li] = mkref(tab, 16 * count, true);
+}
+
+// One '&'-piece (QueryStringFieldDissector.java:75-104): the name is
+// lower-cased and keeps URIUtil's escapes, never decoded; a piece without '='
+// has value ""; else the value goes through Utils.resilientUrlDecode.
+// region: the owning line's arena region; slot: its table slot.
+// Returns the region bytes written.
 template <typename LN>
-__host__ __device__ LP_INLINE void query_piece(const Program& P, const QueryStage& Q, const LN& L, int s, int e, int eq,
-                                               bool rw, bool pv, Arena& A, uint32_t tab, uint32_t& count,
-                                               DeferredDecodes& dd) {
+__host__ __device__ LP_INLINE uint32_t query_piece(const Program& P, const QueryStage& Q, const LN& L, uint8_t* region,
+                                                   uint64_t* slot) {
+    const uint64_t a0 = slot[0];
+    const int s = (int)(uint32_t)a0, e = (int)(uint32_t)(a0 >> 32);
+    int eq = -1;
+    bool rw = false, pv = false;  // name needs rewriting / value needs decoding
+    for_uev(L, s, e, [&](int q, uint32_t c) {
+        if (c == '=') {
+            if (eq < 0) eq = q;
+        } else if (c == '%' || c == '+') {
+            if (eq >= 0) pv = true;
+        } else if (eq < 0 && (uri_needs_encode(c) || (c - 'A') < 26u)) {
+            rw = true;
+        }
+        return true;
+    });
     const int ne = eq >= 0 ? eq : e;
+    const uint64_t a1 = slot[1];
+    Arena A{region, (uint32_t)a1, 0};
     // name [s, ne): URIUtil-escaped and lower-cased as in the rawQuery
-    const uint32_t mark = A.used;
     uint64_t nref;
     if (rw) {
         const char* HX = "0123456789abcdef";  // URIUtil's %XX, lower-cased with the name
+        const uint32_t mark = A.used;
         for (int q = s; q < ne; ++q) {
-            uint32_t c = L[q];
+            const uint32_t c = L[q];
             if (uri_needs_encode(c)) { A.put('%'); A.put(HX[c >> 4]); A.put(HX[c & 15]); }
             else A.put((c - 'A') < 26u ? (c | 32) : c);
         }
@@ -870,103 +1205,35 @@ __host__ __device__ LP_INLINE void query_piece(const Program& P, const QueryStag
         if (Q.name_len[k] != nlen) continue;
         bool same = true;
         for (uint32_t q = 0; q < nlen && same; ++q) {
-            uint32_t c = rw ? (uint32_t)A.p[mark + q] : L[s + (int)q];
+            const uint32_t c = rw ? (uint32_t)region[ref_off(nref) + q] : L[s + (int)q];
             same = c == P.lit[Q.name_off[k] + q];
         }
         want = same;
     }
     if (!want) {
-        A.used = mark;
-        return;
+        slot[0] = REF_SKIP;
+        slot[1] = 0;
+        return A.used - (uint32_t)a1;
     }
     uint64_t vref;
     if (eq < 0) vref = mkref(0, 0, false);  // no '=' -> ""
     else if (!pv) vref = mkref(eq + 1, e - eq - 1, false);
-    else if (dd.n < 8) {
-        dd.span.set((int)dd.n, (uint32_t)(eq + 1) | ((uint32_t)e << 16));
-        dd.slot.set((int)dd.n, count);
-        ++dd.n;
-        vref = 0;  // filled in by query_pass
-    } else {
-        vref = url_decode_value(L, eq + 1, e, A);
-    }
-    uint64_t* t = (uint64_t*)(A.p + tab);
-    t[2 * count] = nref;
-    t[2 * count + 1] = vref;
-    ++count;
+    else vref = url_decode_value(L, eq + 1, e, A);
+    slot[0] = nref;
+    slot[1] = vref;
+    return A.used - (uint32_t)a1;
 }
 
-// The query part [qa, qb) of a URI, one word-at-a-time pass.  Returns
-// whether the rawQuery is "&" + these bytes unchanged (no further '?', no
-// URIUtil-escaped byte).  With qs >= 0 it also runs the
-// QueryStringFieldDissector (QueryStringFieldDissector.java:56-108): the
-// rawQuery's '&'-pieces are the pieces of [qa, qb) split at '&' and '?'.
+// The query pieces of one line, one after the other (the test-only CPU
+// emulation; the kernel spreads them over the wave).
 template <typename LN, typename Cols>
-__host__ __device__ LP_INLINE bool query_pass(const Program& P, int qs, const LN& L, int qa, int qb, uint32_t max_pieces,
-                                              Arena& A, Cols& C, int64_t li) {
-    bool plain = true;
-    uint32_t tab = 0, count = 0;
-    if (qs >= 0) {
-        tab = (A.used + 7) & ~7u;
-        A.used = tab + 16 * max_pieces;
+__host__ __device__ LP_INLINE void query_pieces_serial(const Program& P, const LN& L, uint8_t* region, Cols& C,
+                                                       int64_t li) {
+    for (int qs = 0; qs < P.n_query; ++qs) {
+        const uint32_t cnt = C.q_count[qs][li];
+        uint64_t* t = (uint64_t*)(region + ref_off(C.q_params[qs][li]));
+        for (uint32_t k = 0; k < cnt; ++k) query_piece(P, P.query[qs], L, region, t + 2 * k);
     }
-    DeferredDecodes dd;
-    dd.n = 0;
-    dd.span.fill(0);
-    dd.slot.fill(0);
-    if (qa < qb) {
-        int s = qa, eqp = -1;
-        bool rw = false, pv = false;
-        const uint32_t AA = L.o + (uint32_t)qa, E = L.o + (uint32_t)qb;
-        const uint32_t W0 = AA >> 2, W1 = (E - 1) >> 2;
-        for (uint32_t W = W0; W <= W1; ++W) {
-            const uint32_t w = L.word(W);
-            uint32_t keep = swar::HI;
-            if (W == W0) keep &= swar::HI << (8 * (AA & 3));
-            if (W == W1) keep &= swar::HI >> (8 * (3 - ((E - 1) & 3)));
-            const uint32_t qm = swar::eq(w, '?') & keep;
-            const uint32_t sep = (swar::eq(w, '&') & keep) | qm;
-            const uint32_t enc = swar::needs_encode(w) & keep;
-            if (qs < 0) {
-                if (qm | enc) { plain = false; break; }
-                continue;
-            }
-            const uint32_t eqm = swar::eq(w, '=') & keep;
-            const uint32_t rwm = (swar::upper(w) & keep) | enc;
-            const uint32_t pvm = (swar::eq(w, '%') | swar::eq(w, '+')) & keep;
-            if (qm | enc) plain = false;
-            uint32_t ev = sep | eqm | rwm | pvm;
-            while (ev) {
-                const int k = swar::first(ev);
-                const uint32_t bit = 0x80u << (8 * k);
-                const int pos = (int)((W << 2) + (uint32_t)k - L.o);
-                if (sep & bit) {
-                    if (pos > s) query_piece(P, P.query[qs], L, s, pos, eqp, rw, pv, A, tab, count, dd);
-                    s = pos + 1;
-                    eqp = -1;
-                    rw = pv = false;
-                } else if (eqm & bit) {
-                    if (eqp < 0) eqp = pos;
-                } else if (rwm & bit) {
-                    if (eqp < 0) rw = true;
-                } else if (eqp >= 0) {
-                    pv = true;
-                }
-                ev &= ~bit;
-            }
-        }
-        if (qs >= 0 && qb > s) query_piece(P, P.query[qs], L, s, qb, eqp, rw, pv, A, tab, count, dd);
-    }
-    for (uint32_t j = 0; j < dd.n; ++j) {
-        const uint32_t sp = dd.span.get((int)j);
-        const uint64_t vref = url_decode_value(L, (int)(sp & 0xFFFF), (int)(sp >> 16), A);
-        ((uint64_t*)(A.p + tab))[2 * dd.slot.get((int)j) + 1] = vref;
-    }
-    if (qs >= 0) {
-        C.q_count[qs][li] = count;
-        C.q_params[qs][li] = mkref(tab, 16 * count, true);
-    }
-    return plain;
 }
 
 // HttpUriDissector fast path on the line bytes [a,b).  Returns status.
@@ -977,48 +1244,38 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
     // ---- guards (FALLBACK when a cleanup step of the reference would change
     // the string), one pass over the special bytes % # & ? ;
     int fa = -1, h = -1, nh = 0, first_pct = -1;
-    bool frag_plain = true;  // no '%' '?' '&' after the '#'
-    {
-        const uint32_t AA = L.o + (uint32_t)a, E = L.o + (uint32_t)b;
-        const uint32_t W0 = AA >> 2, W1 = (E - 1) >> 2;
-        uint32_t wn = L.word(W0);
-        for (uint32_t W = W0; W <= W1; ++W) {
-            const uint32_t w = wn;
-            wn = L.word_or0(W + 1);  // look-ahead: '%' checks and the next iteration
-            uint32_t keep = swar::HI;
-            if (W == W0) keep &= swar::HI << (8 * (AA & 3));
-            if (W == W1) keep &= swar::HI >> (8 * (3 - ((E - 1) & 3)));
-            uint32_t ev = (swar::eq(w, '%') | swar::eq(w, '#') | swar::eq(w, '&') | swar::eq(w, '?') | swar::eq(w, ';')) & keep;
-            while (ev) {
-                const int k = swar::first(ev);
-                ev &= ~(0x80u << (8 * k));
-                const int q = (int)((W << 2) + (uint32_t)k - L.o);
-                const uint32_t c = (w >> (8 * k)) & 0xFFu;
-                if (c == '%') {
-                    const uint64_t ww = (uint64_t)w | ((uint64_t)wn << 32);
-                    if (q + 2 >= b || !is_hex((uint32_t)(ww >> (8 * k + 8)) & 0xFFu) ||
-                        !is_hex((uint32_t)(ww >> (8 * k + 16)) & 0xFFu))
-                        return ST_FALLBACK;  // BAD_EXCAPE_PATTERN
-                    if (first_pct < 0) first_pct = q;
-                    if (h >= 0) frag_plain = false;
-                } else if (c == '#') {
-                    ++nh;
-                    if (h < 0) h = q;
-                    if (q + 1 < b && (L[q + 1] == '&' || L[q + 1] == '?')) return ST_FALLBACK;     // HASH_AMP
-                    if (q + 1 < b && L[q + 1] == 'x') return ST_FALLBACK;                          // ALMOST_HTML_ENCODED
-                    if (q > a && L[q - 1] == '=') return ST_FALLBACK;                              // EQUALS_HASH
-                } else if (c == ';') {
-                    // unescapeHtml4 candidate: [&?][a-zA-Z0-9#]*;
-                    int r = q - 1;
-                    while (r >= a && (is_alnum(L[r]) || L[r] == '#')) --r;
-                    if (r >= a && (L[r] == '&' || L[r] == '?')) return ST_FALLBACK;
-                } else {  // '&' '?'
-                    if (fa < 0) fa = q;
-                    if (h >= 0) frag_plain = false;
-                }
+    // bit 0: the fragment holds '%' '?' or '&' (decoded / rewritten, not a plain span);
+    // bit 1: the rawQuery is not "&" + the bytes between the first '&'/'?' and the '#'
+    uint32_t rewr = 0;
+    int st = ST_OK;
+    for_uev(L, a, b, [&](int q, uint32_t c) {
+        if (c == '%') {
+            if (q + 2 >= b || !is_hex(L[q + 1]) || !is_hex(L[q + 2])) { st = ST_FALLBACK; return false; }  // BAD_EXCAPE_PATTERN
+            if (first_pct < 0) first_pct = q;
+            rewr |= h >= 0 ? 1u : 0u;
+        } else if (c == '#') {
+            ++nh;
+            if (h < 0) h = q;
+            if (q + 1 < b) {
+                const uint32_t d = L[q + 1];
+                if (d == '&' || d == '?' || d == 'x') { st = ST_FALLBACK; return false; }  // HASH_AMP, ALMOST_HTML_ENCODED
             }
+            if (q > a && L[q - 1] == '=') { st = ST_FALLBACK; return false; }  // EQUALS_HASH
+        } else if (c == ';') {
+            // unescapeHtml4 candidate: [&?][a-zA-Z0-9#]*;
+            int r = q - 1;
+            while (r >= a && (is_alnum(L[r]) || L[r] == '#')) --r;
+            if (r >= a && (L[r] == '&' || L[r] == '?')) { st = ST_FALLBACK; return false; }
+        } else if (c == '&' || c == '?') {
+            rewr |= (c == '?' && fa >= 0 && h < 0) ? 2u : 0u;  // a later '?' becomes '&'
+            if (fa < 0) fa = q;
+            rewr |= h >= 0 ? 1u : 0u;
+        } else {
+            rewr |= (fa >= 0 && h < 0 && uri_needs_encode(c)) ? 2u : 0u;  // URIUtil escapes it
         }
-    }
+        return true;
+    });
+    if (st != ST_OK) return st;
     LP_PROF(30 + 8 * u);
     if (nh > 1) return ST_FALLBACK;                                                       // DOUBLE_HASH
     int pend = b;                              // end of path: first '?'(=fa) or '#'
@@ -1113,8 +1370,8 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
             // the gfx950 build (ROCm 7.2, -O3) delivered a wrong offset on
             // lanes whose scan ran an extra word (parity tests caught it)
             const uint64_t amp_ref = mkref(qs0, qe - qs0, false) | REF_AMP;
-            const bool plain = query_pass(P, U.query_stage, L, qs0, qe, usep + 1, A, C, li);
-            if (plain) {
+            if (U.query_stage >= 0) query_enum(U.query_stage, L, qs0, qe, usep + 1, A, C, li);
+            if (!(rewr & 2u)) {
                 C.u_query[u][li] = amp_ref;
             } else {
                 uint32_t st = A.used;
@@ -1136,7 +1393,7 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
     if (U.want_ref && h >= 0) {
         flags |= UF_FRAG;
         // fragment = decode(normalized text after '#')
-        if (frag_plain) C.u_frag[u][li] = mkref(h + 1, b - h - 1, false);
+        if (!(rewr & 1u)) C.u_frag[u][li] = mkref(h + 1, b - h - 1, false);
         else {
             uint32_t st = A.used;
             for (int q = h + 1; q < b;) {

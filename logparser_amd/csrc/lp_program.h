@@ -68,7 +68,8 @@ struct Elem {
     uint16_t lit_len;
     uint8_t nlit;      // token followed by a literal
     uint8_t need;      // ANY_GREEDY: occurrences of the literal's first byte in the literals from here to '$'
-    uint8_t pad[2];
+    int8_t acls;       // mask class (MC_*) holding the first byte of that literal, -1 none
+    uint8_t pad;
     uint32_t lit4;     // first (up to) 4 bytes of that literal, little-endian
 };
 

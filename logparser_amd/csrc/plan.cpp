@@ -15,6 +15,7 @@
 //                                         core/Parser.java:237-490, 904-1012
 //   Parsable.addDissection                core/Parsable.java:142-193 (replay)
 #include "plan.h"
+#include "lp_device.h"
 
 #include <algorithm>
 #include <cstdio>
@@ -744,6 +745,7 @@ void Plan::compile_program() {
         Elem& e = P.elems[P.n_elems++];
         memset(&e, 0, sizeof e);
         e.cap = -1;
+        e.acls = -1;
         if (t.fixed) {
             e.kind = EK_LIT;
             int off = add_lit(t.regex);
@@ -782,6 +784,7 @@ void Plan::compile_program() {
         }
         uint8_t c0 = e.nlit ? P.lit[e.lit_off] : 0;
         if (e.nlit) e.lit4 = P.elems[i + 1].lit4;
+        e.acls = (int8_t)(e.nlit ? bcls::class_of(c0) : -1);
         bool ws0 = c0 == ' ' || (c0 >= 9 && c0 <= 13);
         bool dig0 = c0 >= '0' && c0 <= '9';
         bool hex0 = dig0 || ((c0 | 32) >= 'a' && (c0 | 32) <= 'f');
@@ -1108,6 +1111,7 @@ void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const 
         const uint64_t* t = (const uint64_t*)(c.arena + ref_off(tab));
         set_origin(O_NONE, 0);
         for (uint32_t k = 0; k < cnt; ++k) {
+            if (t[2 * k] == REF_SKIP) continue;  // name not requested
             MVal nm = line_ref(t[2 * k]);
             MVal val = line_ref(t[2 * k + 1]);
             emit(c, name, "STRING", std::string((const char*)nm.p, nm.len), val);

@@ -19,10 +19,13 @@ def oracle():
     return oracle_lib
 
 
-@pytest.fixture(scope="session")
-def emu():
+@pytest.fixture(scope="session", params=["masks", "swar"])
+def emu(request):
+    """The device per-line code on the CPU, once with the byte-class masks of
+    the kernel's LDS path and once with the SWAR scanners of its HBM path."""
     import emu_lib
     emu_lib.build()
+    emu_lib.lib().emu_set_masks(1 if request.param == "masks" else 0)
     return emu_lib
 
 

@@ -61,6 +61,29 @@ int emu_parse_in(void* h, const char* buf, int64_t start, int len, char* out, in
     return parse_impl((Emu*)h, buf + start, len, (const uint8_t*)buf, (uint32_t)start, out, cap);
 }
 
+static int g_masks = 1;  // 1: lines carry byte-class masks (the kernel's LDS path), 0: SWAR scanners (HBM path)
+
+void emu_set_masks(int on) { g_masks = on; }
+
+}  // extern "C"
+
+template <typename LN>
+static int run_line(const Program& P, const LN& L, LineOut& o, uint32_t* stk, Columns& C, HostResults& R, char* out,
+                    int cap) {
+    phase1(P, P.elems, L, o, stk, C, 0);
+    if (o.status == ST_OK && o.arena_need) {
+        R.arena.assign(o.arena_need + 64, 0);
+        Arena A{R.arena.data(), 0, o.arena_need};
+        phase2(P, L, o, A, C, 0);
+        if (o.status == ST_OK) query_pieces_serial(P, L, A.p, C, 0);
+        if (A.used > o.arena_need) { snprintf(out, cap, "ARENA OVERFLOW %u > %u", A.used, o.arena_need); return 3; }
+    }
+    write_line(P, o, C, 0);
+    return 0;
+}
+
+extern "C" {
+
 static int parse_impl(Emu* e, const char* line, int len, const uint8_t* base, uint32_t base_off, char* out, int cap) {
     if (!e->plan.device_ok()) return 2;
     const Program& P = e->plan.program();
@@ -97,17 +120,26 @@ static int parse_impl(Emu* e, const char* line, int len, const uint8_t* base, ui
         C.u_frag[u] = R.u_frag[u].data();
     }
     for (int q = 0; q < MAX_QUERY; ++q) { C.q_count[q] = R.q_count[q].data(); C.q_params[q] = R.q_params[q].data(); }
-    Line L{base, base_off, len};
     LineOut o;
     uint32_t stk[MAX_STACK];
-    phase1(P, P.elems, L, o, stk, C, 0);
-    if (o.status == ST_OK && o.arena_need) {
-        R.arena.assign(o.arena_need + 64, 0);
-        Arena A{R.arena.data(), 0, o.arena_need};
-        phase2(P, L, o, A, C, 0);
-        if (A.used > o.arena_need) { snprintf(out, cap, "ARENA OVERFLOW %u > %u", A.used, o.arena_need); return 3; }
+    int st = 0;
+    if (g_masks) {
+        // as the kernel's LDS window: a 64-byte aligned copy of the bytes
+        // around the line plus the byte-class masks of that copy
+        const uint32_t lo = base_off & ~63u, hi = (base_off + (uint32_t)len + 4) & ~3u;
+        const uint32_t wn = ((hi - lo) + 63) & ~63u;
+        std::vector<uint64_t> wbuf(wn / 8 + 8, ~0ull);
+        memcpy(wbuf.data(), base + lo, hi - lo);
+        const uint32_t ms = wn / 64;
+        std::vector<uint64_t> masks(MC_N * ms);
+        build_masks((const uint8_t*)wbuf.data(), wn, masks.data(), ms);
+        MLine L{(const uint8_t*)wbuf.data(), base_off - lo, len, masks.data(), ms};
+        st = run_line(P, L, o, stk, C, R, out, cap);
+    } else {
+        Line L{base, base_off, len};
+        st = run_line(P, L, o, stk, C, R, out, cap);
     }
-    write_line(P, o, C, 0);
+    if (st) return st;
     if (o.status != ST_OK) return o.status;
     std::string js = e->plan.record_json(R, 0);
     if ((int)js.size() + 1 > cap) return -1;

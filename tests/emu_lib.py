@@ -38,6 +38,7 @@ def lib():
         L.emu_parse_in.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_char_p,
                                    ctypes.c_int]
         L.emu_describe.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]
+        L.emu_set_masks.argtypes = [ctypes.c_int]
         L.emu_possible_paths.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
         _lib = L
     return _lib

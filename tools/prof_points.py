@@ -24,11 +24,11 @@ st = p.run(t.data_ptr(), len(data))
 L.lp_profile_read(buf, 64)
 names = {0: "start", 1: "staged", 2: "phase1 entry", 3: "guard", 4: "match", 5: "tok flags", 6: "time",
          7: "first line", 8: "arena need", 9: "phase1 exit", 10: "uri0 in", 11: "uri0 out", 12: "uri1 in",
-         13: "uri1 out", 20: "phase2 exit", 21: "written"}
+         13: "uri1 out", 20: "phase2 exit", 21: "rows written", 22: "query pieces"}
 for u in range(2):
     for j, nm in enumerate(["pass1", "authority", "path", "query", "frag"]):
         names[30 + 8 * u + j] = "u%d %s done" % (u, nm)
-order = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 30, 31, 32, 33, 34, 11, 12, 38, 39, 40, 41, 42, 13, 20, 21]
+order = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 30, 31, 32, 33, 34, 11, 12, 38, 39, 40, 41, 42, 13, 20, 21, 22]
 pts = [k for k in order if buf[2 * k + 1]]
 print("parse ms %.3f  waves %d" % (st["ms_parse"], buf[1]))
 prev = None
