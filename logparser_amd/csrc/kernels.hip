@@ -31,14 +31,34 @@ __device__ __forceinline__ uint32_t nl_mask(uint32_t w) {
     return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
 }
 
-__device__ __forceinline__ uint32_t count_nl16(const uint8_t* p, uint64_t pos, uint64_t nbytes) {
-    if (pos + 16 <= nbytes && ((uintptr_t)(p + pos) & 15) == 0) {
-        uint4 v = *reinterpret_cast<const uint4*>(p + pos);
-        return __popc(nl_mask(v.x)) + __popc(nl_mask(v.y)) + __popc(nl_mask(v.z)) + __popc(nl_mask(v.w));
+// the 16 bytes at pos (zero past nbytes) and their '\n' masks (bit 7 of
+// each byte, one 32-bit mask per word)
+struct Piece16 {
+    uint32_t m[4];
+    __device__ __forceinline__ uint32_t count() const {
+        return __popc(m[0]) + __popc(m[1]) + __popc(m[2]) + __popc(m[3]);
     }
-    uint32_t c = 0;
-    for (uint64_t k = pos; k < pos + 16 && k < nbytes; ++k) c += p[k] == '\n';
-    return c;
+};
+__device__ __forceinline__ Piece16 nl16(const uint8_t* p, uint64_t pos, uint64_t nbytes) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (pos + 16 <= nbytes && ((uintptr_t)(p + pos) & 15) == 0) {
+        v = *reinterpret_cast<const uint4*>(p + pos);
+    } else {
+        uint32_t w[4] = {0, 0, 0, 0};
+        for (uint64_t k = pos; k < pos + 16 && k < nbytes; ++k) w[(k - pos) >> 2] |= (uint32_t)p[k] << (8 * ((k - pos) & 3));
+        v = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    Piece16 r;
+    r.m[0] = nl_mask(v.x);
+    r.m[1] = nl_mask(v.y);
+    r.m[2] = nl_mask(v.z);
+    r.m[3] = nl_mask(v.w);
+    if (pos + 16 > nbytes) {  // zero bytes past the end are not newlines anyway
+        for (int j = 0; j < 4; ++j)
+            for (int b = 0; b < 4; ++b)
+                if (pos + 4 * j + b >= nbytes) r.m[j] &= ~(0x80u << (8 * b));
+    }
+    return r;
 }
 
 __global__ __launch_bounds__(NL_THREADS) void k_count_newlines(const uint8_t* __restrict__ buf, uint64_t nbytes,
@@ -47,7 +67,7 @@ __global__ __launch_bounds__(NL_THREADS) void k_count_newlines(const uint8_t* __
     uint32_t c = 0;
     for (int it = 0; it < CHUNK / (NL_THREADS * 16); ++it) {
         uint64_t pos = base + ((uint64_t)it * NL_THREADS + threadIdx.x) * 16;
-        if (pos < nbytes) c += count_nl16(buf, pos, nbytes);
+        if (pos < nbytes) c += nl16(buf, pos, nbytes).count();
     }
     // block reduction
     __shared__ uint32_t red[NL_THREADS / 64];
@@ -91,7 +111,9 @@ __global__ __launch_bounds__(NL_THREADS) void k_line_offsets(const uint8_t* __re
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int it = 0; it < CHUNK / (NL_THREADS * 16); ++it) {
         uint64_t pos = base + ((uint64_t)it * NL_THREADS + threadIdx.x) * 16;
-        uint32_t c = pos < nbytes ? count_nl16(buf, pos, nbytes) : 0;
+        Piece16 pc{{0, 0, 0, 0}};
+        if (pos < nbytes) pc = nl16(buf, pos, nbytes);
+        const uint32_t c = pc.count();
         // block exclusive scan of c
         uint32_t x = c;
         for (int d = 1; d < 64; d <<= 1) {
@@ -106,9 +128,13 @@ __global__ __launch_bounds__(NL_THREADS) void k_line_offsets(const uint8_t* __re
             tot += wsum[w];
         }
         uint64_t k = run + wpre + x - c;  // index of this thread's first '\n'
-        if (c) {
-            for (uint64_t q = pos; q < pos + 16 && q < nbytes; ++q)
-                if (buf[q] == '\n') line_off[++k] = q + 1;
+        for (int j = 0; j < 4; ++j) {
+            uint32_t m = pc.m[j];
+            while (m) {
+                const uint32_t b = (uint32_t)__builtin_ctz(m) >> 3;
+                m &= m - 1;
+                line_off[++k] = pos + 4 * j + b + 1;
+            }
         }
         run += tot;
         __syncthreads();
@@ -187,8 +213,8 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
         const bool has = active && o.status == ST_OK && need != 0;
         const unsigned long long my_ab = has ? C.arena_base[li] : 0ull;
         for (int qs = 0; qs < P.n_query; ++qs) {
-            const uint32_t np = has ? C.q_count[qs][li] : 0u;
-            const uint32_t my_tab = np ? ref_off(C.q_params[qs][li]) : 0u;
+            const uint32_t np = has ? o.qpend.get(qs) : 0u;
+            const uint32_t my_list = o.qlist.get(qs);
             uint32_t incl = np;
             for (int d = 1; d < 64; d <<= 1) {
                 const uint32_t y = __shfl_up(incl, d);
@@ -197,16 +223,18 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
             const uint32_t base = incl - np, total = __shfl(incl, 63);
             for (uint32_t g0 = 0; g0 < total; g0 += PW) {
                 const uint32_t g = g0 + (uint32_t)lane;
-                int own = 0;  // last lane whose first piece index is <= g
+                int own = 0;  // last lane whose first pending piece index is <= g
                 for (int st = 32; st; st >>= 1)
                     if (__shfl(base, own + st) <= g) own += st;
-                const uint32_t ob = __shfl(base, own), otab = __shfl(my_tab, own);
+                const uint32_t ob = __shfl(base, own), olist = __shfl(my_list, own);
                 const unsigned long long oab = __shfl(my_ab, own);
                 const auto OL = owner_line(L, own);
                 if (g < total) {
                     uint8_t* region = C.arena + oab;
-                    uint64_t* slot = reinterpret_cast<uint64_t*>(region + otab) + 2 * (g - ob);
-                    const uint32_t reserved = 3u * (uint32_t)((slot[0] >> 32) - (uint32_t)slot[0]);
+                    const uint32_t so = reinterpret_cast<const uint32_t*>(region + olist)[g - ob];
+                    uint64_t* slot = reinterpret_cast<uint64_t*>(region + so);
+                    const uint64_t a0 = slot[0];
+                    const uint32_t reserved = 3u * (uint32_t)(((a0 >> 16) & 0xFFFFu) - (a0 & 0xFFFFu));
                     const uint32_t used = query_piece(P, P.query[qs], OL, region, slot);
                     written += used - reserved;  // modulo 2^32: the wave sum is exact
                 }

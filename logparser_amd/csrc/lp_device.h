@@ -832,6 +832,7 @@ struct LineOut {
     uint32_t tok_flags;
     RegArr<MAX_FL> fl_kind, fl_method, fl_uri, fl_proto;
     RegArr<MAX_URI> usep;  // '&' + '?' count of each URI source (query table bound)
+    RegArr<MAX_QUERY> qlist, qpend;  // per query stage: pending-piece list (arena region offset), its length
     uint32_t arena_need;
 };
 
@@ -885,6 +886,8 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
     o.fl_uri.fill(0);
     o.fl_proto.fill(0);
     o.usep.fill(0);
+    o.qlist.fill(0);
+    o.qpend.fill(0);
     if (L.n > MAX_LINE) { o.status = ST_FALLBACK; return; }
     // fast-path guard: printable ASCII + TAB only (no \r, no line
     // terminators, no bytes that need UTF-8 decoding or URIUtil UTF-8 bytes)
@@ -976,7 +979,7 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
         if (U.want_query) n += tl;
         if (U.want_path) n += ulen;
         if (U.want_ref) n += tl;
-        if (U.query_stage >= 0) n += 8 + 16 * (sep + 1) + 3 * ulen;
+        if (U.query_stage >= 0) n += 16 + 20 * (sep + 1) + 3 * ulen;  // slots, pending list, piece regions
         need += n;
     }
     o.arena_need = (need + 15) & ~15u;
@@ -992,55 +995,92 @@ struct Arena {
     __host__ __device__ uint32_t put(uint32_t c) { p[used] = (uint8_t)c; return used++; }
 };
 
+// Forward byte reader over a line: 8 bytes in registers, one aligned word
+// read per 4 bytes for increasing positions (any position < n works).
+template <typename LN>
+struct Fwd {
+    const LN& L;
+    uint32_t W;
+    uint64_t ww;
+    __host__ __device__ LP_INLINE Fwd(const LN& l, int p) : L(l) {
+        W = (L.o + (uint32_t)p) >> 2;
+        ww = (uint64_t)L.word_or0(W) | ((uint64_t)L.word_or0(W + 1) << 32);
+    }
+    __host__ __device__ LP_INLINE uint32_t at(int p) {
+        const uint32_t A = L.o + (uint32_t)p, w = A >> 2;
+        if (w != W) {
+            if (w == W + 1) ww = (ww >> 32) | ((uint64_t)L.word_or0(w + 1) << 32);
+            else ww = (uint64_t)L.word_or0(w) | ((uint64_t)L.word_or0(w + 1) << 32);
+            W = w;
+        }
+        return (uint32_t)(ww >> (8 * (A & 3))) & 0xFFu;
+    }
+};
+
+// 128-bit character sets
+__host__ __device__ LP_INLINE bool in_set(uint32_t c, uint64_t lo, uint64_t hi) {
+    return c < 0x80 && (((c < 64 ? lo : hi) >> (c & 63)) & 1u);
+}
+// chars in both L_SERVER and L_REG_NAME of java.net.URI without '@' and
+// escapes: alnum . - : _ ! ~ * ' ( ) ; = + $ ,
+__host__ __device__ LP_INLINE bool authority_char(uint32_t c) { return in_set(c, 0x2FFF7F9200000000ull, 0x47FFFFFE87FFFFFEull); }
+// scheme = alpha *( alpha | digit | "+" | "-" | "." )
+__host__ __device__ LP_INLINE bool scheme_char(uint32_t c) { return in_set(c, 0x03FF680000000000ull, 0x07FFFFFE07FFFFFEull); }
+
 // java.net.URI.Parser.parseIPv4Address/scanIPv4Address on [a,b) of the
-// authority (JDK 8); returns end or -1.
+// authority (JDK 8); returns end or -1.  One forward pass: up to four
+// dot-separated octets of at most 9 digits (Integer.parseInt), each <= 255,
+// then neither another digit/'.' nor anything but ':'.
 template <typename LN>
 __host__ __device__ LP_INLINE int jdk_ipv4(const LN& L, int a, int b) {
-    int m = a;
-    while (m < b && (is_digit(L[m]) || L[m] == '.')) ++m;
-    if (m <= a) return -1;
+    Fwd<LN> cur(L, a);
     int p = a;
     for (int o = 0; o < 4; ++o) {
         int q = p;
-        while (q < m && is_digit(L[q])) ++q;
-        if (q <= p) return -1;
-        if (q - p > 9) return -1;  // Integer.parseInt would overflow -> NumberFormatException -> -1
         uint32_t v = 0;
-        for (int r = p; r < q; ++r) v = v * 10 + (L[r] - '0');
-        if (v > 255) return -1;
+        uint32_t c = 0;
+        while (q < b && is_digit(c = cur.at(q))) {
+            if (v < 1000) v = v * 10 + (c - '0');
+            ++q;
+        }
+        if (q <= p || q - p > 9 || v > 255) return -1;
         p = q;
         if (o < 3) {
-            if (p >= m || L[p] != '.') return -1;
+            if (p >= b || c != '.') return -1;
             ++p;
+        } else if (p < b && c != ':') {
+            return -1;  // a '.' continues the digit/dot run (scanIPv4Address fails); else not ':'
         }
     }
-    if (p < m) return -1;
-    if (p < b && L[p] != ':') return -1;
     return p;
 }
 
 // java.net.URI.Parser.parseHostname on [a,b); returns end or -1 (fail)
 template <typename LN>
 __host__ __device__ LP_INLINE int jdk_hostname(const LN& L, int a, int b) {
+    Fwd<LN> cur(L, a);
     int p = a, l = -1;
+    uint32_t l0 = 0;  // first char of the last label
+    uint32_t c = p < b ? cur.at(p) : 0u;
     do {
-        int q = p;
-        while (q < b && is_alnum(L[q])) ++q;
-        if (q <= p) break;
+        // label: alnum (alnum | '-')*, not ending in '-'
+        if (!(p < b && is_alnum(c))) break;
         l = p;
-        p = q;
-        q = p;
-        while (q < b && (is_alnum(L[q]) || L[q] == '-')) ++q;
-        if (q > p) {
-            if (L[q - 1] == '-') return -1;
-            p = q;
-        }
-        if (!(p < b && L[p] == '.')) break;
+        l0 = c;
+        uint32_t last = c;
         ++p;
+        while (p < b && (is_alnum(c = cur.at(p)) || c == '-')) {
+            last = c;
+            ++p;
+        }
+        if (last == '-') return -1;
+        if (!(p < b && c == '.')) break;
+        ++p;
+        c = p < b ? cur.at(p) : 0u;
     } while (p < b);
-    if (p < b && L[p] != ':') return -1;
+    if (p < b && c != ':') return -1;
     if (l < 0) return -1;
-    if (l > a && !is_alpha(L[l])) return -1;
+    if (l > a && !is_alpha(l0)) return -1;
     return p;
 }
 
@@ -1118,71 +1158,59 @@ __host__ __device__ LP_INLINE uint64_t url_decode_value(const LN& L, int vs, int
     return mkref(st, A.used - st, true);
 }
 
-// ---- QueryStringFieldDissector (QueryStringFieldDissector.java:56-108) in
-// two steps.  query_enum (per line, inside the URI stage) splits the rawQuery
-// at '&' / '?' and writes one table slot per non-empty piece:
-//     slot[0] = start | end << 32 (line positions), slot[1] = region offset
-// (3 bytes of the line's arena region per piece byte, enough for a rewritten
-// name plus a decoded value).  query_piece then turns a slot into the
-// (name ref, value ref) pair the replay delivers, or (REF_SKIP, 0) for a name
-// that was not requested.  The kernel runs query_piece on the pieces of all
-// 64 lines of a wave spread evenly over its lanes.
-constexpr uint64_t REF_SKIP = ~0ull;
+// ---- QueryStringFieldDissector (QueryStringFieldDissector.java:56-108).
+// The URI stage's event pass splits the rawQuery at '&' / '?' into a table of
+// one (name ref, value ref) slot per non-empty piece, noting for each piece
+// its first '=' and whether the name needs rewriting (upper case / URIUtil
+// escapes) or the value decoding ('%' / '+').  A plain piece of a stage that
+// wants every name is final at once (two line refs).  Any other piece is
+// left "pending": slot[0] = start | end << 16 | (eq + 1) << 32 | flags << 48,
+// slot[1] = offset of 3 bytes of the line's arena region per piece byte, and
+// its slot offset is appended to the line's pending list; query_piece
+// completes it.  The kernel runs query_piece on the pending pieces of all 64
+// lines of a wave spread evenly over its lanes.
+constexpr uint64_t REF_SKIP = ~0ull;  // slot of a piece whose name was not requested
+constexpr uint32_t QP_RW = 1, QP_PV = 2;
 
-template <typename LN, typename Cols>
-__host__ __device__ LP_INLINE void query_enum(int qs, const LN& L, int qa, int qb, uint32_t max_pieces, Arena& A,
-                                              Cols& C, int64_t li) {
-    const uint32_t tab = (A.used + 7) & ~7u;
-    uint64_t* t = (uint64_t*)(A.p + tab);
-    uint32_t reg = tab + 16 * max_pieces;
-    uint32_t count = 0;
-    int s = qa;
-    auto piece = [&](int e) {
+struct QueryTable {
+    uint32_t tab = 0, list = 0, reg = 0, count = 0, npend = 0, maxp = 0;
+    int s = 0, eq = -1;
+    uint32_t pf = 0;
+    bool on = false, set = false;  // enumerating now / table laid out
+    // piece [s, e) ends: finalize or leave pending
+    __host__ __device__ LP_INLINE void emit(const QueryStage& Q, uint8_t* region, int e) {
         if (e > s) {
-            t[2 * count] = (uint32_t)s | ((uint64_t)(uint32_t)e << 32);
-            t[2 * count + 1] = reg;
-            reg += 3 * (uint32_t)(e - s);
+            uint64_t* t = (uint64_t*)(region + tab) + 2 * count;
+            if (pf == 0 && Q.want_all) {
+                const int ne = eq >= 0 ? eq : e;
+                t[0] = mkref((uint32_t)s, (uint32_t)(ne - s), false);
+                t[1] = eq < 0 ? mkref(0, 0, false) : mkref((uint32_t)eq + 1, (uint32_t)(e - eq - 1), false);
+            } else {
+                t[0] = (uint64_t)(uint32_t)s | ((uint64_t)(uint32_t)e << 16) | ((uint64_t)(uint32_t)(eq + 1) << 32) |
+                       ((uint64_t)pf << 48);
+                t[1] = reg;
+                reg += 3 * (uint32_t)(e - s);
+                ((uint32_t*)(region + list))[npend++] = tab + 16 * count;
+            }
             ++count;
         }
-    };
-    for_uev(L, qa, qb, [&](int q, uint32_t c) {
-        if (c == '&' || c == '?') {
-            piece(q);
-            s = q + 1;
-        }
-        return true;
-    });
-    piece(qb);
-    A.used = reg;
-    A.slack += 16 * (max_pieces - count);
-    C.q_count[qs][li] = count;
-    C.q_params[qs][li] = mkref(tab, 16 * count, true);
-}
+        eq = -1;
+        pf = 0;
+    }
+};
 
-// One '&'-piece (QueryStringFieldDissector.java:75-104): the name is
-// lower-cased and keeps URIUtil's escapes, never decoded; a piece without '='
-// has value ""; else the value goes through Utils.resilientUrlDecode.
-// region: the owning line's arena region; slot: its table slot.
-// Returns the region bytes written.
+// Completes a pending piece (QueryStringFieldDissector.java:75-104): the name
+// is lower-cased and keeps URIUtil's escapes, never decoded; a piece without
+// '=' has value ""; else the value goes through Utils.resilientUrlDecode.
+// region: the owning line's arena region; slot: its table slot.  Returns the
+// region bytes written.
 template <typename LN>
 __host__ __device__ LP_INLINE uint32_t query_piece(const Program& P, const QueryStage& Q, const LN& L, uint8_t* region,
                                                    uint64_t* slot) {
-    const uint64_t a0 = slot[0];
-    const int s = (int)(uint32_t)a0, e = (int)(uint32_t)(a0 >> 32);
-    int eq = -1;
-    bool rw = false, pv = false;  // name needs rewriting / value needs decoding
-    for_uev(L, s, e, [&](int q, uint32_t c) {
-        if (c == '=') {
-            if (eq < 0) eq = q;
-        } else if (c == '%' || c == '+') {
-            if (eq >= 0) pv = true;
-        } else if (eq < 0 && (uri_needs_encode(c) || (c - 'A') < 26u)) {
-            rw = true;
-        }
-        return true;
-    });
+    const uint64_t a0 = slot[0], a1 = slot[1];
+    const int s = (int)(a0 & 0xFFFFu), e = (int)((a0 >> 16) & 0xFFFFu), eq = (int)((a0 >> 32) & 0xFFFFu) - 1;
+    const bool rw = (a0 >> 48) & QP_RW, pv = (a0 >> 48) & QP_PV;
     const int ne = eq >= 0 ? eq : e;
-    const uint64_t a1 = slot[1];
     Arena A{region, (uint32_t)a1, 0};
     // name [s, ne): URIUtil-escaped and lower-cased as in the rawQuery
     uint64_t nref;
@@ -1224,23 +1252,13 @@ __host__ __device__ LP_INLINE uint32_t query_piece(const Program& P, const Query
     return A.used - (uint32_t)a1;
 }
 
-// The query pieces of one line, one after the other (the test-only CPU
-// emulation; the kernel spreads them over the wave).
-template <typename LN, typename Cols>
-__host__ __device__ LP_INLINE void query_pieces_serial(const Program& P, const LN& L, uint8_t* region, Cols& C,
-                                                       int64_t li) {
-    for (int qs = 0; qs < P.n_query; ++qs) {
-        const uint32_t cnt = C.q_count[qs][li];
-        uint64_t* t = (uint64_t*)(region + ref_off(C.q_params[qs][li]));
-        for (uint32_t k = 0; k < cnt; ++k) query_piece(P, P.query[qs], L, region, t + 2 * k);
-    }
-}
-
 // HttpUriDissector fast path on the line bytes [a,b).  Returns status.
 template <typename LN, typename Cols>
 __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L, int a, int b, uint32_t usep, Arena& A,
-                                            Cols& C, int64_t li) {
+                                            Cols& C, int64_t li, LineOut& o) {
     const UriStage& U = P.uri[u];
+    const int qsi = U.want_query ? U.query_stage : -1;
+    QueryTable T;
     // ---- guards (FALLBACK when a cleanup step of the reference would change
     // the string), one pass over the special bytes % # & ? ;
     int fa = -1, h = -1, nh = 0, first_pct = -1;
@@ -1253,8 +1271,13 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
             if (q + 2 >= b || !is_hex(L[q + 1]) || !is_hex(L[q + 2])) { st = ST_FALLBACK; return false; }  // BAD_EXCAPE_PATTERN
             if (first_pct < 0) first_pct = q;
             rewr |= h >= 0 ? 1u : 0u;
+            if (T.on && h < 0 && T.eq >= 0) T.pf |= QP_PV;
         } else if (c == '#') {
             ++nh;
+            if (T.on && h < 0) {
+                T.emit(P.query[qsi], A.p, q);
+                T.on = false;  // the rawQuery ends at the first '#'
+            }
             if (h < 0) h = q;
             if (q + 1 < b) {
                 const uint32_t d = L[q + 1];
@@ -1268,14 +1291,45 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
             if (r >= a && (L[r] == '&' || L[r] == '?')) { st = ST_FALLBACK; return false; }
         } else if (c == '&' || c == '?') {
             rewr |= (c == '?' && fa >= 0 && h < 0) ? 2u : 0u;  // a later '?' becomes '&'
+            if (T.on) {
+                T.emit(P.query[qsi], A.p, q);
+                T.s = q + 1;
+            } else if (fa < 0 && h < 0 && qsi >= 0) {
+                // the rawQuery starts: table, pending list, piece regions
+                T.on = T.set = true;
+                T.maxp = usep + 1;
+                T.tab = (A.used + 7) & ~7u;
+                T.list = T.tab + 16 * T.maxp;
+                T.reg = T.list + ((4 * T.maxp + 7) & ~7u);
+                T.s = q + 1;
+            }
             if (fa < 0) fa = q;
             rewr |= h >= 0 ? 1u : 0u;
-        } else {
-            rewr |= (fa >= 0 && h < 0 && uri_needs_encode(c)) ? 2u : 0u;  // URIUtil escapes it
+        } else {  // = + A-Z and URIUtil-escaped bytes
+            const bool enc = uri_needs_encode(c);
+            rewr |= (fa >= 0 && h < 0 && enc) ? 2u : 0u;  // URIUtil escapes it
+            if (T.on) {
+                if (c == '=') {
+                    if (T.eq < 0) T.eq = q;
+                } else if (c == '+') {
+                    if (T.eq >= 0) T.pf |= QP_PV;
+                } else if (T.eq < 0) {
+                    T.pf |= QP_RW;
+                }
+            }
         }
         return true;
     });
     if (st != ST_OK) return st;
+    if (T.set) {
+        if (T.on) T.emit(P.query[qsi], A.p, b);
+        A.used = T.reg;
+        A.slack += 16 * (T.maxp - T.count) + ((4 * T.maxp + 7) & ~7u);  // unused slots; the pending list is scratch
+        C.q_count[qsi][li] = T.count;
+        C.q_params[qsi][li] = mkref(T.tab, 16 * T.count, true);
+        o.qlist.set(qsi, T.list);
+        o.qpend.set(qsi, T.npend);
+    }
     LP_PROF(30 + 8 * u);
     if (nh > 1) return ST_FALLBACK;                                                       // DOUBLE_HASH
     int pend = b;                              // end of path: first '?'(=fa) or '#'
@@ -1290,34 +1344,34 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
     } else {
         flags |= UF_IS_URL;
         // scheme: ':' before any of "/?#" (in the normalized string '?' is at fa)
+        Fwd<LN> cur(L, a);
+        bool sch_ok = is_alpha(cur.at(a));
         int p = a;
-        while (p < b && L[p] != ':' && L[p] != '/' && L[p] != '#' && p != fa) ++p;
-        if (p < b && L[p] == ':') {
-            if (p == a || !is_alpha(L[a])) return ST_BAD;                                  // URISyntaxException
-            for (int q = a + 1; q < p; ++q) {
-                uint32_t c = L[q];
-                if (!(is_alnum(c) || c == '+' || c == '-' || c == '.')) return ST_BAD;
-            }
+        uint32_t c = 0;
+        while (p < b && p != fa) {
+            c = cur.at(p);
+            if (c == ':' || c == '/' || c == '#') break;
+            sch_ok = sch_ok && scheme_char(c);
+            ++p;
+        }
+        if (p < b && p != fa && c == ':') {
+            if (p == a || !sch_ok) return ST_BAD;                                          // URISyntaxException
             flags |= UF_SCHEME;
             scheme_ref = (int64_t)mkref(a, p - a, false);
             ++p;
-            if (!(p < b && L[p] == '/')) return ST_FALLBACK;                              // opaque URI
-            if (p + 1 < b && L[p + 1] == '/') {
+            if (!(p < b && cur.at(p) == '/')) return ST_FALLBACK;                          // opaque URI
+            if (p + 1 < b && cur.at(p + 1) == '/') {
+                // authority [as, ae): up to '/', '#' or the first '?'; only chars
+                // in both L_SERVER and L_REG_NAME of java.net.URI (no '@'
+                // userinfo, no escapes), else FALLBACK
                 int as = p + 2, ae = as;
-                while (ae < b && L[ae] != '/' && L[ae] != '#' && ae != fa) ++ae;
-                if (ae == as) return ST_FALLBACK;                                          // empty authority
-                // chars in both L_SERVER and L_REG_NAME of java.net.URI (no '@'
-                // userinfo, no escapes): server parse, else registry (host null)
-                for (int q = as; q < ae; ++q) {
-                    uint32_t c = L[q];
-                    bool ok = is_alnum(c);
-                    switch (c) {
-                    case '.': case '-': case ':': case '_': case '!': case '~': case '*': case '\'':
-                    case '(': case ')': case ';': case '=': case '+': case '$': case ',':
-                        ok = true;
-                    }
-                    if (!ok) return ST_FALLBACK;
+                while (ae < b && ae != fa) {
+                    const uint32_t d = cur.at(ae);
+                    if (d == '/' || d == '#') break;
+                    if (!authority_char(d)) return ST_FALLBACK;
+                    ++ae;
                 }
+                if (ae == as) return ST_FALLBACK;                                          // empty authority
                 // parseServer; any failure -> registry-based authority (host null)
                 int he = jdk_ipv4(L, as, ae);
                 if (he <= as) he = jdk_hostname(L, as, ae);
@@ -1327,10 +1381,12 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
                     // ":" port digits up to the end of the authority
                     int q = he + 1;
                     if (q < ae) {
+                        Fwd<LN> pc(L, q);
                         uint64_t v = 0;
                         for (int r = q; r < ae; ++r) {
-                            if (!is_digit(L[r])) { ok = false; break; }
-                            v = v * 10 + (L[r] - '0');
+                            const uint32_t d = pc.at(r);
+                            if (!is_digit(d)) { ok = false; break; }
+                            v = v * 10 + (d - '0');
                             if (v > 0x7FFFFFFFull) { ok = false; break; }
                         }
                         if (ok) pt = (int)v;
@@ -1370,7 +1426,6 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
             // the gfx950 build (ROCm 7.2, -O3) delivered a wrong offset on
             // lanes whose scan ran an extra word (parity tests caught it)
             const uint64_t amp_ref = mkref(qs0, qe - qs0, false) | REF_AMP;
-            if (U.query_stage >= 0) query_enum(U.query_stage, L, qs0, qe, usep + 1, A, C, li);
             if (!(rewr & 2u)) {
                 C.u_query[u][li] = amp_ref;
             } else {
@@ -1412,6 +1467,17 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
     return ST_OK;
 }
 
+// The pending query pieces of one line, one after the other (the test-only
+// CPU emulation; the kernel spreads them over the wave).
+template <typename LN>
+__host__ __device__ LP_INLINE void query_pieces_serial(const Program& P, const LN& L, const LineOut& o, uint8_t* region) {
+    for (int qs = 0; qs < P.n_query; ++qs) {
+        const uint32_t* list = (const uint32_t*)(region + o.qlist.get(qs));
+        for (uint32_t k = 0; k < o.qpend.get(qs); ++k)
+            query_piece(P, P.query[qs], L, region, (uint64_t*)(region + list[k]));
+    }
+}
+
 // Phase 2: URI + query stages into the line's arena region.
 template <typename LN, typename Cols>
 __host__ __device__ LP_INLINE void phase2(const Program& P, const LN& L, LineOut& o, Arena& A, Cols& C, int64_t li) {
@@ -1423,7 +1489,7 @@ __host__ __device__ LP_INLINE void phase2(const Program& P, const LN& L, LineOut
             continue;
         }
         LP_PROF(10 + 2 * u);
-        int st = uri_stage(P, u, L, a, b, o.usep.get(u), A, C, li);
+        int st = uri_stage(P, u, L, a, b, o.usep.get(u), A, C, li, o);
         LP_PROF(11 + 2 * u);
         if (st != ST_OK) o.status = st;
     }

@@ -75,7 +75,7 @@ static int run_line(const Program& P, const LN& L, LineOut& o, uint32_t* stk, Co
         R.arena.assign(o.arena_need + 64, 0);
         Arena A{R.arena.data(), 0, o.arena_need};
         phase2(P, L, o, A, C, 0);
-        if (o.status == ST_OK) query_pieces_serial(P, L, A.p, C, 0);
+        if (o.status == ST_OK) query_pieces_serial(P, L, o, A.p);
         if (A.used > o.arena_need) { snprintf(out, cap, "ARENA OVERFLOW %u > %u", A.used, o.arena_need); return 3; }
     }
     write_line(P, o, C, 0);
