@@ -293,6 +293,210 @@ static void apache_token_parsers(tplist *l) {
     first_last(l, "%{referer}i", "request.referer", "HTTP.URI", STRING_ONLY, FORMAT_STRING, 1);
 }
 
+/* ---------------------------------------------------------------- NGINX
+ * NginxHttpdLogFormatDissector.createAllTokenParsers (hp/NginxHttpdLogFormatDissector.java:121-142):
+ * the token parsers of every module, in module order.  TokenParser's default
+ * prio is 10 (tokenformat/TokenParser.java:81-88), NamedTokenParser's 0
+ * (tokenformat/NamedTokenParser.java:34-41). */
+#define FORMAT_STANDARD_TIME_ISO8601 "[1-9][0-9][0-9][0-9]-[0-1][0-9]-[0-3][0-9]T[0-9][0-9]:[0-9][0-9]:[0-9][0-9][\\+|\\-][0-9][0-9]:[0-9][0-9]"
+#define FORMAT_NUMBER_DECIMAL FORMAT_NUMBER "\\." FORMAT_NUMBER
+#define FORMAT_NUMBER_OPTIONAL_DECIMAL FORMAT_NUMBER "(?:\\." FORMAT_NUMBER ")?"
+/* UpstreamModule.upstreamListOf (nginxmodules/UpstreamModule.java:42-44) */
+#define UPSTREAM_LIST(X) X "(?: *, *" X "(?: *: *" X ")?)*"
+
+static void ng(tplist *l, const char *tok, const char *name, const char *type, int casts, const char *regex, int prio) {
+    tp_out(tp_add(l, TP_PLAIN, tok, regex, prio), type, name, casts);
+}
+static void ng_named(tplist *l, const char *pat, const char *name, const char *type, int casts, const char *regex, int prio) {
+    tp_out(tp_add(l, TP_NAMED, pat, regex, prio), type, name, casts);
+}
+/* TokenFormatDissector.NotImplementedTokenParser (tokenformat/TokenFormatDissector.java:89-103) */
+static void ng_notimpl(tplist *l, const char *tok, const char *prefix, const char *regex, int prio) {
+    char name[256];
+    int k = snprintf(name, sizeof name, "%s_", prefix);
+    for (const char *p = tok; *p && k < 250; p++) {
+        char c = (*p >= 'A' && *p <= 'Z') ? (char)(*p + 32) : *p;
+        name[k++] = ((c >= 'a' && c <= 'z') || (c >= '0' && c <= '9') || c == '_') ? c : '_';
+    }
+    name[k] = 0;
+    ng(l, tok, name, "NOT_IMPLEMENTED", STRING_ONLY, regex, prio);
+}
+
+static void nginx_token_parsers(tplist *l) {
+    /* CoreLogModule (nginxmodules/CoreLogModule.java:45-489) */
+    ng(l, "$bytes_sent", "response.bytes", "BYTES", STRING_OR_LONG, FORMAT_NUMBER, 10);
+    ng(l, "$bytes_received", "request.bytes", "BYTES", STRING_OR_LONG, FORMAT_NUMBER, 10);
+    ng(l, "$connection", "connection.serial_number", "NUMBER", STRING_OR_LONG, FORMAT_CLF_NUMBER, -1);
+    ng(l, "$connection_requests", "connection.requestnr", "NUMBER", STRING_OR_LONG, FORMAT_CLF_NUMBER, 10);
+    ng(l, "$msec", "request.receive.time.epoch", "TIME.EPOCH_SECOND_MILLIS", STRING_ONLY, "[0-9]+\\.[0-9][0-9][0-9]", 10);
+    ng(l, "$status", "request.status.last", "STRING", STRING_ONLY, FORMAT_NO_SPACE_STRING, 10);
+    ng(l, "$time_iso8601", "request.receive.time", "TIME.ISO8601", STRING_ONLY, FORMAT_STANDARD_TIME_ISO8601, 10);
+    ng(l, "$time_local", "request.receive.time", "TIME.STAMP", STRING_ONLY, FORMAT_STANDARD_TIME_US, 10);
+    ng_named(l, "\\$arg_([a-z0-9\\-\\_]*)", "request.firstline.uri.query.", "STRING", STRING_ONLY, FORMAT_STRING, 0);
+    ng(l, "$is_args", "request.firstline.uri.is_args", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$args", "request.firstline.uri.query", "HTTP.QUERYSTRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$query_string", "request.firstline.uri.query", "HTTP.QUERYSTRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$body_bytes_sent", "response.body.bytes", "BYTES", STRING_OR_LONG, FORMAT_NUMBER, 10);
+    ng(l, "$content_length", "request.header.content_length", "HTTP.HEADER", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$content_type", "request.header.content_type", "HTTP.HEADER", STRING_ONLY, FORMAT_STRING, 10);
+    ng_named(l, "\\$cookie_([a-z0-9\\-_]*)", "request.cookies.", "HTTP.COOKIE", STRING_ONLY, FORMAT_STRING, 0);
+    ng(l, "$document_root", "request.firstline.document_root", "STRING", STRING_ONLY, FORMAT_NO_SPACE_STRING, 10);
+    ng(l, "$realpath_root", "request.firstline.realpath_root", "STRING", STRING_ONLY, FORMAT_NO_SPACE_STRING, 10);
+    ng(l, "$host", "connection.server.name", "STRING", STRING_ONLY, FORMAT_NO_SPACE_STRING, -1);
+    ng(l, "$hostname", "connection.client.host", "STRING", STRING_ONLY, FORMAT_NO_SPACE_STRING, 10);
+    ng_named(l, "\\$http_([a-z0-9\\-_]*)", "request.header.", "HTTP.HEADER", STRING_ONLY, FORMAT_STRING, 0);
+    ng(l, "$http_user_agent", "request.user-agent", "HTTP.USERAGENT", STRING_ONLY, FORMAT_STRING, 1);
+    ng(l, "$http_referer", "request.referer", "HTTP.URI", STRING_ONLY, FORMAT_NO_SPACE_STRING, 1);
+    ng(l, "$https", "connection.https", "STRING", STRING_ONLY, FORMAT_NO_SPACE_STRING, 10);
+    ng_notimpl(l, "$limit_rate", "nginx_parameter_not_intended_for_logging", FORMAT_NO_SPACE_STRING, 0);
+    ng(l, "$nginx_version", "server.nginx.version", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$pid", "connection.server.child.processid", "NUMBER", STRING_OR_LONG, FORMAT_NUMBER, 10);
+    ng(l, "$protocol", "connection.protocol", "STRING", STRING_ONLY, FORMAT_NO_SPACE_STRING, 10);
+    ng(l, "$pipe", "connection.nginx.pipe", "STRING", STRING_ONLY, ".", 10);
+    ng(l, "$proxy_protocol_addr", "connection.client.proxy.host", "IP", STRING_OR_LONG, FORMAT_CLF_IP, 10);
+    ng(l, "$proxy_protocol_port", "connection.client.proxy.port", "PORT", STRING_OR_LONG, FORMAT_CLF_NUMBER, 10);
+    ng(l, "$remote_addr", "connection.client.host", "IP", STRING_OR_LONG, FORMAT_CLF_IP, 10);
+    ng(l, "$binary_remote_addr", "connection.client.host", "IP_BINARY", STRING_OR_LONG,
+       "\\\\x" FORMAT_HEXDIGIT FORMAT_HEXDIGIT "\\\\x" FORMAT_HEXDIGIT FORMAT_HEXDIGIT
+       "\\\\x" FORMAT_HEXDIGIT FORMAT_HEXDIGIT "\\\\x" FORMAT_HEXDIGIT FORMAT_HEXDIGIT, 10);
+    ng(l, "$remote_port", "connection.client.port", "PORT", STRING_OR_LONG, FORMAT_NUMBER, 10);
+    ng(l, "$remote_user", "connection.client.user", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$request", "request.firstline", "HTTP.FIRSTLINE", STRING_ONLY,
+       FORMAT_NO_SPACE_STRING " " FORMAT_NO_SPACE_STRING " " FORMAT_NO_SPACE_STRING, -2);
+    ng_notimpl(l, "$request_body", "nginx_parameter_not_intended_for_logging", FORMAT_STRING, -1);
+    ng_notimpl(l, "$request_body_file", "nginx_parameter_not_intended_for_logging", FORMAT_STRING, -1);
+    ng(l, "$request_completion", "request.completion", "STRING", STRING_ONLY, FORMAT_NO_SPACE_STRING, 10);
+    ng(l, "$request_filename", "server.filename", "FILENAME", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$request_length", "request.bytes", "BYTES", STRING_OR_LONG, FORMAT_CLF_NUMBER, 10);
+    ng(l, "$request_method", "request.firstline.method", "HTTP.METHOD", STRING_ONLY, FORMAT_NO_SPACE_STRING, 10);
+    ng(l, "$request_time", "response.server.processing.time", "SECOND_MILLIS", STRING_ONLY, FORMAT_NUMBER_DECIMAL, 10);
+    ng(l, "$request_uri", "request.firstline.uri", "HTTP.URI", STRING_ONLY, FORMAT_NO_SPACE_STRING, 10);
+    ng(l, "$request_id", "request.id", "STRING", STRING_ONLY, FORMAT_HEXNUMBER, 10);
+    ng(l, "$uri", "request.firstline.uri.normalized", "HTTP.URI", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$document_uri", "request.firstline.uri.normalized", "HTTP.URI", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$scheme", "request.firstline.uri.protocol", "HTTP.PROTOCOL", STRING_ONLY, FORMAT_NO_SPACE_STRING, 10);
+    ng_named(l, "\\$sent_http_([a-z0-9\\-_]*)", "response.header.", "HTTP.HEADER", STRING_ONLY, FORMAT_STRING, 0);
+    ng_named(l, "\\$sent_trailer_([a-z0-9\\-_]*)", "response.trailer.", "HTTP.TRAILER", STRING_ONLY, FORMAT_STRING, 0);
+    ng(l, "$server_addr", "connection.server.ip", "IP", STRING_OR_LONG, FORMAT_CLF_IP, 10);
+    ng(l, "$server_name", "connection.server.name", "STRING", STRING_ONLY, FORMAT_NO_SPACE_STRING, 10);
+    ng(l, "$server_port", "connection.server.port", "PORT", STRING_OR_LONG, FORMAT_NUMBER, 10);
+    ng(l, "$server_protocol", "request.firstline.protocol", "HTTP.PROTOCOL_VERSION", STRING_OR_LONG, FORMAT_NO_SPACE_STRING, 10);
+    ng(l, "$session_time", "connection.session.time", "SECOND_MILLIS", STRING_ONLY, FORMAT_NUMBER_DECIMAL, 10);
+    ng(l, "$tcpinfo_rtt", "connection.tcpinfo.rtt", "MICROSECONDS", STRING_OR_LONG, FORMAT_NUMBER, -1);
+    ng(l, "$tcpinfo_rttvar", "connection.tcpinfo.rttvar", "MICROSECONDS", STRING_OR_LONG, FORMAT_NUMBER, 10);
+    ng(l, "$tcpinfo_snd_cwnd", "connection.tcpinfo.send.cwnd", "BYTES", STRING_OR_LONG, FORMAT_NUMBER, 10);
+    ng(l, "$tcpinfo_rcv_space", "connection.tcpinfo.receive.space", "BYTES", STRING_OR_LONG, FORMAT_NUMBER, 10);
+    ng_named(l, "\\$([a-z0-9\\-\\_]*)", "nginx.unknown.", "UNKNOWN_NGINX_VARIABLE", STRING_ONLY, FORMAT_NO_SPACE_STRING, -10);
+    /* UpstreamModule (nginxmodules/UpstreamModule.java:46-160) */
+#define UP "nginxmodule.upstream"
+    ng(l, "$upstream_addr", UP ".addr", "UPSTREAM_ADDR_LIST", STRING_ONLY, UPSTREAM_LIST(FORMAT_NO_SPACE_STRING), 10);
+    ng(l, "$upstream_bytes_received", UP ".bytes.received", "UPSTREAM_BYTES_LIST", STRING_ONLY, UPSTREAM_LIST(FORMAT_NUMBER), 10);
+    ng(l, "$upstream_bytes_sent", UP ".bytes.sent", "UPSTREAM_BYTES_LIST", STRING_ONLY, UPSTREAM_LIST(FORMAT_NUMBER), 10);
+    ng(l, "$upstream_cache_status", UP ".cache.status", "UPSTREAM_CACHE_STATUS", STRING_ONLY,
+       "(?:MISS|BYPASS|EXPIRED|STALE|UPDATING|REVALIDATED|HIT)", 10);
+    ng(l, "$upstream_connect_time", UP ".connect.time", "UPSTREAM_SECOND_MILLIS_LIST", STRING_ONLY, UPSTREAM_LIST(FORMAT_NUMBER_DECIMAL), 10);
+    ng_named(l, "\\$upstream_cookie_([a-z0-9\\-_]*)", UP ".response.cookies.", "HTTP.COOKIE", STRING_ONLY, FORMAT_STRING, 0);
+    ng(l, "$upstream_header_time", UP ".header.time", "UPSTREAM_SECOND_MILLIS_LIST", STRING_ONLY, UPSTREAM_LIST(FORMAT_NUMBER_DECIMAL), 10);
+    ng_named(l, "\\$upstream_http_([a-z0-9\\-_]*)", UP ".header.", "HTTP.HEADER", STRING_ONLY, FORMAT_STRING, 0);
+    ng(l, "$upstream_queue_time", UP ".queue.time", "UPSTREAM_SECOND_MILLIS_LIST", STRING_ONLY, UPSTREAM_LIST(FORMAT_NUMBER_DECIMAL), 10);
+    ng(l, "$upstream_response_length", UP ".response.length", "UPSTREAM_BYTES_LIST", STRING_ONLY, UPSTREAM_LIST(FORMAT_NUMBER), 10);
+    ng(l, "$upstream_response_time", UP ".response.time", "UPSTREAM_SECOND_MILLIS_LIST", STRING_ONLY, UPSTREAM_LIST(FORMAT_NUMBER_DECIMAL), 10);
+    ng(l, "$upstream_status", UP ".status", "UPSTREAM_STATUS_LIST", STRING_ONLY, UPSTREAM_LIST(FORMAT_NO_SPACE_STRING), 10);
+    ng_named(l, "\\$upstream_trailer_([a-z0-9\\-_]*)", UP ".trailer.", "HTTP.TRAILER", STRING_ONLY, FORMAT_STRING, 0);
+    ng(l, "$upstream_first_byte_time", UP ".first_byte.time", "UPSTREAM_SECOND_MILLIS_LIST", STRING_ONLY, UPSTREAM_LIST(FORMAT_NUMBER_DECIMAL), 10);
+    ng(l, "$upstream_session_time", UP ".session.time", "UPSTREAM_SECOND_MILLIS_LIST", STRING_ONLY, UPSTREAM_LIST(FORMAT_NUMBER_DECIMAL), 10);
+#undef UP
+    /* SslModule (nginxmodules/SslModule.java:37-200) */
+#define SSL "nginxmodule.ssl"
+    ng(l, "$ssl_cipher", SSL ".cipher", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$ssl_ciphers", SSL ".client.ciphers", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$ssl_client_escaped_cert", SSL ".client.cert", "PEM_CERT_URLENCODED", STRING_ONLY, FORMAT_NO_SPACE_STRING, 10);
+    ng(l, "$ssl_client_cert", SSL ".client.cert", "PEM_CERT", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$ssl_client_raw_cert", SSL ".client.cert", "PEM_CERT_RAW", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$ssl_client_fingerprint", SSL ".client.cert.fingerprint", "SHA1", STRING_ONLY, FORMAT_NO_SPACE_STRING, 10);
+    ng(l, "$ssl_client_i_dn", SSL ".client.cert.issuer_dn", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$ssl_client_i_dn_legacy", SSL ".client.cert.issuer_dn.legacy", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$ssl_client_s_dn", SSL ".client.cert.subject_dn", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$ssl_client_s_dn_legacy", SSL ".client.cert.subject_dn.legacy", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$ssl_client_serial", SSL ".client.cert.serial", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$ssl_client_v_end", SSL ".client.cert.end_date", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$ssl_client_v_remain", SSL ".client.cert.remain_days", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$ssl_client_v_start", SSL ".client.cert.start_date", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$ssl_client_verify", SSL ".client.cert.verify", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$ssl_curves", SSL ".client.curves", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$ssl_early_data", SSL ".early_data", "STRING", STRING_ONLY, "1?", 10);
+    ng(l, "$ssl_protocol", SSL ".protocol", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$ssl_server_name", SSL ".server_name", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$ssl_session_id", SSL ".session.id", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$ssl_session_reused", SSL ".session.reused", "STRING", STRING_ONLY, "(r|.)", 10);
+    ng(l, "$ssl_preread_protocol", SSL ".preread.protocol", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$ssl_preread_server_name", SSL ".preread.server_name", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$ssl_preread_alpn_protocols", SSL ".preread.alpn_protocols", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+#undef SSL
+    /* GeoIPModule (nginxmodules/GeoIPModule.java:35-104) */
+#define GEO "nginxmodule.geoip"
+    ng(l, "$geoip_country_code", GEO ".country.code", "STRING", STRING_ONLY, FORMAT_NO_SPACE_STRING, 10);
+    ng(l, "$geoip_country_code3", GEO ".country.code3", "STRING", STRING_ONLY, FORMAT_NO_SPACE_STRING, 10);
+    ng(l, "$geoip_country_name", GEO ".country.name", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$geoip_area_code", GEO ".area.code", "STRING", STRING_ONLY, FORMAT_NO_SPACE_STRING, 10);
+    ng(l, "$geoip_city_continent_code", GEO ".continent.code", "STRING", STRING_ONLY, FORMAT_NO_SPACE_STRING, 10);
+    ng(l, "$geoip_city_country_code", GEO ".country.code", "STRING", STRING_ONLY, FORMAT_NO_SPACE_STRING, 10);
+    ng(l, "$geoip_city_country_code3", GEO ".country.code3", "STRING", STRING_ONLY, FORMAT_NO_SPACE_STRING, 10);
+    ng(l, "$geoip_city_country_name", GEO ".country.name", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$geoip_dma_code", GEO ".dma.code", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$geoip_latitude", GEO ".location.latitude", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$geoip_longitude", GEO ".location.longitude", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$geoip_region", GEO ".region.code", "STRING", STRING_ONLY, FORMAT_NO_SPACE_STRING, 10);
+    ng(l, "$geoip_region_name", GEO ".region.name", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$geoip_city", GEO ".city", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$geoip_postal_code", GEO ".postal.code", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$geoip_org", GEO ".organization", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+#undef GEO
+    /* VariousModule (nginxmodules/VariousModule.java:37-212) */
+#define VAR "nginxmodule"
+    ng(l, "$secure_link", VAR ".secure_link.status", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$session_log_id", VAR ".session_log.id", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$slice_range", VAR ".slice_range", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$proxy_host", VAR ".proxy.host", "STRING", STRING_ONLY, FORMAT_NO_SPACE_STRING, 10);
+    ng(l, "$proxy_port", VAR ".proxy.port", "STRING", STRING_ONLY, FORMAT_NO_SPACE_STRING, 10);
+    ng(l, "$proxy_add_x_forwarded_for", VAR ".proxy.add_x_forwarded_for", "STRING", STRING_ONLY, FORMAT_NO_SPACE_STRING, 10);
+    ng(l, "$uid_got", VAR ".userid.uid_got", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$uid_reset", VAR ".userid.uid_reset", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$uid_set", VAR ".userid.uid_set", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$modern_browser", VAR ".browser.modern", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$ancient_browser", VAR ".browser.ancient", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$msie", VAR ".browser.msie", "STRING", STRING_ONLY, FORMAT_NO_SPACE_STRING, 10);
+    ng(l, "$connections_active", VAR ".stub_status.connections.active", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$connections_reading", VAR ".stub_status.connections.reading", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$connections_writing", VAR ".stub_status.connections.writing", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$connections_waiting", VAR ".stub_status.connections.waiting", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$date_local", VAR ".date.local", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$date_gmt", VAR ".date.gmt", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$fastcgi_script_name", VAR ".fastcgi.script_name", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$fastcgi_path_info", VAR ".fastcgi.path_info", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$gzip_ratio", VAR ".gzip.ratio", "STRING", STRING_ONLY, FORMAT_NUMBER_OPTIONAL_DECIMAL, 10);
+    ng(l, "$spdy", VAR ".spdy.version", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$spdy_request_priority", VAR ".spdy.request_priority", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$http2", VAR ".http2.negotiated_protocol", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$invalid_referer", VAR ".referer.invalid", "STRING", STRING_ONLY, "1?", 10);
+    ng_named(l, "\\$jwt_header_([a-z0-9\\-_]*)", VAR ".jwt.header.", "STRING", STRING_ONLY, FORMAT_STRING, 0);
+    ng_named(l, "\\$jwt_claim_([a-z0-9\\-_]*)", VAR ".jwt.claim.", "STRING", STRING_ONLY, FORMAT_STRING, 0);
+    ng(l, "$memcached_key", VAR ".memcached.key", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$realip_remote_addr", VAR ".realip.remote_addr", "IP", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$realip_remote_port", VAR ".realip.remote_port", "PORT", STRING_OR_LONG, FORMAT_STRING, 10);
+#undef VAR
+    /* KubernetesIngressModule (nginxmodules/KubernetesIngressModule.java:35-68) */
+#define K8S "nginxmodule.kubernetes"
+    ng(l, "$the_real_ip", K8S ".the_real_ip", "IP", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$proxy_upstream_name", K8S ".proxy_upstream_name", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$req_id", K8S ".req_id", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$namespace", K8S ".namespace", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$ingress_name", K8S ".ingress_name", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$service_name", K8S ".service.name", "STRING", STRING_ONLY, FORMAT_STRING, 10);
+    ng(l, "$service_port", K8S ".service.port", "PORT", STRING_ONLY, FORMAT_STRING, 10);
+#undef K8S
+}
+
 /* =============================================================== tokens */
 typedef struct {
     int fixed;          /* FixedStringToken */
