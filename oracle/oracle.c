@@ -746,9 +746,19 @@ static int looks_apache(const char *f) {
 }
 static int looks_nginx(const char *f) { return strchr(f, '$') != NULL || ieq(f, "combined"); }
 
-static tplist g_apache_tps;
+static tplist g_apache_tps, g_nginx_tps;
 static pthread_once_t g_tps_once = PTHREAD_ONCE_INIT;
-static void init_tps(void) { apache_token_parsers(&g_apache_tps); }
+static void init_tps(void) {
+    apache_token_parsers(&g_apache_tps);
+    nginx_token_parsers(&g_nginx_tps);
+}
+
+/* NginxHttpdLogFormatDissector.setLogFormat alias (hp/NginxHttpdLogFormatDissector.java:75-92) */
+static const char *nginx_alias(const char *f) {
+    if (ieq(f, "combined"))
+        return "$remote_addr - $remote_user [$time_local] \"$request\" $status $body_bytes_sent \"$http_referer\" \"$http_user_agent\"";
+    return f;
+}
 
 static fmtd *fmt_new(int kind, const char *logformat) {
     pthread_once(&g_tps_once, init_tps);
@@ -759,9 +769,10 @@ static fmtd *fmt_new(int kind, const char *logformat) {
         f->cleaned = apache_cleanup(f->logformat);
         parse_token_def(f, &g_apache_tps);
     } else {
-        f->logformat = xstrdup(logformat);
-        f->cleaned = xstrdup(logformat);
-        f->unsupported = 1; /* NGINX: not restated in this oracle version */
+        /* NGINX: no cleanup step (TokenFormatDissector.cleanupLogFormat default) */
+        f->logformat = xstrdup(nginx_alias(logformat));
+        f->cleaned = xstrdup(f->logformat);
+        parse_token_def(f, &g_nginx_tps);
     }
     return f;
 }
@@ -830,7 +841,8 @@ static void fmt_prepare_for_run(fmtd *f) {
 enum {
     D_ROOT, D_TIMESTAMP, D_TIMESTAMP_ISO, D_FIRSTLINE, D_PROTOCOL, D_URI, D_QUERY,
     D_COOKIES, D_SETCOOKIES, D_SETCOOKIE, D_UNIQUEID, D_CLF2NUM, D_NUM2CLF,
-    D_STRFTIME, D_LOCALIZED
+    D_STRFTIME, D_LOCALIZED,
+    D_BINIP, D_SECMILLIS, D_MS2US, D_UPSTREAM  /* NGINX createAdditionalDissectors */
 };
 
 typedef struct {
@@ -889,6 +901,32 @@ static dissector *dis_new(int cls, const char *in_type) {
     }
     case D_LOCALIZED: sl_add(&d->outs, "TIME.LOCALIZEDSTRING:"); break;
     default: break;
+    }
+    return d;
+}
+
+/* TypeConvertBaseDissector (translate/TypeConvertBaseDissector.java:42-46): one
+ * output "OUT:" */
+static dissector *dis_conv(int cls, const char *in_type, const char *out_type) {
+    dissector *d = dis_new(cls, in_type);
+    d->out_type = xstrdup(out_type);
+    char *o = xfmt("%s:", out_type);
+    sl_add(&d->outs, o);
+    free(o);
+    return d;
+}
+/* UpstreamListDissector.getPossibleOutput (nginxmodules/UpstreamListDissector.java:127-135):
+ * N.value and N.redirected for N < 32 (same type for both in every use) */
+static dissector *dis_upstream(const char *in_type, const char *out_type) {
+    dissector *d = dis_new(D_UPSTREAM, in_type);
+    d->out_type = xstrdup(out_type);
+    for (int i = 0; i < 32; i++) {
+        char *o = xfmt("%s:%d.value", out_type, i);
+        sl_add(&d->outs, o);
+        free(o);
+        o = xfmt("%s:%d.redirected", out_type, i);
+        sl_add(&d->outs, o);
+        free(o);
     }
     return d;
 }
@@ -1100,6 +1138,23 @@ static int build_dissectors(orc_parser *p, const char *logformat, char *err, int
     n2c->out_type = xstrdup("BYTESCLF");
     sl_add(&n2c->outs, "BYTESCLF:");
     p->dis[nd++] = n2c;
+    /* NginxHttpdLogFormatDissector.createAdditionalDissectors
+     * (hp/NginxHttpdLogFormatDissector.java:144-152 + UpstreamModule.getDissectors,
+     * nginxmodules/UpstreamModule.java:163-198), once for any NGINX format */
+    int any_nginx = 0;
+    for (int i = 0; i < root->nfmts; i++) any_nginx |= root->fmts[i]->kind == FMT_NGINX;
+    if (any_nginx) {
+        dissector *b = dis_new(D_BINIP, "IP_BINARY");
+        sl_add(&b->outs, "IP:");
+        p->dis[nd++] = b;
+        p->dis[nd++] = dis_conv(D_SECMILLIS, "SECOND_MILLIS", "MILLISECONDS");
+        p->dis[nd++] = dis_conv(D_SECMILLIS, "TIME.EPOCH_SECOND_MILLIS", "TIME.EPOCH");
+        p->dis[nd++] = dis_conv(D_MS2US, "MILLISECONDS", "MICROSECONDS");
+        p->dis[nd++] = dis_upstream("UPSTREAM_ADDR_LIST", "UPSTREAM_ADDR");
+        p->dis[nd++] = dis_upstream("UPSTREAM_BYTES_LIST", "BYTES");
+        p->dis[nd++] = dis_upstream("UPSTREAM_SECOND_MILLIS_LIST", "SECOND_MILLIS");
+        p->dis[nd++] = dis_upstream("UPSTREAM_STATUS_LIST", "UPSTREAM_STATUS");
+    }
     /* createAdditionalDissectors (core/Parser.java:281-292): token custom
      * dissectors (StrfTimeStampDissector) + LocalizedTimeDissector */
     for (int i = 0; i < root->nfmts; i++) {
@@ -2067,6 +2122,127 @@ static void d_num2clf(parsable *ps, instance *in, const char *inputname) {
     else add_dissection(ps, inputname, in->d->out_type, "", *vp);
 }
 
+/* Java Long.parseLong of an all-digit string; 0 on overflow
+ * (NumberFormatException, a RuntimeException: not restated). */
+static int parse_long_digits(js s, int a, int b, int64_t *out) {
+    if (b <= a) return 0;
+    uint64_t v = 0;
+    for (int i = a; i < b; i++) {
+        int c = s.c[i];
+        if (c < '0' || c > '9') return 0;
+        if (v > (uint64_t)(INT64_MAX - (c - '0')) / 10) return 0;
+        v = v * 10 + (uint64_t)(c - '0');
+    }
+    *out = (int64_t)v;
+    return 1;
+}
+
+/* ConvertSecondsWithMillisStringDissector.dissect (translate/ConvertSecondsWithMillisStringDissector.java:33-40):
+ * split("\\.", 2), both halves Long.parseLong, seconds * 1000 + millis (the
+ * fraction is read as an integer: "1.5" -> 1005).  A null value
+ * (NullPointerException), a missing or non-numeric half
+ * (ArrayIndexOutOfBounds / NumberFormatException) are runtime exceptions of
+ * the reference: not restated. */
+static void d_secmillis(parsable *ps, instance *in, const char *inputname) {
+    val *vp = cache_get(ps, in->d->in_type, inputname);
+    js sv = v_getstring(ps->a, *vp);
+    if (sv.null) { ps->unsupported = 1; return; }
+    int dot = js_index_of_char(sv, '.', 0);
+    int64_t sec, ms;
+    if (dot < 0 || !parse_long_digits(sv, 0, dot, &sec) || !parse_long_digits(sv, dot + 1, sv.n, &ms)) {
+        ps->unsupported = 1;
+        return;
+    }
+    add_long(ps, inputname, in->d->out_type, "", (int64_t)((uint64_t)sec * 1000u + (uint64_t)ms));  /* long wraps */
+}
+
+/* ConvertMillisecondsIntoMicroseconds.dissect (translate/ConvertMillisecondsIntoMicroseconds.java:33-35):
+ * value.getLong() * 1000; a null Long is a NullPointerException (not restated) */
+static void d_ms2us(parsable *ps, instance *in, const char *inputname) {
+    val *vp = cache_get(ps, in->d->in_type, inputname);
+    int64_t l;
+    if (vp->filled == V_LONG) {
+        if (vp->lnull) { ps->unsupported = 1; return; }
+        l = vp->l;
+    } else {
+        js sv = vp->s;  /* Value.getLong: Long.parseLong, null on NumberFormatException */
+        int neg = sv.n > 0 && sv.c[0] == '-';
+        if (sv.null || !parse_long_digits(sv, neg || (sv.n > 0 && sv.c[0] == '+'), sv.n, &l)) { ps->unsupported = 1; return; }
+        if (neg) l = -l;
+    }
+    add_long(ps, inputname, in->d->out_type, "", (int64_t)((uint64_t)l * 1000u));
+}
+
+/* NginxHttpdLogFormatDissector.BinaryIPDissector (hp/NginxHttpdLogFormatDissector.java:151-178):
+ * \\xHH x4 (matches() the whole value) -> the SIGNED bytes joined by '.' */
+static void d_binip(parsable *ps, instance *in, const char *inputname) {
+    val *vp = cache_get(ps, in->d->in_type, inputname);
+    js sv = v_getstring(ps->a, *vp);
+    if (sv.null) { ps->unsupported = 1; return; }
+    if (sv.n != 16) return;
+    int b[4];
+    for (int k = 0; k < 4; k++) {
+        const int *c = sv.c + 4 * k;
+        if (c[0] != '\\' || c[1] != 'x' || !is_hexc(c[2]) || !is_hexc(c[3])) return;
+        int v = 0;
+        for (int j = 2; j < 4; j++) v = v * 16 + (c[j] <= '9' ? c[j] - '0' : (c[j] | 32) - 'a' + 10);
+        b[k] = v >= 128 ? v - 256 : v;  /* (byte) */
+    }
+    char out[64];
+    snprintf(out, sizeof out, "%d.%d.%d.%d", b[0], b[1], b[2], b[3]);
+    add_str(ps, inputname, "IP", "", js_lit(ps->a, out));
+}
+
+/* Java String.split(sep) for a two-char literal separator: pieces [start,
+ * end) into v; trailing empty pieces removed (limit 0).  Returns the count. */
+static int java_split2(js s, int a, int b, int c0, int c1, int *st, int *en, int cap) {
+    int n = 0, from = a;
+    for (int i = a; i + 1 < b; i++) {
+        if (s.c[i] == c0 && s.c[i + 1] == c1) {
+            if (n < cap) { st[n] = from; en[n] = i; }
+            n++;
+            from = i + 2;
+            i++;
+        }
+    }
+    if (n < cap) { st[n] = from; en[n] = b; }
+    n++;
+    if (n > cap) return -1;
+    if (n == 1) return 1;  /* no match: the whole input, even when empty */
+    while (n > 0 && en[n - 1] == st[n - 1]) n--;
+    return n;
+}
+/* String.trim(): strip chars <= ' ' at both ends */
+static js js_trim(js s, int a, int b) {
+    while (a < b && s.c[a] <= ' ') a++;
+    while (b > a && s.c[b - 1] <= ' ') b--;
+    return js_sub(s, a, b);
+}
+
+/* UpstreamListDissector.dissect (nginxmodules/UpstreamListDissector.java:79-125):
+ * split(", ") into servers, each split(": ") into original / redirected,
+ * both trimmed; N.value and N.redirected per server. */
+static void d_upstream(parsable *ps, instance *in, const char *inputname) {
+    val *vp = cache_get(ps, in->d->in_type, inputname);
+    js sv = v_getstring(ps->a, *vp);
+    if (sv.null) { ps->unsupported = 1; return; }  /* NullPointerException */
+    int ss[256], se[256];
+    int ns = java_split2(sv, 0, sv.n, ',', ' ', ss, se, 256);
+    if (ns < 0) { ps->unsupported = 1; return; }
+    for (int k = 0; k < ns; k++) {
+        int ps_[256], pe[256];
+        int np = java_split2(sv, ss[k], se[k], ':', ' ', ps_, pe, 256);
+        if (np <= 0) { ps->unsupported = 1; return; }  /* parts[0] of an empty array */
+        char nm[64];
+        js orig = js_trim(sv, ps_[0], pe[0]);
+        js redir = np == 1 ? orig : js_trim(sv, ps_[1], pe[1]);
+        snprintf(nm, sizeof nm, "%d.value", k);
+        add_str(ps, inputname, in->d->out_type, nm, orig);
+        snprintf(nm, sizeof nm, "%d.redirected", k);
+        add_str(ps, inputname, in->d->out_type, nm, redir);
+    }
+}
+
 static void run_instance(parsable *ps, instance *in, const char *name) {
     switch (in->d->cls) {
     case D_ROOT: d_root(ps, in, name); break;
@@ -2077,6 +2253,10 @@ static void run_instance(parsable *ps, instance *in, const char *name) {
     case D_QUERY: d_query(ps, in, name); break;
     case D_CLF2NUM: d_clf2num(ps, in, name); break;
     case D_NUM2CLF: d_num2clf(ps, in, name); break;
+    case D_BINIP: d_binip(ps, in, name); break;
+    case D_SECMILLIS: d_secmillis(ps, in, name); break;
+    case D_MS2US: d_ms2us(ps, in, name); break;
+    case D_UPSTREAM: d_upstream(ps, in, name); break;
     default: ps->unsupported = 1; break;
     }
 }

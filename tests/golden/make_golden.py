@@ -352,6 +352,160 @@ if FLINK_LINE:
                                                       "AppleWebKit/533.17.8 (KHTML, like Gecko) Version/5.0.1 Safari/533.17.8"},
          skipped=["STRING:request.firstline.uri.query.g.query.promo (type remapping)", "GeoIP fields", "HTTP.COOKIE:request.cookies.bui"])
 
+# --------------------------------------------------------------------- NGINX
+# hpt/nginxmodules/NginxUpstreamTest.java:49-90 (testBasicLogFormat)
+UP_ADDR = "192.168.1.1:80, 192.168.1.2:80, unix:/tmp/sock : 192.168.10.1:80, 192.168.10.2:80"
+UP_NUM = "1, 2, 3 : 4, 5"
+UP_TIME = "1.001, 2.002, 3.003 : 4.004, 5.005"
+UP_STATUS = "111, 222, 333 : 444, 555"
+
+
+def up_expect(typ, base, vals):
+    """N.value / N.redirected for the 4 servers of the lists above + absent N=4"""
+    e, a = {}, []
+    for k, (v, r) in enumerate(vals):
+        e["%s:%s.%d.value" % (typ, base, k)] = v
+        e["%s:%s.%d.redirected" % (typ, base, k)] = r
+    a = ["%s:%s.4.value" % (typ, base), "%s:%s.4.redirected" % (typ, base)]
+    return e, a
+
+
+e1, a1 = up_expect("UPSTREAM_ADDR", "nginxmodule.upstream.addr",
+                   [("192.168.1.1:80",) * 2, ("192.168.1.2:80",) * 2, ("unix:/tmp/sock", "192.168.10.1:80"),
+                    ("192.168.10.2:80",) * 2])
+e2, a2 = up_expect("BYTES", "nginxmodule.upstream.bytes.received", [("1", "1"), ("2", "2"), ("3", "4"), ("5", "5")])
+e1.update(e2)
+e1["UPSTREAM_ADDR_LIST:nginxmodule.upstream.addr"] = UP_ADDR
+e1["UPSTREAM_BYTES_LIST:nginxmodule.upstream.bytes.received"] = UP_NUM
+case("hpt/nginxmodules/NginxUpstreamTest.java:49-90", "\"$upstream_addr\" \"$upstream_bytes_received\"",
+     "\"%s\" \"%s\"" % (UP_ADDR, UP_NUM), list(e1) + a1 + a2, expect=e1, absent=a1 + a2)
+
+# hpt/nginxmodules/NginxUpstreamTest.java:93-113 (testFullLine; config 4's log_format)
+NGINX_CFG4 = ("$remote_addr - $remote_user [$time_local] \"$request\" $status $body_bytes_sent \"$http_referer\" "
+              "\"$http_user_agent\" \"$http_x_forwarded_for\" $request_time $upstream_response_time $pipe")
+UPR = "nginxmodule.upstream.response.time"
+case("hpt/nginxmodules/NginxUpstreamTest.java:93-113", NGINX_CFG4,
+     "10.77.150.123 - - [15/Dec/2018:19:27:57 -0500] \"GET /25.chunk.js HTTP/1.1\" 200 84210 "
+     "\"https://api.demo.com/\" \"Mozilla/5.0 (Windows NT 10.0; Win64; x64) AppleWebKit/537.36 (KHTML, like Gecko) "
+     "Chrome/70.0.3538.110 Safari/537.36\" \"-\" 0.002 0.002 .",
+     ["SECOND_MILLIS:%s.0.value" % UPR, "SECOND_MILLIS:%s.0.redirected" % UPR,
+      "MICROSECONDS:%s.0.value" % UPR, "MICROSECONDS:%s.0.redirected" % UPR],
+     expect={"SECOND_MILLIS:%s.0.value" % UPR: "0.002", "SECOND_MILLIS:%s.0.redirected" % UPR: "0.002",
+             "MICROSECONDS:%s.0.value" % UPR: {"l": 2000}, "MICROSECONDS:%s.0.redirected" % UPR: {"l": 2000}})
+
+# hpt/nginxmodules/NginxUpstreamTest.java:116-267 (validateAllFields): one-variable formats
+UPS = [("$upstream_addr", UP_ADDR, "UPSTREAM_ADDR", "nginxmodule.upstream.addr",
+        [("192.168.1.1:80",) * 2, ("192.168.1.2:80",) * 2, ("unix:/tmp/sock", "192.168.10.1:80"), ("192.168.10.2:80",) * 2])]
+for var, base in [("$upstream_bytes_received", "bytes.received"), ("$upstream_bytes_sent", "bytes.sent"),
+                  ("$upstream_response_length", "response.length")]:
+    UPS.append((var, UP_NUM, "BYTES", "nginxmodule.upstream." + base, [("1", "1"), ("2", "2"), ("3", "4"), ("5", "5")]))
+for var, base in [("$upstream_connect_time", "connect.time"), ("$upstream_header_time", "header.time"),
+                  ("$upstream_queue_time", "queue.time"), ("$upstream_response_time", "response.time"),
+                  ("$upstream_first_byte_time", "first_byte.time"), ("$upstream_session_time", "session.time")]:
+    UPS.append((var, UP_TIME, "SECOND_MILLIS", "nginxmodule.upstream." + base,
+                [("1.001", "1.001"), ("2.002", "2.002"), ("3.003", "4.004"), ("5.005", "5.005")]))
+UPS.append(("$upstream_status", UP_STATUS, "UPSTREAM_STATUS", "nginxmodule.upstream.status",
+            [("111", "111"), ("222", "222"), ("333", "444"), ("555", "555")]))
+for var, line, typ, base, vals in UPS:
+    e, a = up_expect(typ, base, vals)
+    case("hpt/nginxmodules/NginxUpstreamTest.java:116-267", var, line, list(e) + a, expect=e, absent=a)
+for var, line, field in [("$upstream_cache_status", "STALE", "UPSTREAM_CACHE_STATUS:nginxmodule.upstream.cache.status"),
+                         ("$upstream_cookie_mycookie", "MyValue", "HTTP.COOKIE:nginxmodule.upstream.response.cookies.mycookie"),
+                         ("$upstream_http_myheader", "MyValue", "HTTP.HEADER:nginxmodule.upstream.header.myheader"),
+                         ("$upstream_trailer_mytrailer", "MyValue", "HTTP.TRAILER:nginxmodule.upstream.trailer.mytrailer")]:
+    case("hpt/nginxmodules/NginxUpstreamTest.java:116-267", var, line, [field], expect={field: line})
+
+# hpt/NginxLogFormatTest.java:78-92 (unknown variables)
+case("hpt/NginxLogFormatTest.java:78-92",
+     "$foobar $remote_user_age $remote_addr - $remote_user [$time_local] \"$request\" $status $body_bytes_sent "
+     "\"$http_referer\" \"$http_user_agent\"",
+     "something 42 123.65.150.10 - - [23/Aug/2010:03:50:59 +0000] \"POST /wordpress3/wp-admin/admin-ajax.php HTTP/1.1\" "
+     "200 2 \"http://www.example.com/wordpress3/wp-admin/post-new.php\" \"Mozilla/5.0 (Macintosh; U; Intel Mac OS X "
+     "10_6_4; en-US) AppleWebKit/534.3 (KHTML, like Gecko) Chrome/6.0.472.25 Safari/534.3\"",
+     ["UNKNOWN_NGINX_VARIABLE:nginx.unknown.foobar", "UNKNOWN_NGINX_VARIABLE:nginx.unknown.remote_user_age"],
+     expect={"UNKNOWN_NGINX_VARIABLE:nginx.unknown.foobar": "something",
+             "UNKNOWN_NGINX_VARIABLE:nginx.unknown.remote_user_age": "42"})
+
+# hpt/NginxLogFormatTest.java:347-425 (validateAllFields): (format, line, field, value); long-valued
+# outputs of the converters and the timestamp dissector are {"l": n} in the canonical record
+NGINX_FIELDS = [
+    ("$status", "200", "STRING:request.status.last", "200"),
+    ("$time_iso8601", "2017-01-03T15:56:36+01:00", "TIME.ISO8601:request.receive.time", "2017-01-03T15:56:36+01:00"),
+    ("$time_local", "03/Jan/2017:15:56:36 +0100", "TIME.STAMP:request.receive.time", "03/Jan/2017:15:56:36 +0100"),
+    ("$time_local", "03/Jan/2017:15:56:36 +0100", "TIME.EPOCH:request.receive.time.epoch", {"l": 1483455396000}),
+    ("$msec", "1483455396.639", "TIME.EPOCH:request.receive.time.epoch", {"l": 1483455396639}),
+    ("$remote_addr", "127.0.0.1", "IP:connection.client.host", "127.0.0.1"),
+    ("$binary_remote_addr", "\\x7F\\x00\\x00\\x01", "IP_BINARY:connection.client.host", "\\x7F\\x00\\x00\\x01"),
+    ("$binary_remote_addr", "\\x7F\\x00\\x00\\x01", "IP:connection.client.host", "127.0.0.1"),
+    ("$remote_port", "44448", "PORT:connection.client.port", "44448"),
+    ("$remote_user", "-", "STRING:connection.client.user", None),
+    ("$is_args", "?", "STRING:request.firstline.uri.is_args", "?"),
+    ("$query_string", "aap&noot=&mies=wim", "HTTP.QUERYSTRING:request.firstline.uri.query", "aap&noot=&mies=wim"),
+    ("$args", "aap&noot=&mies=wim", "HTTP.QUERYSTRING:request.firstline.uri.query", "aap&noot=&mies=wim"),
+    ("$args", "aap&noot=&mies=wim", "STRING:request.firstline.uri.query.aap", ""),
+    ("$args", "aap&noot=&mies=wim", "STRING:request.firstline.uri.query.noot", ""),
+    ("$args", "aap&noot=&mies=wim", "STRING:request.firstline.uri.query.mies", "wim"),
+    ("$arg_name", "foo", "STRING:request.firstline.uri.query.name", "foo"),
+    ("$bytes_sent", "694", "BYTES:response.bytes", "694"),
+    ("$bytes_received", "694", "BYTES:request.bytes", "694"),
+    ("$body_bytes_sent", "436", "BYTES:response.body.bytes", "436"),
+    ("$connection", "5", "NUMBER:connection.serial_number", "5"),
+    ("$connection_requests", "4", "NUMBER:connection.requestnr", "4"),
+    ("$https", "", "STRING:connection.https", ""),
+    ("$content_length", "-", "HTTP.HEADER:request.header.content_length", None),
+    ("$content_type", "-", "HTTP.HEADER:request.header.content_type", None),
+    ("$cookie_name", "Something", "HTTP.COOKIE:request.cookies.name", "Something"),
+    ("$document_root", "/var/www/html", "STRING:request.firstline.document_root", "/var/www/html"),
+    ("$realpath_root", "/var/www/html", "STRING:request.firstline.realpath_root", "/var/www/html"),
+    ("$host", "localhost", "STRING:connection.server.name", "localhost"),
+    ("$hostname", "hackbox", "STRING:connection.client.host", "hackbox"),
+    ("$http_foobar", "Something", "HTTP.HEADER:request.header.foobar", "Something"),
+    ("$sent_http_foobar", "Something", "HTTP.HEADER:response.header.foobar", "Something"),
+    ("$sent_trailer_foobar", "Something", "HTTP.TRAILER:response.trailer.foobar", "Something"),
+    ("$nginx_version", "1.10.0", "STRING:server.nginx.version", "1.10.0"),
+    ("$pid", "5137", "NUMBER:connection.server.child.processid", "5137"),
+    ("$pipe", ".", "STRING:connection.nginx.pipe", "."),
+    ("$pipe", "p", "STRING:connection.nginx.pipe", "p"),
+    ("$protocol", "TCP", "STRING:connection.protocol", "TCP"),
+    ("$proxy_protocol_addr", "1.2.3.4", "IP:connection.client.proxy.host", "1.2.3.4"),
+    ("$proxy_protocol_port", "1234", "PORT:connection.client.proxy.port", "1234"),
+    ("$request", "GET /?aap&noot=&mies=wim HTTP/1.1", "HTTP.FIRSTLINE:request.firstline", "GET /?aap&noot=&mies=wim HTTP/1.1"),
+    ("$request_completion", "OK", "STRING:request.completion", "OK"),
+    ("$request_filename", "/var/www/html/index.html", "FILENAME:server.filename", "/var/www/html/index.html"),
+    ("$request_length", "491", "BYTES:request.bytes", "491"),
+    ("$request_method", "GET", "HTTP.METHOD:request.firstline.method", "GET"),
+    ("$request_time", "123.456", "SECOND_MILLIS:response.server.processing.time", "123.456"),
+    ("$request_time", "123.456", "MILLISECONDS:response.server.processing.time", {"l": 123456}),
+    ("$request_time", "123.456", "MICROSECONDS:response.server.processing.time", {"l": 123456000}),
+    ("$request_uri", "/?aap&noot=&mies=wim", "HTTP.URI:request.firstline.uri", "/?aap&noot=&mies=wim"),
+    ("$scheme", "http", "HTTP.PROTOCOL:request.firstline.uri.protocol", "http"),
+    ("$sent_http_etag", "W/\\x22586bbb8b-29e\\x22", "HTTP.HEADER:response.header.etag", "W/\\x22586bbb8b-29e\\x22"),
+    ("$sent_http_last_modified", "Tue, 03 Jan 2017 14:56:11 GMT", "HTTP.HEADER:response.header.last_modified",
+     "Tue, 03 Jan 2017 14:56:11 GMT"),
+    ("$server_addr", "127.0.0.1", "IP:connection.server.ip", "127.0.0.1"),
+    ("$server_name", "_", "STRING:connection.server.name", "_"),
+    ("$server_port", "80", "PORT:connection.server.port", "80"),
+    ("$server_protocol", "HTTP/1.1", "HTTP.PROTOCOL_VERSION:request.firstline.protocol", "HTTP/1.1"),
+    ("$server_protocol", "HTTP/1.1", "HTTP.PROTOCOL:request.firstline.protocol", "HTTP"),
+    ("$server_protocol", "HTTP/1.1", "HTTP.PROTOCOL.VERSION:request.firstline.protocol.version", "1.1"),
+    ("$tcpinfo_rtt", "52", "MICROSECONDS:connection.tcpinfo.rtt", "52"),
+    ("$tcpinfo_rttvar", "30", "MICROSECONDS:connection.tcpinfo.rttvar", "30"),
+    ("$tcpinfo_snd_cwnd", "10", "BYTES:connection.tcpinfo.send.cwnd", "10"),
+    ("$tcpinfo_rcv_space", "43690", "BYTES:connection.tcpinfo.receive.space", "43690"),
+    ("$uri", "/index.html", "HTTP.URI:request.firstline.uri.normalized", "/index.html"),
+    ("$document_uri", "/index.html", "HTTP.URI:request.firstline.uri.normalized", "/index.html"),
+    ("$http_user_agent", "Mozilla/5.0 (Foo)", "HTTP.USERAGENT:request.user-agent", "Mozilla/5.0 (Foo)"),
+    ("$http_foo_user_agent", "Mozilla/5.0 (Foo)", "HTTP.HEADER:request.header.foo_user_agent", "Mozilla/5.0 (Foo)"),
+    ("$http_user_agent_foo", "Mozilla/5.0 (Foo)", "HTTP.HEADER:request.header.user_agent_foo", "Mozilla/5.0 (Foo)"),
+    ("$http_referer", "http://localhost/", "HTTP.URI:request.referer", "http://localhost/"),
+    ("$request_body", "-", "NOT_IMPLEMENTED:nginx_parameter_not_intended_for_logging__request_body", None),
+    ("$request_body_file", "-", "NOT_IMPLEMENTED:nginx_parameter_not_intended_for_logging__request_body_file", None),
+    ("$limit_rate", "0", "NOT_IMPLEMENTED:nginx_parameter_not_intended_for_logging__limit_rate", "0"),
+]
+for fmt, line, field, want in NGINX_FIELDS:
+    case("hpt/NginxLogFormatTest.java:347-425", fmt, line, [field], expect={field: want})
+# (:350 $time_iso8601 -> TIME.EPOCH goes through TimeStampDissector("TIME.ISO8601"), not restated: left out)
+
 # resilientUrlDecode (hpt/UtilsTest.java:27-49): unit vectors, not whole lines
 URLDECODE = [
     ["  ", "  "], [" %20", "  "], ["%20 ", "  "], ["%20%20", "  "], ["%u0020%u0020", "  "], ["%20%u0020", "  "],

@@ -38,7 +38,7 @@ def test_regex_combined(oracle):
     assert o.regex() == COMBINED_REGEX
 
 
-@pytest.mark.parametrize("idx", range(56))
+@pytest.mark.parametrize("idx", range(len(__import__("golden_check").load_vectors()["cases"])))
 def test_golden_vector(oracle, vectors, idx):
     cases = vectors["cases"]
     if idx >= len(cases):
@@ -85,3 +85,58 @@ def test_bad_lines(oracle):
     st, rec = oracle.Oracle("combined", ["TIME.DAY:request.receive.time.day"]).parse(
         good.replace(b"31/Dec/2012", b"31/Apr/2012"))
     assert st == oracle.OK and rec["TIME.DAY:request.receive.time.day"] == [{"l": 30}]
+
+
+# hpt/NginxLogFormatTest.java:95-204 (testCompareApacheAndNginxOutput): the NGINX
+# 'combined' and the Apache combined-without-logname formats deliver the same
+# values for the same line
+NGINX_VS_APACHE_FIELDS = [
+    "HTTP.URI:request.referer", "HTTP.PROTOCOL:request.referer.protocol", "HTTP.USERINFO:request.referer.userinfo",
+    "HTTP.HOST:request.referer.host", "HTTP.PORT:request.referer.port", "HTTP.PATH:request.referer.path",
+    "HTTP.QUERYSTRING:request.referer.query", "STRING:request.referer.query.*", "HTTP.REF:request.referer.ref",
+    "TIME.STAMP:request.receive.time", "TIME.DAY:request.receive.time.day",
+    "TIME.MONTHNAME:request.receive.time.monthname", "TIME.MONTH:request.receive.time.month",
+    "TIME.WEEK:request.receive.time.weekofweekyear", "TIME.YEAR:request.receive.time.weekyear",
+    "TIME.YEAR:request.receive.time.year", "TIME.HOUR:request.receive.time.hour",
+    "TIME.MINUTE:request.receive.time.minute", "TIME.SECOND:request.receive.time.second",
+    "TIME.MILLISECOND:request.receive.time.millisecond", "TIME.DATE:request.receive.time.date",
+    "TIME.TIME:request.receive.time.time", "TIME.ZONE:request.receive.time.timezone",
+    "TIME.EPOCH:request.receive.time.epoch", "TIME.DAY:request.receive.time.day_utc",
+    "TIME.MONTHNAME:request.receive.time.monthname_utc", "TIME.MONTH:request.receive.time.month_utc",
+    "TIME.WEEK:request.receive.time.weekofweekyear_utc", "TIME.YEAR:request.receive.time.weekyear_utc",
+    "TIME.YEAR:request.receive.time.year_utc", "TIME.HOUR:request.receive.time.hour_utc",
+    "TIME.MINUTE:request.receive.time.minute_utc", "TIME.SECOND:request.receive.time.second_utc",
+    "TIME.MILLISECOND:request.receive.time.millisecond_utc", "TIME.DATE:request.receive.time.date_utc",
+    "TIME.TIME:request.receive.time.time_utc", "BYTESCLF:response.body.bytes", "BYTES:response.body.bytes",
+    "STRING:request.status.last", "HTTP.USERAGENT:request.user-agent", "HTTP.FIRSTLINE:request.firstline",
+    "HTTP.METHOD:request.firstline.method", "HTTP.URI:request.firstline.uri",
+    "HTTP.PROTOCOL:request.firstline.uri.protocol", "HTTP.USERINFO:request.firstline.uri.userinfo",
+    "HTTP.HOST:request.firstline.uri.host", "HTTP.PORT:request.firstline.uri.port",
+    "HTTP.PATH:request.firstline.uri.path", "HTTP.QUERYSTRING:request.firstline.uri.query",
+    "STRING:request.firstline.uri.query.*", "HTTP.REF:request.firstline.uri.ref",
+    "HTTP.PROTOCOL_VERSION:request.firstline.protocol", "HTTP.PROTOCOL:request.firstline.protocol",
+    "HTTP.PROTOCOL.VERSION:request.firstline.protocol.version", "IP:connection.client.host"]
+
+
+def test_nginx_equals_apache(oracle):
+    nginx = ("$remote_addr - $remote_user [$time_local] \"$request\" $status $body_bytes_sent \"$http_referer\" "
+             "\"$http_user_agent\"")
+    apache = "%h - %u %t \"%r\" %>s %b \"%{Referer}i\" \"%{User-Agent}i\""
+    line = ("1.2.3.4 - - [23/Aug/2010:03:50:59 +0000] \"POST /foo.html?aap&noot=mies HTTP/1.1\" 200 2 "
+            "\"http://www.example.com/bar.html?wim&zus=jet\" \"Niels Basjes/1.0\"")
+    fields = []
+    for f in NGINX_VS_APACHE_FIELDS:
+        if f.endswith(".*"):
+            fields += [f[:-1] + p for p in ("aap", "noot", "mies", "wim", "zus", "jet")]
+        else:
+            fields.append(f)
+    sa, ra = oracle.Oracle(apache, fields).parse(line)
+    sn, rn = oracle.Oracle(nginx, fields).parse(line)
+    assert sa == sn == 0
+
+    def as_str(vals):  # TestRecord.setStringValue: Value.getString of each delivered value
+        return [v if not isinstance(v, dict) else (None if v["l"] is None else str(v["l"])) for v in vals]
+    for f in fields:
+        assert (f in ra) == (f in rn), f
+        if f in ra:
+            assert as_str(ra[f]) == as_str(rn[f]), f
