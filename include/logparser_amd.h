@@ -121,6 +121,19 @@ int64_t lp_describe(lp_handle *h, char *out, size_t cap);
 int64_t lp_synth_combined(uint64_t seed, int64_t first_line, int64_t max_lines,
                           char *out, size_t cap, int64_t *n_lines);
 
+/* The same for each BASELINE.json workload:
+ *   LP_SYNTH_COMBINED  config 2, 'combined'
+ *   LP_SYNTH_STRFTIME  config 3, '%h %l %u [%{%d/%b/%Y %T}t.%{msec_frac}t] "%r" %>s %b
+ *                      "%{Referer}i" "%{User-Agent}i" %I %O', 5 % malformed lines
+ *   LP_SYNTH_NGINX     config 4, the NGINX log_format of
+ *                      hpt/nginxmodules/NginxUpstreamTest.java:94
+ * Returns LP_E_INVALID for an unknown workload. */
+#define LP_SYNTH_COMBINED 2
+#define LP_SYNTH_STRFTIME 3
+#define LP_SYNTH_NGINX 4
+int64_t lp_synth(int workload, uint64_t seed, int64_t first_line, int64_t max_lines,
+                 char *out, size_t cap, int64_t *n_lines);
+
 #ifdef __cplusplus
 }
 #endif

@@ -94,6 +94,9 @@ def lib():
     L.lp_synth_combined.restype = ctypes.c_int64
     L.lp_synth_combined.argtypes = [ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t,
                                     ctypes.POINTER(ctypes.c_int64)]
+    L.lp_synth.restype = ctypes.c_int64
+    L.lp_synth.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+                           ctypes.c_size_t, ctypes.POINTER(ctypes.c_int64)]
     _lib = L
     return L
 
@@ -114,6 +117,28 @@ def synth_combined(seed, first_line, n_lines):
     buf = ctypes.create_string_buffer(cap)
     got = ctypes.c_int64(0)
     nb = lib().lp_synth_combined(seed, first_line, n_lines, buf, cap, ctypes.byref(got))
+    return buf.raw[:nb]
+
+
+SYNTH_COMBINED, SYNTH_STRFTIME, SYNTH_NGINX = 2, 3, 4
+
+# the LogFormat of each synthetic workload (BASELINE.json configs 2-4)
+SYNTH_FORMATS = {
+    SYNTH_COMBINED: "combined",
+    SYNTH_STRFTIME: '%h %l %u [%{%d/%b/%Y %T}t.%{msec_frac}t] "%r" %>s %b "%{Referer}i" "%{User-Agent}i" %I %O',
+    SYNTH_NGINX: '$remote_addr - $remote_user [$time_local] "$request" $status $body_bytes_sent "$http_referer" '
+                 '"$http_user_agent" "$http_x_forwarded_for" $request_time $upstream_response_time $pipe',
+}
+
+
+def synth(workload, seed, first_line, n_lines):
+    """Deterministic synthetic lines of a BASELINE.json workload (SYNTH_*) as bytes."""
+    cap = n_lines * 800 + 1024
+    buf = ctypes.create_string_buffer(cap)
+    got = ctypes.c_int64(0)
+    nb = lib().lp_synth(workload, seed, first_line, n_lines, buf, cap, ctypes.byref(got))
+    if nb < 0:
+        raise ValueError("unknown synthetic workload %r" % workload)
     return buf.raw[:nb]
 
 

@@ -581,6 +581,73 @@ __host__ __device__ LP_INLINE int lit_first(const Program& P, const LN& L, const
     }
 }
 
+// End of the digit run starting at p (p if none).
+template <typename LN>
+__host__ __device__ LP_INLINE int digits_end(const LN& L, int p) {
+    return find_fwd(L, p, L.n, [](uint32_t w) { return ~swar::digit(w) & swar::HI; });
+}
+
+// [0-9]+\.[0-9]+ at p: end (the fraction greedy, maximal), -1 none, -2 when
+// a run is longer than 18 digits (Long.parseLong of the SECOND_MILLIS
+// converters could overflow: a runtime exception of the reference).
+template <typename LN>
+__host__ __device__ LP_INLINE int decimal_at(const LN& L, int p) {
+    const int d = digits_end(L, p);
+    if (d == p || d >= L.n || L[d] != '.') return -1;
+    const int r = digits_end(L, d + 1);
+    if (r == d + 1) return -1;
+    if (d - p > 18 || r - d - 1 > 18) return -2;
+    return r;
+}
+
+// UpstreamModule.upstreamListOf(X) = X(?: *, *X(?: *: *X)?)* at p: the
+// first candidate in java.util.regex order (every X, star iteration and
+// optional group taken as far as it goes), -1 none, -2 FALLBACK.  Lists
+// whose ',' or ':' is not followed by ' ' would not split into clean items
+// in UpstreamListDissector (split(", ") / split(": ")): FALLBACK.
+template <typename LN>
+__host__ __device__ LP_INLINE int uplist_at(const LN& L, int p, bool dec) {
+    auto X = [&](int q) { return dec ? decimal_at(L, q) : (digits_end(L, q) > q ? digits_end(L, q) : -1); };
+    auto spaces = [&](int q) { while (q < L.n && L[q] == ' ') ++q; return q; };
+    int e = X(p);
+    if (e < 0) return e;
+    for (;;) {
+        int q = spaces(e);
+        if (q >= L.n || L[q] != ',') break;
+        const int e2 = X(spaces(q + 1));
+        if (e2 == -2) return -2;
+        if (e2 < 0) break;
+        e = e2;
+        q = spaces(e);
+        if (q < L.n && L[q] == ':') {
+            const int e3 = X(spaces(q + 1));
+            if (e3 == -2) return -2;
+            if (e3 >= 0) e = e3;
+        }
+    }
+    for (int q = p; q < e; ++q) {
+        const uint32_t c = L[q];
+        if ((c == ',' || c == ':') && (q + 1 >= e || L[q + 1] != ' ')) return -2;
+    }
+    return e;
+}
+
+// The largest item end of the list at p that is < cur (-1 none).  The list
+// was accepted by uplist_at, so its items split cleanly.
+template <typename LN>
+__host__ __device__ LP_INLINE int uplist_prev_end(const LN& L, int p, int cur, bool dec) {
+    auto X = [&](int q) { return dec ? decimal_at(L, q) : (digits_end(L, q) > q ? digits_end(L, q) : -1); };
+    auto spaces = [&](int q) { while (q < L.n && L[q] == ' ') ++q; return q; };
+    int e = X(p), best = -1;
+    while (e >= 0 && e < cur) {
+        best = e;
+        int q = spaces(e);
+        if (q >= L.n || (L[q] != ',' && L[q] != ':')) break;
+        e = X(spaces(q + 1));
+    }
+    return best;
+}
+
 // First candidate end of element e at position p (exact leftmost-first
 // order), -1 = none, -2 = FALLBACK.  '.' runs to the end of the line: the
 // fast-path guard already rejected every line terminator.
@@ -627,8 +694,76 @@ __host__ __device__ LP_INLINE int cand_first(const Program& P, const Elem& e, co
         if (e.kind == EK_CLF_IP && p < L.n && L[p] == '-' && e.nlit && (e.lit4 & 0xFFu) != '-') return p + 1;
         return -2;
     }
+    case EK_ANYCHAR: return p < L.n ? p + 1 : -1;  // '.': the guard already rejected line terminators
+    case EK_DECIMAL: return decimal_at(L, p);
+    case EK_MSEC: {
+        const int d = digits_end(L, p);
+        if (d == p || d + 4 > L.n || L[d] != '.' || !is_digit(L[d + 1]) || !is_digit(L[d + 2]) || !is_digit(L[d + 3]))
+            return -1;
+        return d - p > 18 ? -2 : d + 4;
+    }
+    case EK_NOSPACE3: {
+        // only the maximal first and second runs can be followed by ' '
+        const int q1 = find_ws(L, p, L.n);
+        if (q1 >= L.n || L[q1] != ' ') return -1;
+        const int q2 = find_ws(L, q1 + 1, L.n);
+        if (q2 >= L.n || L[q2] != ' ') return -1;
+        return find_ws(L, q2 + 1, L.n);
+    }
+    case EK_UPLIST_DEC: return uplist_at(L, p, true);
+    case EK_UPLIST_NUM: return uplist_at(L, p, false);
     }
     return -2;
+}
+
+// Could another alternative of FORMAT_IP (TokenParser.java:43-51) at p end
+// somewhere other than cur and be followed by the rest of the format (its
+// next literal, or '$')?  Every IPv4 end is also an end of the IPv6 branch
+// ":?(?:H{1,4}(?::|.)?){0,8}(?::|::)?(?:H{1,4}(?::|.)?){0,8}" (digits are
+// hex, '.' matches the dots), so the reachable ends of that branch are
+// simulated as bit sets over the <= 83 bytes it can span.
+template <typename LN>
+__host__ __device__ LP_INLINE bool ip_alt_end_possible(const Program& P, const LN& L, const Elem& e, int p, int cur) {
+    constexpr int W = 96;
+    uint32_t cur_set[3] = {1u, 0u, 0u}, all[3];
+    auto add = [](uint32_t* m, int k) { if (k < W) m[k >> 5] |= 1u << (k & 31); };
+    auto has = [](const uint32_t* m, int k) { return (m[k >> 5] >> (k & 31)) & 1u; };
+    auto hexat = [&](int q) {
+        if (q >= L.n) return false;
+        const uint32_t c = L[q];
+        return (c - '0' < 10u) || ((c | 32u) - 'a' < 6u);
+    };
+    if (p < L.n && L[p] == ':') add(cur_set, 1);
+    // one (H{1,4}(?::|.)?) group from every position of m
+    auto groups = [&](uint32_t* m, uint32_t* acc) {
+        for (int it = 0; it < 8; ++it) {
+            uint32_t nx[3] = {0u, 0u, 0u};
+            for (int k = 0; k < W; ++k) {
+                if (!has(m, k)) continue;
+                for (int h = 1; h <= 4 && hexat(p + k + h - 1); ++h) {
+                    add(nx, k + h);
+                    if (p + k + h < L.n) add(nx, k + h + 1);  // (?::|.): any byte but a line terminator
+                }
+            }
+            if (!(nx[0] | nx[1] | nx[2])) break;
+            for (int w = 0; w < 3; ++w) { acc[w] |= nx[w]; m[w] = nx[w]; }
+        }
+    };
+    for (int w = 0; w < 3; ++w) all[w] = cur_set[w];
+    groups(cur_set, all);
+    uint32_t mid[3] = {all[0], all[1], all[2]};
+    for (int k = 0; k < W; ++k) {
+        if (!has(all, k) || p + k >= L.n || L[p + k] != ':') continue;
+        add(mid, k + 1);
+        if (p + k + 1 < L.n && L[p + k + 1] == ':') add(mid, k + 2);
+    }
+    uint32_t fin[3] = {mid[0], mid[1], mid[2]};
+    groups(mid, fin);
+    for (int k = 0; k < W; ++k) {
+        if (!has(fin, k) || p + k == cur || p + k > L.n) continue;
+        if (e.last ? p + k == L.n : (!e.nlit || lit_at(P, L, p + k, e))) return true;
+    }
+    return false;
 }
 
 // Next candidate after 'cur' (same priority order).
@@ -651,7 +786,29 @@ __host__ __device__ LP_INLINE int cand_next(const Program& P, const Elem& e, con
     }
     case EK_TIME_US: return -1;
     case EK_CLF_IP: case EK_IP:
-        return (L[p] == '-') ? -1 : -2;  // shorter IPv4 / IPv6 alternatives: not proven here
+        if (L[p] == '-') return -1;
+        // shorter IPv4 / IPv6 alternatives: exact only when none of them can
+        // be followed by the rest of the format
+        return ip_alt_end_possible(P, L, e, p, cur) ? -2 : -1;
+    case EK_ANYCHAR: case EK_MSEC: return -1;
+    case EK_DECIMAL: {  // a shorter fraction
+        const int d = digits_end(L, p);
+        return cur - 1 >= d + 2 ? cur - 1 : -1;
+    }
+    case EK_NOSPACE3: {  // a shorter third run
+        const int q2 = find_ws(L, find_ws(L, p, L.n) + 1, L.n);
+        return cur - 1 >= q2 + 1 ? cur - 1 : -1;
+    }
+    case EK_UPLIST_DEC: case EK_UPLIST_NUM: {
+        // Backtracking into X(?: *, *X(?: *: *X)?)* yields, in priority order,
+        // every shorter end: fewer digits in an item's last run (followed by
+        // a digit) and fewer items (item ends, descending).  Followed by the
+        // end of the line or a literal that does not start with a digit, only
+        // the item ends can succeed.
+        if (e.last) return -1;
+        if (!e.nlit || is_digit(e.lit4 & 0xFFu)) return -2;
+        return uplist_prev_end(L, p, cur, e.kind == EK_UPLIST_DEC);
+    }
     }
     return -2;
 }

@@ -57,6 +57,13 @@ enum ElemKind : uint8_t {
     EK_TIME_US,      // [0-3][0-9]/(?:[a-zA-Z]{3})/[1-9][0-9]{3}:[0-9]{2}:[0-9]{2}:[0-9]{2} [\+|\-][0-9]{4}
     EK_CLF_IP,       // IPv4|IPv6|-  (IPv4 dotted quad or '-' on device, else FALLBACK)
     EK_IP,           // IPv4|IPv6
+    // NGINX token regexes (nginxmodules/CoreLogModule.java, UpstreamModule.java)
+    EK_ANYCHAR,      // .                                  ($pipe)
+    EK_DECIMAL,      // [0-9]+\.[0-9]+                      ($request_time, SECOND_MILLIS)
+    EK_MSEC,         // [0-9]+\.[0-9][0-9][0-9]             ($msec)
+    EK_NOSPACE3,     // [^\s]* [^\s]* [^\s]*                ($request)
+    EK_UPLIST_DEC,   // X(?: *, *X(?: *: *X)?)*, X = [0-9]+\.[0-9]+   (upstream time lists)
+    EK_UPLIST_NUM,   // X(?: *, *X(?: *: *X)?)*, X = [0-9]+            (upstream byte lists)
 };
 
 struct Elem {

@@ -48,6 +48,14 @@ const std::string R_NO_SPACE = "[^\\s]*";
 const std::string R_TIME_US =
     "[0-3][0-9]/(?:[a-zA-Z][a-zA-Z][a-zA-Z])/[1-9][0-9][0-9][0-9]:[0-9][0-9]:[0-9][0-9]:[0-9][0-9] [\\+|\\-][0-9][0-9][0-9][0-9]";
 const std::string R_FIRSTLINE = ".*";  // hp/dissectors/HttpFirstLineDissector.java:56-57
+const std::string R_TIME_ISO8601 =
+    "[1-9][0-9][0-9][0-9]-[0-1][0-9]-[0-3][0-9]T[0-9][0-9]:[0-9][0-9]:[0-9][0-9][\\+|\\-][0-9][0-9]:[0-9][0-9]";
+const std::string R_NUMBER_DECIMAL = R_NUMBER + "\\." + R_NUMBER;
+const std::string R_NUMBER_OPT_DECIMAL = R_NUMBER + "(?:\\." + R_NUMBER + ")?";
+const std::string R_MSEC = "[0-9]+\\.[0-9][0-9][0-9]";      // nginxmodules/CoreLogModule.java:56-58
+const std::string R_NOSPACE3 = R_NO_SPACE + " " + R_NO_SPACE + " " + R_NO_SPACE;  // $request (CoreLogModule.java:296-300)
+// UpstreamModule.upstreamListOf (nginxmodules/UpstreamModule.java:42-44)
+std::string upstream_list(const std::string& x) { return x + "(?: *, *" + x + "(?: *: *" + x + ")?)*"; }
 
 int elem_kind_of(const std::string& r) {
     if (r == R_NO_SPACE) return EK_NOSPACE;
@@ -61,11 +69,17 @@ int elem_kind_of(const std::string& r) {
     if (r == R_TIME_US) return EK_TIME_US;
     if (r == R_CLF_IP) return EK_CLF_IP;
     if (r == R_IP) return EK_IP;
+    if (r == ".") return EK_ANYCHAR;
+    if (r == R_NUMBER_DECIMAL) return EK_DECIMAL;
+    if (r == R_MSEC) return EK_MSEC;
+    if (r == R_NOSPACE3) return EK_NOSPACE3;
+    if (r == upstream_list(R_NUMBER_DECIMAL)) return EK_UPLIST_DEC;
+    if (r == upstream_list(R_NUMBER)) return EK_UPLIST_NUM;
     return -1;
 }
 
 // ----------------------------------------------------------- token table
-enum TpKind { TP_PLAIN, TP_FIXED, TP_NAMED, TP_PARAM };
+enum TpKind { TP_PLAIN, TP_FIXED, TP_NAMED, TP_PARAM, TP_DOLLAR };
 
 struct TParser {
     TpKind kind;
@@ -77,7 +91,7 @@ struct TParser {
     // NAMED pattern: "%{" NAMECLASS* "}" suffix ; PARAM: "%{" prefix [^}]*%[^}]* "}t"
     std::string suffix;     // NAMED suffix after '}' (e.g. "i", "^ti")
     bool underscore = true; // NAMED class includes '_'
-    std::string pprefix;    // PARAM prefix inside braces ("", "begin:", "end:")
+    std::string pprefix;    // PARAM prefix inside braces ("", "begin:", "end:"); DOLLAR: "$" + name prefix
 };
 
 std::string lower(std::string s) {
@@ -122,6 +136,23 @@ struct TokenTable {
         t.suffix = suffix;
         t.underscore = underscore;
         out(t, type, name, CAST_S);
+    }
+    // NGINX (nginxmodules/*.java): TokenParser (default prio 10), NamedTokenParser
+    // "\\$prefix([a-z0-9\\-_]*)" (default prio 0), NotImplementedTokenParser
+    void ng(const std::string& token, const std::string& name, const std::string& type, int casts,
+            const std::string& re, int prio) {
+        out(add(TP_PLAIN, token, re, prio), type, name, casts);
+    }
+    void ngnamed(const std::string& pattern, const std::string& name, const std::string& type, int casts,
+                 const std::string& re, int prio) {
+        auto& t = add(TP_DOLLAR, pattern, re, prio);
+        t.pprefix = "$" + pattern.substr(2, pattern.find('(') - 2);  // "\\$http_(...)" -> "$http_"
+        out(t, type, name, casts);
+    }
+    void ngnotimpl(const std::string& token, const std::string& prefix, const std::string& re, int prio) {
+        std::string n = prefix + "_";  // TokenFormatDissector.java:95-102
+        for (char c : lower(token)) n += ((c >= 'a' && c <= 'z') || (c >= '0' && c <= '9') || c == '_') ? c : '_';
+        out(add(TP_PLAIN, token, re, prio), "NOT_IMPLEMENTED", n, CAST_S);
     }
     void param(const std::string& prefix, const std::string& name, int prio) {
         auto& t = add(TP_PARAM, "param:" + prefix, R_STRING, prio);
@@ -215,6 +246,188 @@ const TokenTable& apache_table() {
     return T;
 }
 
+// NginxHttpdLogFormatDissector.createAllTokenParsers (hp/NginxHttpdLogFormatDissector.java:121-142):
+// the token parsers of every NGINX module, in module order
+const TokenTable& nginx_table() {
+    static TokenTable T;
+    static bool init = false;
+    if (init) return T;
+    init = true;
+    const int CAST_SL = CAST_S | CAST_L;
+    (void)CAST_SL;
+
+    /* CoreLogModule (nginxmodules/CoreLogModule.java:45-489) */
+    T.ng("$bytes_sent", "response.bytes", "BYTES", CAST_SL, R_NUMBER, 10);
+    T.ng("$bytes_received", "request.bytes", "BYTES", CAST_SL, R_NUMBER, 10);
+    T.ng("$connection", "connection.serial_number", "NUMBER", CAST_SL, R_CLF_NUMBER, -1);
+    T.ng("$connection_requests", "connection.requestnr", "NUMBER", CAST_SL, R_CLF_NUMBER, 10);
+    T.ng("$msec", "request.receive.time.epoch", "TIME.EPOCH_SECOND_MILLIS", CAST_S, "[0-9]+\\.[0-9][0-9][0-9]", 10);
+    T.ng("$status", "request.status.last", "STRING", CAST_S, R_NO_SPACE, 10);
+    T.ng("$time_iso8601", "request.receive.time", "TIME.ISO8601", CAST_S, R_TIME_ISO8601, 10);
+    T.ng("$time_local", "request.receive.time", "TIME.STAMP", CAST_S, R_TIME_US, 10);
+    T.ngnamed("\\$arg_([a-z0-9\\-\\_]*)", "request.firstline.uri.query.", "STRING", CAST_S, R_STRING, 0);
+    T.ng("$is_args", "request.firstline.uri.is_args", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$args", "request.firstline.uri.query", "HTTP.QUERYSTRING", CAST_S, R_STRING, 10);
+    T.ng("$query_string", "request.firstline.uri.query", "HTTP.QUERYSTRING", CAST_S, R_STRING, 10);
+    T.ng("$body_bytes_sent", "response.body.bytes", "BYTES", CAST_SL, R_NUMBER, 10);
+    T.ng("$content_length", "request.header.content_length", "HTTP.HEADER", CAST_S, R_STRING, 10);
+    T.ng("$content_type", "request.header.content_type", "HTTP.HEADER", CAST_S, R_STRING, 10);
+    T.ngnamed("\\$cookie_([a-z0-9\\-_]*)", "request.cookies.", "HTTP.COOKIE", CAST_S, R_STRING, 0);
+    T.ng("$document_root", "request.firstline.document_root", "STRING", CAST_S, R_NO_SPACE, 10);
+    T.ng("$realpath_root", "request.firstline.realpath_root", "STRING", CAST_S, R_NO_SPACE, 10);
+    T.ng("$host", "connection.server.name", "STRING", CAST_S, R_NO_SPACE, -1);
+    T.ng("$hostname", "connection.client.host", "STRING", CAST_S, R_NO_SPACE, 10);
+    T.ngnamed("\\$http_([a-z0-9\\-_]*)", "request.header.", "HTTP.HEADER", CAST_S, R_STRING, 0);
+    T.ng("$http_user_agent", "request.user-agent", "HTTP.USERAGENT", CAST_S, R_STRING, 1);
+    T.ng("$http_referer", "request.referer", "HTTP.URI", CAST_S, R_NO_SPACE, 1);
+    T.ng("$https", "connection.https", "STRING", CAST_S, R_NO_SPACE, 10);
+    T.ngnotimpl("$limit_rate", "nginx_parameter_not_intended_for_logging", R_NO_SPACE, 0);
+    T.ng("$nginx_version", "server.nginx.version", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$pid", "connection.server.child.processid", "NUMBER", CAST_SL, R_NUMBER, 10);
+    T.ng("$protocol", "connection.protocol", "STRING", CAST_S, R_NO_SPACE, 10);
+    T.ng("$pipe", "connection.nginx.pipe", "STRING", CAST_S, ".", 10);
+    T.ng("$proxy_protocol_addr", "connection.client.proxy.host", "IP", CAST_SL, R_CLF_IP, 10);
+    T.ng("$proxy_protocol_port", "connection.client.proxy.port", "PORT", CAST_SL, R_CLF_NUMBER, 10);
+    T.ng("$remote_addr", "connection.client.host", "IP", CAST_SL, R_CLF_IP, 10);
+    T.ng("$binary_remote_addr", "connection.client.host", "IP_BINARY", CAST_SL, std::string("\\\\x") + R_HEXDIGIT + R_HEXDIGIT + "\\\\x" + R_HEXDIGIT + R_HEXDIGIT + "\\\\x" + R_HEXDIGIT + R_HEXDIGIT + "\\\\x" + R_HEXDIGIT + R_HEXDIGIT, 10);
+    T.ng("$remote_port", "connection.client.port", "PORT", CAST_SL, R_NUMBER, 10);
+    T.ng("$remote_user", "connection.client.user", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$request", "request.firstline", "HTTP.FIRSTLINE", CAST_S, R_NO_SPACE + " " + R_NO_SPACE + " " + R_NO_SPACE, -2);
+    T.ngnotimpl("$request_body", "nginx_parameter_not_intended_for_logging", R_STRING, -1);
+    T.ngnotimpl("$request_body_file", "nginx_parameter_not_intended_for_logging", R_STRING, -1);
+    T.ng("$request_completion", "request.completion", "STRING", CAST_S, R_NO_SPACE, 10);
+    T.ng("$request_filename", "server.filename", "FILENAME", CAST_S, R_STRING, 10);
+    T.ng("$request_length", "request.bytes", "BYTES", CAST_SL, R_CLF_NUMBER, 10);
+    T.ng("$request_method", "request.firstline.method", "HTTP.METHOD", CAST_S, R_NO_SPACE, 10);
+    T.ng("$request_time", "response.server.processing.time", "SECOND_MILLIS", CAST_S, R_NUMBER_DECIMAL, 10);
+    T.ng("$request_uri", "request.firstline.uri", "HTTP.URI", CAST_S, R_NO_SPACE, 10);
+    T.ng("$request_id", "request.id", "STRING", CAST_S, R_HEXNUMBER, 10);
+    T.ng("$uri", "request.firstline.uri.normalized", "HTTP.URI", CAST_S, R_STRING, 10);
+    T.ng("$document_uri", "request.firstline.uri.normalized", "HTTP.URI", CAST_S, R_STRING, 10);
+    T.ng("$scheme", "request.firstline.uri.protocol", "HTTP.PROTOCOL", CAST_S, R_NO_SPACE, 10);
+    T.ngnamed("\\$sent_http_([a-z0-9\\-_]*)", "response.header.", "HTTP.HEADER", CAST_S, R_STRING, 0);
+    T.ngnamed("\\$sent_trailer_([a-z0-9\\-_]*)", "response.trailer.", "HTTP.TRAILER", CAST_S, R_STRING, 0);
+    T.ng("$server_addr", "connection.server.ip", "IP", CAST_SL, R_CLF_IP, 10);
+    T.ng("$server_name", "connection.server.name", "STRING", CAST_S, R_NO_SPACE, 10);
+    T.ng("$server_port", "connection.server.port", "PORT", CAST_SL, R_NUMBER, 10);
+    T.ng("$server_protocol", "request.firstline.protocol", "HTTP.PROTOCOL_VERSION", CAST_SL, R_NO_SPACE, 10);
+    T.ng("$session_time", "connection.session.time", "SECOND_MILLIS", CAST_S, R_NUMBER_DECIMAL, 10);
+    T.ng("$tcpinfo_rtt", "connection.tcpinfo.rtt", "MICROSECONDS", CAST_SL, R_NUMBER, -1);
+    T.ng("$tcpinfo_rttvar", "connection.tcpinfo.rttvar", "MICROSECONDS", CAST_SL, R_NUMBER, 10);
+    T.ng("$tcpinfo_snd_cwnd", "connection.tcpinfo.send.cwnd", "BYTES", CAST_SL, R_NUMBER, 10);
+    T.ng("$tcpinfo_rcv_space", "connection.tcpinfo.receive.space", "BYTES", CAST_SL, R_NUMBER, 10);
+    T.ngnamed("\\$([a-z0-9\\-\\_]*)", "nginx.unknown.", "UNKNOWN_NGINX_VARIABLE", CAST_S, R_NO_SPACE, -10);
+    /* UpstreamModule (nginxmodules/UpstreamModule.java:46-160) */
+const std::string UP = "nginxmodule.upstream";
+    T.ng("$upstream_addr", UP + ".addr", "UPSTREAM_ADDR_LIST", CAST_S, upstream_list(R_NO_SPACE), 10);
+    T.ng("$upstream_bytes_received", UP + ".bytes.received", "UPSTREAM_BYTES_LIST", CAST_S, upstream_list(R_NUMBER), 10);
+    T.ng("$upstream_bytes_sent", UP + ".bytes.sent", "UPSTREAM_BYTES_LIST", CAST_S, upstream_list(R_NUMBER), 10);
+    T.ng("$upstream_cache_status", UP + ".cache.status", "UPSTREAM_CACHE_STATUS", CAST_S, "(?:MISS|BYPASS|EXPIRED|STALE|UPDATING|REVALIDATED|HIT)", 10);
+    T.ng("$upstream_connect_time", UP + ".connect.time", "UPSTREAM_SECOND_MILLIS_LIST", CAST_S, upstream_list(R_NUMBER_DECIMAL), 10);
+    T.ngnamed("\\$upstream_cookie_([a-z0-9\\-_]*)", UP + ".response.cookies.", "HTTP.COOKIE", CAST_S, R_STRING, 0);
+    T.ng("$upstream_header_time", UP + ".header.time", "UPSTREAM_SECOND_MILLIS_LIST", CAST_S, upstream_list(R_NUMBER_DECIMAL), 10);
+    T.ngnamed("\\$upstream_http_([a-z0-9\\-_]*)", UP + ".header.", "HTTP.HEADER", CAST_S, R_STRING, 0);
+    T.ng("$upstream_queue_time", UP + ".queue.time", "UPSTREAM_SECOND_MILLIS_LIST", CAST_S, upstream_list(R_NUMBER_DECIMAL), 10);
+    T.ng("$upstream_response_length", UP + ".response.length", "UPSTREAM_BYTES_LIST", CAST_S, upstream_list(R_NUMBER), 10);
+    T.ng("$upstream_response_time", UP + ".response.time", "UPSTREAM_SECOND_MILLIS_LIST", CAST_S, upstream_list(R_NUMBER_DECIMAL), 10);
+    T.ng("$upstream_status", UP + ".status", "UPSTREAM_STATUS_LIST", CAST_S, upstream_list(R_NO_SPACE), 10);
+    T.ngnamed("\\$upstream_trailer_([a-z0-9\\-_]*)", UP + ".trailer.", "HTTP.TRAILER", CAST_S, R_STRING, 0);
+    T.ng("$upstream_first_byte_time", UP + ".first_byte.time", "UPSTREAM_SECOND_MILLIS_LIST", CAST_S, upstream_list(R_NUMBER_DECIMAL), 10);
+    T.ng("$upstream_session_time", UP + ".session.time", "UPSTREAM_SECOND_MILLIS_LIST", CAST_S, upstream_list(R_NUMBER_DECIMAL), 10);
+
+    /* SslModule (nginxmodules/SslModule.java:37-200) */
+const std::string SSL = "nginxmodule.ssl";
+    T.ng("$ssl_cipher", SSL + ".cipher", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$ssl_ciphers", SSL + ".client.ciphers", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$ssl_client_escaped_cert", SSL + ".client.cert", "PEM_CERT_URLENCODED", CAST_S, R_NO_SPACE, 10);
+    T.ng("$ssl_client_cert", SSL + ".client.cert", "PEM_CERT", CAST_S, R_STRING, 10);
+    T.ng("$ssl_client_raw_cert", SSL + ".client.cert", "PEM_CERT_RAW", CAST_S, R_STRING, 10);
+    T.ng("$ssl_client_fingerprint", SSL + ".client.cert.fingerprint", "SHA1", CAST_S, R_NO_SPACE, 10);
+    T.ng("$ssl_client_i_dn", SSL + ".client.cert.issuer_dn", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$ssl_client_i_dn_legacy", SSL + ".client.cert.issuer_dn.legacy", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$ssl_client_s_dn", SSL + ".client.cert.subject_dn", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$ssl_client_s_dn_legacy", SSL + ".client.cert.subject_dn.legacy", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$ssl_client_serial", SSL + ".client.cert.serial", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$ssl_client_v_end", SSL + ".client.cert.end_date", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$ssl_client_v_remain", SSL + ".client.cert.remain_days", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$ssl_client_v_start", SSL + ".client.cert.start_date", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$ssl_client_verify", SSL + ".client.cert.verify", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$ssl_curves", SSL + ".client.curves", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$ssl_early_data", SSL + ".early_data", "STRING", CAST_S, "1?", 10);
+    T.ng("$ssl_protocol", SSL + ".protocol", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$ssl_server_name", SSL + ".server_name", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$ssl_session_id", SSL + ".session.id", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$ssl_session_reused", SSL + ".session.reused", "STRING", CAST_S, "(r|.)", 10);
+    T.ng("$ssl_preread_protocol", SSL + ".preread.protocol", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$ssl_preread_server_name", SSL + ".preread.server_name", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$ssl_preread_alpn_protocols", SSL + ".preread.alpn_protocols", "STRING", CAST_S, R_STRING, 10);
+
+    /* GeoIPModule (nginxmodules/GeoIPModule.java:35-104) */
+const std::string GEO = "nginxmodule.geoip";
+    T.ng("$geoip_country_code", GEO + ".country.code", "STRING", CAST_S, R_NO_SPACE, 10);
+    T.ng("$geoip_country_code3", GEO + ".country.code3", "STRING", CAST_S, R_NO_SPACE, 10);
+    T.ng("$geoip_country_name", GEO + ".country.name", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$geoip_area_code", GEO + ".area.code", "STRING", CAST_S, R_NO_SPACE, 10);
+    T.ng("$geoip_city_continent_code", GEO + ".continent.code", "STRING", CAST_S, R_NO_SPACE, 10);
+    T.ng("$geoip_city_country_code", GEO + ".country.code", "STRING", CAST_S, R_NO_SPACE, 10);
+    T.ng("$geoip_city_country_code3", GEO + ".country.code3", "STRING", CAST_S, R_NO_SPACE, 10);
+    T.ng("$geoip_city_country_name", GEO + ".country.name", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$geoip_dma_code", GEO + ".dma.code", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$geoip_latitude", GEO + ".location.latitude", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$geoip_longitude", GEO + ".location.longitude", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$geoip_region", GEO + ".region.code", "STRING", CAST_S, R_NO_SPACE, 10);
+    T.ng("$geoip_region_name", GEO + ".region.name", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$geoip_city", GEO + ".city", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$geoip_postal_code", GEO + ".postal.code", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$geoip_org", GEO + ".organization", "STRING", CAST_S, R_STRING, 10);
+
+    /* VariousModule (nginxmodules/VariousModule.java:37-212) */
+const std::string VAR = "nginxmodule";
+    T.ng("$secure_link", VAR + ".secure_link.status", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$session_log_id", VAR + ".session_log.id", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$slice_range", VAR + ".slice_range", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$proxy_host", VAR + ".proxy.host", "STRING", CAST_S, R_NO_SPACE, 10);
+    T.ng("$proxy_port", VAR + ".proxy.port", "STRING", CAST_S, R_NO_SPACE, 10);
+    T.ng("$proxy_add_x_forwarded_for", VAR + ".proxy.add_x_forwarded_for", "STRING", CAST_S, R_NO_SPACE, 10);
+    T.ng("$uid_got", VAR + ".userid.uid_got", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$uid_reset", VAR + ".userid.uid_reset", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$uid_set", VAR + ".userid.uid_set", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$modern_browser", VAR + ".browser.modern", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$ancient_browser", VAR + ".browser.ancient", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$msie", VAR + ".browser.msie", "STRING", CAST_S, R_NO_SPACE, 10);
+    T.ng("$connections_active", VAR + ".stub_status.connections.active", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$connections_reading", VAR + ".stub_status.connections.reading", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$connections_writing", VAR + ".stub_status.connections.writing", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$connections_waiting", VAR + ".stub_status.connections.waiting", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$date_local", VAR + ".date.local", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$date_gmt", VAR + ".date.gmt", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$fastcgi_script_name", VAR + ".fastcgi.script_name", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$fastcgi_path_info", VAR + ".fastcgi.path_info", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$gzip_ratio", VAR + ".gzip.ratio", "STRING", CAST_S, R_NUMBER_OPT_DECIMAL, 10);
+    T.ng("$spdy", VAR + ".spdy.version", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$spdy_request_priority", VAR + ".spdy.request_priority", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$http2", VAR + ".http2.negotiated_protocol", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$invalid_referer", VAR + ".referer.invalid", "STRING", CAST_S, "1?", 10);
+    T.ngnamed("\\$jwt_header_([a-z0-9\\-_]*)", VAR + ".jwt.header.", "STRING", CAST_S, R_STRING, 0);
+    T.ngnamed("\\$jwt_claim_([a-z0-9\\-_]*)", VAR + ".jwt.claim.", "STRING", CAST_S, R_STRING, 0);
+    T.ng("$memcached_key", VAR + ".memcached.key", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$realip_remote_addr", VAR + ".realip.remote_addr", "IP", CAST_S, R_STRING, 10);
+    T.ng("$realip_remote_port", VAR + ".realip.remote_port", "PORT", CAST_SL, R_STRING, 10);
+
+    /* KubernetesIngressModule (nginxmodules/KubernetesIngressModule.java:35-68) */
+const std::string K8S = "nginxmodule.kubernetes";
+    T.ng("$the_real_ip", K8S + ".the_real_ip", "IP", CAST_S, R_STRING, 10);
+    T.ng("$proxy_upstream_name", K8S + ".proxy_upstream_name", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$req_id", K8S + ".req_id", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$namespace", K8S + ".namespace", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$ingress_name", K8S + ".ingress_name", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$service_name", K8S + ".service.name", "STRING", CAST_S, R_STRING, 10);
+    T.ng("$service_port", K8S + ".service.port", "PORT", CAST_S, R_STRING, 10);
+
+
+    return T;
+}
+
 // commons-codec Hex(MD5) for ParameterizedTokenParser.tokenParameterToTypeName
 std::string md5_hex(const std::string& msg) {
     static const uint32_t K[64] = {
@@ -272,6 +485,16 @@ std::string md5_hex(const std::string& msg) {
 // the patterns \%\{([a-z0-9\-_]*)\}X and \%\{PREFIX([^\}]*%[^\}]*)\}t).
 bool find_pattern(const TParser& tp, const std::string& s, size_t from, size_t& start, size_t& end,
                   std::string& field) {
+    if (tp.kind == TP_DOLLAR) {  // \$prefix([a-z0-9\-_]*): leftmost prefix, greedy name
+        size_t p = s.find(tp.pprefix, from);
+        if (p == std::string::npos) return false;
+        size_t q = p + tp.pprefix.size();
+        while (q < s.size() && ((s[q] >= 'a' && s[q] <= 'z') || (s[q] >= '0' && s[q] <= '9') || s[q] == '-' || s[q] == '_')) ++q;
+        field = s.substr(p + tp.pprefix.size(), q - p - tp.pprefix.size());
+        start = p;
+        end = q;
+        return true;
+    }
     for (size_t p = from; p + 1 < s.size(); ++p) {
         if (s[p] != '%' || s[p + 1] != '{') continue;
         size_t q = p + 2;
@@ -329,7 +552,7 @@ void collect_tokens(const TParser& tp, const std::string& fmt, std::vector<Token
         t.prio = t.fixed ? 0 : tp.prio;
         for (const auto& o : tp.outs) {
             TokOut x = o;
-            if (tp.kind == TP_NAMED) x.name = lower(o.name + field);
+            if (tp.kind == TP_NAMED || tp.kind == TP_DOLLAR) x.name = lower(o.name + field);
             if (tp.kind == TP_PARAM) {
                 std::string clean;
                 for (char c : field) if (isalnum((unsigned char)c)) clean += c;
@@ -560,10 +783,13 @@ int Plan::build_dissectors(const std::string& logformats, std::string& err) {
             fm->cleaned = apache_cleanup(fm->logformat);
             parse_token_def(*fm, apache_table());
         } else {
-            fm->logformat = f;
-            fm->cleaned = f;
-            device_ok_ = false;
-            why_ = "NGINX log_format not yet compiled for the device";
+            // NginxHttpdLogFormatDissector.setLogFormat (hp/NginxHttpdLogFormatDissector.java:75-92):
+            // the "combined" alias, no cleanup
+            fm->logformat = ieq(f, "combined") ? "$remote_addr - $remote_user [$time_local] \"$request\" $status "
+                                                 "$body_bytes_sent \"$http_referer\" \"$http_user_agent\""
+                                               : f;
+            fm->cleaned = fm->logformat;
+            parse_token_def(*fm, nginx_table());
         }
         for (const auto& o : fm->output_types)
             if (std::find(root->outs.begin(), root->outs.end(), o) == root->outs.end()) root->outs.push_back(o);
@@ -588,6 +814,35 @@ int Plan::build_dissectors(const std::string& logformats, std::string& err) {
     n2c->out_type = "BYTESCLF";
     n2c->outs = {"BYTESCLF:"};
     dis_.push_back(std::move(n2c));
+    // NginxHttpdLogFormatDissector.createAdditionalDissectors (hp/NginxHttpdLogFormatDissector.java:144-152)
+    // and UpstreamModule.getDissectors (nginxmodules/UpstreamModule.java:163-198)
+    bool any_nginx = false;
+    for (const auto& f : formats_) any_nginx |= f->kind == FMT_NGINX;
+    if (any_nginx) {
+        auto conv = [&](int cls, const char* in, const char* out) {
+            auto d = mkdis(cls, in);
+            d->out_type = out;
+            d->outs = {std::string(out) + ":"};
+            dis_.push_back(std::move(d));
+        };
+        conv(D_BINIP, "IP_BINARY", "IP");
+        conv(D_SECMILLIS, "SECOND_MILLIS", "MILLISECONDS");
+        conv(D_SECMILLIS, "TIME.EPOCH_SECOND_MILLIS", "TIME.EPOCH");
+        conv(D_MS2US, "MILLISECONDS", "MICROSECONDS");
+        auto up = [&](const char* in, const char* out) {
+            auto d = mkdis(D_UPSTREAM, in);
+            d->out_type = out;
+            for (int k = 0; k < 32; ++k) {  // UpstreamListDissector.getPossibleOutput (:127-135)
+                d->outs.push_back(std::string(out) + ":" + std::to_string(k) + ".value");
+                d->outs.push_back(std::string(out) + ":" + std::to_string(k) + ".redirected");
+            }
+            dis_.push_back(std::move(d));
+        };
+        up("UPSTREAM_ADDR_LIST", "UPSTREAM_ADDR");
+        up("UPSTREAM_BYTES_LIST", "BYTES");
+        up("UPSTREAM_SECOND_MILLIS_LIST", "SECOND_MILLIS");
+        up("UPSTREAM_STATUS_LIST", "UPSTREAM_STATUS");
+    }
     for (const auto& f : formats_)
         for (const auto& t : f->tokens)
             if (t.strftime) {
@@ -793,7 +1048,9 @@ void Plan::compile_program() {
         case EK_NUMBER: case EK_CLFNUMBER: case EK_NONZERO: e.det = (e.nlit && !dig0) || e.last; break;
         case EK_HEXNUMBER: case EK_CLFHEXNUMBER: e.det = (e.nlit && !hex0) || e.last; break;
         case EK_ANY_GREEDY: case EK_ANY_LAZY: e.det = e.last; break;
-        case EK_TIME_US: e.det = 1; break;
+        case EK_TIME_US: case EK_ANYCHAR: case EK_MSEC: e.det = 1; break;
+        case EK_DECIMAL: e.det = (e.nlit && !dig0) || e.last; break;
+        case EK_NOSPACE3: e.det = (e.nlit && ws0) || e.last; break;
         default: e.det = 0; break;
         }
     }
@@ -897,10 +1154,20 @@ void Plan::compile_program() {
                     }
                     break;
                 }
-                case D_CLF2NUM: case D_NUM2CLF:
+                case D_CLF2NUM: case D_NUM2CLF: case D_SECMILLIS: case D_MS2US:
+                    // value-level conversions, done in the replay from the token / list item
                     if (ok != O_TOKEN && ok != O_CONV) { device_ok_ = false; why_ = "converter on a derived value"; return; }
                     walk(O_CONV, oi, in.d->out_type, complete);
                     break;
+                case D_UPSTREAM: {
+                    // the list token's element kind (EK_UPLIST_*) proves the list
+                    // splits into clean items; the split is done in the replay
+                    if (ok != O_TOKEN) { device_ok_ = false; why_ = "upstream list from a derived value"; return; }
+                    for (int k = 0; k < 32; ++k)
+                        for (const char* sfx : {".value", ".redirected"})
+                            walk(O_CONV, oi, in.d->out_type, complete + "." + std::to_string(k) + sfx);
+                    break;
+                }
                 default:
                     device_ok_ = false;
                     why_ = "dissector for input type " + in.d->in_type + " not on the device";
@@ -1124,6 +1391,57 @@ void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const 
         set_origin(O_CONV, oi);
         if (v.null || dash) emit(c, name, in.d->out_type, "", mlong(0));
         else emit(c, name, in.d->out_type, "", v);
+        return;
+    }
+    case D_SECMILLIS: {
+        // ConvertSecondsWithMillisStringDissector (translate/ConvertSecondsWithMillisStringDissector.java:33-40):
+        // "S.F" -> S * 1000 + Long.parseLong(F); the token / list item kinds
+        // guarantee digits '.' digits of at most 18 digits each
+        uint32_t d = 0;
+        while (d < v.len && v.p[d] != '.') ++d;
+        int64_t sec = 0, ms = 0;
+        for (uint32_t k = 0; k < d; ++k) sec = sec * 10 + (v.p[k] - '0');
+        for (uint32_t k = d + 1; k < v.len; ++k) ms = ms * 10 + (v.p[k] - '0');
+        set_origin(O_CONV, oi);
+        emit(c, name, in.d->out_type, "", mlong((int64_t)((uint64_t)sec * 1000u + (uint64_t)ms)));
+        return;
+    }
+    case D_MS2US: {
+        // ConvertMillisecondsIntoMicroseconds (translate/ConvertMillisecondsIntoMicroseconds.java:33-35)
+        set_origin(O_CONV, oi);
+        emit(c, name, in.d->out_type, "", mlong((int64_t)((uint64_t)v.l * 1000u)));
+        return;
+    }
+    case D_UPSTREAM: {
+        // UpstreamListDissector.dissect (nginxmodules/UpstreamListDissector.java:79-125): split(", "),
+        // each split(": "), trimmed.  EK_UPLIST_* accepted only lists whose ','
+        // and ':' are all followed by ' ', so every piece is a clean item.
+        if (v.null) return;
+        auto trim = [](const uint8_t* p, uint32_t n) {
+            uint32_t a = 0, b = n;
+            while (a < b && p[a] <= ' ') ++a;
+            while (b > a && p[b - 1] <= ' ') --b;
+            return mstr(p + a, b - a);
+        };
+        uint32_t s0 = 0;
+        int k = 0;
+        for (uint32_t q = 0; q <= v.len; ++q) {
+            if (q < v.len && !(v.p[q] == ',' && q + 1 < v.len && v.p[q + 1] == ' ')) continue;
+            const uint8_t* sp = v.p + s0;
+            const uint32_t sn = q - s0;
+            uint32_t colon = sn;
+            for (uint32_t r = 0; r + 1 < sn; ++r)
+                if (sp[r] == ':' && sp[r + 1] == ' ') { colon = r; break; }
+            MVal orig = trim(sp, colon);
+            MVal redir = colon < sn ? trim(sp + colon + 2, sn - colon - 2) : orig;
+            set_origin(O_CONV, oi);
+            emit(c, name, in.d->out_type, std::to_string(k) + ".value", orig);
+            set_origin(O_CONV, oi);
+            emit(c, name, in.d->out_type, std::to_string(k) + ".redirected", redir);
+            ++k;
+            s0 = q + 2;
+            ++q;
+        }
         return;
     }
     case D_NUM2CLF: {

@@ -42,7 +42,8 @@ struct Format {
 
 enum DisClass {
     D_ROOT, D_TIMESTAMP, D_TIMESTAMP_ISO, D_FIRSTLINE, D_PROTOCOL, D_URI, D_QUERY, D_COOKIES, D_SETCOOKIES,
-    D_SETCOOKIE, D_UNIQUEID, D_CLF2NUM, D_NUM2CLF, D_STRFTIME, D_LOCALIZED
+    D_SETCOOKIE, D_UNIQUEID, D_CLF2NUM, D_NUM2CLF, D_STRFTIME, D_LOCALIZED,
+    D_BINIP, D_SECMILLIS, D_MS2US, D_UPSTREAM  // NGINX additional dissectors
 };
 
 struct Dissector {

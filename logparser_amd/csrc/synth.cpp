@@ -1,5 +1,5 @@
-// Deterministic synthetic Apache 'combined' access-log generator for
-// BASELINE.json config 2: every line i is a pure function
+// Deterministic synthetic access-log generators for BASELINE.json configs
+// 2, 3 and 4: every line i is a pure function
 // of (seed, i), so any range of lines can be generated independently (and in
 // parallel) and re-generated bit-identically for parity checks.
 #include <cstdint>
@@ -116,49 +116,46 @@ void path(Out& o, Rng& r) {
     }
 }
 
-void one_line(Out& o, uint64_t seed, int64_t i) {
-    Rng r(seed * 0x2545F4914F6CDD1Dull ^ (uint64_t)i * 0x9E3779B97F4A7C15ull);
-    r.next();
-    // %h
-    if (r.pct(5)) hostname(o, r);
-    else {
-        for (int k = 0; k < 4; ++k) {
-            if (k) o.c('.');
-            o.u(r.below(256));
-        }
+struct Civil { int d, m; int64_t y; };
+
+// uniform day in 2010-01-01 .. 2025-12-31 (days_from_civil inverse)
+Civil civil_day(Rng& r) {
+    uint64_t days = r.below(5844);
+    int64_t z = 14610 + (int64_t)days + 719468;  // 2010-01-01 = day 14610
+    int64_t era = z / 146097, doe = z - era * 146097;
+    int64_t yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
+    int64_t doy = doe - (365 * yoe + yoe / 4 - yoe / 100), mp = (5 * doy + 2) / 153;
+    Civil c;
+    c.d = (int)(doy - (153 * mp + 2) / 5 + 1);
+    c.m = (int)(mp < 10 ? mp + 3 : mp - 9);
+    c.y = yoe + era * 400 + (c.m <= 2);
+    return c;
+}
+
+void ipv4(Out& o, Rng& r) {
+    for (int k = 0; k < 4; ++k) {
+        if (k) o.c('.');
+        o.u(r.below(256));
     }
-    o.c(' ');
-    // %l
-    if (r.pct(99)) o.c('-'); else o.u(1 + r.below(65535));
-    o.c(' ');
-    // %u
-    if (r.pct(90)) o.c('-'); else word(o, r, ALNUM, 26, 3, 10);
-    // [%t] uniform 2010-01-01 .. 2025-12-31
-    o.s(" [");
-    {
-        uint64_t days = r.below(5844);  // days in 2010..2025
-        int64_t z = 14610 + (int64_t)days + 719468;  // 2010-01-01 = day 14610
-        int64_t era = z / 146097, doe = z - era * 146097;
-        int64_t yoe = (doe - doe / 1460 + doe / 36524 - doe / 146096) / 365;
-        int64_t doy = doe - (365 * yoe + yoe / 4 - yoe / 100), mp = (5 * doy + 2) / 153;
-        int d = (int)(doy - (153 * mp + 2) / 5 + 1), m = (int)(mp < 10 ? mp + 3 : mp - 9);
-        int64_t y = yoe + era * 400 + (m <= 2);
-        o.u(d, 2);
-        o.c('/');
-        o.s(MONTHS[m - 1]);
-        o.c('/');
-        o.u((uint64_t)y, 4);
-        o.c(':');
-        o.u(r.below(24), 2);
-        o.c(':');
-        o.u(r.below(60), 2);
-        o.c(':');
-        o.u(r.below(60), 2);
-        o.c(' ');
-        o.s(OFFSETS[r.below(7)]);
-    }
-    o.s("] \"");
-    // %r
+}
+
+// dd/MMM/yyyy:HH:mm:ss (sep = ':' for %t, ' ' for strftime %d/%b/%Y %T)
+void stamp(Out& o, Rng& r, char sep, const char* month_override = nullptr, bool day00 = false) {
+    Civil c = civil_day(r);
+    o.u(day00 ? 0 : c.d, 2);
+    o.c('/');
+    o.s(month_override ? month_override : MONTHS[c.m - 1]);
+    o.c('/');
+    o.u((uint64_t)c.y, 4);
+    o.c(sep);
+    o.u(r.below(24), 2);
+    o.c(':');
+    o.u(r.below(60), 2);
+    o.c(':');
+    o.u(r.below(60), 2);
+}
+
+void request(Out& o, Rng& r) {
     uint32_t mth = r.below(100);
     static const char* OTHER[] = {"HEAD", "PUT", "DELETE", "OPTIONS", "HEAD"};
     o.s(mth < 80 ? "GET" : mth < 95 ? "POST" : OTHER[r.below(5)]);
@@ -167,12 +164,9 @@ void one_line(Out& o, uint64_t seed, int64_t i) {
     if (r.pct(35)) query(o, r);
     uint32_t pv = r.below(3);
     o.s(pv == 0 ? " HTTP/1.0" : pv == 1 ? " HTTP/1.1" : " HTTP/2.0");
-    o.s("\" ");
-    o.u(STATUS[r.below(12)]);
-    o.c(' ');
-    if (r.pct(95)) o.u(r.below(200000)); else o.c('-');
-    o.s(" \"");
-    // referer
+}
+
+void referer(Out& o, Rng& r) {
     if (r.pct(40)) o.c('-');
     else {
         o.s(r.pct(50) ? "https://" : "http://");
@@ -180,22 +174,146 @@ void one_line(Out& o, uint64_t seed, int64_t i) {
         path(o, r);
         if (r.pct(30)) query(o, r);
     }
+}
+
+// %h %l %u: host, logname, user
+void who(Out& o, Rng& r) {
+    if (r.pct(5)) hostname(o, r); else ipv4(o, r);
+    o.c(' ');
+    if (r.pct(99)) o.c('-'); else o.u(1 + r.below(65535));
+    o.c(' ');
+    if (r.pct(90)) o.c('-'); else word(o, r, ALNUM, 26, 3, 10);
+}
+
+Rng line_rng(uint64_t seed, int64_t i) {
+    Rng r(seed * 0x2545F4914F6CDD1Dull ^ (uint64_t)i * 0x9E3779B97F4A7C15ull);
+    r.next();
+    return r;
+}
+
+// config 2: Apache 'combined'
+void combined_line(Out& o, uint64_t seed, int64_t i) {
+    Rng r = line_rng(seed, i);
+    who(o, r);
+    o.s(" [");
+    stamp(o, r, ':');
+    o.c(' ');
+    o.s(OFFSETS[r.below(7)]);
+    o.s("] \"");
+    request(o, r);
+    o.s("\" ");
+    o.u(STATUS[r.below(12)]);
+    o.c(' ');
+    if (r.pct(95)) o.u(r.below(200000)); else o.c('-');
+    o.s(" \"");
+    referer(o, r);
     o.s("\" \"");
     o.s(user_agent(r.below(50)));
     o.s("\"\n");
 }
 
+// config 3: '%h %l %u [%{%d/%b/%Y %T}t.%{msec_frac}t] "%r" %>s %b
+// "%{Referer}i" "%{User-Agent}i" %I %O' with 5 % malformed lines, uniform over
+// {truncated, missing closing quote, month Foo, day 00, non-numeric %b,
+// extra field}
+void strftime_line(Out& o, uint64_t seed, int64_t i) {
+    Rng r = line_rng(seed, i);
+    const size_t start = o.n;
+    const int bad = r.pct(5) ? 1 + (int)r.below(6) : 0;
+    who(o, r);
+    o.s(" [");
+    stamp(o, r, ' ', bad == 3 ? "Foo" : nullptr, bad == 4);
+    o.c('.');
+    o.u(r.below(1000), 3);
+    o.s("] \"");
+    request(o, r);
+    o.s(bad == 2 ? " " : "\" ");
+    o.u(STATUS[r.below(12)]);
+    o.c(' ');
+    if (bad == 5) o.s("12x");
+    else if (r.pct(95)) o.u(r.below(200000));
+    else o.c('-');
+    o.s(" \"");
+    referer(o, r);
+    o.s("\" \"");
+    o.s(user_agent(r.below(50)));
+    o.s("\" ");
+    o.u(200 + r.below(4000));
+    o.c(' ');
+    o.u(200 + r.below(200000));
+    if (bad == 6) o.s(" extra");
+    if (bad == 1 && o.ok) o.n = start + 1 + (o.n - start - 1) * (20 + r.below(70)) / 100;  // truncated
+    o.c('\n');
+}
+
+// config 4: NGINX log_format of hpt/nginxmodules/NginxUpstreamTest.java:94
+// '$remote_addr - $remote_user [$time_local] "$request" $status
+// $body_bytes_sent "$http_referer" "$http_user_agent" "$http_x_forwarded_for"
+// $request_time $upstream_response_time $pipe'
+void nginx_line(Out& o, uint64_t seed, int64_t i) {
+    Rng r = line_rng(seed, i);
+    ipv4(o, r);
+    o.s(" - ");
+    if (r.pct(90)) o.c('-'); else word(o, r, ALNUM, 26, 3, 10);
+    o.s(" [");
+    stamp(o, r, ':');
+    o.c(' ');
+    o.s(OFFSETS[r.below(7)]);
+    o.s("] \"");
+    request(o, r);
+    o.s("\" ");
+    o.u(STATUS[r.below(12)]);
+    o.c(' ');
+    o.u(r.below(200000));
+    o.s(" \"");
+    referer(o, r);
+    o.s("\" \"");
+    o.s(user_agent(r.below(50)));
+    o.s("\" \"");
+    if (r.pct(70)) o.c('-');
+    else {
+        ipv4(o, r);
+        if (r.pct(30)) { o.s(", "); ipv4(o, r); }
+    }
+    o.s("\" ");
+    auto secs = [&]() { o.u(r.below(r.pct(90) ? 2 : 100)); o.c('.'); o.u(r.below(1000), 3); };
+    secs();
+    o.c(' ');
+    secs();
+    if (r.pct(10)) {  // 2-3 upstreams: "X, X" or "X, X : X" (UpstreamModule.upstreamListOf)
+        o.s(", ");
+        secs();
+        if (r.pct(50)) {
+            o.s(r.pct(50) ? ", " : " : ");
+            secs();
+        }
+    }
+    o.c(' ');
+    o.c(r.pct(20) ? 'p' : '.');
+    o.c('\n');
+}
+
 }  // namespace
 
-extern "C" int64_t lp_synth_combined(uint64_t seed, int64_t first_line, int64_t max_lines, char* out, size_t cap,
-                                     int64_t* n_lines) {
+extern "C" int64_t lp_synth(int workload, uint64_t seed, int64_t first_line, int64_t max_lines, char* out,
+                            size_t cap, int64_t* n_lines) {
+    void (*gen)(Out&, uint64_t, int64_t) = workload == LP_SYNTH_COMBINED   ? combined_line
+                                           : workload == LP_SYNTH_STRFTIME ? strftime_line
+                                           : workload == LP_SYNTH_NGINX    ? nginx_line
+                                                                           : nullptr;
+    if (!gen) return LP_E_INVALID;
     Out o{out, 0, cap};
     int64_t k = 0;
     for (; k < max_lines; ++k) {
         size_t mark = o.n;
-        one_line(o, seed, first_line + k);
+        gen(o, seed, first_line + k);
         if (!o.ok) { o.n = mark; break; }
     }
     if (n_lines) *n_lines = k;
     return (int64_t)o.n;
+}
+
+extern "C" int64_t lp_synth_combined(uint64_t seed, int64_t first_line, int64_t max_lines, char* out, size_t cap,
+                                     int64_t* n_lines) {
+    return lp_synth(LP_SYNTH_COMBINED, seed, first_line, max_lines, out, cap, n_lines);
 }

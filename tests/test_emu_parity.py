@@ -157,3 +157,60 @@ def test_lines_in_batch_context_emulated(oracle, emu, vectors, demolog_lines):
             assert len(got) == len(lines)
             for l, (st, js) in zip(lines, got):
                 assert (st, js) == e.parse_raw(l), (fmt, l)
+
+
+NGINX = lpa.SYNTH_FORMATS[lpa.SYNTH_NGINX]
+
+
+def mutate_nginx(rng, line):
+    """Config-4 corner cases: upstream lists (UpstreamModule.upstreamListOf),
+    SECOND_MILLIS values, the strict 3-part $request, $pipe."""
+    ops = [
+        lambda l: l.replace(b" .", b" p", 1),
+        lambda l: l[:-1] + b"..",                                     # $pipe is one char
+        lambda l: l.replace(b" HTTP/", b" x HTTP/", 1),               # 4-part request: no match
+        lambda l: l.replace(b'"GET ', b'"GET  ', 1),
+        lambda l: l.rsplit(b" ", 2)[0] + b" 0.002, 0.003 : 0.004 .",
+        lambda l: l.rsplit(b" ", 2)[0] + b" 0.002 , 0.003 .",
+        lambda l: l.rsplit(b" ", 2)[0] + b" 0.002,0.003 .",           # not split by ', ': FALLBACK
+        lambda l: l.rsplit(b" ", 2)[0] + b" 0.002 : 0.003 .",
+        lambda l: l.rsplit(b" ", 2)[0] + b" - .",                     # '-' is not a SECOND_MILLIS
+        lambda l: l.rsplit(b" ", 2)[0] + b" 12345678901234567890.1 .",
+        lambda l: l.rsplit(b" ", 2)[0] + b" 1.5 .",
+        lambda l: l.rsplit(b" ", 3)[0] + b" 7 0.1 .",
+        lambda l: l.rsplit(b" ", 3)[0] + b" 000.000100 0.1 .",
+        lambda l: l.replace(b'"-" ', b'"1.2.3.4, 5.6.7.8" ', 1),
+        lambda l: l.replace(b" - - [", b" - user name [", 1),
+        lambda l: l.replace(b" - - [", b" - \"q\" [", 1),
+        lambda l: l.replace(b'" 200 ', b'" 200 -', 1),
+        lambda l: b"::1" + l[l.index(b" "):],
+        lambda l: b"-" + l[l.index(b" "):],
+        lambda l: l,
+    ]
+    return rng.choice(ops)(line)
+
+
+def test_nginx_config4_emulated(oracle, emu):
+    paths = oracle.possible_paths(NGINX)
+    o = oracle.Oracle(NGINX, paths)
+    e = emu.Emu(NGINX, paths)
+    assert e.status == 0, e.err
+    lines = lpa.synth(lpa.SYNTH_NGINX, 20261017, 0, 4000).split(b"\n")[:-1]
+    assert compare(o, e, lines, allow_fallback=False)["ok"] == 4000
+    rng = random.Random(77)
+    mut = [mutate_nginx(rng, l) for l in lines[:2000]] + [mutate(rng, l) for l in lines[2000:]]
+    s = compare(o, e, mut)
+    assert s["bad"] > 50 and s["ok"] > 500, s
+
+
+def test_nginx_combined_format_emulated(oracle, emu):
+    """The NGINX 'combined' log_format (hp/NginxHttpdLogFormatDissector.java:82-90)
+    written out, on config-4 lines cut after the user agent."""
+    lines = lpa.synth(lpa.SYNTH_NGINX, 5, 0, 300).split(b"\n")[:-1]
+    ng = "$remote_addr - $remote_user [$time_local] \"$request\" $status $body_bytes_sent \"$http_referer\" \"$http_user_agent\""
+    paths = oracle.possible_paths(ng)
+    o = oracle.Oracle(ng, paths)
+    e = emu.Emu(ng, paths)
+    assert e.status == 0, e.err
+    s = compare(o, e, [l.rsplit(b' "', 1)[0] for l in lines])
+    assert s["ok"] > 250, s

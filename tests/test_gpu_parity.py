@@ -185,3 +185,17 @@ def test_offsets_beyond_4gb(oracle, staged, monkeypatch):
         assert s1 == 0 and js == r.record_json(i), i
     del dev
     torch.cuda.empty_cache()
+
+
+def test_nginx_config4_gpu(oracle):
+    """BASELINE config 4: the NGINX log_format of NginxUpstreamTest.java:94,
+    all possible paths (upstream lists, SECOND_MILLIS -> ms / us, query)."""
+    from test_emu_parity import NGINX, mutate, mutate_nginx
+    fields = paths(oracle, NGINX)
+    lines = lpa.synth(lpa.SYNTH_NGINX, 20261017, 0, 20000).split(b"\n")[:-1]
+    s, _ = gpu_vs_oracle(oracle, NGINX, fields, lines, allow_fallback=False)
+    assert s["ok"] == 20000
+    rng = random.Random(78)
+    mut = [mutate_nginx(rng, l) for l in lines[:3000]] + [mutate(rng, l) for l in lines[3000:6000]]
+    s, _ = gpu_vs_oracle(oracle, NGINX, fields, mut)
+    assert s["bad"] > 100 and s["ok"] > 1000, s
