@@ -13,6 +13,8 @@
 // scaffolding around it.
 #include <hip/hip_runtime.h>
 
+#define LP_KERNEL_TU 1  // device column pointers are global-memory pointers (lp_program.h)
+
 #include <cstdlib>
 
 #include "kernels.h"
@@ -230,9 +232,9 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
                 const unsigned long long oab = __shfl(my_ab, own);
                 const auto OL = owner_line(L, own);
                 if (g < total) {
-                    uint8_t* region = C.arena + oab;
-                    const uint32_t so = reinterpret_cast<const uint32_t*>(region + olist)[g - ob];
-                    uint64_t* slot = reinterpret_cast<uint64_t*>(region + so);
+                    LP_G uint8_t* region = C.arena + oab;
+                    const uint32_t so = reinterpret_cast<const LP_G uint32_t*>(region + olist)[g - ob];
+                    LP_G uint64_t* slot = reinterpret_cast<LP_G uint64_t*>(region + so);
                     const uint64_t a0 = slot[0];
                     const uint32_t reserved = 3u * (uint32_t)(((a0 >> 16) & 0xFFFFu) - (a0 & 0xFFFFu));
                     const uint32_t used = query_piece(P, P.query[qs], OL, region, slot);
@@ -294,22 +296,35 @@ __global__ __launch_bounds__(PW) void k_parse_lines(const uint8_t* __restrict__ 
         const int nv = (int)((w1 - w0 + 15) >> 4);
         const int nv4 = (nv + 3) & ~3;  // whole 64-bit mask words
         uint32_t bad = 0;  // guard-failing bytes other than '\n' anywhere in the window
-        for (int k = lane; k < nv4; k += PW) {
-            const uint64_t p = w0 + 16ull * k;
-            u32x4 v = u32x4{0, 0, 0, 0};
-            if (k < nv) {
-                if (p + 16 <= nbytes) {
-                    v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(buf + p));
-                } else {
-                    for (int j = 0; j < 16 && p + j < nbytes; ++j) v[j >> 2] |= (uint32_t)buf[p + j] << (8 * (j & 3));
-                }
-                for (int j = 0; j < 4; ++j) bad |= swar::guard_bad(v[j]) & ~swar::eq(v[j], '\n');
+        // SB loads in flight per lane before the first LDS store (one HBM
+        // round trip per SB x 1 KiB of window instead of one per 1 KiB)
+        constexpr int SB = 8;
+        const uint64_t full_end = nbytes & ~15ull;  // 16-byte pieces wholly inside the buffer
+        for (int k0 = lane; k0 < nv4; k0 += SB * PW) {
+            u32x4 v[SB];
+#pragma unroll
+            for (int j = 0; j < SB; ++j) {
+                const int k = k0 + j * PW;
+                const uint64_t p = w0 + 16ull * k;
+                v[j] = u32x4{0, 0, 0, 0};
+                if (k < nv && p + 16 <= full_end) v[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(buf + p));
             }
-            *reinterpret_cast<u32x4*>(win + 16 * k) = v;
-            uint32_t m0, m1;
-            bcls::classify16(v[0], v[1], v[2], v[3], m0, m1);
-            msk16[4 * mwords * MC_QUOTE + k] = (uint16_t)m0;
-            msk16[4 * mwords * MC_UEV + k] = (uint16_t)m1;
+#pragma unroll
+            for (int j = 0; j < SB; ++j) {
+                const int k = k0 + j * PW;
+                if (k >= nv4) break;
+                const uint64_t p = w0 + 16ull * k;
+                if (k < nv && p + 16 > full_end) {  // the buffer's last partial piece
+                    for (int b = 0; b < 16 && p + b < nbytes; ++b) v[j][b >> 2] |= (uint32_t)buf[p + b] << (8 * (b & 3));
+                }
+                if (k < nv)
+                    for (int w = 0; w < 4; ++w) bad |= swar::guard_bad(v[j][w]) & ~swar::eq(v[j][w], '\n');
+                *reinterpret_cast<u32x4*>(win + 16 * k) = v[j];
+                uint32_t m0, m1;
+                bcls::classify16(v[j][0], v[j][1], v[j][2], v[j][3], m0, m1);
+                msk16[4 * mwords * MC_QUOTE + k] = (uint16_t)m0;
+                msk16[4 * mwords * MC_UEV + k] = (uint16_t)m1;
+            }
         }
         const bool clean = !__any(bad != 0);
         __syncthreads();
@@ -320,9 +335,9 @@ __global__ __launch_bounds__(PW) void k_parse_lines(const uint8_t* __restrict__ 
         __syncthreads();
         // base = the line start aligned down to 4 bytes: word reads never
         // leave the 4-byte words holding the line's bytes
-        const uint8_t* ls = buf + s;
+        const LP_G uint8_t* ls = (const LP_G uint8_t*)(buf) + s;
         const uint32_t mis = (uint32_t)((uintptr_t)ls & 3);
-        const LineT<const uint8_t*> L{ls - mis, mis, n};
+        const LineT<const LP_G uint8_t*> L{ls - mis, mis, n};
         parse_wave(P, s_elems, C, L, active, li, stk, false);
     }
 }

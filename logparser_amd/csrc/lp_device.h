@@ -36,6 +36,10 @@ __device__ __forceinline__ void lp_prof_mark(int k) {
 #else
 #define LP_PROF(k)
 #endif
+// profiling experiments only (tools/build_exp.sh): 0 = the product
+#ifndef LP_EXP
+#define LP_EXP 0
+#endif
 
 // ----------------------------------------------------------- byte classes
 __host__ __device__ LP_INLINE bool is_ws(uint32_t c) { return c == ' ' || (c >= 9 && c <= 13); }      // \s
@@ -73,6 +77,11 @@ __host__ __device__ LP_INLINE uint32_t load_word(const uint8_t* p) {
 typedef const __attribute__((address_space(3))) uint8_t* lds_bytes;
 typedef const __attribute__((address_space(3))) uint32_t* lds_words;
 __device__ LP_INLINE uint32_t load_word(lds_bytes p) { return *(lds_words)p; }
+#endif
+#if defined(__HIP_DEVICE_COMPILE__) && defined(LP_KERNEL_TU)
+__device__ LP_INLINE uint32_t load_word(const LP_G uint8_t* p) {
+    return *reinterpret_cast<const LP_G uint32_t*>(__builtin_assume_aligned(p, 4));
+}
 #endif
 
 // ---- byte-class bitmasks (1 bit per byte, one 64-bit word per 64 bytes),
@@ -352,6 +361,45 @@ __host__ __device__ LP_INLINE bool for_uev(const LN& L, int a, int b, F&& f) {
         }
     }
     return true;
+}
+
+// for_uev with the event's byte and the two after it: f(q, w), w = the 4
+// bytes at q (little-endian, bytes past the line's last word read as 0).
+template <typename LN, typename F>
+__host__ __device__ LP_INLINE bool for_uev_w(const LN& L, int a, int b, F&& f) {
+    if (a >= b) return true;
+    const uint32_t A = L.o + (uint32_t)a, E = L.o + (uint32_t)b;
+    if constexpr (LN::has_masks) {
+        const uint32_t W1 = (E - 1) >> 6;
+        const uint64_t last = ~0ull >> (63 - ((E - 1) & 63));
+        uint32_t W = A >> 6;
+        uint64_t m = L.mask(MC_UEV, W) & (~0ull << (A & 63));
+        if (W == W1) m &= last;
+        auto next = [&](int& q) {
+            while (!m) {
+                if (++W > W1) return false;
+                m = L.mask(MC_UEV, W);
+                if (W == W1) m &= last;
+            }
+            q = (int)((W << 6) + (uint32_t)ctz64(m) - L.o);
+            m &= m - 1;
+            return true;
+        };
+        int q;
+        if (!next(q)) return true;
+        uint32_t w = load_u32_at(L, q);
+        for (;;) {
+            int q2 = 0;
+            const bool more = next(q2);
+            const uint32_t w2 = more ? load_u32_at(L, q2) : 0u;
+            if (!f(q, w)) return false;
+            if (!more) return true;
+            q = q2;
+            w = w2;
+        }
+    } else {
+        return for_uev(L, a, b, [&](int q, uint32_t) { return f(q, load_u32_at(L, q)); });
+    }
 }
 
 // Number of URI event bytes in [a, b).
@@ -1145,7 +1193,7 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
 
 // ------------------------------------------------------------ URI stage
 struct Arena {
-    uint8_t* p;     // this line's region
+    LP_G uint8_t* p;  // this line's region
     uint32_t used;
     uint32_t cap;
     uint32_t slack = 0;  // reserved, never written
@@ -1242,7 +1290,8 @@ __host__ __device__ LP_INLINE int jdk_hostname(const LN& L, int a, int b) {
 }
 
 // strict UTF-8 validation of a decoded byte string
-__host__ __device__ LP_INLINE bool utf8_ok(const uint8_t* b, uint32_t n) {
+template <typename BP>
+__host__ __device__ LP_INLINE bool utf8_ok(BP b, uint32_t n) {
     for (uint32_t i = 0; i < n;) {
         uint32_t c = b[i];
         if (c < 0x80) { ++i; continue; }
@@ -1335,9 +1384,9 @@ struct QueryTable {
     uint32_t pf = 0;
     bool on = false, set = false;  // enumerating now / table laid out
     // piece [s, e) ends: finalize or leave pending
-    __host__ __device__ LP_INLINE void emit(const QueryStage& Q, uint8_t* region, int e) {
+    __host__ __device__ LP_INLINE void emit(const QueryStage& Q, LP_G uint8_t* region, int e) {
         if (e > s) {
-            uint64_t* t = (uint64_t*)(region + tab) + 2 * count;
+            LP_G uint64_t* t = (LP_G uint64_t*)(region + tab) + 2 * count;
             if (pf == 0 && Q.want_all) {
                 const int ne = eq >= 0 ? eq : e;
                 t[0] = mkref((uint32_t)s, (uint32_t)(ne - s), false);
@@ -1347,7 +1396,7 @@ struct QueryTable {
                        ((uint64_t)pf << 48);
                 t[1] = reg;
                 reg += 3 * (uint32_t)(e - s);
-                ((uint32_t*)(region + list))[npend++] = tab + 16 * count;
+                ((LP_G uint32_t*)(region + list))[npend++] = tab + 16 * count;
             }
             ++count;
         }
@@ -1362,8 +1411,8 @@ struct QueryTable {
 // region: the owning line's arena region; slot: its table slot.  Returns the
 // region bytes written.
 template <typename LN>
-__host__ __device__ LP_INLINE uint32_t query_piece(const Program& P, const QueryStage& Q, const LN& L, uint8_t* region,
-                                                   uint64_t* slot) {
+__host__ __device__ LP_INLINE uint32_t query_piece(const Program& P, const QueryStage& Q, const LN& L,
+                                                   LP_G uint8_t* region, LP_G uint64_t* slot) {
     const uint64_t a0 = slot[0], a1 = slot[1];
     const int s = (int)(a0 & 0xFFFFu), e = (int)((a0 >> 16) & 0xFFFFu), eq = (int)((a0 >> 32) & 0xFFFFu) - 1;
     const bool rw = (a0 >> 48) & QP_RW, pv = (a0 >> 48) & QP_PV;
@@ -1423,7 +1472,52 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
     // bit 1: the rawQuery is not "&" + the bytes between the first '&'/'?' and the '#'
     uint32_t rewr = 0;
     int st = ST_OK;
-    for_uev(L, a, b, [&](int q, uint32_t c) {
+    // Fast walk over the events before the first '#' or ';' (the common
+    // bytes % & ? = + A-Z and URIUtil-escaped ones, few branches); it stops
+    // at the first '#', ';' or invalid escape and the general walk below
+    // continues from there with the same state.
+    int resume = -1;
+    for_uev_w(L, a, b, [&](int q, uint32_t w) {
+        const uint32_t c = w & 0xFFu;
+        if (c == '#' || c == ';') { resume = q; return false; }
+        if (c == '%') {
+            if (q + 2 >= b || !is_hex((w >> 8) & 0xFFu) || !is_hex((w >> 16) & 0xFFu)) { resume = q; return false; }
+            first_pct = first_pct < 0 ? q : first_pct;
+            T.pf |= (T.on && T.eq >= 0) ? (uint32_t)QP_PV : 0u;
+            return true;
+        }
+        if (c == '&' || c == '?') {
+            rewr |= (c == '?' && fa >= 0) ? 2u : 0u;  // a later '?' becomes '&'
+            if (T.on) {
+                T.emit(P.query[qsi], A.p, q);
+                T.s = q + 1;
+            } else if (fa < 0 && qsi >= 0) {
+                T.on = T.set = true;
+                T.maxp = usep + 1;
+                T.tab = (A.used + 7) & ~7u;
+                T.list = T.tab + 16 * T.maxp;
+                T.reg = T.list + ((4 * T.maxp + 7) & ~7u);
+                T.s = q + 1;
+            }
+            fa = fa < 0 ? q : fa;
+            return true;
+        }
+        // = + A-Z and URIUtil-escaped bytes
+        rewr |= (fa >= 0 && uri_needs_encode(c)) ? 2u : 0u;
+        const bool on = T.on;
+        const bool noeq = T.eq < 0;
+        T.eq = (on && noeq && c == '=') ? q : T.eq;
+        T.pf |= (on && !noeq && c == '+') ? (uint32_t)QP_PV : 0u;
+        T.pf |= (on && noeq && c != '=' && c != '+') ? (uint32_t)QP_RW : 0u;
+        return true;
+    });
+#if LP_EXP == 2
+    if (0)
+#endif
+    if (resume >= 0) for_uev(L, resume, b, [&](int q, uint32_t c) {
+#if LP_EXP == 1
+        return true;
+#endif
         if (c == '%') {
             if (q + 2 >= b || !is_hex(L[q + 1]) || !is_hex(L[q + 2])) { st = ST_FALLBACK; return false; }  // BAD_EXCAPE_PATTERN
             if (first_pct < 0) first_pct = q;
@@ -1517,7 +1611,7 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
             scheme_ref = (int64_t)mkref(a, p - a, false);
             ++p;
             if (!(p < b && cur.at(p) == '/')) return ST_FALLBACK;                          // opaque URI
-            if (p + 1 < b && cur.at(p + 1) == '/') {
+            if (LP_EXP != 3 && p + 1 < b && cur.at(p + 1) == '/') {
                 // authority [as, ae): up to '/', '#' or the first '?'; only chars
                 // in both L_SERVER and L_REG_NAME of java.net.URI (no '@'
                 // userinfo, no escapes), else FALLBACK
@@ -1627,11 +1721,11 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
 // The pending query pieces of one line, one after the other (the test-only
 // CPU emulation; the kernel spreads them over the wave).
 template <typename LN>
-__host__ __device__ LP_INLINE void query_pieces_serial(const Program& P, const LN& L, const LineOut& o, uint8_t* region) {
+__host__ __device__ LP_INLINE void query_pieces_serial(const Program& P, const LN& L, const LineOut& o, LP_G uint8_t* region) {
     for (int qs = 0; qs < P.n_query; ++qs) {
-        const uint32_t* list = (const uint32_t*)(region + o.qlist.get(qs));
+        const LP_G uint32_t* list = (const LP_G uint32_t*)(region + o.qlist.get(qs));
         for (uint32_t k = 0; k < o.qpend.get(qs); ++k)
-            query_piece(P, P.query[qs], L, region, (uint64_t*)(region + list[k]));
+            query_piece(P, P.query[qs], L, region, (LP_G uint64_t*)(region + list[k]));
     }
 }
 

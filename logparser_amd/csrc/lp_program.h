@@ -175,32 +175,43 @@ enum : uint32_t {
 };
 
 // Output column set of one batch (device pointers).
+// Device pointers of the result columns and the arena are global-memory
+// pointers on the device (global_load/global_store: a FLAT store would also
+// count against lgkmcnt and stall the next LDS read of the same wave until
+// the store is acknowledged).  Host code (and other translation units) sees
+// plain pointers of the same size.
+#if defined(__HIP_DEVICE_COMPILE__) && defined(LP_KERNEL_TU)
+#define LP_G __attribute__((address_space(1)))
+#else
+#define LP_G
+#endif
+
 struct Columns {
-    uint8_t* status;          // [n]
-    const uint64_t* line_off; // [n+1]
-    uint32_t* tok_span[MAX_TOK];
-    uint32_t* tok_flags;      // bit k: value "-" (null); bit 16+k: value == "0"
-    int64_t* t_epoch[MAX_TIME];
-    uint64_t* t_local[MAX_TIME];
-    uint64_t* t_utc[MAX_TIME];
-    uint32_t* fl_kind[MAX_FL];
-    uint32_t* fl_method[MAX_FL];  // spans
-    uint32_t* fl_uri[MAX_FL];
-    uint32_t* fl_proto[MAX_FL];
-    uint32_t* u_flags[MAX_URI];
-    uint64_t* u_scheme[MAX_URI];
-    uint64_t* u_host[MAX_URI];
-    int32_t* u_port[MAX_URI];
-    uint64_t* u_path[MAX_URI];
-    uint64_t* u_query[MAX_URI];
-    uint64_t* u_frag[MAX_URI];
-    uint32_t* q_count[MAX_QUERY]; // params are (name ref, value ref) pairs in the arena
-    uint64_t* q_params[MAX_QUERY];// ref to the param table in the arena
-    uint64_t* arena_base;         // [n]
-    uint8_t* arena;
+    LP_G uint8_t* status;          // [n]
+    const LP_G uint64_t* line_off; // [n+1]
+    LP_G uint32_t* tok_span[MAX_TOK];
+    LP_G uint32_t* tok_flags;      // bit k: value "-" (null); bit 16+k: value == "0"
+    LP_G int64_t* t_epoch[MAX_TIME];
+    LP_G uint64_t* t_local[MAX_TIME];
+    LP_G uint64_t* t_utc[MAX_TIME];
+    LP_G uint32_t* fl_kind[MAX_FL];
+    LP_G uint32_t* fl_method[MAX_FL];  // spans
+    LP_G uint32_t* fl_uri[MAX_FL];
+    LP_G uint32_t* fl_proto[MAX_FL];
+    LP_G uint32_t* u_flags[MAX_URI];
+    LP_G uint64_t* u_scheme[MAX_URI];
+    LP_G uint64_t* u_host[MAX_URI];
+    LP_G int32_t* u_port[MAX_URI];
+    LP_G uint64_t* u_path[MAX_URI];
+    LP_G uint64_t* u_query[MAX_URI];
+    LP_G uint64_t* u_frag[MAX_URI];
+    LP_G uint32_t* q_count[MAX_QUERY]; // params are (name ref, value ref) pairs in the arena
+    LP_G uint64_t* q_params[MAX_QUERY];// ref to the param table in the arena
+    LP_G uint64_t* arena_base;         // [n]
+    LP_G uint8_t* arena;
     uint64_t arena_cap;
-    unsigned long long* arena_top;  // bump pointer
-    uint32_t* wave_counts;          // [n_waves][4] lines ok bad fallback (reduced after the launch)
+    LP_G unsigned long long* arena_top;  // bump pointer
+    LP_G uint32_t* wave_counts;          // [n_waves][4] lines ok bad fallback (reduced after the launch)
 };
 
 }  // namespace lp
