@@ -848,6 +848,7 @@ enum {
 typedef struct {
     int cls;
     char *in_type;
+    char *param;         /* D_STRFTIME: the strftime pattern */
     slist outs;          /* "TYPE:name" */
     char *out_type;      /* converters */
     /* root */
@@ -993,13 +994,96 @@ static instance *inst_new(dissector *d) {
     return in;
 }
 
+/* ---------------------------------------------------------- strftime
+ * StrfTimeToDateTimeFormatter (hp/dissectors/StrfTimeToDateTimeFormatter.java)
+ * restated for the subset of StrfTime.g4 whose DateTimeFormatter is a
+ * sequence of fixed-width fields: %d (DAY_OF_MONTH, 2), %m (MONTH_OF_YEAR,
+ * 2), %b / %h (MONTH_OF_YEAR short text, default locale en_US: Jan..Dec),
+ * %Y (YEAR, 4), %H (CLOCK_HOUR_OF_DAY, 2), %M (MINUTE_OF_HOUR, 2), %S
+ * (SECOND_OF_MINUTE, 2), %T (= HOUR_OF_DAY:%M:%S, :360-368), %F (= %Y-%m-%d),
+ * %z (appendOffset("+HHMM","+0000")), [%]msec_frac (MILLI_OF_SECOND, 3),
+ * [%]usec_frac (MICRO_OF_SECOND, 6), %% %t %n and literal text; the E / O
+ * modifiers are ignored (StrfTime.g4 MOD).  Patterns with any other
+ * conversion, a field given twice, or without all of day, month, year, hour,
+ * minute and second are outside the subset (ORC_UNSUPPORTED).  No %z: the
+ * formatter is withZone(UTC) (:97-105). */
+enum { SF_LIT, SF_DAY, SF_MON, SF_MONTXT, SF_YEAR, SF_CLOCKH, SF_HOD, SF_MIN, SF_SEC, SF_MSEC, SF_USEC, SF_OFF };
+typedef struct { unsigned char op, off, ch; } strf_op;
+typedef struct { strf_op ops[64]; int nops, width, zone; } strf_prog;
+
+static int strf_add(strf_prog *sp, int op, int w, int ch) {
+    if (sp->nops >= 64 || sp->width + w > 200) return 0;
+    sp->ops[sp->nops].op = (unsigned char)op;
+    sp->ops[sp->nops].off = (unsigned char)sp->width;
+    sp->ops[sp->nops].ch = (unsigned char)ch;
+    sp->nops++;
+    sp->width += w;
+    return 1;
+}
+
+static int strf_compile(const char *f, strf_prog *sp) {
+    memset(sp, 0, sizeof *sp);
+    int seen[16] = {0};
+    size_t n = strlen(f);
+#define SF(op, w) do { if (seen[op]++ || !strf_add(sp, op, w, 0)) return 0; } while (0)
+#define SL(c) do { if (!strf_add(sp, SF_LIT, 1, (c))) return 0; } while (0)
+    for (size_t i = 0; i < n;) {
+        /* MsecFrac / UsecFrac : '%'? 'msec_frac' (longest match wins over LITERAL) */
+        size_t j = i + (f[i] == '%');
+        if (n - j >= 9 && (!strncmp(f + j, "msec_frac", 9) || !strncmp(f + j, "usec_frac", 9))) {
+            if (f[j] == 'm') SF(SF_MSEC, 3); else SF(SF_USEC, 6);
+            i = j + 9;
+            continue;
+        }
+        if (f[i] != '%') { SL((unsigned char)f[i]); i++; continue; }
+        if (i + 1 >= n) return 0;
+        char c = f[i + 1];
+        if (c == '%') { SL('%'); i += 2; continue; }
+        if (c == 't') { SL('\t'); i += 2; continue; }
+        if (c == 'n') { SL('\n'); i += 2; continue; }
+        size_t k = i + 1;
+        if (c == 'E' || c == 'O') { if (i + 2 >= n) return 0; c = f[i + 2]; k++; }
+        switch (c) {
+        case 'd': SF(SF_DAY, 2); break;
+        case 'm': SF(SF_MON, 2); break;
+        case 'b': case 'h': SF(SF_MONTXT, 3); break;
+        case 'Y': SF(SF_YEAR, 4); break;
+        case 'H': SF(SF_CLOCKH, 2); break;
+        case 'M': SF(SF_MIN, 2); break;
+        case 'S': SF(SF_SEC, 2); break;
+        case 'T': SF(SF_HOD, 2); SL(':'); SF(SF_MIN, 2); SL(':'); SF(SF_SEC, 2); break;
+        case 'F': SF(SF_YEAR, 4); SL('-'); SF(SF_MON, 2); SL('-'); SF(SF_DAY, 2); break;
+        case 'z': SF(SF_OFF, 5); sp->zone = 1; break;
+        default: return 0;
+        }
+        i = k + 1;
+    }
+#undef SF
+#undef SL
+    if (!seen[SF_DAY] || !(seen[SF_MON] + seen[SF_MONTXT]) || !seen[SF_YEAR]) return 0;
+    if (seen[SF_MON] && seen[SF_MONTXT]) return 0;
+    if (seen[SF_CLOCKH] + seen[SF_HOD] != 1 || !seen[SF_MIN] || !seen[SF_SEC]) return 0;
+    if (seen[SF_MSEC] && seen[SF_USEC]) return 0;
+    return 1;
+}
+
 static void inst_prepare(orc_parser *p, instance *in, const char *subroot, const char *check) {
     char *name = extract_field_name(subroot, check);
     sl_add_unique(&in->requested, name);
     if (in->d->cls == D_ROOT)
         for (int i = 0; i < in->nfmts; i++) fmt_prepare_for_dissect(in->fmts[i], check);
     switch (in->d->cls) {
-    case D_TIMESTAMP_ISO: case D_STRFTIME: case D_LOCALIZED: case D_COOKIES: case D_SETCOOKIES:
+    case D_STRFTIME: {
+        strf_prog sp;
+        if (!strf_compile(in->d->param, &sp) && !p->unsupported) {
+            p->unsupported = 1;
+            snprintf(p->unsupported_why, sizeof p->unsupported_why, "strftime pattern outside the restated subset: %s",
+                     in->d->param);
+        }
+        break;
+    }
+    case D_LOCALIZED: break;
+    case D_TIMESTAMP_ISO: case D_COOKIES: case D_SETCOOKIES:
     case D_SETCOOKIE: case D_UNIQUEID:
         if (!p->unsupported) {
             p->unsupported = 1;
@@ -1161,7 +1245,8 @@ static int build_dissectors(orc_parser *p, const char *logformat, char *err, int
         fmtd *f = root->fmts[i];
         for (int k = 0; k < f->ntokens; k++) {
             if (f->tokens[k].custom == CUSTOM_STRFTIME && nd < 60) {
-                p->dis[nd++] = dis_new(D_STRFTIME, f->tokens[k].custom_type);
+                p->dis[nd] = dis_new(D_STRFTIME, f->tokens[k].custom_type);
+                p->dis[nd++]->param = xstrdup(f->tokens[k].custom_param);
                 p->dis[nd++] = dis_new(D_LOCALIZED, f->tokens[k].custom_type);
             }
         }
@@ -1433,19 +1518,140 @@ static js fmt2(parsable *ps, const char *f, int64_t a, int b, int c) {
     return js_lit(ps->a, buf);
 }
 
+/* DateTimeFormatter.parse(text, ZonedDateTime::from) with the program above,
+ * parseCaseInsensitive, ResolverStyle.SMART (JDK 8 Parsed.resolveDate /
+ * resolveTimeFields / resolveTime, ZoneOffset.ofTotalSeconds).  Returns 0 ok
+ * (local date-time as parsed, nanos, offset seconds), 1 failure. */
+static int strf_parse(const strf_prog *sp, js s, int64_t *ly, int *lm, int *ld, int *lh, int *lmi, int *ls,
+                      int *nanos, int *offset_secs) {
+    if (s.n != sp->width) return 1; /* fixed-width fields: anything else leaves text or runs short */
+    const int *c = s.c;
+    int day = 0, month = 0, hod = -1, clockh = -1, mi = 0, ss = 0, nos = 0, off = 0;
+    int64_t year = 0;
+    for (int k = 0; k < sp->nops; k++) {
+        const strf_op *o = &sp->ops[k];
+        const int *p = c + o->off;
+        int v = 0, w = 0;
+        switch (o->op) {
+        case SF_LIT: {
+            int x = p[0], y = o->ch;
+            if (x >= 'A' && x <= 'Z') x += 32;
+            if (y >= 'A' && y <= 'Z') y += 32;
+            if (x != y) return 1;
+            continue;
+        }
+        case SF_MONTXT: {
+            month = 0;
+            for (int m = 0; m < 12 && !month; m++) {
+                int ok = 1;
+                for (int q = 0; q < 3; q++) {
+                    int x = p[q], y = MONTH_SHORT[m][q];
+                    if (x >= 'a' && x <= 'z') x -= 32;
+                    if (y >= 'a' && y <= 'z') y -= 32;
+                    if (x != y) ok = 0;
+                }
+                if (ok) month = m + 1;
+            }
+            if (!month) return 1;
+            continue;
+        }
+        case SF_OFF: {
+            if (p[0] == '+' && p[1] == '0' && p[2] == '0' && p[3] == '0' && p[4] == '0') { off = 0; continue; }
+            if (p[0] != '+' && p[0] != '-') return 1;
+            int a1 = dig(p[1]), a2 = dig(p[2]), b1 = dig(p[3]), b2 = dig(p[4]);
+            if (a1 < 0 || a2 < 0 || b1 < 0 || b2 < 0) return 1;
+            int oh = a1 * 10 + a2, om = b1 * 10 + b2;
+            if (oh > 59 || om > 59) return 1;
+            off = (p[0] == '-' ? -1 : 1) * (oh * 3600 + om * 60);
+            continue;
+        }
+        case SF_YEAR: w = 4; break;
+        case SF_MSEC: w = 3; break;
+        case SF_USEC: w = 6; break;
+        default: w = 2; break;
+        }
+        for (int q = 0; q < w; q++) {
+            int d = dig(p[q]);
+            if (d < 0) return 1;
+            v = v * 10 + d;
+        }
+        switch (o->op) {
+        case SF_DAY: day = v; break;
+        case SF_MON: month = v; break;
+        case SF_YEAR: year = v; break;
+        case SF_CLOCKH: clockh = v; break;
+        case SF_HOD: hod = v; break;
+        case SF_MIN: mi = v; break;
+        case SF_SEC: ss = v; break;
+        case SF_MSEC: nos = v * 1000000; break;
+        case SF_USEC: nos = v * 1000; break;
+        }
+    }
+    if (off > 18 * 3600 || off < -18 * 3600) return 1;                     /* ZoneOffset.ofTotalSeconds */
+    /* resolveTimeFields: CLOCK_HOUR_OF_DAY, SMART allows 0-24, 24 -> 0 */
+    if (clockh >= 0) {
+        if (clockh != 0 && (clockh < 1 || clockh > 24)) return 1;
+        hod = clockh == 24 ? 0 : clockh;
+    }
+    /* resolveDate (IsoChronology.resolveYMD, SMART) */
+    if (month < 1 || month > 12) return 1;
+    if (day < 1 || day > 31) return 1;
+    int ml = month_len(year, month);
+    if (day > ml) day = ml;
+    /* resolveTime (SMART): minute checked first, 24:00:00.0 = end of day */
+    if (mi > 59) return 1;
+    int plus_day = 0;
+    if (hod == 24 && mi == 0 && ss == 0 && nos == 0) { hod = 0; plus_day = 1; }
+    else if (hod > 23 || ss > 59) return 1;
+    if (plus_day) {
+        int64_t days = days_from_civil(year, month, day) + 1;
+        civil_from_days(days, &year, &month, &day);
+    }
+    *ly = year; *lm = month; *ld = day; *lh = hod; *lmi = mi; *ls = ss; *nanos = nos; *offset_secs = off;
+    return 0;
+}
+
 /* TimeStampDissector.dissect (:404-564) */
+static void emit_time(parsable *ps, instance *in, const char *inputname, int64_t y, int m, int d, int h, int mi,
+                      int sec, int nanos, int off);
 static void d_timestamp(parsable *ps, instance *in, const char *inputname) {
     val *vp = cache_get(ps, in->d->in_type, inputname);
     js s = v_getstring(ps->a, *vp);
     if (s.null || s.n == 0) return;
     int64_t y; int m, d, h, mi, sec, off;
     if (parse_apache_time(s, &y, &m, &d, &h, &mi, &sec, &off)) { ps->failed = 1; return; }
+    emit_time(ps, in, inputname, y, m, d, h, mi, sec, 0, off);
+}
+
+/* StrfTimeStampDissector.dissect (StrfTimeStampDissector.java:66-70): the
+ * TimeStampDissector with the converted formatter */
+static void d_strftime(parsable *ps, instance *in, const char *inputname) {
+    val *vp = cache_get(ps, in->d->in_type, inputname);
+    js s = v_getstring(ps->a, *vp);
+    if (s.null || s.n == 0) return;
+    strf_prog sp;
+    strf_compile(in->d->param, &sp);
+    int64_t y; int m, d, h, mi, sec, nanos, off;
+    if (strf_parse(&sp, s, &y, &m, &d, &h, &mi, &sec, &nanos, &off)) { ps->failed = 1; return; }
+    emit_time(ps, in, inputname, y, m, d, h, mi, sec, nanos, off);
+}
+
+/* StrfTimeStampDissector.LocalizedTimeDissector.dissect (:117-120): the raw value */
+static void d_localized(parsable *ps, instance *in, const char *inputname) {
+    val *vp = cache_get(ps, in->d->in_type, inputname);
+    if (has_req(in, "")) add_str(ps, inputname, "TIME.LOCALIZEDSTRING", "", v_getstring(ps->a, *vp));
+}
+
+/* the outputs of TimeStampDissector.dissect (:425-564) for a parsed
+ * date-time (local fields as parsed, nanos, offset seconds) */
+static void emit_time(parsable *ps, instance *in, const char *inputname, int64_t y, int m, int d, int h, int mi,
+                      int sec, int nanos, int off) {
     int64_t epoch_s = days_from_civil(y, m, d) * 86400 + h * 3600 + mi * 60 + sec - off;
     int any_tz = has_req(in, "timezone") || has_req(in, "epoch");
     if (any_tz) {
         /* timezone: emitted as TIME.TIMEZONE but advertised as TIME.ZONE ->
          * never stored (:429); only epoch matters */
-        if (has_req(in, "epoch")) add_long(ps, inputname, "TIME.EPOCH", "epoch", epoch_s * 1000);
+        if (has_req(in, "epoch")) add_long(ps, inputname, "TIME.EPOCH", "epoch", epoch_s * 1000 + nanos / 1000000);
     }
     const char *asp[] = {"day", "monthname", "month", "weekofweekyear", "weekyear", "year", "hour", "minute", "second",
                          "millisecond", "microsecond", "nanosecond", "date", "time", NULL};
@@ -1480,9 +1686,9 @@ static void d_timestamp(parsable *ps, instance *in, const char *inputname) {
         if (WANT("hour")) add_long(ps, inputname, "TIME.HOUR", nm, H);
         if (WANT("minute")) add_long(ps, inputname, "TIME.MINUTE", nm, MI);
         if (WANT("second")) add_long(ps, inputname, "TIME.SECOND", nm, S);
-        if (WANT("millisecond")) add_long(ps, inputname, "TIME.MILLISECOND", nm, 0);
-        if (WANT("microsecond")) add_long(ps, inputname, "TIME.MICROSECOND", nm, 0);
-        if (WANT("nanosecond")) add_long(ps, inputname, "TIME.NANOSECOND", nm, 0);
+        if (WANT("millisecond")) add_long(ps, inputname, "TIME.MILLISECOND", nm, nanos / 1000000);
+        if (WANT("microsecond")) add_long(ps, inputname, "TIME.MICROSECOND", nm, nanos / 1000);
+        if (WANT("nanosecond")) add_long(ps, inputname, "TIME.NANOSECOND", nm, nanos);
         if (WANT("date")) add_str(ps, inputname, "TIME.DATE", nm, fmt2(ps, "%04lld-%02d-%02d", Y, M, D));
         if (WANT("time")) add_str(ps, inputname, "TIME.TIME", nm, fmt2(ps, "%02lld:%02d:%02d", H, MI, S));
 #undef WANT
@@ -2247,6 +2453,8 @@ static void run_instance(parsable *ps, instance *in, const char *name) {
     switch (in->d->cls) {
     case D_ROOT: d_root(ps, in, name); break;
     case D_TIMESTAMP: d_timestamp(ps, in, name); break;
+    case D_STRFTIME: d_strftime(ps, in, name); break;
+    case D_LOCALIZED: d_localized(ps, in, name); break;
     case D_FIRSTLINE: d_firstline(ps, in, name); break;
     case D_PROTOCOL: d_protocol(ps, in, name); break;
     case D_URI: d_uri(ps, in, name); break;

@@ -336,6 +336,47 @@ for m in ["sep", "Sep", "sEp", "SEp", "seP", "SeP", "sEP", "SEP"]:
          expect={tsf("TIME.YEAR:year_utc"): {"l": 2016}, tsf("TIME.MONTH:month_utc"): {"l": 9},
                  tsf("TIME.DAY:day_utc"): {"l": 30}})
 
+# StrfTimeStampDissector (hpt/dissectors/TestTimeStampDissector.java) through "%{...}t" tokens
+STRF_EXPECT = {
+    "TIME.EPOCH:epoch": {"l": 1357020044000}, "TIME.YEAR:year": {"l": 2012}, "TIME.MONTH:month": {"l": 12},
+    "TIME.MONTHNAME:monthname": "December", "TIME.DAY:day": {"l": 31}, "TIME.HOUR:hour": {"l": 23},
+    "TIME.MINUTE:minute": {"l": 0}, "TIME.SECOND:second": {"l": 44}, "TIME.DATE:date": "2012-12-31",
+    "TIME.TIME:time": "23:00:44", "TIME.YEAR:year_utc": {"l": 2013}, "TIME.MONTH:month_utc": {"l": 1},
+    "TIME.MONTHNAME:monthname_utc": "January", "TIME.DAY:day_utc": {"l": 1}, "TIME.HOUR:hour_utc": {"l": 6},
+    "TIME.MINUTE:minute_utc": {"l": 0}, "TIME.SECOND:second_utc": {"l": 44}, "TIME.DATE:date_utc": "2013-01-01",
+    "TIME.TIME:time_utc": "06:00:44"}
+case("hpt/dissectors/TestTimeStampDissector.java:185-226", "%{%Y-%m-%dT%H:%M:%S%z}t", "2012-12-31T23:00:44-0700",
+     [tsf(f) for f in TS_F], expect={tsf(k): v for k, v in STRF_EXPECT.items()})
+case("hpt/dissectors/TestTimeStampDissector.java:228-235", "%{begin:%Y-%m-%dT%H:%M:%S%z}t", "2012-12-31T23:00:44-0700",
+     ["TIME.EPOCH:request.receive.time.begin.epoch"],
+     expect={"TIME.EPOCH:request.receive.time.begin.epoch": {"l": 1357020044000}})
+case("hpt/dissectors/TestTimeStampDissector.java:237-244", "%{end:%Y-%m-%dT%H:%M:%S%z}t", "2012-12-31T23:00:44-0700",
+     ["TIME.EPOCH:request.receive.time.end.epoch"],
+     expect={"TIME.EPOCH:request.receive.time.end.epoch": {"l": 1357020044000}})
+case("hpt/dissectors/TestTimeStampDissector.java:351-372", "%{%d/%b/%Y %T.msec_frac %z}t", "01/Jan/2017 21:52:58.483 +0100",
+     [tsf("TIME.EPOCH:epoch")], expect={tsf("TIME.EPOCH:epoch"): {"l": 1483303978483}})
+case("hpt/dissectors/TestTimeStampDissector.java:374-384", "%{%d/%b/%Y:%H:%M:%S %z}t", "28/feb/2017:03:39:40 +0800",
+     [tsf("TIME.EPOCH:epoch")], expect={tsf("TIME.EPOCH:epoch"): {"l": 1488224380000}})
+case("hpt/dissectors/TestTimeStampDissector.java:524-530", "%{%F %H:%M:%S}t", "2017-12-25 00:00:00",
+     [tsf("TIME.EPOCH:epoch")], expect={tsf("TIME.EPOCH:epoch"): {"l": 1514160000000}})
+STRF_LINE_FMT = "%a %l %u {} \"%r\" %>s %b \"%{{Referer}}i\" \"%{{User-Agent}}i\" \"%{{Cookie}}i\" t=%D"
+case("hpt/dissectors/TestTimeStampDissector.java:532-537", STRF_LINE_FMT.format("%{%F %H:%M:%S}t"),
+     "192.168.85.3 - - 2017-12-25 00:00:00 \"GET /up.html HTTP/1.0\" 203 8 \"-\" \"HTTP-Monitor/1.1\" \"-\" t=4920",
+     [tsf("TIME.EPOCH:epoch")], expect={tsf("TIME.EPOCH:epoch"): {"l": 1514160000000}})
+FRAC_F = ["TIME.EPOCH:epoch", "TIME.SECOND:second", "TIME.MILLISECOND:millisecond", "TIME.MICROSECOND:microsecond",
+          "TIME.NANOSECOND:nanosecond", "TIME.MILLISECOND:millisecond_utc", "TIME.MICROSECOND:microsecond_utc",
+          "TIME.NANOSECOND:nanosecond_utc"]
+for src, frac, digits, ms, us, ns, epoch in [
+        ("hpt/dissectors/TestTimeStampDissector.java:540-555", "msec_frac", "123", 123, 123000, 123000000, 1514160042123),
+        ("hpt/dissectors/TestTimeStampDissector.java:557-572", "%msec_frac", "123", 123, 123000, 123000000, 1514160042123),
+        ("hpt/dissectors/TestTimeStampDissector.java:574-589", "usec_frac", "123456", 123, 123456, 123456000, 1514160042123),
+        ("hpt/dissectors/TestTimeStampDissector.java:591-606", "%usec_frac", "123456", 123, 123456, 123456000, 1514160042123)]:
+    vals = [{"l": epoch}, {"l": 42}, {"l": ms}, {"l": us}, {"l": ns}, {"l": ms}, {"l": us}, {"l": ns}]
+    case(src, STRF_LINE_FMT.format("%{%F %H:%M:%S." + frac + "}t"),
+         "192.168.85.3 - - 2017-12-25 00:00:42." + digits + " \"GET /up.html HTTP/1.0\" 203 8 \"-\" \"HTTP-Monitor/1.1\" \"-\" t=4920",
+         [tsf(f) for f in FRAC_F], expect={tsf(f): v for f, v in zip(FRAC_F, vals)})
+# (:246-349 %D %R %r %a %A %B %G %I %j %k %l %p %s %u fields: outside the restated strftime subset, left out)
+
 # examples/apache-flink/.../TestCase.java:37-43,86-94 (IPv6 %h, long query string); GeoIP / remapped fields skipped.
 FLINK_LINE = open(os.path.join(HERE, "flink_testcase_line.txt"), encoding="utf-8").read().rstrip("\n") \
     if os.path.exists(os.path.join(HERE, "flink_testcase_line.txt")) else None
