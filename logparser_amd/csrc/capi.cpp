@@ -81,6 +81,7 @@ bool alloc_columns(lp_handle* h, int64_t n) {
         cols.push_back({(void**)&C.t_epoch[t], 8});
         cols.push_back({(void**)&C.t_local[t], 8});
         cols.push_back({(void**)&C.t_utc[t], 8});
+        if (P.time[t].kind == lp::TK_STRF) cols.push_back({(void**)&C.t_nano[t], 4});  // only strftime has fractions
     }
     for (int f = 0; f < P.n_fl; ++f) {
         cols.push_back({(void**)&C.fl_kind[f], 4});
@@ -141,10 +142,12 @@ bool fetch_host(lp_handle* h) {
     for (int k = 0; k < P.n_tok; ++k) fetch(R.tok_span[k], h->C.tok_span[k], n);
     fetch(R.tok_flags, h->C.tok_flags, n);
     R.t_epoch.resize(lp::MAX_TIME); R.t_local.resize(lp::MAX_TIME); R.t_utc.resize(lp::MAX_TIME);
+    R.t_nano.resize(lp::MAX_TIME);
     for (int t = 0; t < P.n_time; ++t) {
         fetch(R.t_epoch[t], h->C.t_epoch[t], n);
         fetch(R.t_local[t], h->C.t_local[t], n);
         fetch(R.t_utc[t], h->C.t_utc[t], n);
+        if (P.time[t].kind == lp::TK_STRF) fetch(R.t_nano[t], h->C.t_nano[t], n);
     }
     R.fl_kind.resize(lp::MAX_FL); R.fl_method.resize(lp::MAX_FL); R.fl_uri.resize(lp::MAX_FL); R.fl_proto.resize(lp::MAX_FL);
     for (int f = 0; f < P.n_fl; ++f) {

@@ -968,6 +968,29 @@ __host__ __device__ LP_INLINE void iso_week(int32_t y, int32_t days, int32_t& wy
     wk = w;
 }
 
+// Packed local ("as parsed") and UTC calendar fields and epoch seconds of a
+// resolved local date-time (day number `days`) at offset `off` seconds.
+__host__ __device__ LP_INLINE void time_fields(int32_t y, int m, int d, int hh, int mi, int ss, int off, int32_t days,
+                                               int64_t& epoch_s, uint64_t& local, uint64_t& utc) {
+    const int sod = hh * 3600 + mi * 60 + ss;
+    epoch_s = (int64_t)days * 86400 + sod - off;
+    int32_t wy;
+    int wk;
+    iso_week(y, days, wy, wk);
+    local = pack_cal((uint32_t)y, m, d, hh, mi, ss, (uint32_t)wy, wk);
+    // UTC: the same date unless the offset moves the time across midnight
+    int t = sod - off;
+    int32_t ud = days;
+    if (t < 0) { t += 86400; --ud; }
+    else if (t >= 86400) { t -= 86400; ++ud; }
+    if (ud != days) {
+        civil_from_days(ud, y, m, d);
+        iso_week(y, ud, wy, wk);
+    }
+    utc = pack_cal((uint32_t)y, m, d, (uint32_t)(t / 3600), (uint32_t)(t % 3600 / 60), (uint32_t)(t % 60),
+                   (uint32_t)wy, wk);
+}
+
 // DateTimeFormatter "dd/MMM/yyyy:HH:mm:ss ZZ", parseCaseInsensitive,
 // Locale.UK, ResolverStyle.SMART (TimeStampDissector.java:46,100-109,418):
 // day 1..31 clamped to the month length, 24:00:00 = next day 00:00:00,
@@ -1010,24 +1033,94 @@ __host__ __device__ LP_INLINE bool parse_apache_time(const LN& L, int a, int64_t
     } else if (hh > 23 || ss > 59) {
         return false;
     }
-    const int sod = hh * 3600 + mi * 60 + ss;
-    epoch_s = (int64_t)days * 86400 + sod - off;
-    int32_t wy;
-    int wk;
-    iso_week(y, days, wy, wk);
-    local = pack_cal((uint32_t)y, m, d, hh, mi, ss, (uint32_t)wy, wk);
-    // UTC: the same date unless the offset moves the time across midnight
-    int t = sod - off;
-    int32_t ud = days;
-    if (t < 0) { t += 86400; --ud; }
-    else if (t >= 86400) { t -= 86400; ++ud; }
-    if (ud != days) {
-        civil_from_days(ud, y, m, d);
-        iso_week(y, ud, wy, wk);
-    }
-    utc = pack_cal((uint32_t)y, m, d, (uint32_t)(t / 3600), (uint32_t)(t % 3600 / 60), (uint32_t)(t % 60),
-                   (uint32_t)wy, wk);
+    time_fields(y, m, d, hh, mi, ss, off, days, epoch_s, local, utc);
     return true;
+}
+
+// StrfTimeStampDissector with a fixed-width converted formatter
+// (StrfTimeToDateTimeFormatter: appendValue(DAY_OF_MONTH, 2), appendText(
+// MONTH_OF_YEAR, SHORT) in the default locale en_US, appendValue(YEAR, 4),
+// CLOCK_HOUR_OF_DAY (%H) / HOUR_OF_DAY (%T), MINUTE, SECOND, MILLI_ /
+// MICRO_OF_SECOND, appendOffset("+HHMM", "+0000"); parseCaseInsensitive,
+// SMART resolver, zone UTC without %z) on the value [a, b).
+// Returns ST_OK, ST_BAD (DateTimeParseException) or ST_FALLBACK (year 0).
+template <typename LN>
+__host__ __device__ LP_INLINE int parse_strf_time(const TimeStage& T, const LN& L, int a, int b, int64_t& epoch_ms,
+                                                  uint64_t& local, uint64_t& utc, uint32_t& nanos) {
+    if (b - a != (int)T.width) return ST_BAD;  // fixed-width fields: text left over or missing
+    int day = 0, month = 0, year = 0, hod = -1, clockh = -1, mi = 0, ss = 0, off = 0;
+    uint32_t nos = 0;
+    auto low = [](uint32_t c) { return (c - 'A') < 26u ? (c | 32u) : c; };
+    for (int k = 0; k < T.n_ops; ++k) {
+        const int p = a + T.off[k];
+        const uint32_t op = T.op[k];
+        if (op == SF_LIT) {
+            if (low(L[p]) != low(T.ch[k])) return ST_BAD;
+            continue;
+        }
+        if (op == SF_MONTXT) {
+            const uint32_t m3 = (low(L[p]) << 16) | (low(L[p + 1]) << 8) | low(L[p + 2]);
+            const uint32_t names[12] = {0x6a616e, 0x666562, 0x6d6172, 0x617072, 0x6d6179, 0x6a756e,
+                                        0x6a756c, 0x617567, 0x736570, 0x6f6374, 0x6e6f76, 0x646563};
+            month = 0;
+            for (int q = 0; q < 12; ++q) month = names[q] == m3 ? q + 1 : month;
+            if (!month) return ST_BAD;
+            continue;
+        }
+        if (op == SF_OFF) {
+            const uint32_t sg = L[p];
+            if (sg == '+' && L[p + 1] == '0' && L[p + 2] == '0' && L[p + 3] == '0' && L[p + 4] == '0') { off = 0; continue; }
+            if (sg != '+' && sg != '-') return ST_BAD;
+            for (int q = 1; q <= 4; ++q) if (!is_digit(L[p + q])) return ST_BAD;
+            const int oh = (int)(L[p + 1] - '0') * 10 + (int)(L[p + 2] - '0'), om = (int)(L[p + 3] - '0') * 10 + (int)(L[p + 4] - '0');
+            if (oh > 59 || om > 59) return ST_BAD;
+            off = (sg == '-' ? -1 : 1) * (oh * 3600 + om * 60);
+            continue;
+        }
+        const int w = op == SF_YEAR ? 4 : op == SF_MSEC ? 3 : op == SF_USEC ? 6 : 2;
+        int v = 0;
+        for (int q = 0; q < w; ++q) {
+            const uint32_t c = L[p + q];
+            if (!is_digit(c)) return ST_BAD;
+            v = v * 10 + (int)(c - '0');
+        }
+        switch (op) {
+        case SF_DAY: day = v; break;
+        case SF_MON: month = v; break;
+        case SF_YEAR: year = v; break;
+        case SF_CLOCKH: clockh = v; break;
+        case SF_HOD: hod = v; break;
+        case SF_MIN: mi = v; break;
+        case SF_SEC: ss = v; break;
+        case SF_MSEC: nos = (uint32_t)v * 1000000u; break;
+        case SF_USEC: nos = (uint32_t)v * 1000u; break;
+        }
+    }
+    if (off > 64800 || off < -64800) return ST_BAD;                     // ZoneOffset.ofTotalSeconds
+    if (clockh >= 0) {                                                  // SMART: 0..24, 24 -> 0
+        if (clockh > 24) return ST_BAD;
+        hod = clockh == 24 ? 0 : clockh;
+    }
+    if (month < 1 || month > 12 || day < 1 || day > 31) return ST_BAD;  // resolveDate
+    if (year == 0) return ST_FALLBACK;                                  // year 0: outside the 32-bit calendar
+    const int ml = month_len(year, month);
+    if (day > ml) day = ml;
+    if (mi > 59) return ST_BAD;                                         // resolveTime
+    int32_t y = year;
+    int m = month, d = day;
+    int32_t days = days_from_civil(y, m, d);
+    if (hod == 24 && mi == 0 && ss == 0 && nos == 0) {                  // SMART end of day
+        hod = 0;
+        ++days;
+        civil_from_days(days, y, m, d);
+    } else if (hod > 23 || ss > 59) {
+        return ST_BAD;
+    }
+    int64_t es;
+    time_fields(y, m, d, hod, mi, ss, off, days, es, local, utc);
+    epoch_ms = es * 1000 + (int64_t)(nos / 1000000u);
+    nanos = nos;
+    return ST_OK;
 }
 
 // ----------------------------------------------------------- per-line state
@@ -1122,11 +1215,23 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
     LP_PROF(5);
     // TimeStampDissector
     for (int t = 0; t < P.n_time; ++t) {
-        int k = P.time[t].tok;
-        int a = o.caps.get(k) & 0xFFFF;
+        const TimeStage& T = P.time[t];
+        const int k = T.tok;
+        const uint32_t sp = o.caps.get(k);
+        const int a = sp & 0xFFFF, b = sp >> 16;
         int64_t ep; uint64_t lo, ut;
-        if (!parse_apache_time(L, a, ep, lo, ut)) { o.status = ST_BAD; return; }
-        C.t_epoch[t][li] = ep * 1000;
+        uint32_t ns = 0;
+        if (T.kind == TK_APACHE) {
+            if (!parse_apache_time(L, a, ep, lo, ut)) { o.status = ST_BAD; return; }
+            ep *= 1000;
+        } else {
+            // an empty or "-" (null) value has no outputs (TimeStampDissector.java:412-415)
+            if (b == a || (o.tok_flags & (1u << k))) continue;
+            const int st = parse_strf_time(T, L, a, b, ep, lo, ut, ns);
+            if (st != ST_OK) { o.status = st; return; }
+            C.t_nano[t][li] = ns;
+        }
+        C.t_epoch[t][li] = ep;
         C.t_local[t][li] = lo;
         C.t_utc[t][li] = ut;
     }

@@ -82,9 +82,22 @@ struct Elem {
 
 // TimeStampDissector on a TIME.STAMP token (dd/MMM/yyyy:HH:mm:ss ZZ,
 // hp/dissectors/TimeStampDissector.java:46, 404-564).
+// TimeStampDissector on a TIME.STAMP token (TK_APACHE: the fixed
+// "dd/MMM/yyyy:HH:mm:ss ZZ" of hp/dissectors/TimeStampDissector.java:46), or
+// StrfTimeStampDissector on a %{...}t token (TK_STRF,
+// hp/dissectors/StrfTimeStampDissector.java:44-70) whose strftime pattern
+// converts to fixed-width DateTimeFormatter fields
+// (hp/dissectors/StrfTimeToDateTimeFormatter.java): the value must be exactly
+// `width` bytes, op k reads its field at byte off[k].
+enum : uint8_t { TK_APACHE = 0, TK_STRF = 1 };
+enum : uint8_t { SF_LIT, SF_DAY, SF_MON, SF_MONTXT, SF_YEAR, SF_CLOCKH, SF_HOD, SF_MIN, SF_SEC, SF_MSEC, SF_USEC, SF_OFF };
+constexpr int MAX_SF_OPS = 32;
 struct TimeStage {
     int8_t tok;
-    uint8_t pad[3];
+    uint8_t kind;   // TK_*
+    uint8_t width;  // TK_STRF: exact byte length of the value
+    uint8_t n_ops;
+    uint8_t op[MAX_SF_OPS], off[MAX_SF_OPS], ch[MAX_SF_OPS];  // ch: SF_LIT byte
 };
 
 // HttpFirstLineDissector on an HTTP.FIRSTLINE token
@@ -194,6 +207,7 @@ struct Columns {
     LP_G int64_t* t_epoch[MAX_TIME];
     LP_G uint64_t* t_local[MAX_TIME];
     LP_G uint64_t* t_utc[MAX_TIME];
+    LP_G uint32_t* t_nano[MAX_TIME];   // nano-of-second (strftime msec_frac / usec_frac)
     LP_G uint32_t* fl_kind[MAX_FL];
     LP_G uint32_t* fl_method[MAX_FL];  // spans
     LP_G uint32_t* fl_uri[MAX_FL];

@@ -162,6 +162,73 @@ struct TokenTable {
     }
 };
 
+// StrfTimeToDateTimeFormatter (hp/dissectors/StrfTimeToDateTimeFormatter.java,
+// grammar StrfTime.g4) for the conversions that become fixed-width
+// DateTimeFormatter fields: %d %m %b %h %Y %H %M %S, %T (HOUR_OF_DAY:%M:%S,
+// :360-368), %F (%Y-%m-%d), %z, [%]msec_frac, [%]usec_frac, %% %t %n and
+// literal text, E/O modifiers ignored.  The pattern must give day, month,
+// year, hour, minute and second exactly once; anything else stays off the
+// device.
+static bool strf_compile(const std::string& f, TimeStage& T) {
+    int seen[16] = {0};
+    auto add = [&](int op, int w, int ch) {
+        if (T.n_ops >= MAX_SF_OPS || T.width + w > 255) return false;
+        T.op[T.n_ops] = (uint8_t)op;
+        T.off[T.n_ops] = (uint8_t)T.width;
+        T.ch[T.n_ops] = (uint8_t)ch;
+        ++T.n_ops;
+        T.width = (uint8_t)(T.width + w);
+        return true;
+    };
+    auto fld = [&](int op, int w) { return seen[op]++ == 0 && add(op, w, 0); };
+    const size_t n = f.size();
+    for (size_t i = 0; i < n;) {
+        const size_t j = i + (f[i] == '%');
+        if (n - j >= 9 && (f.compare(j, 9, "msec_frac") == 0 || f.compare(j, 9, "usec_frac") == 0)) {
+            if (!(f[j] == 'm' ? fld(SF_MSEC, 3) : fld(SF_USEC, 6))) return false;
+            i = j + 9;
+            continue;
+        }
+        if (f[i] != '%') {
+            if (!add(SF_LIT, 1, (uint8_t)f[i])) return false;
+            ++i;
+            continue;
+        }
+        if (i + 1 >= n) return false;
+        char c = f[i + 1];
+        size_t k = i + 1;
+        if (c == '%' || c == 't' || c == 'n') {
+            if (!add(SF_LIT, 1, c == '%' ? '%' : c == 't' ? '\t' : '\n')) return false;
+            i += 2;
+            continue;
+        }
+        if (c == 'E' || c == 'O') {
+            if (i + 2 >= n) return false;
+            c = f[i + 2];
+            ++k;
+        }
+        bool ok;
+        switch (c) {
+        case 'd': ok = fld(SF_DAY, 2); break;
+        case 'm': ok = fld(SF_MON, 2); break;
+        case 'b': case 'h': ok = fld(SF_MONTXT, 3); break;
+        case 'Y': ok = fld(SF_YEAR, 4); break;
+        case 'H': ok = fld(SF_CLOCKH, 2); break;
+        case 'M': ok = fld(SF_MIN, 2); break;
+        case 'S': ok = fld(SF_SEC, 2); break;
+        case 'T': ok = fld(SF_HOD, 2) && add(SF_LIT, 1, ':') && fld(SF_MIN, 2) && add(SF_LIT, 1, ':') && fld(SF_SEC, 2); break;
+        case 'F': ok = fld(SF_YEAR, 4) && add(SF_LIT, 1, '-') && fld(SF_MON, 2) && add(SF_LIT, 1, '-') && fld(SF_DAY, 2); break;
+        case 'z': ok = fld(SF_OFF, 5); break;
+        default: ok = false; break;
+        }
+        if (!ok) return false;
+        i = k + 1;
+    }
+    if (!seen[SF_DAY] || seen[SF_MON] + seen[SF_MONTXT] != 1 || !seen[SF_YEAR]) return false;
+    if (seen[SF_CLOCKH] + seen[SF_HOD] != 1 || !seen[SF_MIN] || !seen[SF_SEC]) return false;
+    return seen[SF_MSEC] + seen[SF_USEC] <= 1;
+}
+
 // ApacheHttpdLogFormatDissector.createAllTokenParsers (:199-638)
 const TokenTable& apache_table() {
     static TokenTable T = [] {
@@ -1089,6 +1156,29 @@ void Plan::compile_program() {
                     }
                     break;
                 }
+                case D_STRFTIME: {
+                    if (ok != O_TOKEN) { device_ok_ = false; why_ = "strftime from a derived value"; return; }
+                    if (!time_of_tok_.count(oi)) {
+                        if (P.n_time == MAX_TIME) { device_ok_ = false; why_ = "too many timestamps"; return; }
+                        const Token* tk = nullptr;
+                        for (const auto& kv : tok_slot_)
+                            if (kv.second == oi) tk = &formats_[0]->tokens[kv.first];
+                        TimeStage& T = P.time[P.n_time];
+                        memset(&T, 0, sizeof T);
+                        T.tok = (int8_t)oi;
+                        T.kind = TK_STRF;
+                        if (!tk || !tk->strftime || !strf_compile(tk->custom_param, T)) {
+                            device_ok_ = false;
+                            why_ = "strftime pattern outside the device subset";
+                            return;
+                        }
+                        time_of_tok_[oi] = P.n_time++;
+                    }
+                    break;
+                }
+                case D_LOCALIZED:
+                    if (ok != O_TOKEN) { device_ok_ = false; why_ = "localized time from a derived value"; return; }
+                    break;
                 case D_FIRSTLINE: {
                     if (ok != O_TOKEN) { device_ok_ = false; why_ = "first line from a derived value"; return; }
                     int fidx;
@@ -1275,10 +1365,14 @@ void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const 
         return mstr((ref_arena(r) ? c.arena : c.line) + ref_off(r), ref_len(r));
     };
     switch (in.cls) {
-    case D_TIMESTAMP: {
+    case D_LOCALIZED:  // StrfTimeStampDissector.LocalizedTimeDissector (:117-120): the raw value
+        if (has("")) emit(c, name, "TIME.LOCALIZEDSTRING", "", v);
+        return;
+    case D_TIMESTAMP: case D_STRFTIME: {
         if (v.null || v.len == 0) return;
         int t = time_of_tok_.at(oi);
         int64_t epoch = R.t_epoch[t][i];
+        const int64_t nanos = in.cls == D_STRFTIME ? (int64_t)R.t_nano[t][i] : 0;
         if (has("epoch")) { set_origin(O_TIME, t); emit(c, name, "TIME.EPOCH", "epoch", mlong(epoch)); }
         for (int pass = 0; pass < 2; ++pass) {
             uint64_t w = pass == 0 ? R.t_local[t][i] : R.t_utc[t][i];
@@ -1299,9 +1393,9 @@ void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const 
             if (has(nm("hour").c_str())) emit(c, name, "TIME.HOUR", nm("hour"), mlong(H));
             if (has(nm("minute").c_str())) emit(c, name, "TIME.MINUTE", nm("minute"), mlong(MI));
             if (has(nm("second").c_str())) emit(c, name, "TIME.SECOND", nm("second"), mlong(S));
-            if (has(nm("millisecond").c_str())) emit(c, name, "TIME.MILLISECOND", nm("millisecond"), mlong(0));
-            if (has(nm("microsecond").c_str())) emit(c, name, "TIME.MICROSECOND", nm("microsecond"), mlong(0));
-            if (has(nm("nanosecond").c_str())) emit(c, name, "TIME.NANOSECOND", nm("nanosecond"), mlong(0));
+            if (has(nm("millisecond").c_str())) emit(c, name, "TIME.MILLISECOND", nm("millisecond"), mlong(nanos / 1000000));
+            if (has(nm("microsecond").c_str())) emit(c, name, "TIME.MICROSECOND", nm("microsecond"), mlong(nanos / 1000));
+            if (has(nm("nanosecond").c_str())) emit(c, name, "TIME.NANOSECOND", nm("nanosecond"), mlong(nanos));
             if (has(nm("date").c_str())) {
                 char b[32];
                 snprintf(b, sizeof b, "%04lld-%02lld-%02lld", (long long)Y, (long long)MO, (long long)D);

@@ -80,6 +80,7 @@ struct HostResults {
     std::vector<uint32_t> tok_flags;
     std::vector<std::vector<int64_t>> t_epoch;
     std::vector<std::vector<uint64_t>> t_local, t_utc;
+    std::vector<std::vector<uint32_t>> t_nano;
     std::vector<std::vector<uint32_t>> fl_kind, fl_method, fl_uri, fl_proto;
     std::vector<std::vector<uint32_t>> u_flags;
     std::vector<std::vector<uint64_t>> u_scheme, u_host, u_path, u_query, u_frag;

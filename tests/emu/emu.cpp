@@ -98,6 +98,7 @@ static int parse_impl(Emu* e, const char* line, int len, const uint8_t* base, ui
     R.t_epoch.assign(MAX_TIME, std::vector<int64_t>(1));
     R.t_local.assign(MAX_TIME, std::vector<uint64_t>(1));
     R.t_utc.assign(MAX_TIME, std::vector<uint64_t>(1));
+    R.t_nano.assign(MAX_TIME, std::vector<uint32_t>(1));
     for (auto* v : {&R.fl_kind, &R.fl_method, &R.fl_uri, &R.fl_proto}) v->assign(MAX_FL, std::vector<uint32_t>(1));
     R.u_flags.assign(MAX_URI, std::vector<uint32_t>(1));
     for (auto* v : {&R.u_scheme, &R.u_host, &R.u_path, &R.u_query, &R.u_frag})
@@ -112,7 +113,7 @@ static int parse_impl(Emu* e, const char* line, int len, const uint8_t* base, ui
     C.line_off = R.line_off.data();
     for (int k = 0; k < MAX_TOK; ++k) C.tok_span[k] = R.tok_span[k].data();
     C.tok_flags = R.tok_flags.data();
-    for (int t = 0; t < MAX_TIME; ++t) { C.t_epoch[t] = R.t_epoch[t].data(); C.t_local[t] = R.t_local[t].data(); C.t_utc[t] = R.t_utc[t].data(); }
+    for (int t = 0; t < MAX_TIME; ++t) { C.t_epoch[t] = R.t_epoch[t].data(); C.t_local[t] = R.t_local[t].data(); C.t_utc[t] = R.t_utc[t].data(); C.t_nano[t] = R.t_nano[t].data(); }
     for (int f = 0; f < MAX_FL; ++f) { C.fl_kind[f] = R.fl_kind[f].data(); C.fl_method[f] = R.fl_method[f].data(); C.fl_uri[f] = R.fl_uri[f].data(); C.fl_proto[f] = R.fl_proto[f].data(); }
     for (int u = 0; u < MAX_URI; ++u) {
         C.u_flags[u] = R.u_flags[u].data(); C.u_scheme[u] = R.u_scheme[u].data(); C.u_host[u] = R.u_host[u].data();

@@ -214,3 +214,47 @@ def test_nginx_combined_format_emulated(oracle, emu):
     assert e.status == 0, e.err
     s = compare(o, e, [l.rsplit(b' "', 1)[0] for l in lines])
     assert s["ok"] > 250, s
+
+
+STRF = lpa.SYNTH_FORMATS[lpa.SYNTH_STRFTIME]
+
+
+def mutate_strf(rng, line):
+    """Config-3 timestamp corners (StrfTimeToDateTimeFormatter + SMART resolver)."""
+    i = line.index(b"[") + 1
+    ts = line[i:i + 20]
+    ops = [
+        lambda t: t[:3] + b"APR" + t[6:],
+        lambda t: t[:3] + b"sEp" + t[6:],
+        lambda t: b"31/Apr" + t[6:],
+        lambda t: b"29/Feb/2015" + t[11:],
+        lambda t: b"29/Feb/2016" + t[11:],
+        lambda t: t[:12] + b"24:00:00",
+        lambda t: t[:12] + b"24:00:01",
+        lambda t: t[:12] + b"23:60:00",
+        lambda t: t[:12] + b"23:59:60",
+        lambda t: b"32" + t[2:],
+        lambda t: b"00" + t[2:],
+        lambda t: t[:7] + b"0000" + t[11:],
+        lambda t: t[:7] + b"0001" + t[11:],
+        lambda t: t[:6] + b"-" + t[7:],
+        lambda t: t[:11] + b":" + t[12:],
+        lambda t: t[:2] + b"/Sept" + t[6:],
+        lambda t: t,
+    ]
+    return line[:i] + rng.choice(ops)(ts) + line[i + 20:]
+
+
+def test_strftime_config3_emulated(oracle, emu):
+    paths = oracle.possible_paths(STRF)
+    assert any(p.startswith("TIME.LOCALIZEDSTRING:") for p in paths)
+    o = oracle.Oracle(STRF, paths)
+    e = emu.Emu(STRF, paths)
+    assert e.status == 0, e.err
+    lines = lpa.synth(lpa.SYNTH_STRFTIME, 20261016, 0, 4000).split(b"\n")[:-1]
+    s = compare(o, e, lines, allow_fallback=False)
+    assert s["ok"] > 3700 and s["bad"] > 100, s  # 5 % malformed lines (BASELINE config 3)
+    rng = random.Random(33)
+    mut = [mutate_strf(rng, l) for l in lines[:2500] if b"[" in l and len(l) > 60] + [mutate(rng, l) for l in lines[2500:]]
+    s = compare(o, e, mut)
+    assert s["bad"] > 300 and s["ok"] > 1000, s

@@ -199,3 +199,17 @@ def test_nginx_config4_gpu(oracle):
     mut = [mutate_nginx(rng, l) for l in lines[:3000]] + [mutate(rng, l) for l in lines[3000:6000]]
     s, _ = gpu_vs_oracle(oracle, NGINX, fields, mut)
     assert s["bad"] > 100 and s["ok"] > 1000, s
+
+
+def test_strftime_config3_gpu(oracle):
+    """BASELINE config 3: 'combinedio' with %{%d/%b/%Y %T}t.%{msec_frac}t and
+    5 % malformed lines, all possible paths (StrfTimeStampDissector on the device)."""
+    from test_emu_parity import STRF, mutate, mutate_strf
+    fields = paths(oracle, STRF)
+    lines = lpa.synth(lpa.SYNTH_STRFTIME, 20261016, 0, 20000).split(b"\n")[:-1]
+    s, _ = gpu_vs_oracle(oracle, STRF, fields, lines, allow_fallback=False)
+    assert s["ok"] > 18500 and s["bad"] > 500, s
+    rng = random.Random(34)
+    mut = [mutate_strf(rng, l) for l in lines[:3000] if b"[" in l and len(l) > 60] + [mutate(rng, l) for l in lines[3000:6000]]
+    s, _ = gpu_vs_oracle(oracle, STRF, fields, mut)
+    assert s["bad"] > 300 and s["ok"] > 1000, s
