@@ -7,9 +7,11 @@ then an RCCL all-reduce of the line counters (world > 1).
 
 Default workload: 100M synthetic 'combined' lines per GPU (~25 GB, seed
 20261015), weak scaling over GPUs (each rank parses its own 100M lines).
-Prints ONE JSON line on rank 0.
+Prints ONE JSON line on rank 0.  --workload 3 / 4 runs BASELINE.json configs
+3 (strftime timestamps, 5 % malformed lines) and 4 (NGINX upstream log
+format) the same way, for the records in DESIGN.md; the headline is config 2.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--lines L]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--lines L] [--workload 2|3|4]
 """
 import argparse
 import concurrent.futures as cf
@@ -22,7 +24,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-SEED = 20261015
+SEEDS = {2: 20261015, 3: 20261016, 4: 20261017}
+WORKLOAD_NAMES = {2: "config 2: %d synthetic 'combined' lines",
+                  3: "config 3: %d synthetic 'combinedio' + %%{%%d/%%b/%%Y %%T}t.%%{msec_frac}t lines (5%% malformed)",
+                  4: "config 4: %d synthetic NGINX '$request_time $upstream_response_time $pipe' lines"}
 
 
 def log(*a):
@@ -30,7 +35,7 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def generate_to_device(lpa, torch, first_line, n_lines, device, chunk=1 << 20, workers=16):
+def generate_to_device(lpa, torch, workload, first_line, n_lines, device, chunk=1 << 20, workers=16):
     """Deterministic synthetic lines [first_line, first_line+n_lines) straight
     into one HBM buffer (host generation in parallel chunks, H2D in order)."""
     upper = n_lines * 320 + (1 << 20)
@@ -43,7 +48,7 @@ def generate_to_device(lpa, torch, first_line, n_lines, device, chunk=1 << 20, w
         window = 2 * workers
         while nxt < len(starts) and len(futs) < window:
             s = starts[nxt]
-            futs.append(ex.submit(lpa.synth_combined, SEED, s, min(chunk, first_line + n_lines - s)))
+            futs.append(ex.submit(lpa.synth, workload, SEEDS[workload], s, min(chunk, first_line + n_lines - s)))
             nxt += 1
         done = 0
         t0 = time.time()
@@ -51,7 +56,7 @@ def generate_to_device(lpa, torch, first_line, n_lines, device, chunk=1 << 20, w
             data = futs.pop(0).result()
             if nxt < len(starts):
                 s = starts[nxt]
-                futs.append(ex.submit(lpa.synth_combined, SEED, s, min(chunk, first_line + n_lines - s)))
+                futs.append(ex.submit(lpa.synth, workload, SEEDS[workload], s, min(chunk, first_line + n_lines - s)))
                 nxt += 1
             if pos + len(data) > upper:
                 raise RuntimeError("synthetic data larger than the device buffer bound")
@@ -65,28 +70,29 @@ def generate_to_device(lpa, torch, first_line, n_lines, device, chunk=1 << 20, w
     return dev, pos
 
 
-def cpu_baseline(lpa, fields, sample_lines, threads):
+def cpu_baseline(lpa, workload, fields, sample_lines, threads):
     """The oracle (C restatement of the reference semantics) on the GPU box's
     host cores, on the first sample_lines lines of the same workload."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
     oracle_lib.lib()
-    probe = lpa.synth_combined(SEED, 0, 2000)
-    secs, _ = oracle_lib.bench("combined", fields, probe, 1)
+    fmt = lpa.SYNTH_FORMATS[workload]
+    probe = lpa.synth(workload, SEEDS[workload], 0, 2000)
+    secs, _ = oracle_lib.bench(fmt, fields, probe, 1)
     rate1 = 2000 / max(secs, 1e-6)
     # aim at ~15 s of work on `threads` threads
     n = int(min(sample_lines, max(20000, rate1 * threads * 15)))
-    data = lpa.synth_combined(SEED, 0, n)
-    secs, counts = oracle_lib.bench("combined", fields, data, threads)
+    data = lpa.synth(workload, SEEDS[workload], 0, n)
+    secs, counts = oracle_lib.bench(fmt, fields, data, threads)
     return {
         "value": round(len(data) / secs / 1e9, 6),
         "unit": "GB/s",
         "lines_per_s": round(counts[0] / secs, 1),
         "cores": threads,
         "kind": "port",
-        "sample": "first %d lines (%.1f MB) of the config-2 workload, all 123 paths, oracle/ C restatement, "
+        "sample": "first %d lines (%.1f MB) of the config-%d workload, all %d paths, oracle/ C restatement, "
                   "%d threads, one parser per thread; ok=%d bad=%d unsupported=%d" % (
-                      counts[0], len(data) / 1e6, threads, counts[1], counts[2], counts[3]),
+                      counts[0], len(data) / 1e6, workload, len(fields), threads, counts[1], counts[2], counts[3]),
         "seconds": round(secs, 2),
     }
 
@@ -113,6 +119,7 @@ def main():
     ap.add_argument("--cpu-sample-lines", type=int, default=2_000_000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--workload", type=int, default=2, choices=(2, 3, 4), help="BASELINE.json config")
     ap.add_argument("--fields", default="all",
                     help="all (the config-2 workload) | comma list of TYPE:path (profiling experiments only)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic_latest.json"),
@@ -134,12 +141,14 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=device)
 
-    fields = lpa.get_possible_paths("combined") if args.fields == "all" else args.fields.split(",")
-    log("rank %d/%d: generating %d lines (seed %d) on %s" % (rank, world, args.lines, SEED, device))
-    buf, nbytes = generate_to_device(lpa, torch, rank * args.lines, args.lines, device)
+    wl = args.workload
+    fmt = lpa.SYNTH_FORMATS[wl]
+    fields = lpa.get_possible_paths(fmt) if args.fields == "all" else args.fields.split(",")
+    log("rank %d/%d: generating %d lines (config %d, seed %d) on %s" % (rank, world, args.lines, wl, SEEDS[wl], device))
+    buf, nbytes = generate_to_device(lpa, torch, wl, rank * args.lines, args.lines, device)
     log("input resident in HBM: %.2f GB" % (nbytes / 1e9))
 
-    parser = lpa.HttpdLoglineParser("combined", fields, device=local)
+    parser = lpa.HttpdLoglineParser(fmt, fields, device=local)
     counters = torch.zeros(4, dtype=torch.int64, device=device)
 
     def step():
@@ -186,12 +195,11 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (lp_synth_combined, seed %d; deterministic per line)" % SEED,
+        "data": "synthetic (lp_synth workload %d, seed %d; deterministic per line)" % (wl, SEEDS[wl]),
         "config": {
-            "workload": "config 2: %d synthetic 'combined' lines per GPU (%.2f GB), all %d paths requested "
-                        "(epoch, first line, URI parts, query params), input resident in HBM" % (
-                            stats["lines"], nbytes / 1e9, len(fields)),
-            "logformat": "combined",
+            "workload": (WORKLOAD_NAMES[wl] % stats["lines"]) + " per GPU (%.2f GB), all %d paths requested "
+                        "(epoch, first line, URI parts, query params), input resident in HBM" % (nbytes / 1e9, len(fields)),
+            "logformat": fmt,
             "lines_per_gpu": stats["lines"],
             "bytes_per_gpu": nbytes,
             "parallelism": "dp%d (newline-aligned shards, RCCL counter all-reduce)" % world,
@@ -204,7 +212,7 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": pmc_traffic(args.pmc_json, stats["lines"], lpa.LIB_PATH),
+            "traffic": pmc_traffic(args.pmc_json, stats["lines"], lpa.LIB_PATH) if wl == 2 and args.fields == "all" else None,
             "kernel": "k_parse_lines",
             "algorithmic_bytes_per_launch": int(algo_bytes),
             "bytes_per_line": round(algo_bytes / max(1, stats["lines"]), 1),
@@ -213,7 +221,7 @@ def main():
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline (oracle, %d threads) ..." % args.cpu_threads)
-        result["cpu_baseline"] = cpu_baseline(lpa, fields, args.cpu_sample_lines, args.cpu_threads)
+        result["cpu_baseline"] = cpu_baseline(lpa, wl, fields, args.cpu_sample_lines, args.cpu_threads)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
