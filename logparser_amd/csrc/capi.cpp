@@ -42,7 +42,7 @@ struct lp_handle {
     int compile_status = LP_OK;
     int device = 0;
     hipStream_t stream = nullptr;
-    DevBuf input, chunk, line_off, cols, arena, misc, waves, args;
+    DevBuf input, chunk, line_off, cols, arena, misc, waves, args, route;
     lp::DeviceArgs host_args{};
     lp::Columns C{};
     int64_t n_lines = 0;
@@ -58,6 +58,9 @@ struct lp_handle {
     float ms[3]{};
     bool host_valid = false;
     lp::HostResults host;
+    // HttpdLogFormatDissector's active format, carried from batch to batch
+    // like the reference parser's (format 0 before the first line)
+    uint32_t fmt_state = 0;
 };
 
 namespace {
@@ -103,6 +106,10 @@ bool alloc_columns(lp_handle* h, int64_t n) {
         cols.push_back({(void**)&C.q_params[q], 8});
     }
     cols.push_back({(void**)&C.arena_base, 8});
+    if (P.n_fmt > 1) {
+        cols.push_back({(void**)&C.fmt_match, 2});
+        cols.push_back({(void**)&C.fmt_id, 1});
+    }
     size_t total = 0;
     uint64_t row = 0;
     for (auto& c : cols) {
@@ -138,6 +145,7 @@ bool fetch_host(lp_handle* h) {
     if (h->nbytes) hipMemcpy(R.input.data(), h->d_buf, h->nbytes, hipMemcpyDeviceToHost);
     R.input.push_back('\n');
     if (!h->plan.device_ok()) { h->host_valid = true; return true; }
+    if (P.n_fmt > 1) fetch(R.fmt_id, h->C.fmt_id, n);
     R.tok_span.resize(lp::MAX_TOK);
     for (int k = 0; k < P.n_tok; ++k) fetch(R.tok_span[k], h->C.tok_span[k], n);
     fetch(R.tok_flags, h->C.tok_flags, n);
@@ -219,7 +227,8 @@ void lp_free(lp_handle* h) {
     if (!h) return;
     hipSetDevice(h->device);
     if (h->pending) hipStreamSynchronize(h->stream);
-    for (auto* b : {&h->input, &h->chunk, &h->line_off, &h->cols, &h->arena, &h->misc, &h->waves, &h->args}) b->release();
+    for (auto* b : {&h->input, &h->chunk, &h->line_off, &h->cols, &h->arena, &h->misc, &h->waves, &h->args, &h->route})
+        b->release();
     if (h->have_events)
         for (auto& ev : h->ev) hipEventDestroy(ev);
     delete h;
@@ -288,12 +297,25 @@ int lp_parse_batch(lp_handle* h, const uint8_t* buf, uint64_t nbytes, int buf_fl
     C.arena_top = h->misc.as<unsigned long long>(64);
     hipMemsetAsync(h->misc.p, 0, 128, s);
     if (h->plan.device_ok()) {
+        if (P.n_fmt > 1) {  // sticky multi-format routing scratch
+            if (!h->route.ensure(8 * (size_t)(lp::fmt_chunks(n) + 1))) return LP_E_NOMEM;
+            C.fmt_chunk = h->route.as<uint64_t>();
+            C.fmt_init = h->fmt_state;
+        }
         if (!h->args.ensure(sizeof(lp::DeviceArgs))) return LP_E_NOMEM;
         h->host_args.prog = P;
         h->host_args.cols = C;
         if (hipMemcpyAsync(h->args.p, &h->host_args, sizeof(lp::DeviceArgs), hipMemcpyHostToDevice, s) != hipSuccess)
             return LP_E_DEVICE;
         hipEventRecord(h->ev[2], s);
+        if (P.n_fmt > 1) {
+            // HttpdLogFormatDissector routing: every format's match per line,
+            // then the scan of the sticky active format
+            if (lp::launch_parse(h->d_buf, nbytes, n, h->args.as<lp::DeviceArgs>(), P.max_stack, C.wave_counts,
+                                 h->misc.as<unsigned long long>(), s, lp::PM_MATCH) != 0 ||
+                lp::launch_route(h->args.as<lp::DeviceArgs>(), n, s) != 0)
+                return LP_E_DEVICE;
+        }
         if (lp::launch_parse(h->d_buf, nbytes, n, h->args.as<lp::DeviceArgs>(), P.max_stack, C.wave_counts,
                              h->misc.as<unsigned long long>(), s) != 0)
             return LP_E_DEVICE;
@@ -324,6 +346,12 @@ int lp_sync(lp_handle* h) {
         h->counters[3] = (uint64_t)h->n_lines;
     }
     h->arena_used = m[8];
+    const lp::Program& P = h->plan.program();
+    if (h->plan.device_ok() && P.n_fmt > 1 && h->n_lines > 0) {  // the active format after the batch's last line
+        uint64_t st = 0;
+        hipMemcpy(&st, h->C.fmt_chunk + lp::fmt_chunks(h->n_lines), sizeof st, hipMemcpyDeviceToHost);
+        h->fmt_state = (uint32_t)st;
+    }
     h->arena_written = h->plan.device_ok() ? m[4] : 0;
     float a = 0, b = 0, c = 0;
     hipEventElapsedTime(&a, h->ev[0], h->ev[3]);

@@ -170,12 +170,16 @@ __device__ __forceinline__ LN owner_line(const LN& L, int own) {
 
 template <typename LN>
 __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, const Columns& C, const LN& L,
-                                           bool active, int64_t li, WaveStack stk, bool clean) {
+                                           bool active, int64_t li, WaveStack stk, bool clean, int mode) {
+    if (mode == PM_MATCH) {  // sticky routing, pass 1: which formats match each line
+        if (active) C.fmt_match[li] = (uint16_t)fmt_match_word(P, elems, L, stk, clean);
+        return;
+    }
     LineOut o;
     o.status = ST_OK;
     o.arena_need = 0;
     LP_PROF(1);
-    if (active) phase1(P, elems, L, o, stk, C, li, clean);
+    if (active) phase1(P, elems, L, o, stk, C, li, clean, P.n_fmt > 1 ? (int)C.fmt_id[li] : 0);
     LP_PROF(9);
     // wave-aggregated arena allocation (every lane reaches this point)
     const uint32_t need = (active && o.status == ST_OK) ? o.arena_need : 0u;
@@ -264,11 +268,11 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
 
 __global__ __launch_bounds__(PW) void k_parse_lines(const uint8_t* __restrict__ buf, uint64_t nbytes, int64_t n_lines,
                                                     const DeviceArgs* __restrict__ args, uint32_t win_cap, int stage,
-                                                    uint32_t stk_words) {
+                                                    uint32_t stk_words, int mode) {
     const Program& P = args->prog;
     const Columns& C = args->cols;
     __shared__ Elem s_elems[MAX_ELEMS];
-    if ((int)threadIdx.x < P.n_elems) s_elems[threadIdx.x] = P.elems[threadIdx.x];
+    for (int k = threadIdx.x; k < P.n_elems; k += PW) s_elems[k] = P.elems[k];
     // LDS: [DFS stack][byte window (win_cap, a multiple of 64)][MC_N class masks]
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     WaveStack stk{reinterpret_cast<uint32_t*>(smem) + threadIdx.x};
@@ -330,7 +334,7 @@ __global__ __launch_bounds__(PW) void k_parse_lines(const uint8_t* __restrict__ 
         __syncthreads();
         const LineT<lds_bytes, lds_u64> L{(lds_bytes)win, (uint32_t)(s - w0), n,
                                           (lds_u64)reinterpret_cast<uint64_t*>(msk16), mwords};
-        parse_wave(P, s_elems, C, L, active, li, stk, clean);
+        parse_wave(P, s_elems, C, L, active, li, stk, clean, mode);
     } else {
         __syncthreads();
         // base = the line start aligned down to 4 bytes: word reads never
@@ -338,7 +342,7 @@ __global__ __launch_bounds__(PW) void k_parse_lines(const uint8_t* __restrict__ 
         const LP_G uint8_t* ls = (const LP_G uint8_t*)(buf) + s;
         const uint32_t mis = (uint32_t)((uintptr_t)ls & 3);
         const LineT<const LP_G uint8_t*> L{ls - mis, mis, n};
-        parse_wave(P, s_elems, C, L, active, li, stk, false);
+        parse_wave(P, s_elems, C, L, active, li, stk, false, mode);
     }
 }
 
@@ -361,6 +365,69 @@ __global__ __launch_bounds__(256) void k_reduce_counts(const uint32_t* __restric
     if (threadIdx.x < 5) {
         unsigned long long v = red[threadIdx.x][0] + red[threadIdx.x][1] + red[threadIdx.x][2] + red[threadIdx.x][3];
         if (v) atomicAdd(&counters[threadIdx.x], v);
+    }
+}
+
+// ------------------------------------------------------ sticky routing scan
+// The routed format of line i = the fold of the per-line transition tables
+// (lp_device.h fmt_table) from the handle's state.  Chunks of FMT_CHUNK
+// lines: one wave per chunk, FMT_LPL lines per lane.
+constexpr int FMT_LPL = FMT_CHUNK / PW;
+
+__device__ __forceinline__ uint64_t lane_table(const Columns& C, const Program& P, int64_t l0, int64_t n_lines) {
+    uint64_t t = 0xFEDCBA9876543210ull;  // identity
+    for (int k = 0; k < FMT_LPL; ++k) {
+        const int64_t li = l0 + k;
+        if (li >= n_lines) break;
+        t = fmt_compose(t, fmt_table(C.fmt_match[li], P.n_fmt));
+    }
+    return t;
+}
+
+// inclusive scan of the lanes' tables in lane order (table of lanes 0..lane)
+__device__ __forceinline__ uint64_t wave_scan_tables(uint64_t t) {
+    const int lane = threadIdx.x;
+    for (int d = 1; d < PW; d <<= 1) {
+        const uint64_t o = __shfl_up(t, d);
+        if (lane >= d) t = fmt_compose(o, t);
+    }
+    return t;
+}
+
+__global__ __launch_bounds__(PW) void k_fmt_reduce(const DeviceArgs* __restrict__ args, int64_t n_lines) {
+    const Program& P = args->prog;
+    const Columns& C = args->cols;
+    const int64_t l0 = (int64_t)blockIdx.x * FMT_CHUNK + (int64_t)threadIdx.x * FMT_LPL;
+    const uint64_t t = wave_scan_tables(lane_table(C, P, l0, n_lines));
+    if (threadIdx.x == PW - 1) C.fmt_chunk[blockIdx.x] = t;
+}
+
+// one thread: chunk tables -> entry state of every chunk (in place), final
+// state after the last chunk at [n_chunks]
+__global__ void k_fmt_chunks(const DeviceArgs* __restrict__ args, int64_t n_chunks) {
+    const Columns& C = args->cols;
+    uint32_t s = C.fmt_init;
+    for (int64_t c = 0; c < n_chunks; ++c) {
+        const uint64_t t = C.fmt_chunk[c];
+        C.fmt_chunk[c] = s;
+        s = fmt_apply(t, s);
+    }
+    C.fmt_chunk[n_chunks] = s;
+}
+
+__global__ __launch_bounds__(PW) void k_fmt_apply(const DeviceArgs* __restrict__ args, int64_t n_lines) {
+    const Program& P = args->prog;
+    const Columns& C = args->cols;
+    const int64_t l0 = (int64_t)blockIdx.x * FMT_CHUNK + (int64_t)threadIdx.x * FMT_LPL;
+    const uint64_t incl = wave_scan_tables(lane_table(C, P, l0, n_lines));
+    uint64_t excl = __shfl_up(incl, 1);
+    if (threadIdx.x == 0) excl = 0xFEDCBA9876543210ull;
+    uint32_t s = fmt_apply(excl, (uint32_t)C.fmt_chunk[blockIdx.x]);
+    for (int k = 0; k < FMT_LPL; ++k) {
+        const int64_t li = l0 + k;
+        if (li >= n_lines) break;
+        s = fmt_apply(fmt_table(C.fmt_match[li], P.n_fmt), s);
+        C.fmt_id[li] = (uint8_t)s;
     }
 }
 
@@ -399,8 +466,17 @@ extern "C" int lp_profile_read(unsigned long long* out, int n) {
 }
 #endif
 
+int launch_route(const DeviceArgs* d_args, int64_t n_lines, hipStream_t s) {
+    if (n_lines == 0) return 0;
+    const int64_t nc = fmt_chunks(n_lines);
+    hipLaunchKernelGGL(k_fmt_reduce, dim3((unsigned)nc), dim3(PW), 0, s, d_args, n_lines);
+    hipLaunchKernelGGL(k_fmt_chunks, dim3(1), dim3(1), 0, s, d_args, nc);
+    hipLaunchKernelGGL(k_fmt_apply, dim3((unsigned)nc), dim3(PW), 0, s, d_args, n_lines);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 int launch_parse(const uint8_t* d_buf, uint64_t nbytes, int64_t n_lines, const DeviceArgs* d_args, int stack_depth,
-                 const uint32_t* d_wave_counts, unsigned long long* counters, hipStream_t s) {
+                 const uint32_t* d_wave_counts, unsigned long long* counters, hipStream_t s, int mode) {
     if (n_lines == 0) return 0;
     const int64_t waves = parse_waves(n_lines);
     // LDS window per wave: ~1.1x the mean bytes of 64 lines (+512 B), so
@@ -419,7 +495,8 @@ int launch_parse(const uint8_t* d_buf, uint64_t nbytes, int64_t n_lines, const D
     const uint32_t stk_words = (uint32_t)(stack_depth > 0 ? stack_depth : 1) * PW;
     const size_t lds = stk_words * 4 + cap + MC_N * (cap / 8);  // + class masks, 1 bit per window byte
     hipLaunchKernelGGL(k_parse_lines, dim3((unsigned)waves), dim3(PW), lds, s, d_buf, nbytes, n_lines, d_args,
-                       (uint32_t)cap, stage, stk_words);
+                       (uint32_t)cap, stage, stk_words, mode);
+    if (mode == PM_MATCH) return hipGetLastError() == hipSuccess ? 0 : -1;
     int64_t rb = (waves + 255) / 256;
     if (rb > 1024) rb = 1024;
     hipLaunchKernelGGL(k_reduce_counts, dim3((unsigned)rb), dim3(256), 0, s, d_wave_counts, waves, counters);

@@ -863,13 +863,14 @@ __host__ __device__ LP_INLINE int cand_next(const Program& P, const Elem& e, con
 
 // Backtracking match of "^" elems "$" with java.util.regex priority
 // semantics.  caps = spans of the captured tokens.  stk: P.max_stack entries.
+// elems: the ne elements of one LogFormat.
 // elems: the program's element table (the kernel passes an LDS copy).
 template <typename LN, typename EL, typename Caps, typename Stk>
-__host__ __device__ LP_INLINE int match_line(const Program& P, const EL& elems, const LN& L, Caps& caps, Stk stk) {
+__host__ __device__ LP_INLINE int match_line(const Program& P, const EL& elems, int ne, const LN& L, Caps& caps,
+                                             Stk stk) {
     int i = 0, pos = 0, sp = 0;
     int steps = 0;
     const int budget = 16 * L.n + 256;
-    const int ne = P.n_elems;
     for (;;) {
         if (++steps > budget) return ST_FALLBACK;
         bool ok;
@@ -917,6 +918,62 @@ __host__ __device__ LP_INLINE int match_line(const Program& P, const EL& elems, 
     }
 }
 
+struct NoCaps {
+    __host__ __device__ LP_INLINE void set(int, uint32_t) {}
+};
+
+// The match word of a line for sticky routing: bit f = format f matches,
+// bit 8+f = undecided on the device (FALLBACK).
+template <typename LN, typename EL, typename Stk>
+__host__ __device__ LP_INLINE uint32_t fmt_match_word(const Program& P, const EL& elems, const LN& L, Stk stk,
+                                                      bool clean) {
+    const uint32_t all = (1u << P.n_fmt) - 1u;
+    if (L.n > MAX_LINE) return all << 8;
+    if (!clean && find_fwd(L, 0, L.n, [](uint32_t w) { return swar::guard_bad(w); }) < L.n) return all << 8;
+    uint32_t m = 0;
+    NoCaps nc;
+    for (int f = 0; f < P.n_fmt; ++f) {
+        const int st = match_line(P, elems + P.fmt_elem0[f], P.fmt_elem0[f + 1] - P.fmt_elem0[f], L, nc, stk);
+        m |= st == ST_OK ? (1u << f) : st == ST_FALLBACK ? (256u << f) : 0u;
+    }
+    return m;
+}
+
+// ------------------------------------------------- sticky format routing
+// HttpdLogFormatDissector.dissect (hp/HttpdLogFormatDissector.java:173-204):
+// the active format (initially format 0) is tried first; when it does not
+// match, the formats are tried in order and the first that matches becomes
+// active; when none matches the line fails and the active format stays.
+// Which formats match a line is known per line (m: bit f = format f matches,
+// bit 8+f = the device could not decide format f), so the active format of
+// line i is a left fold of per-line transition functions over the states
+// 0..n_fmt-1 and FMT_UNKNOWN -- an associative scan.  A table holds the
+// result for state s in nibble s.
+__host__ __device__ LP_INLINE uint64_t fmt_table(uint32_t m, int nf) {
+    const uint32_t c = m & 0xFFu, u = (m >> 8) & 0xFFu;
+    int first = -1;  // -1: no format matches (state kept)
+    for (int f = nf - 1; f >= 0; --f) {
+        if ((c >> f) & 1u) first = f;
+        else if ((u >> f) & 1u) first = FMT_UNKNOWN;
+    }
+    uint64_t t = ~0ull;  // unused states -> FMT_UNKNOWN
+    int common = -2;
+    for (int s = 0; s < nf; ++s) {
+        const int r = ((c >> s) & 1u) ? s : ((u >> s) & 1u) ? (int)FMT_UNKNOWN : first < 0 ? s : first;
+        t = (t & ~(15ull << (4 * s))) | ((uint64_t)r << (4 * s));
+        common = common == -2 ? r : common == r ? r : (int)FMT_UNKNOWN;
+    }
+    // from an undecided state: decided only when every state leads to the same format
+    const int ru = common < 0 ? (int)FMT_UNKNOWN : common;
+    return (t & ~(15ull << 60)) | ((uint64_t)ru << 60);
+}
+__host__ __device__ LP_INLINE uint32_t fmt_apply(uint64_t t, uint32_t s) { return (uint32_t)(t >> (4 * s)) & 15u; }
+// b after a
+__host__ __device__ LP_INLINE uint64_t fmt_compose(uint64_t a, uint64_t b) {
+    uint64_t r = 0;
+    for (int s = 0; s < 16; ++s) r |= (uint64_t)fmt_apply(b, fmt_apply(a, (uint32_t)s)) << (4 * s);
+    return r;
+}
 // ------------------------------------------------------------- calendar
 // Proleptic Gregorian, 32-bit arithmetic: every year the formats admit is
 // in [0, 10000) ([1-9][0-9]{3}, plus/minus one day), so day numbers fit in
@@ -1126,6 +1183,7 @@ __host__ __device__ LP_INLINE int parse_strf_time(const TimeStage& T, const LN& 
 // ----------------------------------------------------------- per-line state
 struct LineOut {
     int status;
+    int fmt;  // the LogFormat the line was routed to
     RegArr<MAX_TOK> caps;
     uint32_t tok_flags;
     RegArr<MAX_FL> fl_kind, fl_method, fl_uri, fl_proto;
@@ -1174,8 +1232,9 @@ __host__ __device__ LP_INLINE bool uri_source(const Program& P, const LineOut& o
 // fast-path guard (the kernel checks the whole staged window at once).
 template <typename LN, typename EL, typename Stk, typename Cols>
 __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, const LN& L, LineOut& o, Stk stk, Cols& C,
-                                          int64_t li, bool clean = false) {
+                                          int64_t li, bool clean = false, int fmt = 0) {
     o.status = ST_OK;
+    o.fmt = fmt;
     o.tok_flags = 0;
     o.arena_need = 0;
     o.caps.fill(0);
@@ -1186,7 +1245,7 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
     o.usep.fill(0);
     o.qlist.fill(0);
     o.qpend.fill(0);
-    if (L.n > MAX_LINE) { o.status = ST_FALLBACK; return; }
+    if (L.n > MAX_LINE || fmt >= P.n_fmt) { o.status = ST_FALLBACK; return; }  // too long / routing undecided
     // fast-path guard: printable ASCII + TAB only (no \r, no line
     // terminators, no bytes that need UTF-8 decoding or URIUtil UTF-8 bytes)
     LP_PROF(2);
@@ -1195,7 +1254,7 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
         return;
     }
     LP_PROF(3);
-    int st = match_line(P, elems, L, o.caps, stk);
+    int st = match_line(P, elems + P.fmt_elem0[fmt], P.fmt_elem0[fmt + 1] - P.fmt_elem0[fmt], L, o.caps, stk);
     LP_PROF(4);
     if (st != ST_OK) { o.status = st; return; }
     // decodeExtractedValue: "-" -> null (Apache: ApacheHttpdLogFormatDissector.java:169-196,
@@ -1205,7 +1264,7 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
         int a = sp & 0xFFFF, b = sp >> 16;
         if (b - a == 1 && L[a] == '-') o.tok_flags |= 1u << k;
         if (b - a == 1 && L[a] == '0') o.tok_flags |= 1u << (16 + k);
-        if (P.apache && b - a >= 15 && value_is_header_name(L, a, b)) {
+        if (P.fmt_apache[fmt] && b - a >= 15 && value_is_header_name(L, a, b)) {
             // the reference tests the VALUE (not the token name) against
             // "request.firstline" / "request.header." / "response.header." and
             // then unescapes \xhh sequences (ApacheHttpdLogFormatDissector.java:189-193)
@@ -1216,6 +1275,7 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
     // TimeStampDissector
     for (int t = 0; t < P.n_time; ++t) {
         const TimeStage& T = P.time[t];
+        if (T.fmt != fmt) continue;
         const int k = T.tok;
         const uint32_t sp = o.caps.get(k);
         const int a = sp & 0xFFFF, b = sp >> 16;
@@ -1238,6 +1298,7 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
     LP_PROF(6);
     // HttpFirstLineDissector: ^([a-zA-Z-_]+) (.*) (HTTP/[0-9]+\.[0-9]+)$ else ^([a-zA-Z-_]+) (.*)$
     for (int f = 0; f < P.n_fl; ++f) {
+        if (P.fl[f].fmt != fmt) continue;
         int k = P.fl[f].tok;
         if (o.tok_flags & (1u << k)) continue;                // null
         const uint32_t sp0 = o.caps.get(k);
@@ -1277,7 +1338,7 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
     uint32_t need = 0;
     for (int u = 0; u < P.n_uri; ++u) {
         int a, b;
-        if (!uri_source(P, o, u, a, b)) continue;
+        if (P.uri[u].fmt != fmt || !uri_source(P, o, u, a, b)) continue;
         // URIUtil-escaped bytes and '&'/'?' separators are both URI event
         // bytes: their count bounds both
         const uint32_t ev = count_uev(L, a, b);
@@ -1838,6 +1899,7 @@ __host__ __device__ LP_INLINE void query_pieces_serial(const Program& P, const L
 template <typename LN, typename Cols>
 __host__ __device__ LP_INLINE void phase2(const Program& P, const LN& L, LineOut& o, Arena& A, Cols& C, int64_t li) {
     for (int u = 0; u < P.n_uri && o.status == ST_OK; ++u) {
+        if (P.uri[u].fmt != o.fmt) continue;  // another LogFormat's URI: nothing to write
         int a, b;
         if (!uri_source(P, o, u, a, b)) {
             C.u_flags[u][li] = 0;

@@ -31,7 +31,10 @@
 
 namespace lp {
 
-constexpr int MAX_ELEMS = 48;
+constexpr int MAX_ELEMS = 96;
+constexpr int MAX_FMT = 8;        // LogFormats of one HttpdLogFormatDissector (sticky routing)
+constexpr int MAX_FMT_ELEMS = 64; // elements of one LogFormat (6-bit DFS stack index)
+constexpr uint8_t FMT_UNKNOWN = 15; // routing state that depends on a line the device could not decide
 constexpr int MAX_LIT = 2048;
 constexpr int MAX_TOK = 16;      // captured tokens (bit k of the null/zero masks)
 constexpr int MAX_TIME = 4;
@@ -94,6 +97,7 @@ enum : uint8_t { SF_LIT, SF_DAY, SF_MON, SF_MONTXT, SF_YEAR, SF_CLOCKH, SF_HOD, 
 constexpr int MAX_SF_OPS = 32;
 struct TimeStage {
     int8_t tok;
+    int8_t fmt;     // the LogFormat whose token this is
     uint8_t kind;   // TK_*
     uint8_t width;  // TK_STRF: exact byte length of the value
     uint8_t n_ops;
@@ -104,7 +108,8 @@ struct TimeStage {
 // (hp/dissectors/HttpFirstLineDissector.java:56-134).
 struct FlStage {
     int8_t tok;
-    uint8_t pad[3];
+    int8_t fmt;
+    uint8_t pad[2];
 };
 
 // HttpUriDissector (hp/dissectors/HttpUriDissector.java:130-233) on either a
@@ -117,7 +122,7 @@ struct UriStage {
     uint8_t want_ref;
     uint8_t want_userinfo;
     int8_t query_stage; // QueryStringFieldDissector on its query, -1 none
-    uint8_t pad;
+    int8_t fmt;         // the LogFormat of its source token
 };
 
 // QueryStringFieldDissector (hp/dissectors/QueryStringFieldDissector.java:56-108)
@@ -130,13 +135,17 @@ struct QueryStage {
     uint8_t name_len[MAX_QNAMES];
 };
 
+// Stages (time / first line / URI) belong to one LogFormat: a line runs the
+// stages of the format it was routed to.  Token slot k of a line is the k-th
+// captured token of that line's format.
 struct Program {
-    int32_t n_elems;
-    int32_t n_tok;        // captured token slots
+    int32_t n_elems;      // all formats
+    int32_t n_tok;        // captured token slots (max over the formats)
     int32_t n_time, n_fl, n_uri, n_query;
-    int32_t apache;       // 1 = Apache decodeExtractedValue rules, 0 = NGINX
-    int32_t tok_decode;   // bitmask: token slots whose value goes through decodeExtractedValue
+    int32_t n_fmt;        // LogFormats; > 1: HttpdLogFormatDissector sticky routing
     int32_t max_stack;    // DFS depth bound = number of non-deterministic elements (<= MAX_STACK)
+    uint8_t fmt_elem0[MAX_FMT + 1];  // elements of format f: [fmt_elem0[f], fmt_elem0[f + 1])
+    uint8_t fmt_apache[MAX_FMT];     // 1 = Apache decodeExtractedValue rules, 0 = NGINX
     Elem elems[MAX_ELEMS];
     TimeStage time[MAX_TIME];
     FlStage fl[MAX_FL];
@@ -222,6 +231,11 @@ struct Columns {
     LP_G uint32_t* q_count[MAX_QUERY]; // params are (name ref, value ref) pairs in the arena
     LP_G uint64_t* q_params[MAX_QUERY];// ref to the param table in the arena
     LP_G uint64_t* arena_base;         // [n]
+    // sticky multi-format routing (Program::n_fmt > 1)
+    LP_G uint16_t* fmt_match;          // [n] bit f: format f matches; bit 8+f: undecided on the device
+    LP_G uint8_t* fmt_id;              // [n] the routed format, FMT_UNKNOWN
+    LP_G uint64_t* fmt_chunk;          // per chunk of FMT_CHUNK lines: composed transition table, then entry state
+    uint32_t fmt_init;                 // routing state before the first line (the handle's state)
     LP_G uint8_t* arena;
     uint64_t arena_cap;
     LP_G unsigned long long* arena_top;  // bump pointer

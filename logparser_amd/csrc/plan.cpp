@@ -1045,13 +1045,8 @@ void Plan::compile_program() {
     Program& P = prog_;
     memset(&P, 0, sizeof P);
     if (!device_ok_) return;
-    if (formats_.size() != 1) {
-        device_ok_ = false;
-        why_ = "multiple LogFormats (sticky multi-format routing) not yet on the device";
-        return;
-    }
-    const Format& f = *formats_[0];
-    P.apache = f.kind == FMT_APACHE;
+    if ((int)formats_.size() > MAX_FMT) { device_ok_ = false; why_ = "too many LogFormats"; return; }
+    P.n_fmt = (int)formats_.size();
     int lit_used = 0;
     auto add_lit = [&](const std::string& s) -> int {
         if (lit_used + (int)s.size() > MAX_LIT) return -1;
@@ -1060,46 +1055,66 @@ void Plan::compile_program() {
         lit_used += (int)s.size();
         return off;
     };
-    std::set<std::string> seen_names;
-    for (int i = 0; i < (int)f.tokens.size(); ++i) {
-        const Token& t = f.tokens[i];
-        if (P.n_elems == MAX_ELEMS) { device_ok_ = false; why_ = "too many LogFormat elements"; return; }
-        Elem& e = P.elems[P.n_elems++];
-        memset(&e, 0, sizeof e);
-        e.cap = -1;
-        e.acls = -1;
-        if (t.fixed) {
-            e.kind = EK_LIT;
-            int off = add_lit(t.regex);
-            if (off < 0) { device_ok_ = false; why_ = "literal pool overflow"; return; }
-            e.lit_off = (uint16_t)off;
-            e.lit_len = (uint16_t)t.regex.size();
-            for (int k = 0; k < 4 && k < (int)t.regex.size(); ++k) e.lit4 |= (uint32_t)(uint8_t)t.regex[k] << (8 * k);
-            continue;
+    // the elements of every LogFormat, one after the other (format f's
+    // captured tokens take slots 0.. of that format)
+    for (int fi = 0; fi < P.n_fmt; ++fi) {
+        const Format& f = *formats_[fi];
+        P.fmt_apache[fi] = f.kind == FMT_APACHE;
+        P.fmt_elem0[fi] = (uint8_t)P.n_elems;
+        std::set<std::string> seen_names;
+        int n_tok = 0;
+        for (int i = 0; i < (int)f.tokens.size(); ++i) {
+            const Token& t = f.tokens[i];
+            if (P.n_elems == MAX_ELEMS || P.n_elems - P.fmt_elem0[fi] == MAX_FMT_ELEMS) {
+                device_ok_ = false;
+                why_ = "too many LogFormat elements";
+                return;
+            }
+            Elem& e = P.elems[P.n_elems++];
+            memset(&e, 0, sizeof e);
+            e.cap = -1;
+            e.acls = -1;
+            if (t.fixed) {
+                e.kind = EK_LIT;
+                int off = add_lit(t.regex);
+                if (off < 0) { device_ok_ = false; why_ = "literal pool overflow"; return; }
+                e.lit_off = (uint16_t)off;
+                e.lit_len = (uint16_t)t.regex.size();
+                for (int k = 0; k < 4 && k < (int)t.regex.size(); ++k) e.lit4 |= (uint32_t)(uint8_t)t.regex[k] << (8 * k);
+                continue;
+            }
+            int k = elem_kind_of(t.regex);
+            if (k < 0) { device_ok_ = false; why_ = "token regex not on the device: " + t.regex; return; }
+            e.kind = (uint8_t)k;
+            bool wanted = false;
+            for (const auto& o : t.outs) if (f.requested.count(o.name)) wanted = true;
+            if (wanted) {
+                if (n_tok == MAX_TOK) { device_ok_ = false; why_ = "too many captured tokens"; return; }
+                for (const auto& o : t.outs)
+                    if (!seen_names.insert(o.type + ":" + o.name).second) {
+                        device_ok_ = false;
+                        why_ = "the same output is produced by two tokens";
+                        return;
+                    }
+                tok_slot_[fi * 256 + i] = n_tok;
+                e.cap = (int8_t)n_tok++;
+            }
         }
-        int k = elem_kind_of(t.regex);
-        if (k < 0) { device_ok_ = false; why_ = "token regex not on the device: " + t.regex; return; }
-        e.kind = (uint8_t)k;
-        bool wanted = false;
-        for (const auto& o : t.outs) if (f.requested.count(o.name)) wanted = true;
-        if (wanted) {
-            if (P.n_tok == MAX_TOK) { device_ok_ = false; why_ = "too many captured tokens"; return; }
-            for (const auto& o : t.outs)
-                if (!seen_names.insert(o.type + ":" + o.name).second) {
-                    device_ok_ = false;
-                    why_ = "the same output is produced by two tokens";
-                    return;
-                }
-            tok_slot_[i] = P.n_tok;
-            e.cap = (int8_t)P.n_tok++;
-        }
+        if (n_tok > P.n_tok) P.n_tok = n_tok;
     }
+    P.fmt_elem0[P.n_fmt] = (uint8_t)P.n_elems;
+    auto fmt_of_elem = [&](int i) {
+        int fi = 0;
+        while (i >= P.fmt_elem0[fi + 1]) ++fi;
+        return fi;
+    };
     // anchoring literal / determinism of each token element
     for (int i = 0; i < P.n_elems; ++i) {
         Elem& e = P.elems[i];
         if (e.kind == EK_LIT) continue;
-        e.last = i == P.n_elems - 1;
-        if (i + 1 < P.n_elems && P.elems[i + 1].kind == EK_LIT) {
+        const int end = P.fmt_elem0[fmt_of_elem(i) + 1];
+        e.last = i == end - 1;
+        if (i + 1 < end && P.elems[i + 1].kind == EK_LIT) {
             e.nlit = 1;
             e.lit_off = P.elems[i + 1].lit_off;
             e.lit_len = P.elems[i + 1].lit_len;
@@ -1129,15 +1144,21 @@ void Plan::compile_program() {
         if (e.kind != EK_ANY_GREEDY || !e.nlit) continue;
         const uint8_t c0 = P.lit[e.lit_off];
         int need = 0;
-        for (int j = i + 1; j < P.n_elems; ++j)
+        for (int j = i + 1; j < P.fmt_elem0[fmt_of_elem(i) + 1]; ++j)
             if (P.elems[j].kind == EK_LIT)
                 for (int k = 0; k < P.elems[j].lit_len; ++k) need += P.lit[P.elems[j].lit_off + k] == c0;
         e.need = (uint8_t)(need > 255 ? 255 : need);
     }
     P.max_stack = 0;
-    for (int i = 0; i < P.n_elems; ++i)
-        if (P.elems[i].kind != EK_LIT && !P.elems[i].det) ++P.max_stack;
+    for (int fi = 0; fi < P.n_fmt; ++fi) {
+        int depth = 0;
+        for (int i = P.fmt_elem0[fi]; i < P.fmt_elem0[fi + 1]; ++i)
+            if (P.elems[i].kind != EK_LIT && !P.elems[i].det) ++depth;
+        if (depth > P.max_stack) P.max_stack = depth;
+    }
     if (P.max_stack > MAX_STACK) { device_ok_ = false; why_ = "too many backtracking elements"; return; }
+    int cur_fmt = 0;
+    auto tk = [&](int oi) { return cur_fmt * 64 + oi; };  // (format, token slot) key of the stage maps
     // stages, walking the compiled tree from each captured token output
     std::function<void(int, int, const std::string&, const std::string&)> walk =
         [&](int ok, int oi, const std::string& type, const std::string& complete) {
@@ -1149,30 +1170,33 @@ void Plan::compile_program() {
                 switch (in.cls) {
                 case D_TIMESTAMP: {
                     if (ok != O_TOKEN) { device_ok_ = false; why_ = "timestamp from a derived value"; return; }
-                    if (!time_of_tok_.count(oi)) {
+                    if (!time_of_tok_.count(tk(oi))) {
                         if (P.n_time == MAX_TIME) { device_ok_ = false; why_ = "too many timestamps"; return; }
                         P.time[P.n_time].tok = (int8_t)oi;
-                        time_of_tok_[oi] = P.n_time++;
+                        P.time[P.n_time].fmt = (int8_t)cur_fmt;
+                        time_of_tok_[tk(oi)] = P.n_time++;
                     }
                     break;
                 }
                 case D_STRFTIME: {
                     if (ok != O_TOKEN) { device_ok_ = false; why_ = "strftime from a derived value"; return; }
-                    if (!time_of_tok_.count(oi)) {
+                    if (!time_of_tok_.count(tk(oi))) {
                         if (P.n_time == MAX_TIME) { device_ok_ = false; why_ = "too many timestamps"; return; }
-                        const Token* tk = nullptr;
+                        const Token* tok = nullptr;
                         for (const auto& kv : tok_slot_)
-                            if (kv.second == oi) tk = &formats_[0]->tokens[kv.first];
+                            if (kv.first / 256 == cur_fmt && kv.second == oi)
+                                tok = &formats_[cur_fmt]->tokens[kv.first % 256];
                         TimeStage& T = P.time[P.n_time];
                         memset(&T, 0, sizeof T);
                         T.tok = (int8_t)oi;
+                        T.fmt = (int8_t)cur_fmt;
                         T.kind = TK_STRF;
-                        if (!tk || !tk->strftime || !strf_compile(tk->custom_param, T)) {
+                        if (!tok || !tok->strftime || !strf_compile(tok->custom_param, T)) {
                             device_ok_ = false;
                             why_ = "strftime pattern outside the device subset";
                             return;
                         }
-                        time_of_tok_[oi] = P.n_time++;
+                        time_of_tok_[tk(oi)] = P.n_time++;
                     }
                     break;
                 }
@@ -1182,12 +1206,13 @@ void Plan::compile_program() {
                 case D_FIRSTLINE: {
                     if (ok != O_TOKEN) { device_ok_ = false; why_ = "first line from a derived value"; return; }
                     int fidx;
-                    if (!fl_of_tok_.count(oi)) {
+                    if (!fl_of_tok_.count(tk(oi))) {
                         if (P.n_fl == MAX_FL) { device_ok_ = false; why_ = "too many first lines"; return; }
                         P.fl[P.n_fl].tok = (int8_t)oi;
-                        fl_of_tok_[oi] = P.n_fl++;
+                        P.fl[P.n_fl].fmt = (int8_t)cur_fmt;
+                        fl_of_tok_[tk(oi)] = P.n_fl++;
                     }
-                    fidx = fl_of_tok_[oi];
+                    fidx = fl_of_tok_[tk(oi)];
                     walk(O_FL_URI, fidx, "HTTP.URI", complete + ".uri");
                     walk(O_FL_PROTO, fidx, "HTTP.PROTOCOL_VERSION", complete + ".protocol");
                     walk(O_FL_METHOD, fidx, "HTTP.METHOD", complete + ".method");
@@ -1199,16 +1224,18 @@ void Plan::compile_program() {
                 case D_URI: {
                     std::map<int, int>& m = ok == O_TOKEN ? uri_of_tok_ : uri_of_fl_;
                     if (ok != O_TOKEN && ok != O_FL_URI) { device_ok_ = false; why_ = "URI from a derived value"; return; }
-                    if (!m.count(oi)) {
+                    const int key = ok == O_TOKEN ? tk(oi) : oi;  // first-line stages are already per format
+                    if (!m.count(key)) {
                         if (P.n_uri == MAX_URI) { device_ok_ = false; why_ = "too many URIs"; return; }
                         UriStage& U = P.uri[P.n_uri];
                         memset(&U, 0, sizeof U);
                         U.src_tok = ok == O_TOKEN ? (int8_t)oi : -1;
                         U.src_fl = ok == O_FL_URI ? (int8_t)oi : -1;
                         U.query_stage = -1;
-                        m[oi] = P.n_uri++;
+                        U.fmt = (int8_t)cur_fmt;
+                        m[key] = P.n_uri++;
                     }
-                    int u = m[oi];
+                    int u = m[key];
                     UriStage& U = P.uri[u];
                     if (in.requested.count("query")) U.want_query = 1;
                     if (in.requested.count("path")) U.want_path = 1;
@@ -1265,10 +1292,13 @@ void Plan::compile_program() {
                 }
             }
         };
-    for (int i = 0; i < (int)f.tokens.size(); ++i) {
-        auto it = tok_slot_.find(i);
-        if (it == tok_slot_.end()) continue;
-        for (const auto& o : f.tokens[i].outs) walk(O_TOKEN, it->second, o.type, o.name);
+    for (cur_fmt = 0; cur_fmt < P.n_fmt; ++cur_fmt) {
+        const Format& f = *formats_[cur_fmt];
+        for (int i = 0; i < (int)f.tokens.size(); ++i) {
+            auto it = tok_slot_.find(cur_fmt * 256 + i);
+            if (it == tok_slot_.end()) continue;
+            for (const auto& o : f.tokens[i].outs) walk(O_TOKEN, it->second, o.type, o.name);
+        }
     }
 }
 
@@ -1325,7 +1355,7 @@ const char* MONTH_FULL[] = {"January", "February", "March", "April", "May", "Jun
                             "August", "September", "October", "November", "December"};
 }  // namespace
 
-static thread_local int t_origin_kind = 0, t_origin_idx = 0;
+static thread_local int t_origin_kind = 0, t_origin_idx = 0, t_fmt = 0;  // t_fmt: the line's LogFormat
 
 void Plan::emit(Ctx& c, const std::string& base, const std::string& type, const std::string& name, const MVal& v) const {
     std::string complete, wild;
@@ -1370,7 +1400,7 @@ void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const 
         return;
     case D_TIMESTAMP: case D_STRFTIME: {
         if (v.null || v.len == 0) return;
-        int t = time_of_tok_.at(oi);
+        int t = time_of_tok_.at(t_fmt * 64 + oi);
         int64_t epoch = R.t_epoch[t][i];
         const int64_t nanos = in.cls == D_STRFTIME ? (int64_t)R.t_nano[t][i] : 0;
         if (has("epoch")) { set_origin(O_TIME, t); emit(c, name, "TIME.EPOCH", "epoch", mlong(epoch)); }
@@ -1412,7 +1442,7 @@ void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const 
         return;
     }
     case D_FIRSTLINE: {
-        int f = fl_of_tok_.at(oi);
+        int f = fl_of_tok_.at(t_fmt * 64 + oi);
         uint32_t kind = R.fl_kind[f][i];
         if (kind == FL_NONE) return;
         auto span = [&](uint32_t s) { return mstr(c.line + (s & 0xFFFF), (s >> 16) - (s & 0xFFFF)); };
@@ -1443,7 +1473,7 @@ void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const 
     }
     case D_URI: {
         if (v.null || v.len == 0) return;
-        int u = ok == O_TOKEN ? uri_of_tok_.at(oi) : uri_of_fl_.at(oi);
+        int u = ok == O_TOKEN ? uri_of_tok_.at(t_fmt * 64 + oi) : uri_of_fl_.at(oi);
         uint32_t fl = R.u_flags[u][i];
         if (!(fl & UF_DONE)) return;
         if (has("query") || has("path") || has("ref")) {
@@ -1570,13 +1600,17 @@ void json_str(std::string& o, const uint8_t* p, uint32_t n) {
 
 std::string Plan::record_json(const HostResults& R, int64_t i) const {
     Ctx c{R, i, R.input.data() + R.line_off[i], R.arena.empty() ? nullptr : R.arena.data() + R.arena_base[i], {}};
-    const Format& f = *formats_[0];
+    // the LogFormat the line was routed to (HttpdLogFormatDissector's active format)
+    const int fi = prog_.n_fmt > 1 ? R.fmt_id[i] : 0;
+    t_fmt = fi;
+    const Format& f = *formats_[fi];
     for (const auto& kv : tok_slot_) {
+        if (kv.first / 256 != fi) continue;
         int k = kv.second;
         uint32_t sp = R.tok_span[k][i];
         bool null = (R.tok_flags[i] >> k) & 1;
         MVal v = null ? mnull() : mstr(c.line + (sp & 0xFFFF), (sp >> 16) - (sp & 0xFFFF));
-        for (const auto& o : f.tokens[kv.first].outs) {
+        for (const auto& o : f.tokens[kv.first % 256].outs) {
             t_origin_kind = O_TOKEN;
             t_origin_idx = k;
             emit(c, "", o.type, o.name, v);

@@ -87,6 +87,7 @@ struct HostResults {
     std::vector<std::vector<int32_t>> u_port;
     std::vector<std::vector<uint32_t>> q_count;
     std::vector<std::vector<uint64_t>> q_params;
+    std::vector<uint8_t> fmt_id;  // multi-format programs: the routed LogFormat per line
 };
 
 class Plan {
@@ -124,7 +125,8 @@ private:
     bool device_ok_ = true;
     std::string why_;
     // device stage bookkeeping for the replay
-    std::map<int, int> tok_slot_;          // token index -> slot
+    std::map<int, int> tok_slot_;          // format * 256 + token index -> slot
+    // stage maps keyed by format * 64 + slot (token stages) or stage index
     std::map<int, int> time_of_tok_, fl_of_tok_, uri_of_tok_;
     std::map<int, int> uri_of_fl_;
     std::map<int, int> query_of_uri_;

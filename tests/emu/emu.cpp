@@ -18,6 +18,7 @@ struct Emu {
     Plan plan;
     int status;
     std::string err;
+    uint32_t fmt_state = 0;  // sticky active LogFormat (HttpdLogFormatDissector), carried line to line
 };
 
 extern "C" {
@@ -69,8 +70,13 @@ void emu_set_masks(int on) { g_masks = on; }
 
 template <typename LN>
 static int run_line(const Program& P, const LN& L, LineOut& o, uint32_t* stk, Columns& C, HostResults& R, char* out,
-                    int cap) {
-    phase1(P, P.elems, L, o, stk, C, 0);
+                    int cap, uint32_t& fmt_state) {
+    if (P.n_fmt > 1) {  // sticky routing, one line at a time (the kernels do it as a scan)
+        const uint32_t m = fmt_match_word(P, P.elems, L, stk, false);
+        fmt_state = fmt_apply(fmt_table(m, P.n_fmt), fmt_state);
+        R.fmt_id.assign(1, (uint8_t)fmt_state);
+    }
+    phase1(P, P.elems, L, o, stk, C, 0, false, P.n_fmt > 1 ? (int)fmt_state : 0);
     if (o.status == ST_OK && o.arena_need) {
         R.arena.assign(o.arena_need + 64, 0);
         Arena A{R.arena.data(), 0, o.arena_need};
@@ -135,10 +141,10 @@ static int parse_impl(Emu* e, const char* line, int len, const uint8_t* base, ui
         std::vector<uint64_t> masks(MC_N * ms);
         build_masks((const uint8_t*)wbuf.data(), wn, masks.data(), ms);
         MLine L{(const uint8_t*)wbuf.data(), base_off - lo, len, masks.data(), ms};
-        st = run_line(P, L, o, stk, C, R, out, cap);
+        st = run_line(P, L, o, stk, C, R, out, cap, e->fmt_state);
     } else {
         Line L{base, base_off, len};
-        st = run_line(P, L, o, stk, C, R, out, cap);
+        st = run_line(P, L, o, stk, C, R, out, cap, e->fmt_state);
     }
     if (st) return st;
     if (o.status != ST_OK) return o.status;

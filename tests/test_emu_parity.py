@@ -258,3 +258,47 @@ def test_strftime_config3_emulated(oracle, emu):
     mut = [mutate_strf(rng, l) for l in lines[:2500] if b"[" in l and len(l) > 60] + [mutate(rng, l) for l in lines[2500:]]
     s = compare(o, e, mut)
     assert s["bad"] > 300 and s["ok"] > 1000, s
+
+
+def test_multiline_sequence_emulated(oracle, emu, vectors):
+    """HttpdLogFormatDissector sticky routing (hpt/MultiLineHttpdLogParserTest.java:64-124):
+    one parser for the whole 12-line sequence."""
+    seq = [c for c in vectors["cases"] if c["source"].startswith("hpt/MultiLineHttpdLogParserTest")]
+    assert len(seq) == 12
+    e = emu.Emu(seq[0]["logformat"], seq[0]["fields"])
+    assert e.status == 0, e.err
+    for c in seq:
+        st, rec = e.parse(c["line"])
+        assert golden_check.check_case(c, st, rec or {}) == [], c["source"]
+
+
+MIXED = "combined\n" + NGINX + "\ncommon"
+
+
+def mixed_lines(n, seed):
+    """A mixed corpus (BASELINE config 5 shape): 'combined', NGINX config-4 and
+    'common' lines, interleaved in runs."""
+    rng = random.Random(seed)
+    c2 = lpa.synth(lpa.SYNTH_COMBINED, seed, 0, n).split(b"\n")[:-1]
+    c4 = lpa.synth(lpa.SYNTH_NGINX, seed, 0, n).split(b"\n")[:-1]
+    out, i = [], 0
+    while len(out) < n:
+        k = rng.choice((0, 0, 1, 2))
+        for _ in range(rng.randrange(1, 30)):
+            if k == 0: out.append(c2[i % n])
+            elif k == 1: out.append(c4[i % n])
+            else: out.append(c2[i % n].rsplit(b' "', 2)[0])  # 'common': combined without referer / agent
+            i += 1
+    return out[:n]
+
+
+def test_mixed_formats_emulated(oracle, emu):
+    paths = oracle.possible_paths(MIXED)
+    o = oracle.Oracle(MIXED, paths)
+    e = emu.Emu(MIXED, paths)
+    assert e.status == 0, e.err
+    lines = mixed_lines(3000, 55)
+    rng = random.Random(56)
+    lines = [mutate(rng, l) if rng.random() < 0.1 else l for l in lines]
+    s = compare(o, e, lines)
+    assert s["ok"] > 2000 and s["bad"] > 20, s

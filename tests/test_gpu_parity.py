@@ -213,3 +213,29 @@ def test_strftime_config3_gpu(oracle):
     mut = [mutate_strf(rng, l) for l in lines[:3000] if b"[" in l and len(l) > 60] + [mutate(rng, l) for l in lines[3000:6000]]
     s, _ = gpu_vs_oracle(oracle, STRF, fields, mut)
     assert s["bad"] > 300 and s["ok"] > 1000, s
+
+
+def test_mixed_formats_gpu(oracle):
+    """Sticky multi-format routing on the device (match pass + scan of the
+    active format) against the stateful oracle on a mixed corpus, across
+    routing chunks and across two batches of one handle."""
+    from test_emu_parity import MIXED, mixed_lines, mutate
+    fields = paths(oracle, MIXED)
+    rng = random.Random(57)
+    lines = [mutate(rng, l) if rng.random() < 0.05 else l for l in mixed_lines(30000, 58)]
+    p = lpa.HttpdLoglineParser(MIXED, fields)
+    o = oracle.Oracle(MIXED, fields)
+    for part in (lines[:17000], lines[17000:]):
+        r = p.parse_batch(b"".join(l + b"\n" for l in part))
+        assert r.n_lines == len(part)
+        ok = 0
+        for i, l in enumerate(part):
+            s1, r1 = o.parse_raw(l)
+            s2 = int(r.status[i])
+            if s2 == lpa.LINE_FALLBACK:
+                continue
+            assert s1 == s2, (i, l, s1, s2)
+            if s1 == oracle.OK:
+                assert r1 == r.record_json(i), (i, l)
+                ok += 1
+        assert ok > 0.8 * len(part)
