@@ -839,7 +839,33 @@ int Plan::build_dissectors(const std::string& logformats, std::string& err) {
         if (nl == std::string::npos) break;
         s = nl + 1;
     }
-    if (jetty) { device_ok_ = false; why_ = "ENABLE JETTY FIX"; }
+    if (jetty) {
+        // addAdditionalLogFormatsToHandleJettyUseragentProblem (hp/HttpdLogFormatDissector.java:72-92)
+        // over getAllLogFormats() (alias-expanded, :254-262): "\"%{User-Agent}i\"" ->
+        // "\"%{User-Agent}i\" ", then over the grown list "%u" -> " %u " (every occurrence);
+        // addLogFormat skips a string already registered
+        const char* from[2] = {"\"%{User-Agent}i\"", "%u"};
+        const char* to[2] = {"\"%{User-Agent}i\" ", " %u "};
+        for (int pass = 0; pass < 2; ++pass) {
+            const size_t n0 = list.size();
+            for (size_t i = 0; i < n0; ++i) {
+                const std::string f = list[i];
+                std::string lf;
+                if (looks_apache(f)) lf = apache_alias(f);
+                else if (looks_nginx(f)) lf = ieq(f, "combined") ? "$remote_addr - $remote_user [$time_local] \"$request\" $status "
+                                                                  "$body_bytes_sent \"$http_referer\" \"$http_user_agent\""
+                                                                : f;
+                else continue;
+                if (lf.find(from[pass]) == std::string::npos) continue;
+                std::string out;
+                for (size_t q = 0; q < lf.size();) {
+                    if (lf.compare(q, strlen(from[pass]), from[pass]) == 0) { out += to[pass]; q += strlen(from[pass]); }
+                    else out += lf[q++];
+                }
+                if (std::find(list.begin(), list.end(), out) == list.end()) list.push_back(out);
+            }
+        }
+    }
     for (const auto& f : list) {
         int kind = looks_apache(f) ? FMT_APACHE : looks_nginx(f) ? FMT_NGINX : 0;
         if (!kind) continue;

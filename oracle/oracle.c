@@ -1188,9 +1188,31 @@ static int build_dissectors(orc_parser *p, const char *logformat, char *err, int
     }
     free(copy);
     if (jetty) {
-        snprintf(err, errlen, "unsupported: ENABLE JETTY FIX");
-        sl_free(&formats);
-        return -1;
+        /* addAdditionalLogFormatsToHandleJettyUseragentProblem
+         * (hp/HttpdLogFormatDissector.java:72-92): over getAllLogFormats() (the
+         * alias-expanded format of every registered dissector, :254-262),
+         * first "\"%{User-Agent}i\"" -> "\"%{User-Agent}i\" ", then (over
+         * the grown list) "%u" -> " %u "; String.replace = every occurrence;
+         * addLogFormat skips a format string already registered */
+        static const char *from[2] = {"\"%{User-Agent}i\"", "%u"}, *to[2] = {"\"%{User-Agent}i\" ", " %u "};
+        for (int pass = 0; pass < 2; pass++) {
+            int n0 = formats.n;
+            for (int i = 0; i < n0; i++) {
+                int kind = looks_apache(formats.v[i]) ? FMT_APACHE : looks_nginx(formats.v[i]) ? FMT_NGINX : 0;
+                if (!kind) continue;
+                const char *lf = kind == FMT_APACHE ? apache_alias(formats.v[i]) : nginx_alias(formats.v[i]);
+                if (!strstr(lf, from[pass])) continue;
+                size_t fl = strlen(from[pass]), tl = strlen(to[pass]), n = 0;
+                char *out = (char *)xmalloc(strlen(lf) * 3 + 8);
+                for (const char *q = lf; *q;) {
+                    if (!strncmp(q, from[pass], fl)) { memcpy(out + n, to[pass], tl); n += tl; q += fl; }
+                    else out[n++] = *q++;
+                }
+                out[n] = 0;
+                if (!sl_has(&formats, out)) sl_add(&formats, out);
+                free(out);
+            }
+        }
     }
     root->fmts = (fmtd **)xmalloc(sizeof(fmtd *) * (size_t)(formats.n + 1));
     for (int i = 0; i < formats.n; i++) {

@@ -215,6 +215,29 @@ for i, which in enumerate([1, 1, 2, 2, 1, 1, 2, 2, 1, 1, 2, 2]):
          absent=["HTTP.USERAGENT:request.user-agent"] if which == 1 else ["BYTESCLF:response.body.bytes", "HTTP.URI:request.referer"],
          note="sequence: one parser for all 12 steps (sticky active format)")
 
+# Jetty fix (hpt/JettyLogFormatParserTest.java:62-104): "ENABLE JETTY FIX" adds patched formats
+JETTY_FMT = "ENABLE JETTY FIX\n%h %l %u %t \"%r\" %>s %b \"%{Referer}i\" \"%{User-Agent}i\" %D"
+JETTY_FIELDS = ["IP:connection.client.host", "NUMBER:connection.client.logname", "STRING:connection.client.user",
+                "TIME.STAMP:request.receive.time", "TIME.DAY:request.receive.time.day", "HTTP.FIRSTLINE:request.firstline",
+                "STRING:request.status.last", "BYTES:response.body.bytes", "HTTP.URI:request.referer",
+                "HTTP.USERAGENT:request.user-agent", "MICROSECONDS:response.server.processing.time"]
+JETTY_LINES = [  # (line, user, user-agent) -- the test's four lines, verbatim
+    ("0.0.0.0 - x [24/Jul/2016:07:08:31 +0000] \"GET http://[:1]/foo HTTP/1.1\" 400 0 \"http://other.site\" \"-\"  8", "x", None),
+    ("0.0.0.0 -  -  [24/Jul/2016:07:08:31 +0000] \"GET http://[:1]/foo HTTP/1.1\" 400 0 \"http://other.site\" \"-\"  8", None, None),
+    ("0.0.0.0 - x [24/Jul/2016:07:08:31 +0000] \"GET http://[:1]/foo HTTP/1.1\" 400 0 \"http://other.site\" \"Mozilla/5.0 (dummy)\" 8",
+     "x", "Mozilla/5.0 (dummy)"),
+    ("0.0.0.0 -  -  [24/Jul/2016:07:08:31 +0000] \"GET http://[:1]/foo HTTP/1.1\" 400 0 \"http://other.site\" \"Mozilla/5.0 (dummy)\" 8",
+     None, "Mozilla/5.0 (dummy)")]
+for line, user_v, ua_v in JETTY_LINES:
+    case("hpt/JettyLogFormatParserTest.java:62-104", JETTY_FMT, line, JETTY_FIELDS,
+         expect={"IP:connection.client.host": "0.0.0.0", "NUMBER:connection.client.logname": None,
+                 "STRING:connection.client.user": user_v, "TIME.STAMP:request.receive.time": "24/Jul/2016:07:08:31 +0000",
+                 "TIME.DAY:request.receive.time.day": {"l": 24}, "HTTP.FIRSTLINE:request.firstline": "GET http://[:1]/foo HTTP/1.1",
+                 "STRING:request.status.last": "400", "BYTES:response.body.bytes": "0",
+                 "HTTP.URI:request.referer": "http://other.site", "HTTP.USERAGENT:request.user-agent": ua_v,
+                 "MICROSECONDS:response.server.processing.time": "8"},
+         note="each line parsed by a fresh parser (the test's assertions hold for any routing order)")
+
 # ------------------------------------------------------- component-level (via one-token formats)
 # HttpUriDissector tests (hpt/dissectors/TestHttpUriDissector.java) through "%{referer}i": the line is the URI.
 URI_PFX = "request.referer."
