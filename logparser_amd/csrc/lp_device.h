@@ -91,7 +91,7 @@ __device__ LP_INLINE uint32_t load_word(const LP_G uint8_t* p) {
 // scanner runs).
 enum : int {
     MC_QUOTE = 0,  // '"'
-    MC_UEV = 1,    // URI events: % # & ? ; = + A-Z and the bytes URIUtil.encode escapes
+    MC_UEV = 1,    // URI events: % # & ? ; + A-Z and the bytes URIUtil.encode escapes (not '=')
     MC_N = 2
 };
 __host__ __device__ LP_INLINE uint64_t mask_load(const uint64_t* p) { return *p; }
@@ -161,12 +161,12 @@ __host__ __device__ LP_INLINE int count(uint32_t m) { return __builtin_popcount(
 // ---- byte classes through two nibble look-up tables (the SIMD "shuffle"
 // classifier): class bits(b) = LO[b & 15] & HI[b >> 4], one v_perm_b32 per
 // 8-entry table half.  Bits: 0 ' ', 1 TAB, 2 '"', 3 hi 2 x lo {3,5,6,B}
-// (# % & +), 4 hi 3 x lo {B..F} (; < = > ?), 5 hi {4,7} x lo {B,C,D,F}
+// (# % & +), 4 hi 3 x lo {B,C,E,F} (; < > ?), 5 hi {4,7} x lo {B,C,D,F}
 // (K L M O { | }), 6 hi {4,5} x lo {1..E} (A-N Q-Z [ \ ] ^), 7 hi {5,6} x
 // lo 0 (P `).  WS = bits 0|1, QUOTE = bit 2, UEV = any bit.
 namespace bcls {
 constexpr uint32_t LO0 = 0x48444081u, LO1 = 0x40484840u;  // LO[0..3], LO[4..7]
-constexpr uint32_t LO2 = 0x78404240u, LO3 = 0x30507070u;  // LO[8..11], LO[12..15]
+constexpr uint32_t LO2 = 0x78404240u, LO3 = 0x30506070u;  // LO[8..11], LO[12..15]
 constexpr uint32_t HI0 = 0x100D0002u, HI1 = 0x2080C060u;  // HI[0..3], HI[4..7]
 // v_perm_b32: byte i of the result = byte sel_i (0..7) of (s0:s1), s1 low
 __host__ __device__ LP_INLINE uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) {
@@ -309,7 +309,7 @@ __host__ __device__ LP_INLINE int mfind_bwd(const LN& L, int c, int hi, int lo) 
 }
 
 // Calls f(q, c) for every position q in [a, b) whose byte c is a URI event
-// byte (MC_UEV: % # & ? ; = + A-Z and the URIUtil-escaped bytes), in order,
+// byte (MC_UEV: % # & ? ; + A-Z and the URIUtil-escaped bytes), in order,
 // until f returns false.  Returns false when f stopped the walk.  Lines with
 // masks walk 64 bytes per step and read the next event's byte before f runs
 // on the current one (its LDS latency overlaps f); others classify 4 bytes
@@ -1546,12 +1546,18 @@ constexpr uint32_t QP_RW = 1, QP_PV = 2;
 
 struct QueryTable {
     uint32_t tab = 0, list = 0, reg = 0, count = 0, npend = 0, maxp = 0;
-    int s = 0, eq = -1;
-    uint32_t pf = 0;
+    int s = 0;
+    int fu = -1;  // first upper-case / URIUtil-escaped byte of the piece (lower-cased / escaped name)
+    int lp = -1;  // last '%' / '+' of the piece (a value that needs resilientUrlDecode)
     bool on = false, set = false;  // enumerating now / table laid out
-    // piece [s, e) ends: finalize or leave pending
-    __host__ __device__ LP_INLINE void emit(const QueryStage& Q, LP_G uint8_t* region, int e) {
+    // piece [s, e) ends: finalize or leave pending.  '=' is not a URI event
+    // byte; the piece's first '=' is found here.
+    template <typename LN>
+    __host__ __device__ LP_INLINE void emit(const QueryStage& Q, LP_G uint8_t* region, const LN& L, int e) {
         if (e > s) {
+            const int f = find_fwd(L, s, e, [](uint32_t w) { return swar::eq(w, '='); });
+            const int eq = f < e ? f : -1;
+            const uint32_t pf = ((fu >= 0 && (eq < 0 || fu < eq)) ? QP_RW : 0u) | ((eq >= 0 && lp > eq) ? QP_PV : 0u);
             LP_G uint64_t* t = (LP_G uint64_t*)(region + tab) + 2 * count;
             if (pf == 0 && Q.want_all) {
                 const int ne = eq >= 0 ? eq : e;
@@ -1566,8 +1572,8 @@ struct QueryTable {
             }
             ++count;
         }
-        eq = -1;
-        pf = 0;
+        fu = -1;
+        lp = -1;
     }
 };
 
@@ -1639,7 +1645,7 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
     uint32_t rewr = 0;
     int st = ST_OK;
     // Fast walk over the events before the first '#' or ';' (the common
-    // bytes % & ? = + A-Z and URIUtil-escaped ones, few branches); it stops
+    // bytes % & ? + A-Z and URIUtil-escaped ones, few branches); it stops
     // at the first '#', ';' or invalid escape and the general walk below
     // continues from there with the same state.
     int resume = -1;
@@ -1649,13 +1655,13 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
         if (c == '%') {
             if (q + 2 >= b || !is_hex((w >> 8) & 0xFFu) || !is_hex((w >> 16) & 0xFFu)) { resume = q; return false; }
             first_pct = first_pct < 0 ? q : first_pct;
-            T.pf |= (T.on && T.eq >= 0) ? (uint32_t)QP_PV : 0u;
+            T.lp = q;
             return true;
         }
         if (c == '&' || c == '?') {
             rewr |= (c == '?' && fa >= 0) ? 2u : 0u;  // a later '?' becomes '&'
             if (T.on) {
-                T.emit(P.query[qsi], A.p, q);
+                T.emit(P.query[qsi], A.p, L, q);
                 T.s = q + 1;
             } else if (fa < 0 && qsi >= 0) {
                 T.on = T.set = true;
@@ -1668,13 +1674,11 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
             fa = fa < 0 ? q : fa;
             return true;
         }
-        // = + A-Z and URIUtil-escaped bytes
+        // + A-Z and URIUtil-escaped bytes
         rewr |= (fa >= 0 && uri_needs_encode(c)) ? 2u : 0u;
-        const bool on = T.on;
-        const bool noeq = T.eq < 0;
-        T.eq = (on && noeq && c == '=') ? q : T.eq;
-        T.pf |= (on && !noeq && c == '+') ? (uint32_t)QP_PV : 0u;
-        T.pf |= (on && noeq && c != '=' && c != '+') ? (uint32_t)QP_RW : 0u;
+        const bool plus = c == '+';
+        T.lp = plus ? q : T.lp;
+        T.fu = (!plus && T.fu < 0) ? q : T.fu;
         return true;
     });
 #if LP_EXP == 2
@@ -1688,11 +1692,11 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
             if (q + 2 >= b || !is_hex(L[q + 1]) || !is_hex(L[q + 2])) { st = ST_FALLBACK; return false; }  // BAD_EXCAPE_PATTERN
             if (first_pct < 0) first_pct = q;
             rewr |= h >= 0 ? 1u : 0u;
-            if (T.on && h < 0 && T.eq >= 0) T.pf |= QP_PV;
+            if (T.on && h < 0) T.lp = q;
         } else if (c == '#') {
             ++nh;
             if (T.on && h < 0) {
-                T.emit(P.query[qsi], A.p, q);
+                T.emit(P.query[qsi], A.p, L, q);
                 T.on = false;  // the rawQuery ends at the first '#'
             }
             if (h < 0) h = q;
@@ -1709,7 +1713,7 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
         } else if (c == '&' || c == '?') {
             rewr |= (c == '?' && fa >= 0 && h < 0) ? 2u : 0u;  // a later '?' becomes '&'
             if (T.on) {
-                T.emit(P.query[qsi], A.p, q);
+                T.emit(P.query[qsi], A.p, L, q);
                 T.s = q + 1;
             } else if (fa < 0 && h < 0 && qsi >= 0) {
                 // the rawQuery starts: table, pending list, piece regions
@@ -1722,24 +1726,19 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
             }
             if (fa < 0) fa = q;
             rewr |= h >= 0 ? 1u : 0u;
-        } else {  // = + A-Z and URIUtil-escaped bytes
+        } else {  // + A-Z and URIUtil-escaped bytes
             const bool enc = uri_needs_encode(c);
             rewr |= (fa >= 0 && h < 0 && enc) ? 2u : 0u;  // URIUtil escapes it
             if (T.on) {
-                if (c == '=') {
-                    if (T.eq < 0) T.eq = q;
-                } else if (c == '+') {
-                    if (T.eq >= 0) T.pf |= QP_PV;
-                } else if (T.eq < 0) {
-                    T.pf |= QP_RW;
-                }
+                if (c == '+') T.lp = q;
+                else if (T.fu < 0) T.fu = q;
             }
         }
         return true;
     });
     if (st != ST_OK) return st;
     if (T.set) {
-        if (T.on) T.emit(P.query[qsi], A.p, b);
+        if (T.on) T.emit(P.query[qsi], A.p, L, b);
         A.used = T.reg;
         A.slack += 16 * (T.maxp - T.count) + ((4 * T.maxp + 7) & ~7u);  // unused slots; the pending list is scratch
         C.q_count[qsi][li] = T.count;
