@@ -311,12 +311,12 @@ int lp_parse_batch(lp_handle* h, const uint8_t* buf, uint64_t nbytes, int buf_fl
         if (P.n_fmt > 1) {
             // HttpdLogFormatDissector routing: every format's match per line,
             // then the scan of the sticky active format
-            if (lp::launch_parse(h->d_buf, nbytes, n, h->args.as<lp::DeviceArgs>(), P.max_stack, C.wave_counts,
+            if (lp::launch_parse(h->d_buf, nbytes, n, h->args.as<lp::DeviceArgs>(), P.n_elems, P.max_stack, C.wave_counts,
                                  h->misc.as<unsigned long long>(), s, lp::PM_MATCH) != 0 ||
                 lp::launch_route(h->args.as<lp::DeviceArgs>(), n, s) != 0)
                 return LP_E_DEVICE;
         }
-        if (lp::launch_parse(h->d_buf, nbytes, n, h->args.as<lp::DeviceArgs>(), P.max_stack, C.wave_counts,
+        if (lp::launch_parse(h->d_buf, nbytes, n, h->args.as<lp::DeviceArgs>(), P.n_elems, P.max_stack, C.wave_counts,
                              h->misc.as<unsigned long long>(), s) != 0)
             return LP_E_DEVICE;
     } else {

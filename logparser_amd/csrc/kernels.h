@@ -25,8 +25,9 @@ int64_t parse_waves(int64_t n_lines);
 // parse every line, then counters[0..4] += lines, ok, bad, fallback, arena bytes written
 // (mode PM_PARSE); mode PM_MATCH only writes C.fmt_match (sticky routing pass 1)
 enum { PM_PARSE = 0, PM_MATCH = 1 };
-int launch_parse(const uint8_t* d_buf, uint64_t nbytes, int64_t n_lines, const DeviceArgs* d_args, int stack_depth,
-                 const uint32_t* d_wave_counts, unsigned long long* counters, hipStream_t s, int mode = PM_PARSE);
+int launch_parse(const uint8_t* d_buf, uint64_t nbytes, int64_t n_lines, const DeviceArgs* d_args, int n_elems,
+                 int stack_depth, const uint32_t* d_wave_counts, unsigned long long* counters, hipStream_t s,
+                 int mode = PM_PARSE);
 // sticky routing pass 2: C.fmt_match -> C.fmt_id (C.fmt_chunk: fmt_chunks()+1 words, the
 // state after the last line at [fmt_chunks()])
 constexpr int FMT_CHUNK = 4096;

@@ -266,17 +266,21 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
     }
 }
 
+// MASKS: the staging pass also builds the byte-class masks (MC_N bits per
+// window byte) for the 64-bytes-per-step scanners; without them the
+// scanners classify 4 bytes per step and a wave needs less LDS.
+template <bool MASKS>
 __global__ __launch_bounds__(PW) void k_parse_lines(const uint8_t* __restrict__ buf, uint64_t nbytes, int64_t n_lines,
                                                     const DeviceArgs* __restrict__ args, uint32_t win_cap, int stage,
                                                     uint32_t stk_words, int mode) {
     const Program& P = args->prog;
     const Columns& C = args->cols;
-    __shared__ Elem s_elems[MAX_ELEMS];
-    for (int k = threadIdx.x; k < P.n_elems; k += PW) s_elems[k] = P.elems[k];
-    // LDS: [DFS stack][byte window (win_cap, a multiple of 64)][MC_N class masks]
+    // LDS: [elements (n_elems x 16 B)][DFS stack][byte window (win_cap, a multiple of 64)][MC_N class masks]
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    WaveStack stk{reinterpret_cast<uint32_t*>(smem) + threadIdx.x};
-    uint8_t* win = smem + stk_words * 4;
+    Elem* s_elems = reinterpret_cast<Elem*>(smem);
+    for (int k = threadIdx.x; k < P.n_elems; k += PW) s_elems[k] = P.elems[k];
+    WaveStack stk{reinterpret_cast<uint32_t*>(smem + 16 * P.n_elems) + threadIdx.x};
+    uint8_t* win = smem + 16 * P.n_elems + stk_words * 4;
     const uint32_t mwords = win_cap >> 6;
     uint16_t* msk16 = reinterpret_cast<uint16_t*>(win + win_cap);
     const int lane = threadIdx.x;
@@ -324,17 +328,24 @@ __global__ __launch_bounds__(PW) void k_parse_lines(const uint8_t* __restrict__ 
                 if (k < nv)
                     for (int w = 0; w < 4; ++w) bad |= swar::guard_bad(v[j][w]) & ~swar::eq(v[j][w], '\n');
                 *reinterpret_cast<u32x4*>(win + 16 * k) = v[j];
-                uint32_t m0, m1;
-                bcls::classify16(v[j][0], v[j][1], v[j][2], v[j][3], m0, m1);
-                msk16[4 * mwords * MC_QUOTE + k] = (uint16_t)m0;
-                msk16[4 * mwords * MC_UEV + k] = (uint16_t)m1;
+                if constexpr (MASKS) {
+                    uint32_t m0, m1;
+                    bcls::classify16(v[j][0], v[j][1], v[j][2], v[j][3], m0, m1);
+                    msk16[4 * mwords * MC_QUOTE + k] = (uint16_t)m0;
+                    msk16[4 * mwords * MC_UEV + k] = (uint16_t)m1;
+                }
             }
         }
         const bool clean = !__any(bad != 0);
         __syncthreads();
-        const LineT<lds_bytes, lds_u64> L{(lds_bytes)win, (uint32_t)(s - w0), n,
-                                          (lds_u64)reinterpret_cast<uint64_t*>(msk16), mwords};
-        parse_wave(P, s_elems, C, L, active, li, stk, clean, mode);
+        if constexpr (MASKS) {
+            const LineT<lds_bytes, lds_u64> L{(lds_bytes)win, (uint32_t)(s - w0), n,
+                                              (lds_u64)reinterpret_cast<uint64_t*>(msk16), mwords};
+            parse_wave(P, s_elems, C, L, active, li, stk, clean, mode);
+        } else {
+            const LineT<lds_bytes> L{(lds_bytes)win, (uint32_t)(s - w0), n};
+            parse_wave(P, s_elems, C, L, active, li, stk, clean, mode);
+        }
     } else {
         __syncthreads();
         // base = the line start aligned down to 4 bytes: word reads never
@@ -475,8 +486,8 @@ int launch_route(const DeviceArgs* d_args, int64_t n_lines, hipStream_t s) {
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_parse(const uint8_t* d_buf, uint64_t nbytes, int64_t n_lines, const DeviceArgs* d_args, int stack_depth,
-                 const uint32_t* d_wave_counts, unsigned long long* counters, hipStream_t s, int mode) {
+int launch_parse(const uint8_t* d_buf, uint64_t nbytes, int64_t n_lines, const DeviceArgs* d_args, int n_elems,
+                 int stack_depth, const uint32_t* d_wave_counts, unsigned long long* counters, hipStream_t s, int mode) {
     if (n_lines == 0) return 0;
     const int64_t waves = parse_waves(n_lines);
     // LDS window per wave: ~1.1x the mean bytes of 64 lines (+512 B), so
@@ -493,9 +504,17 @@ int launch_parse(const uint8_t* d_buf, uint64_t nbytes, int64_t n_lines, const D
     cap = (cap + 63) & ~63ull;
     const int stage = ((uintptr_t)d_buf & 15) == 0 && !force_global;
     const uint32_t stk_words = (uint32_t)(stack_depth > 0 ? stack_depth : 1) * PW;
-    const size_t lds = stk_words * 4 + cap + MC_N * (cap / 8);  // + class masks, 1 bit per window byte
-    hipLaunchKernelGGL(k_parse_lines, dim3((unsigned)waves), dim3(PW), lds, s, d_buf, nbytes, n_lines, d_args,
-                       (uint32_t)cap, stage, stk_words, mode);
+    const char* e3 = getenv("LP_LDS_PAD");  // profiling experiments: extra LDS per wave (lower occupancy)
+    const char* e4 = getenv("LP_MASKS");
+    const bool masks = e4 ? atoi(e4) != 0 : true;
+    const size_t lds = 16 * (size_t)n_elems + stk_words * 4 + cap + (masks ? MC_N * (cap / 8) : 0) +
+                       (e3 ? (size_t)atoi(e3) : 0);
+    if (masks)
+        hipLaunchKernelGGL(k_parse_lines<true>, dim3((unsigned)waves), dim3(PW), lds, s, d_buf, nbytes, n_lines, d_args,
+                           (uint32_t)cap, stage, stk_words, mode);
+    else
+        hipLaunchKernelGGL(k_parse_lines<false>, dim3((unsigned)waves), dim3(PW), lds, s, d_buf, nbytes, n_lines,
+                           d_args, (uint32_t)cap, stage, stk_words, mode);
     if (mode == PM_MATCH) return hipGetLastError() == hipSuccess ? 0 : -1;
     int64_t rb = (waves + 255) / 256;
     if (rb > 1024) rb = 1024;
