@@ -497,16 +497,30 @@ int launch_parse(const uint8_t* d_buf, uint64_t nbytes, int64_t n_lines, const D
     // tuning knobs for profiling experiments (defaults are the product setting)
     const char* e1 = getenv("LP_WIN_PCT");
     const char* e2 = getenv("LP_NO_STAGE");
-    const int win_pct = e1 ? atoi(e1) : 110;
-    const int force_global = e2 ? atoi(e2) : 0;
-    uint64_t cap = (PW * mean * (uint64_t)win_pct) / 100 + 512;
-    if (cap > 48 * 1024) cap = 48 * 1024;
-    cap = (cap + 63) & ~63ull;
-    const int stage = ((uintptr_t)d_buf & 15) == 0 && !force_global;
-    const uint32_t stk_words = (uint32_t)(stack_depth > 0 ? stack_depth : 1) * PW;
-    const char* e3 = getenv("LP_LDS_PAD");  // profiling experiments: extra LDS per wave (lower occupancy)
     const char* e4 = getenv("LP_MASKS");
     const bool masks = e4 ? atoi(e4) != 0 : true;
+    const int force_global = e2 ? atoi(e2) : 0;
+    const uint32_t stk_words = (uint32_t)(stack_depth > 0 ? stack_depth : 1) * PW;
+    const uint64_t fixed = 16 * (uint64_t)n_elems + 4 * (uint64_t)stk_words;
+    const uint64_t per8 = masks ? 8 + MC_N : 8;  // LDS bytes per 8 window bytes
+    // The parse kernel is latency bound: its speed follows the waves a CU
+    // holds, and LDS sets that number.  The window of a wave is sized to the
+    // most waves per CU that still leave >= 4 % over the mean 64 lines (the
+    // few windows that do not fit read HBM directly).  Measured on gfx950:
+    // W waves of one 64-thread workgroup each fit when a wave's LDS is at
+    // most 160 KiB / W - 640 B.
+    const uint64_t need = PW * mean + PW * mean / 25 + 64;
+    uint64_t cap = 0;
+    for (int w = 8; w >= 2 && !cap; --w) {
+        const uint64_t budget = 160 * 1024 / w - 640;
+        if (budget <= fixed) continue;
+        const uint64_t c = ((budget - fixed) * 8 / per8) & ~63ull;
+        if (c >= need) cap = c;
+    }
+    if (!cap || e1) cap = ((PW * mean * (uint64_t)(e1 ? atoi(e1) : 110)) / 100 + 512 + 63) & ~63ull;
+    if (cap > 48 * 1024) cap = 48 * 1024;
+    const int stage = ((uintptr_t)d_buf & 15) == 0 && !force_global;
+    const char* e3 = getenv("LP_LDS_PAD");  // profiling experiments: extra LDS per wave (lower occupancy)
     const size_t lds = 16 * (size_t)n_elems + stk_words * 4 + cap + (masks ? MC_N * (cap / 8) : 0) +
                        (e3 ? (size_t)atoi(e3) : 0);
     if (masks)
