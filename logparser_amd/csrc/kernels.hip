@@ -237,8 +237,7 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
                 const auto OL = owner_line(L, own);
                 if (g < total) {
                     LP_G uint8_t* region = C.arena + oab;
-                    const uint32_t so = reinterpret_cast<const LP_G uint32_t*>(region + olist)[g - ob];
-                    LP_G uint64_t* slot = reinterpret_cast<LP_G uint64_t*>(region + so);
+                    LP_G uint64_t* slot = reinterpret_cast<LP_G uint64_t*>(region + olist + 16 * (g - ob));
                     const uint64_t a0 = slot[0];
                     const uint32_t reserved = 3u * (uint32_t)(((a0 >> 16) & 0xFFFFu) - (a0 & 0xFFFFu));
                     const uint32_t used = query_piece(P, P.query[qs], OL, region, slot);

@@ -1188,7 +1188,7 @@ struct LineOut {
     uint32_t tok_flags;
     RegArr<MAX_FL> fl_kind, fl_method, fl_uri, fl_proto;
     RegArr<MAX_URI> usep;  // '&' + '?' count of each URI source (query table bound)
-    RegArr<MAX_QUERY> qlist, qpend;  // per query stage: pending-piece list (arena region offset), its length
+    RegArr<MAX_QUERY> qlist, qpend;  // per query stage: the piece table (arena region offset), its length
     uint32_t arena_need;
 };
 
@@ -1545,31 +1545,21 @@ constexpr uint64_t REF_SKIP = ~0ull;  // slot of a piece whose name was not requ
 constexpr uint32_t QP_RW = 1, QP_PV = 2;
 
 struct QueryTable {
-    uint32_t tab = 0, list = 0, reg = 0, count = 0, npend = 0, maxp = 0;
+    uint32_t tab = 0, reg = 0, count = 0, maxp = 0;
     int s = 0;
     int fu = -1;  // first upper-case / URIUtil-escaped byte of the piece (lower-cased / escaped name)
     int lp = -1;  // last '%' / '+' of the piece (a value that needs resilientUrlDecode)
     bool on = false, set = false;  // enumerating now / table laid out
-    // piece [s, e) ends: finalize or leave pending.  '=' is not a URI event
-    // byte; the piece's first '=' is found here.
-    template <typename LN>
-    __host__ __device__ LP_INLINE void emit(const QueryStage& Q, LP_G uint8_t* region, const LN& L, int e) {
+    // piece [s, e) ends: its slot gets the raw piece (bounds, the two flag
+    // positions, the offset of 3 x its length reserved for rewritten bytes);
+    // query_piece completes every slot afterwards, spread over the wave
+    __host__ __device__ LP_INLINE void emit(LP_G uint8_t* region, int e) {
         if (e > s) {
-            const int f = find_fwd(L, s, e, [](uint32_t w) { return swar::eq(w, '='); });
-            const int eq = f < e ? f : -1;
-            const uint32_t pf = ((fu >= 0 && (eq < 0 || fu < eq)) ? QP_RW : 0u) | ((eq >= 0 && lp > eq) ? QP_PV : 0u);
             LP_G uint64_t* t = (LP_G uint64_t*)(region + tab) + 2 * count;
-            if (pf == 0 && Q.want_all) {
-                const int ne = eq >= 0 ? eq : e;
-                t[0] = mkref((uint32_t)s, (uint32_t)(ne - s), false);
-                t[1] = eq < 0 ? mkref(0, 0, false) : mkref((uint32_t)eq + 1, (uint32_t)(e - eq - 1), false);
-            } else {
-                t[0] = (uint64_t)(uint32_t)s | ((uint64_t)(uint32_t)e << 16) | ((uint64_t)(uint32_t)(eq + 1) << 32) |
-                       ((uint64_t)pf << 48);
-                t[1] = reg;
-                reg += 3 * (uint32_t)(e - s);
-                ((LP_G uint32_t*)(region + list))[npend++] = tab + 16 * count;
-            }
+            t[0] = (uint64_t)(uint32_t)s | ((uint64_t)(uint32_t)e << 16) | ((uint64_t)(uint32_t)(fu + 1) << 32) |
+                   ((uint64_t)(uint32_t)(lp + 1) << 48);
+            t[1] = reg;
+            reg += 3 * (uint32_t)(e - s);
             ++count;
         }
         fu = -1;
@@ -1577,7 +1567,7 @@ struct QueryTable {
     }
 };
 
-// Completes a pending piece (QueryStringFieldDissector.java:75-104): the name
+// Completes a query piece (QueryStringFieldDissector.java:75-104): the name
 // is lower-cased and keeps URIUtil's escapes, never decoded; a piece without
 // '=' has value ""; else the value goes through Utils.resilientUrlDecode.
 // region: the owning line's arena region; slot: its table slot.  Returns the
@@ -1586,8 +1576,13 @@ template <typename LN>
 __host__ __device__ LP_INLINE uint32_t query_piece(const Program& P, const QueryStage& Q, const LN& L,
                                                    LP_G uint8_t* region, LP_G uint64_t* slot) {
     const uint64_t a0 = slot[0], a1 = slot[1];
-    const int s = (int)(a0 & 0xFFFFu), e = (int)((a0 >> 16) & 0xFFFFu), eq = (int)((a0 >> 32) & 0xFFFFu) - 1;
-    const bool rw = (a0 >> 48) & QP_RW, pv = (a0 >> 48) & QP_PV;
+    const int s = (int)(a0 & 0xFFFFu), e = (int)((a0 >> 16) & 0xFFFFu);
+    const int fu = (int)((a0 >> 32) & 0xFFFFu) - 1, lp = (int)((a0 >> 48) & 0xFFFFu) - 1;
+    // the piece's first '=' splits name and value ('=' is not a URI event byte)
+    const int f = find_fwd(L, s, e, [](uint32_t w) { return swar::eq(w, '='); });
+    const int eq = f < e ? f : -1;
+    const bool rw = fu >= 0 && (eq < 0 || fu < eq);  // upper-case / escaped bytes in the name
+    const bool pv = eq >= 0 && lp > eq;               // '%' / '+' in the value
     const int ne = eq >= 0 ? eq : e;
     Arena A{region, (uint32_t)a1, 0};
     // name [s, ne): URIUtil-escaped and lower-cased as in the rawQuery
@@ -1649,6 +1644,7 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
     // at the first '#', ';' or invalid escape and the general walk below
     // continues from there with the same state.
     int resume = -1;
+    LP_PROF(50 + 4 * u);
     for_uev_w(L, a, b, [&](int q, uint32_t w) {
         const uint32_t c = w & 0xFFu;
         if (c == '#' || c == ';') { resume = q; return false; }
@@ -1661,14 +1657,13 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
         if (c == '&' || c == '?') {
             rewr |= (c == '?' && fa >= 0) ? 2u : 0u;  // a later '?' becomes '&'
             if (T.on) {
-                T.emit(P.query[qsi], A.p, L, q);
+                T.emit(A.p, q);
                 T.s = q + 1;
             } else if (fa < 0 && qsi >= 0) {
                 T.on = T.set = true;
                 T.maxp = usep + 1;
                 T.tab = (A.used + 7) & ~7u;
-                T.list = T.tab + 16 * T.maxp;
-                T.reg = T.list + ((4 * T.maxp + 7) & ~7u);
+                T.reg = T.tab + 16 * T.maxp;
                 T.s = q + 1;
             }
             fa = fa < 0 ? q : fa;
@@ -1681,6 +1676,7 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
         T.fu = (!plus && T.fu < 0) ? q : T.fu;
         return true;
     });
+    LP_PROF(51 + 4 * u);
 #if LP_EXP == 2
     if (0)
 #endif
@@ -1696,7 +1692,7 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
         } else if (c == '#') {
             ++nh;
             if (T.on && h < 0) {
-                T.emit(P.query[qsi], A.p, L, q);
+                T.emit(A.p, q);
                 T.on = false;  // the rawQuery ends at the first '#'
             }
             if (h < 0) h = q;
@@ -1713,15 +1709,14 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
         } else if (c == '&' || c == '?') {
             rewr |= (c == '?' && fa >= 0 && h < 0) ? 2u : 0u;  // a later '?' becomes '&'
             if (T.on) {
-                T.emit(P.query[qsi], A.p, L, q);
+                T.emit(A.p, q);
                 T.s = q + 1;
             } else if (fa < 0 && h < 0 && qsi >= 0) {
                 // the rawQuery starts: table, pending list, piece regions
                 T.on = T.set = true;
                 T.maxp = usep + 1;
                 T.tab = (A.used + 7) & ~7u;
-                T.list = T.tab + 16 * T.maxp;
-                T.reg = T.list + ((4 * T.maxp + 7) & ~7u);
+                T.reg = T.tab + 16 * T.maxp;
                 T.s = q + 1;
             }
             if (fa < 0) fa = q;
@@ -1736,15 +1731,16 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
         }
         return true;
     });
+    LP_PROF(52 + 4 * u);
     if (st != ST_OK) return st;
     if (T.set) {
-        if (T.on) T.emit(P.query[qsi], A.p, L, b);
+        if (T.on) T.emit(A.p, b);
         A.used = T.reg;
-        A.slack += 16 * (T.maxp - T.count) + ((4 * T.maxp + 7) & ~7u);  // unused slots; the pending list is scratch
+        A.slack += 16 * (T.maxp - T.count);  // unused slots
         C.q_count[qsi][li] = T.count;
         C.q_params[qsi][li] = mkref(T.tab, 16 * T.count, true);
-        o.qlist.set(qsi, T.list);
-        o.qpend.set(qsi, T.npend);
+        o.qlist.set(qsi, T.tab);
+        o.qpend.set(qsi, T.count);
     }
     LP_PROF(30 + 8 * u);
     if (nh > 1) return ST_FALLBACK;                                                       // DOUBLE_HASH
@@ -1888,9 +1884,8 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
 template <typename LN>
 __host__ __device__ LP_INLINE void query_pieces_serial(const Program& P, const LN& L, const LineOut& o, LP_G uint8_t* region) {
     for (int qs = 0; qs < P.n_query; ++qs) {
-        const LP_G uint32_t* list = (const LP_G uint32_t*)(region + o.qlist.get(qs));
         for (uint32_t k = 0; k < o.qpend.get(qs); ++k)
-            query_piece(P, P.query[qs], L, region, (LP_G uint64_t*)(region + list[k]));
+            query_piece(P, P.query[qs], L, region, (LP_G uint64_t*)(region + o.qlist.get(qs) + 16 * k));
     }
 }
 

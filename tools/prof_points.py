@@ -28,7 +28,12 @@ names = {0: "start", 1: "staged", 2: "phase1 entry", 3: "guard", 4: "match", 5: 
 for u in range(2):
     for j, nm in enumerate(["pass1", "authority", "path", "query", "frag"]):
         names[30 + 8 * u + j] = "u%d %s done" % (u, nm)
-order = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 30, 31, 32, 33, 34, 11, 12, 38, 39, 40, 41, 42, 13, 20, 21, 22]
+for u in range(2):
+    names[50 + 4 * u] = "u%d walk start" % u
+    names[51 + 4 * u] = "u%d fast walk" % u
+    names[52 + 4 * u] = "u%d gen walk" % u
+order = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 50, 51, 52, 30, 31, 32, 33, 34, 11, 12, 54, 55, 56, 38, 39, 40, 41, 42, 13,
+         20, 21, 22]
 pts = [k for k in order if buf[2 * k + 1]]
 print("parse ms %.3f  waves %d" % (st["ms_parse"], buf[1]))
 prev = None
