@@ -187,6 +187,17 @@ __host__ __device__ LP_INLINE uint32_t bits(uint32_t w) {
     const uint32_t rl = (p2 & m8) | (p1 & ~m8);
     return rl & perm(HI1, HI0, (w >> 4) & 0x07070707u);
 }
+// java.net.URI authority bytes: a second table pair whose class is the
+// bytes outside L_SERVER and L_REG_NAME (controls, space, " # % & / < > ? @
+// [ \ ] ^ ` { | } DEL; rectangles hi x lo of the nibbles, one bit each)
+constexpr uint32_t NA_LO0 = 0x0303010Bu, NA_LO1 = 0x01030301u, NA_LO2 = 0x11010101u, NA_LO3 = 0x47251115u;
+constexpr uint32_t NA_HI0 = 0x04020101u, NA_HI1 = 0x50083008u;
+__host__ __device__ LP_INLINE uint32_t nonauth_bits(uint32_t w) {
+    const uint32_t s = w & 0x07070707u;
+    const uint32_t p1 = perm(NA_LO1, NA_LO0, s), p2 = perm(NA_LO3, NA_LO2, s);
+    const uint32_t m8 = ((w >> 3) & 0x01010101u) * 0xFFu;
+    return ((p2 & m8) | (p1 & ~m8)) & perm(NA_HI1, NA_HI0, (w >> 4) & 0x07070707u);
+}
 // bytes with bit 7 set -> 4-bit mask (byte k -> bit k)
 __host__ __device__ LP_INLINE uint32_t nib(uint32_t hb) { return (((hb >> 7) * 0x204081u) >> 21) & 15u; }
 __host__ __device__ LP_INLINE uint32_t quote_hb(uint32_t r) { return (r << 5) & swar::HI; }
@@ -1426,6 +1437,32 @@ __host__ __device__ LP_INLINE int jdk_ipv4(const LN& L, int a, int b) {
     return p;
 }
 
+// java.net.URI.Parser.parseHostname on [a,b) (labels alnum (alnum | '-')*
+// not ending in '-', separated by '.', a trailing '.' allowed, the last
+// label starting with a letter when there are several, then ':' or the end),
+// one SWAR scan for the first byte outside alnum / '-' / '.' and one per
+// label for its '.'.  Returns end or -1 (fail).
+template <typename LN>
+__host__ __device__ LP_INLINE int jdk_hostname_swar(const LN& L, int a, int b) {
+    const int he = find_fwd(L, a, b, [](uint32_t w) {
+        const uint32_t alnum = swar::digit(w) | (swar::ge(w, 'A') & swar::lt(w, 'Z' + 1)) |
+                               (swar::ge(w, 'a') & swar::lt(w, 'z' + 1));
+        return ~(alnum | swar::eq(w, '-') | swar::eq(w, '.')) & swar::HI;
+    });
+    int p = a, l = -1;
+    while (p < he) {
+        if (!is_alnum(L[p])) return -1;  // a label starts with '.' or '-'
+        l = p;
+        const int q = find_fwd(L, p, he, [](uint32_t w) { return swar::eq(w, '.'); });
+        if (L[q - 1] == '-') return -1;
+        p = q < he ? q + 1 : he;
+    }
+    if (he < b && L[he] != ':') return -1;
+    if (l < 0) return -1;
+    if (l > a && !is_alpha(L[l])) return -1;
+    return he;
+}
+
 // java.net.URI.Parser.parseHostname on [a,b); returns end or -1 (fail)
 template <typename LN>
 __host__ __device__ LP_INLINE int jdk_hostname(const LN& L, int a, int b) {
@@ -1776,17 +1813,13 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
                 // authority [as, ae): up to '/', '#' or the first '?'; only chars
                 // in both L_SERVER and L_REG_NAME of java.net.URI (no '@'
                 // userinfo, no escapes), else FALLBACK
-                int as = p + 2, ae = as;
-                while (ae < b && ae != fa) {
-                    const uint32_t d = cur.at(ae);
-                    if (d == '/' || d == '#') break;
-                    if (!authority_char(d)) return ST_FALLBACK;
-                    ++ae;
-                }
+                const int as = p + 2;
+                const int ae = find_fwd(L, as, b, [](uint32_t w) { return bcls::uev_hb(bcls::nonauth_bits(w)); });
+                if (ae < b && ae != fa && cur.at(ae) != '/' && cur.at(ae) != '#') return ST_FALLBACK;
                 if (ae == as) return ST_FALLBACK;                                          // empty authority
                 // parseServer; any failure -> registry-based authority (host null)
                 int he = jdk_ipv4(L, as, ae);
-                if (he <= as) he = jdk_hostname(L, as, ae);
+                if (he <= as) he = jdk_hostname_swar(L, as, ae);
                 bool ok = he > as;
                 int pt = -1;
                 if (ok && he < ae) {

@@ -302,3 +302,24 @@ def test_mixed_formats_emulated(oracle, emu):
     lines = [mutate(rng, l) if rng.random() < 0.1 else l for l in lines]
     s = compare(o, e, lines)
     assert s["ok"] > 2000 and s["bad"] > 20, s
+
+
+HOSTS = ["a..b", "a-.b", "-a", "a.", "a.b.", "1a.b", "a.1b", "a1.b2", "a:80", "a.b:", "a.b:x", "a_b", "a!b", "a~b",
+         "a'b", "a(b)", "a;b", "a=b", "a+b", "a$b", "a,b", "a*b", "a:1:2", "1.2.3.4", "1.2.3.4.5", "256.1.1.1",
+         "01.2.3.4", "1.2.3", "1.2.3.4:99", "1.2.3.4x", "a.b.c-d.e", "a-b-c.d--e.f", "x.y.z.", "A.B.C:0",
+         "a.b:2147483647", "a.b:2147483648", "a.b:00080", "9", "9.9", "9.a", "host-", "h.-x", ":80", "a%41b"]
+
+
+def test_authority_variants_emulated(oracle, emu):
+    """java.net.URI server authority parsing (parseServer / parseHostname /
+    parseIPv4Address) on the referer URL's host part."""
+    paths = all_paths(oracle)
+    o = oracle.Oracle("combined", paths)
+    e = emu.Emu("combined", paths)
+    base = b'1.2.3.4 - - [01/Jan/2021:00:00:00 +0000] "GET / HTTP/1.1" 200 0 "http://%s/p?q=1" "u"'
+    lines = []
+    for h in HOSTS:
+        for tail in ("", "/x", "#f", "?a"):
+            lines.append(base.replace(b"%s/p?q=1", (h + tail + "/p?q=1").encode()))
+    s = compare(o, e, lines)
+    assert s["ok"] > 100, s

@@ -239,3 +239,11 @@ def test_mixed_formats_gpu(oracle):
                 assert r1 == r.record_json(i), (i, l)
                 ok += 1
         assert ok > 0.8 * len(part)
+
+
+def test_authority_variants_gpu(oracle):
+    from test_emu_parity import HOSTS
+    base = b'1.2.3.4 - - [01/Jan/2021:00:00:00 +0000] "GET / HTTP/1.1" 200 0 "http://%s/p?q=1" "u"'
+    lines = [base.replace(b"%s/p?q=1", (h + t + "/p?q=1").encode()) for h in HOSTS for t in ("", "/x", "#f", "?a")]
+    s, _ = gpu_vs_oracle(oracle, "combined", paths(oracle), lines)
+    assert s["ok"] > 100, s
