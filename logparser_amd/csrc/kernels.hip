@@ -305,7 +305,7 @@ __global__ __launch_bounds__(PW) void k_parse_lines(const uint8_t* __restrict__ 
         uint32_t bad = 0;  // guard-failing bytes other than '\n' anywhere in the window
         // SB loads in flight per lane before the first LDS store (one HBM
         // round trip per SB x 1 KiB of window instead of one per 1 KiB)
-        constexpr int SB = 8;
+        constexpr int SB = 20;
         const uint64_t full_end = nbytes & ~15ull;  // 16-byte pieces wholly inside the buffer
         for (int k0 = lane; k0 < nv4; k0 += SB * PW) {
             u32x4 v[SB];
@@ -319,10 +319,16 @@ __global__ __launch_bounds__(PW) void k_parse_lines(const uint8_t* __restrict__ 
 #pragma unroll
             for (int j = 0; j < SB; ++j) {
                 const int k = k0 + j * PW;
-                if (k >= nv4) break;
+                if (k >= nv4) continue;
                 const uint64_t p = w0 + 16ull * k;
                 if (k < nv && p + 16 > full_end) {  // the buffer's last partial piece
-                    for (int b = 0; b < 16 && p + b < nbytes; ++b) v[j][b >> 2] |= (uint32_t)buf[p + b] << (8 * (b & 3));
+                    auto word = [&](uint64_t q) {
+                        uint32_t w = 0;
+#pragma unroll
+                        for (int b = 0; b < 4; ++b) w |= q + b < nbytes ? (uint32_t)buf[q + b] << (8 * b) : 0u;
+                        return w;
+                    };
+                    v[j] = u32x4{word(p), word(p + 4), word(p + 8), word(p + 12)};
                 }
                 if (k < nv)
                     for (int w = 0; w < 4; ++w) bad |= swar::guard_bad(v[j][w]) & ~swar::eq(v[j][w], '\n');
