@@ -929,6 +929,32 @@ __host__ __device__ LP_INLINE int match_line(const Program& P, const EL& elems, 
     }
 }
 
+// The first leaf of match_line's DFS (every element's first candidate) for
+// a one-format program, elements read from the Program with a uniform
+// index.  true: the line matches along that leaf (then it is the DFS's
+// result: its first complete match); false: decide with match_line.
+template <typename LN, typename Caps>
+__host__ __device__ LP_INLINE bool match_first_leaf(const Program& P, const LN& L, Caps& caps) {
+    int pos = 0;
+    bool ok = true;
+    const int ne = P.n_elems;
+    for (int i = 0; i < ne; ++i) {
+        const Elem e = P.elems[i];
+        if (e.kind == EK_LIT) {
+            ok = ok && lit_at(P, L, pos, e);
+            pos += e.lit_len;
+        } else if (ok) {
+            const int c = cand_first(P, e, L, pos);
+            ok = c >= 0;
+            if (ok) {
+                if (e.cap >= 0) caps.set(e.cap, mkspan(pos, c));
+                pos = c;
+            }
+        }
+    }
+    return ok && pos == L.n;
+}
+
 struct NoCaps {
     __host__ __device__ LP_INLINE void set(int, uint32_t) {}
 };
@@ -1265,7 +1291,13 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
         return;
     }
     LP_PROF(3);
-    int st = match_line(P, elems + P.fmt_elem0[fmt], P.fmt_elem0[fmt + 1] - P.fmt_elem0[fmt], L, o.caps, stk);
+    // One LogFormat: every lane walks the same elements, so the DFS's first
+    // leaf (each element's first candidate) is tried in lock step with the
+    // elements read as wave-uniform values (scalar loads, scalar branches on
+    // the element kind); lines it does not match run the backtracking DFS.
+    int st = P.n_fmt == 1 && match_first_leaf(P, L, o.caps) ? ST_OK : ST_BAD;
+    if (st != ST_OK)
+        st = match_line(P, elems + P.fmt_elem0[fmt], P.fmt_elem0[fmt + 1] - P.fmt_elem0[fmt], L, o.caps, stk);
     LP_PROF(4);
     if (st != ST_OK) { o.status = st; return; }
     // decodeExtractedValue: "-" -> null (Apache: ApacheHttpdLogFormatDissector.java:169-196,
