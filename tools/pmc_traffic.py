@@ -19,7 +19,7 @@ def per_kernel(path, counter):
         if r["Counter_Name"] != counter:
             continue
         name = r["Kernel_Name"]
-        m = re.search(r"::(k_\w+)\(", name)
+        m = re.search(r"::(k_\w+)(?:<\w+>)?\(", name)
         short = m.group(1) if m else name[:60]
         acc[short].append(float(r["Counter_Value"]) * 1024.0)
     return {k: sum(v) / len(v) for k, v in acc.items()}
