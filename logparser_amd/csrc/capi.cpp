@@ -261,11 +261,13 @@ int lp_parse_batch(lp_handle* h, const uint8_t* buf, uint64_t nbytes, int buf_fl
         h->d_buf = buf;
     }
     const int64_t nc = lp::count_chunks(nbytes);
-    if (!h->chunk.ensure(sizeof(uint64_t) * (size_t)(nc + 2))) return LP_E_NOMEM;
+    const size_t cbytes = align256(sizeof(uint64_t) * (size_t)(nc + 2));
+    if (!h->chunk.ensure(cbytes + 2 * (size_t)lp::nlmask_words(nbytes))) return LP_E_NOMEM;
     uint64_t* d_chunk = h->chunk.as<uint64_t>();
+    uint16_t* d_nlmask = h->chunk.as<uint16_t>(cbytes);
     hipEventRecord(h->ev[0], s);
     // index pass 1 (count + scan), then the line count on the host
-    if (lp::launch_count(h->d_buf, nbytes, d_chunk, s) != 0) return LP_E_DEVICE;
+    if (lp::launch_count(h->d_buf, nbytes, d_chunk, d_nlmask, s) != 0) return LP_E_DEVICE;
     uint64_t total = 0;
     uint8_t last = '\n';
     if (nc > 0) {
@@ -279,7 +281,7 @@ int lp_parse_batch(lp_handle* h, const uint8_t* buf, uint64_t nbytes, int buf_fl
     uint64_t* d_off = h->line_off.as<uint64_t>();
     uint64_t head = 0, tail = nbytes + 1;
     hipMemcpyAsync(d_off, &head, sizeof head, hipMemcpyHostToDevice, s);
-    if (lp::launch_offsets(h->d_buf, nbytes, d_chunk, d_off, s) != 0) return LP_E_DEVICE;
+    if (lp::launch_offsets(d_nlmask, nbytes, d_chunk, d_off, s) != 0) return LP_E_DEVICE;
     if (nbytes > 0 && last != '\n') hipMemcpyAsync(d_off + n, &tail, sizeof tail, hipMemcpyHostToDevice, s);
     hipEventRecord(h->ev[1], s);
     // results

@@ -16,9 +16,12 @@ struct DeviceArgs {
 int64_t count_chunks(uint64_t nbytes);
 // index pass 1: per-chunk '\n' counts, exclusively scanned in place;
 // d_chunk needs count_chunks()+1 entries, d_chunk[nc] = total '\n' count
-int launch_count(const uint8_t* d_buf, uint64_t nbytes, uint64_t* d_chunk, hipStream_t s);
-// index pass 2: d_line_off[k] = start of line k for k >= 1 (caller sets [0])
-int launch_offsets(const uint8_t* d_buf, uint64_t nbytes, const uint64_t* d_chunk, uint64_t* d_line_off, hipStream_t s);
+// and d_nlmask[i] = '\n' bits of bytes [16 i, 16 i + 16) (nlmask_words() entries)
+int launch_count(const uint8_t* d_buf, uint64_t nbytes, uint64_t* d_chunk, uint16_t* d_nlmask, hipStream_t s);
+inline int64_t nlmask_words(uint64_t nbytes) { return count_chunks(nbytes) * (64 * 1024 / 16); }
+// index pass 2 (from the masks): d_line_off[k] = start of line k for k >= 1 (caller sets [0])
+int launch_offsets(const uint16_t* d_nlmask, uint64_t nbytes, const uint64_t* d_chunk, uint64_t* d_line_off,
+                   hipStream_t s);
 // parse kernels: number of waves (C.wave_counts needs WC_WORDS u32 per wave)
 constexpr int WC_WORDS = 8;
 int64_t parse_waves(int64_t n_lines);

@@ -1,8 +1,8 @@
 // gfx950 kernels of the logparser_amd engine.
 //
-//   k_count_newlines  per-chunk '\n' count (16-byte loads, SWAR byte compare)
+//   k_count_newlines  per-chunk '\n' count and '\n' bit masks (16-byte loads, SWAR byte compare)
 //   k_scan_counts     exclusive scan of the chunk counts (single workgroup)
-//   k_line_offsets    line start offsets (Hadoop LineRecordReader '\n' semantics)
+//   k_line_offsets    line start offsets from the bit masks (Hadoop LineRecordReader '\n' semantics)
 //   k_parse_lines     one wave per 64 lines, one lane per line: the lines'
 //                     byte window staged in LDS, LogFormat match + token /
 //                     time / first-line stages (phase 1), wave-aggregated
@@ -63,13 +63,28 @@ __device__ __forceinline__ Piece16 nl16(const uint8_t* p, uint64_t pos, uint64_t
     return r;
 }
 
+// '\n' bits of a 16-byte piece as a 16-bit mask (bit k = byte k)
+__device__ __forceinline__ uint32_t piece_bits(const Piece16& pc) {
+    return bcls::nib(pc.m[0]) | (bcls::nib(pc.m[1]) << 4) | (bcls::nib(pc.m[2]) << 8) | (bcls::nib(pc.m[3]) << 12);
+}
+
+// Pass 1 of the line index: '\n' count per 64 KiB chunk, and the '\n' bit
+// mask of every 16-byte piece (1 bit per input byte) so that pass 2 reads
+// nbytes / 8 bytes instead of the input again.
 __global__ __launch_bounds__(NL_THREADS) void k_count_newlines(const uint8_t* __restrict__ buf, uint64_t nbytes,
-                                                                uint64_t* __restrict__ counts) {
+                                                                uint64_t* __restrict__ counts,
+                                                                uint16_t* __restrict__ nlmask) {
     const uint64_t base = (uint64_t)blockIdx.x * CHUNK;
     uint32_t c = 0;
     for (int it = 0; it < CHUNK / (NL_THREADS * 16); ++it) {
         uint64_t pos = base + ((uint64_t)it * NL_THREADS + threadIdx.x) * 16;
-        if (pos < nbytes) c += nl16(buf, pos, nbytes).count();
+        uint32_t m = 0;
+        if (pos < nbytes) {
+            const Piece16 pc = nl16(buf, pos, nbytes);
+            c += pc.count();
+            m = piece_bits(pc);
+        }
+        nlmask[pos >> 4] = (uint16_t)m;
     }
     // block reduction
     __shared__ uint32_t red[NL_THREADS / 64];
@@ -104,7 +119,7 @@ __global__ __launch_bounds__(1024) void k_scan_counts(uint64_t* __restrict__ cou
 
 // line_off[j] = start of line j.  line_off[0] = 0 and the entry after every
 // '\n' that is not the last byte; line_off[n_lines] = end sentinel.
-__global__ __launch_bounds__(NL_THREADS) void k_line_offsets(const uint8_t* __restrict__ buf, uint64_t nbytes,
+__global__ __launch_bounds__(NL_THREADS) void k_line_offsets(const uint16_t* __restrict__ nlmask, uint64_t nbytes,
                                                               const uint64_t* __restrict__ chunk_base,
                                                               uint64_t* __restrict__ line_off) {
     const uint64_t base = (uint64_t)blockIdx.x * CHUNK;
@@ -113,9 +128,8 @@ __global__ __launch_bounds__(NL_THREADS) void k_line_offsets(const uint8_t* __re
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int it = 0; it < CHUNK / (NL_THREADS * 16); ++it) {
         uint64_t pos = base + ((uint64_t)it * NL_THREADS + threadIdx.x) * 16;
-        Piece16 pc{{0, 0, 0, 0}};
-        if (pos < nbytes) pc = nl16(buf, pos, nbytes);
-        const uint32_t c = pc.count();
+        uint32_t m = pos < nbytes ? (uint32_t)nlmask[pos >> 4] : 0u;
+        const uint32_t c = (uint32_t)__popc(m);
         // block exclusive scan of c
         uint32_t x = c;
         for (int d = 1; d < 64; d <<= 1) {
@@ -130,13 +144,10 @@ __global__ __launch_bounds__(NL_THREADS) void k_line_offsets(const uint8_t* __re
             tot += wsum[w];
         }
         uint64_t k = run + wpre + x - c;  // index of this thread's first '\n'
-        for (int j = 0; j < 4; ++j) {
-            uint32_t m = pc.m[j];
-            while (m) {
-                const uint32_t b = (uint32_t)__builtin_ctz(m) >> 3;
-                m &= m - 1;
-                line_off[++k] = pos + 4 * j + b + 1;
-            }
+        while (m) {
+            const uint32_t b = (uint32_t)__builtin_ctz(m);
+            m &= m - 1;
+            line_off[++k] = pos + b + 1;
         }
         run += tot;
         __syncthreads();
@@ -452,18 +463,19 @@ __global__ __launch_bounds__(PW) void k_fmt_apply(const DeviceArgs* __restrict__
 
 int64_t count_chunks(uint64_t nbytes) { return (int64_t)((nbytes + CHUNK - 1) / CHUNK); }
 
-int launch_count(const uint8_t* d_buf, uint64_t nbytes, uint64_t* d_chunk, hipStream_t s) {
+int launch_count(const uint8_t* d_buf, uint64_t nbytes, uint64_t* d_chunk, uint16_t* d_nlmask, hipStream_t s) {
     int64_t nc = count_chunks(nbytes);
     if (nc == 0) return 0;
-    hipLaunchKernelGGL(k_count_newlines, dim3((unsigned)nc), dim3(NL_THREADS), 0, s, d_buf, nbytes, d_chunk);
+    hipLaunchKernelGGL(k_count_newlines, dim3((unsigned)nc), dim3(NL_THREADS), 0, s, d_buf, nbytes, d_chunk, d_nlmask);
     hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, d_chunk, nc);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_offsets(const uint8_t* d_buf, uint64_t nbytes, const uint64_t* d_chunk, uint64_t* d_line_off, hipStream_t s) {
+int launch_offsets(const uint16_t* d_nlmask, uint64_t nbytes, const uint64_t* d_chunk, uint64_t* d_line_off,
+                   hipStream_t s) {
     int64_t nc = count_chunks(nbytes);
     if (nc == 0) return 0;
-    hipLaunchKernelGGL(k_line_offsets, dim3((unsigned)nc), dim3(NL_THREADS), 0, s, d_buf, nbytes, d_chunk, d_line_off);
+    hipLaunchKernelGGL(k_line_offsets, dim3((unsigned)nc), dim3(NL_THREADS), 0, s, d_nlmask, nbytes, d_chunk, d_line_off);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
