@@ -10,8 +10,13 @@ Default workload: 100M synthetic 'combined' lines per GPU (~25 GB, seed
 Prints ONE JSON line on rank 0.  --workload 3 / 4 runs BASELINE.json configs
 3 (strftime timestamps, 5 % malformed lines) and 4 (NGINX upstream log
 format) the same way, for the records in DESIGN.md; the headline is config 2.
+--workload 5 is config 5: a mixed-format corpus (40 % 'combined', 30 % config-4
+NGINX, 30 % 'common' lines) parsed by one three-format handle (sticky active
+format on the device), streamed through it in ~1 GiB newline-aligned batches
+so the routing state is carried across batches; it also reports the
+PCIe-inclusive rate of host-resident batches (H2D copy inside the call).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--lines L] [--workload 2|3|4]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--lines L] [--workload 2|3|4|5]
 """
 import argparse
 import concurrent.futures as cf
@@ -24,10 +29,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-SEEDS = {2: 20261015, 3: 20261016, 4: 20261017}
+SEEDS = {2: 20261015, 3: 20261016, 4: 20261017, 5: 20261018}
 WORKLOAD_NAMES = {2: "config 2: %d synthetic 'combined' lines",
                   3: "config 3: %d synthetic 'combinedio' + %%{%%d/%%b/%%Y %%T}t.%%{msec_frac}t lines (5%% malformed)",
-                  4: "config 4: %d synthetic NGINX '$request_time $upstream_response_time $pipe' lines"}
+                  4: "config 4: %d synthetic NGINX '$request_time $upstream_response_time $pipe' lines",
+                  5: "config 5: %d synthetic mixed-format lines (40%% 'combined', 30%% NGINX config-4, 30%% 'common')"}
 
 
 def log(*a):
@@ -37,10 +43,12 @@ def log(*a):
 
 def generate_to_device(lpa, torch, workload, first_line, n_lines, device, chunk=1 << 20, workers=16):
     """Deterministic synthetic lines [first_line, first_line+n_lines) straight
-    into one HBM buffer (host generation in parallel chunks, H2D in order)."""
+    into one HBM buffer (host generation in parallel chunks, H2D in order).
+    Returns (buffer, bytes, end offset of every chunk)."""
     upper = n_lines * 320 + (1 << 20)
     dev = torch.empty(upper, dtype=torch.uint8, device=device)
     pos = 0
+    ends = []
     starts = list(range(first_line, first_line + n_lines, chunk))
     with cf.ThreadPoolExecutor(max_workers=workers) as ex:
         futs = []
@@ -63,11 +71,46 @@ def generate_to_device(lpa, torch, workload, first_line, n_lines, device, chunk=
             host = torch.frombuffer(bytearray(data), dtype=torch.uint8)
             dev[pos:pos + len(data)].copy_(host)
             pos += len(data)
+            ends.append(pos)
             done += 1
             if done % 16 == 0:
                 log("  generated %d/%d chunks (%.1f GB, %.0f s)" % (done, len(starts), pos / 1e9, time.time() - t0))
     torch.cuda.synchronize()
-    return dev, pos
+    return dev, pos, ends
+
+
+def batch_ranges(ends, target):
+    """Group consecutive newline-aligned chunks into batches of about target bytes."""
+    out, start = [], 0
+    for k, e in enumerate(ends):
+        if e - start >= target or k == len(ends) - 1:
+            out.append((start, e - start))
+            start = e
+    return out
+
+
+def pcie_inclusive(torch, parser, buf, batches, max_bytes):
+    """Host-resident batches (pinned), each copied H2D inside lp_parse_batch:
+    the rate a caller handing over host buffers sees (never the headline)."""
+    n = 0
+    sel = []
+    for off, nb in batches:
+        if n + nb > max_bytes and sel:
+            break
+        sel.append((off, nb))
+        n += nb
+    host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    host.copy_(buf[sel[0][0]:sel[0][0] + n])
+    torch.cuda.synchronize()
+    lines = 0
+    t0 = time.perf_counter()
+    pos = 0
+    for _, nb in sel:
+        lines += parser.run(host.data_ptr() + pos, nb, on_device=False)["lines"]
+        pos += nb
+    dt = time.perf_counter() - t0
+    return {"value": round(n / dt / 1e9, 3), "unit": "GB/s", "lines_per_s": round(lines / dt, 1),
+            "sample": "%d host-pinned batches (%.2f GB), H2D copy + newline index + parse per call, serial" % (len(sel), n / 1e9)}
 
 
 def cpu_baseline(lpa, workload, fields, sample_lines, threads):
@@ -119,7 +162,10 @@ def main():
     ap.add_argument("--cpu-sample-lines", type=int, default=2_000_000)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--workload", type=int, default=2, choices=(2, 3, 4), help="BASELINE.json config")
+    ap.add_argument("--workload", type=int, default=2, choices=(2, 3, 4, 5), help="BASELINE.json config")
+    ap.add_argument("--batch-mb", type=int, default=None,
+                    help="split the resident input into newline-aligned batches of about this size "
+                         "(default: one batch; 1024 for --workload 5)")
     ap.add_argument("--fields", default="all",
                     help="all (the config-2 workload) | comma list of TYPE:path (profiling experiments only)")
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic_latest.json"),
@@ -145,14 +191,23 @@ def main():
     fmt = lpa.SYNTH_FORMATS[wl]
     fields = lpa.get_possible_paths(fmt) if args.fields == "all" else args.fields.split(",")
     log("rank %d/%d: generating %d lines (config %d, seed %d) on %s" % (rank, world, args.lines, wl, SEEDS[wl], device))
-    buf, nbytes = generate_to_device(lpa, torch, wl, rank * args.lines, args.lines, device)
+    buf, nbytes, ends = generate_to_device(lpa, torch, wl, rank * args.lines, args.lines, device)
     log("input resident in HBM: %.2f GB" % (nbytes / 1e9))
+    batch_mb = args.batch_mb if args.batch_mb is not None else (1024 if wl == 5 else 0)
+    batches = batch_ranges(ends, batch_mb << 20) if batch_mb > 0 else [(0, nbytes)]
 
     parser = lpa.HttpdLoglineParser(fmt, fields, device=local)
     counters = torch.zeros(4, dtype=torch.int64, device=device)
 
     def step():
-        st = parser.run(buf.data_ptr(), nbytes, on_device=True)
+        st = None
+        for off, nb in batches:
+            r = parser.run(buf.data_ptr() + off, nb, on_device=True)
+            if st is None:
+                st = r
+            else:
+                for k in ("lines", "ok", "bad", "fallback", "ms_total", "ms_index", "ms_parse", "bytes_in", "bytes_out"):
+                    st[k] += r[k]
         if world > 1:
             counters.copy_(torch.tensor([st["lines"], st["ok"], st["bad"], st["fallback"]], dtype=torch.int64))
             reduce_counters(counters)  # RCCL all-reduce: the only cross-GPU traffic
@@ -203,6 +258,7 @@ def main():
             "lines_per_gpu": stats["lines"],
             "bytes_per_gpu": nbytes,
             "parallelism": "dp%d (newline-aligned shards, RCCL counter all-reduce)" % world,
+            "batches_per_step": len(batches),
         },
         "status_counts": {k: int(stats[k]) for k in ("lines", "ok", "bad", "fallback")},
         "kernel_ms": {"parse_avg": round(avg_parse, 3), "index_avg": round(sum(index_ms) / len(index_ms), 3)},
@@ -219,6 +275,11 @@ def main():
         },
         "cpu_baseline": None,
     }
+    if wl == 5:
+        result["config"]["formats"] = fmt.split("\n")
+        result["config"]["corpus_bytes_all_ranks"] = total_bytes
+        if rank == 0:
+            result["pcie_inclusive"] = pcie_inclusive(torch, parser, buf, batches, 4 << 30)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline (oracle, %d threads) ..." % args.cpu_threads)
         result["cpu_baseline"] = cpu_baseline(lpa, wl, fields, args.cpu_sample_lines, args.cpu_threads)

@@ -127,10 +127,13 @@ int64_t lp_synth_combined(uint64_t seed, int64_t first_line, int64_t max_lines,
  *                      "%{Referer}i" "%{User-Agent}i" %I %O', 5 % malformed lines
  *   LP_SYNTH_NGINX     config 4, the NGINX log_format of
  *                      hpt/nginxmodules/NginxUpstreamTest.java:94
+ *   LP_SYNTH_MIXED     config 5, 40 % config-2, 30 % config-4 and 30 % 'common'
+ *                      lines (mutually exclusive formats), chosen per line
  * Returns LP_E_INVALID for an unknown workload. */
 #define LP_SYNTH_COMBINED 2
 #define LP_SYNTH_STRFTIME 3
 #define LP_SYNTH_NGINX 4
+#define LP_SYNTH_MIXED 5
 int64_t lp_synth(int workload, uint64_t seed, int64_t first_line, int64_t max_lines,
                  char *out, size_t cap, int64_t *n_lines);
 

@@ -120,15 +120,18 @@ def synth_combined(seed, first_line, n_lines):
     return buf.raw[:nb]
 
 
-SYNTH_COMBINED, SYNTH_STRFTIME, SYNTH_NGINX = 2, 3, 4
+SYNTH_COMBINED, SYNTH_STRFTIME, SYNTH_NGINX, SYNTH_MIXED = 2, 3, 4, 5
 
-# the LogFormat of each synthetic workload (BASELINE.json configs 2-4)
+# the LogFormat of each synthetic workload (BASELINE.json configs 2-5)
 SYNTH_FORMATS = {
     SYNTH_COMBINED: "combined",
     SYNTH_STRFTIME: '%h %l %u [%{%d/%b/%Y %T}t.%{msec_frac}t] "%r" %>s %b "%{Referer}i" "%{User-Agent}i" %I %O',
     SYNTH_NGINX: '$remote_addr - $remote_user [$time_local] "$request" $status $body_bytes_sent "$http_referer" '
                  '"$http_user_agent" "$http_x_forwarded_for" $request_time $upstream_response_time $pipe',
 }
+# config 5: the three formats of the mixed corpus, one LogFormat per line, in
+# HttpdLogFormatDissector's list order (hp/HttpdLogFormatDissector.java:110-125)
+SYNTH_FORMATS[SYNTH_MIXED] = "\n".join((SYNTH_FORMATS[SYNTH_COMBINED], SYNTH_FORMATS[SYNTH_NGINX], "common"))
 
 
 def synth(workload, seed, first_line, n_lines):

@@ -751,7 +751,7 @@ __host__ __device__ LP_INLINE int cand_first(const Program& P, const Elem& e, co
         // IPv6 alternative can only match empty at '-' (no hex/':'), so '-'
         // is exact when the following literal cannot start at p.
         if (e.kind == EK_CLF_IP && p < L.n && L[p] == '-' && e.nlit && (e.lit4 & 0xFFu) != '-') return p + 1;
-        return -2;
+        return -2;  // resolved by match_line (ip_resolve)
     }
     case EK_ANYCHAR: return p < L.n ? p + 1 : -1;  // '.': the guard already rejected line terminators
     case EK_DECIMAL: return decimal_at(L, p);
@@ -781,8 +781,11 @@ __host__ __device__ LP_INLINE int cand_first(const Program& P, const Elem& e, co
 // ":?(?:H{1,4}(?::|.)?){0,8}(?::|::)?(?:H{1,4}(?::|.)?){0,8}" (digits are
 // hex, '.' matches the dots), so the reachable ends of that branch are
 // simulated as bit sets over the <= 83 bytes it can span.
+// ip_alt_ends: the same ends as a bit set (bit k = end p + k); returns
+// whether there is any.
 template <typename LN>
-__host__ __device__ LP_INLINE bool ip_alt_end_possible(const Program& P, const LN& L, const Elem& e, int p, int cur) {
+__host__ __device__ LP_INLINE bool ip_alt_ends(const Program& P, const LN& L, const Elem& e, int p, int cur,
+                                               uint32_t* ends) {
     constexpr int W = 96;
     uint32_t cur_set[3] = {1u, 0u, 0u}, all[3];
     auto add = [](uint32_t* m, int k) { if (k < W) m[k >> 5] |= 1u << (k & 31); };
@@ -818,11 +821,19 @@ __host__ __device__ LP_INLINE bool ip_alt_end_possible(const Program& P, const L
     }
     uint32_t fin[3] = {mid[0], mid[1], mid[2]};
     groups(mid, fin);
+    bool any = false;
+    ends[0] = ends[1] = ends[2] = 0u;
     for (int k = 0; k < W; ++k) {
         if (!has(fin, k) || p + k == cur || p + k > L.n) continue;
-        if (e.last ? p + k == L.n : (!e.nlit || lit_at(P, L, p + k, e))) return true;
+        if (e.last ? p + k == L.n : (!e.nlit || lit_at(P, L, p + k, e))) { add(ends, k); any = true; }
     }
-    return false;
+    return any;
+}
+
+template <typename LN>
+__host__ __device__ LP_INLINE bool ip_alt_end_possible(const Program& P, const LN& L, const Elem& e, int p, int cur) {
+    uint32_t ends[3];
+    return ip_alt_ends(P, L, e, p, cur, ends);
 }
 
 // Next candidate after 'cur' (same priority order).
@@ -872,16 +883,49 @@ __host__ __device__ LP_INLINE int cand_next(const Program& P, const Elem& e, con
     return -2;
 }
 
+struct NoCapsDfs {
+    __host__ __device__ LP_INLINE void set(int, uint32_t) {}
+};
+
 // Backtracking match of "^" elems "$" with java.util.regex priority
 // semantics.  caps = spans of the captured tokens.  stk: P.max_stack entries.
 // elems: the ne elements of one LogFormat.
 // elems: the program's element table (the kernel passes an LDS copy).
-template <typename LN, typename EL, typename Caps, typename Stk>
+//
+// An IP token whose other alternatives could end elsewhere (cand_* = -2:
+// the IPv6 branch of FORMAT_IP, TokenParser.java:43-52, and FORMAT_CLF_IP's
+// '-') is resolved exactly when none of those ends lets the rest of the
+// format match: a nested DFS over the remaining elements from each such end
+// (stack entries above the caller's; Nested = no further nesting).  Then the
+// token has no further candidate (-1); otherwise the line is FALLBACK, as
+// the priority order among the IPv6 branch's ends is not modelled.
+template <bool Nested = false, typename LN, typename EL, typename Caps, typename Stk>
 __host__ __device__ LP_INLINE int match_line(const Program& P, const EL& elems, int ne, const LN& L, Caps& caps,
-                                             Stk stk) {
-    int i = 0, pos = 0, sp = 0;
+                                             Stk stk, int pos0 = 0, int sp0 = 0) {
+    int i = 0, pos = pos0, sp = sp0;
     int steps = 0;
     const int budget = 16 * L.n + 256;
+    // -1 when no alternative end of the IP element j at p (other than cur)
+    // completes the match, -2 otherwise
+    auto ip_resolve = [&](int j, int p, int cur, int spn) -> int {
+        if constexpr (Nested) {
+            return -2;
+        } else {
+            const Elem& e = elems[j];
+            if (e.kind != EK_IP && e.kind != EK_CLF_IP) return -2;
+            uint32_t ends[3];
+            ip_alt_ends(P, L, e, p, cur, ends);
+            if (e.kind == EK_CLF_IP && p < L.n && L[p] == '-' && p + 1 != cur) ends[0] |= 2u;  // the '-' alternative
+            NoCapsDfs nc;
+            for (int w = 0; w < 3; ++w) {
+                for (uint32_t m = ends[w]; m; m &= m - 1) {
+                    const int k = 32 * w + __builtin_ctz(m);
+                    if (match_line<true>(P, elems + j + 1, ne - j - 1, L, nc, stk, p + k, spn) != ST_BAD) return -2;
+                }
+            }
+            return -1;
+        }
+    };
     for (;;) {
         if (++steps > budget) return ST_FALLBACK;
         bool ok;
@@ -895,6 +939,7 @@ __host__ __device__ LP_INLINE int match_line(const Program& P, const EL& elems, 
                 if (ok) { pos += e.lit_len; ++i; continue; }
             } else {
                 int c = cand_first(P, e, L, pos);
+                if (c == -2) c = ip_resolve(i, pos, -1, sp);
                 if (c == -2) return ST_FALLBACK;
                 ok = c >= 0;
                 if (ok) {
@@ -911,11 +956,12 @@ __host__ __device__ LP_INLINE int match_line(const Program& P, const EL& elems, 
         }
         // backtrack to the most recent choice point with another candidate
         for (;;) {
-            if (sp == 0) return ST_BAD;
+            if (sp == sp0) return ST_BAD;
             uint32_t top = stk[sp - 1];
             int j = top & 63, p = (top >> 6) & 8191, cur = (top >> 19) & 8191;
             const Elem e = elems[j];
             int c = cand_next(P, e, L, p, cur);
+            if (c == -2) c = ip_resolve(j, p, cur, sp);
             if (c == -2) return ST_FALLBACK;
             if (c >= 0) {
                 stk[sp - 1] = (uint32_t)j | ((uint32_t)p << 6) | ((uint32_t)c << 19);
@@ -959,8 +1005,56 @@ struct NoCaps {
     __host__ __device__ LP_INLINE void set(int, uint32_t) {}
 };
 
+// '"' bytes of the line (aligned words of the base, SWAR compare)
+template <typename LN>
+__host__ __device__ LP_INLINE int count_quotes(const LN& L) {
+    if (L.n <= 0) return 0;
+    const uint32_t a = L.o, b = L.o + (uint32_t)L.n - 1;
+    int cnt = 0;
+    for (uint32_t w = a >> 2; w <= b >> 2; ++w) {
+        uint32_t m = swar::eq(L.word(w), '"');
+        if (w == a >> 2) m &= 0xFFFFFFFFu << (8 * (a & 3));
+        if (w == b >> 2) m &= 0xFFFFFFFFu >> (8 * (3 - (b & 3)));
+        cnt += __builtin_popcount(m);
+    }
+    return cnt;
+}
+
+// Necessary conditions for format elems to match the whole line, checked
+// from its end: trailing literals and '.' elements at their fixed places,
+// then the last byte of the token before them in its class.  false = the
+// format cannot match (exact), so the routing pass skips its DFS.
+template <typename LN, typename EL>
+__host__ __device__ LP_INLINE bool fmt_tail_ok(const Program& P, const EL& elems, int ne, const LN& L) {
+    int q = L.n;
+    for (int i = ne - 1; i >= 0; --i) {
+        const Elem e = elems[i];
+        if (e.kind == EK_LIT) {
+            q -= e.lit_len;
+            if (q < 0 || !lit_at(P, L, q, e)) return false;
+            continue;
+        }
+        if (e.kind == EK_ANYCHAR) {
+            if (--q < 0) return false;
+            continue;
+        }
+        const uint32_t c = q > 0 ? L[q - 1] : 0u;
+        switch (e.kind) {
+        case EK_NUMBER: case EK_NONZERO: case EK_DECIMAL: case EK_MSEC: case EK_TIME_US:
+        case EK_UPLIST_DEC: case EK_UPLIST_NUM:
+            return q > 0 && is_digit(c);
+        case EK_CLFNUMBER: return q > 0 && (is_digit(c) || c == '-');
+        case EK_HEXNUMBER: return q > 0 && is_hex(c);
+        case EK_CLFHEXNUMBER: return q > 0 && (is_hex(c) || c == '-');
+        default: return true;
+        }
+    }
+    return q == 0;
+}
+
 // The match word of a line for sticky routing: bit f = format f matches,
-// bit 8+f = undecided on the device (FALLBACK).
+// bit 8+f = undecided on the device (FALLBACK).  Formats whose literal '"'
+// count or line tail rule them out skip the DFS.
 template <typename LN, typename EL, typename Stk>
 __host__ __device__ LP_INLINE uint32_t fmt_match_word(const Program& P, const EL& elems, const LN& L, Stk stk,
                                                       bool clean) {
@@ -969,8 +1063,11 @@ __host__ __device__ LP_INLINE uint32_t fmt_match_word(const Program& P, const EL
     if (!clean && find_fwd(L, 0, L.n, [](uint32_t w) { return swar::guard_bad(w); }) < L.n) return all << 8;
     uint32_t m = 0;
     NoCaps nc;
+    const int quotes = count_quotes(L);
     for (int f = 0; f < P.n_fmt; ++f) {
-        const int st = match_line(P, elems + P.fmt_elem0[f], P.fmt_elem0[f + 1] - P.fmt_elem0[f], L, nc, stk);
+        const int e0 = P.fmt_elem0[f], ne = P.fmt_elem0[f + 1] - e0;
+        if (quotes < P.fmt_quotes[f] || !fmt_tail_ok(P, elems + e0, ne, L)) continue;
+        const int st = match_line(P, elems + e0, ne, L, nc, stk);
         m |= st == ST_OK ? (1u << f) : st == ST_FALLBACK ? (256u << f) : 0u;
     }
     return m;

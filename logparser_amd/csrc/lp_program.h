@@ -146,6 +146,7 @@ struct Program {
     int32_t max_stack;    // DFS depth bound = number of non-deterministic elements (<= MAX_STACK)
     uint8_t fmt_elem0[MAX_FMT + 1];  // elements of format f: [fmt_elem0[f], fmt_elem0[f + 1])
     uint8_t fmt_apache[MAX_FMT];     // 1 = Apache decodeExtractedValue rules, 0 = NGINX
+    uint8_t fmt_quotes[MAX_FMT];     // '"' bytes in format f's literals (a line needs at least as many)
     Elem elems[MAX_ELEMS];
     TimeStage time[MAX_TIME];
     FlStage fl[MAX_FL];

@@ -1129,6 +1129,13 @@ void Plan::compile_program() {
         if (n_tok > P.n_tok) P.n_tok = n_tok;
     }
     P.fmt_elem0[P.n_fmt] = (uint8_t)P.n_elems;
+    for (int fi = 0; fi < P.n_fmt; ++fi) {
+        int q = 0;
+        for (int i = P.fmt_elem0[fi]; i < P.fmt_elem0[fi + 1]; ++i)
+            if (P.elems[i].kind == EK_LIT)
+                for (int k = 0; k < P.elems[i].lit_len; ++k) q += P.lit[P.elems[i].lit_off + k] == '"';
+        P.fmt_quotes[fi] = (uint8_t)(q > 255 ? 255 : q);
+    }
     auto fmt_of_elem = [&](int i) {
         int fi = 0;
         while (i >= P.fmt_elem0[fi + 1]) ++fi;

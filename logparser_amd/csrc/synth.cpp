@@ -1,5 +1,5 @@
 // Deterministic synthetic access-log generators for BASELINE.json configs
-// 2, 3 and 4: every line i is a pure function
+// 2, 3, 4 and 5: every line i is a pure function
 // of (seed, i), so any range of lines can be generated independently (and in
 // parallel) and re-generated bit-identically for parity checks.
 #include <cstdint>
@@ -293,6 +293,39 @@ void nginx_line(Out& o, uint64_t seed, int64_t i) {
     o.c('\n');
 }
 
+// Apache 'common' ('%h %l %u %t "%r" %>s %b'): a combined line without the
+// referer and user agent
+void common_line(Out& o, uint64_t seed, int64_t i) {
+    Rng r = line_rng(seed, i);
+    who(o, r);
+    o.s(" [");
+    stamp(o, r, ':');
+    o.c(' ');
+    o.s(OFFSETS[r.below(7)]);
+    o.s("] \"");
+    request(o, r);
+    o.s("\" ");
+    o.u(STATUS[r.below(12)]);
+    o.c(' ');
+    if (r.pct(95)) o.u(r.below(200000)); else o.c('-');
+    o.c('\n');
+}
+
+// config 5: mixed-format corpus, 40 % config-2 'combined', 30 % config-4
+// NGINX, 30 % 'common' lines.  The three formats are
+// mutually exclusive (a combined line ends in '"', an NGINX line in its $pipe
+// byte after a time, a common line in %b), so the sticky active-format state
+// of HttpdLogFormatDissector is history-independent and every line is
+// decided by its own format.
+void mixed_line(Out& o, uint64_t seed, int64_t i) {
+    Rng r(seed ^ 0xA5A5A5A55A5A5A5Aull);
+    r.s += (uint64_t)i * 0xD1B54A32D192ED03ull;
+    const uint32_t k = r.below(10);
+    if (k < 4) combined_line(o, seed, i);
+    else if (k < 7) nginx_line(o, seed, i);
+    else common_line(o, seed, i);
+}
+
 }  // namespace
 
 extern "C" int64_t lp_synth(int workload, uint64_t seed, int64_t first_line, int64_t max_lines, char* out,
@@ -300,6 +333,7 @@ extern "C" int64_t lp_synth(int workload, uint64_t seed, int64_t first_line, int
     void (*gen)(Out&, uint64_t, int64_t) = workload == LP_SYNTH_COMBINED   ? combined_line
                                            : workload == LP_SYNTH_STRFTIME ? strftime_line
                                            : workload == LP_SYNTH_NGINX    ? nginx_line
+                                           : workload == LP_SYNTH_MIXED    ? mixed_line
                                                                            : nullptr;
     if (!gen) return LP_E_INVALID;
     Out o{out, 0, cap};

@@ -323,3 +323,49 @@ def test_authority_variants_emulated(oracle, emu):
             lines.append(base.replace(b"%s/p?q=1", (h + tail + "/p?q=1").encode()))
     s = compare(o, e, lines)
     assert s["ok"] > 100, s
+
+
+def test_synth_config5_mix():
+    """lp_synth workload 5 (BASELINE config 5): per-line choice of 40 %
+    'combined', 30 % NGINX config-4 and 30 % 'common' lines, deterministic per
+    line index (any range re-generates bit-identically)."""
+    lines = lpa.synth(lpa.SYNTH_MIXED, 20261018, 0, 20000).split(b"\n")[:-1]
+    assert len(lines) == 20000
+    nginx = sum(1 for l in lines if not l.endswith(b'"') and l[-1:] in (b"p", b"."))
+    combined = sum(1 for l in lines if l.endswith(b'"'))
+    common = len(lines) - nginx - combined
+    assert abs(combined / 20000 - 0.4) < 0.02 and abs(nginx / 20000 - 0.3) < 0.02 and abs(common / 20000 - 0.3) < 0.02
+    assert lpa.synth(lpa.SYNTH_MIXED, 20261018, 777, 5).split(b"\n")[:-1] == lines[777:782]
+
+
+def test_mixed_config5_emulated(oracle, emu):
+    """BASELINE config 5 corpus through the three-format handle: every line
+    decided by its own (mutually exclusive) format, all paths, no FALLBACK."""
+    fmt = lpa.SYNTH_FORMATS[lpa.SYNTH_MIXED]
+    assert fmt == MIXED
+    paths = oracle.possible_paths(fmt)
+    o = oracle.Oracle(fmt, paths)
+    e = emu.Emu(fmt, paths)
+    assert e.status == 0, e.err
+    lines = lpa.synth(lpa.SYNTH_MIXED, 20261018, 0, 3000).split(b"\n")[:-1]
+    s = compare(o, e, lines, allow_fallback=False)
+    assert s["ok"] == 3000, s
+
+
+IP_TOKENS = ["api.jdoagd.com", "abc", "::1", "fe80::1", "1.2.3", "dead:beef", "-", "a:b", "1.2.3.4.5", "999.1.1.1",
+             "cafe.babe", "x", "g", "a.b", "1.2.3.4", "01.2.3.4", "ab:cd:ef", "1::", ":", "a-b", "--", "a.-"]
+
+
+@pytest.mark.parametrize("fmt", ["nginx", "common", "mixed"])
+def test_ip_token_variants_emulated(oracle, emu, fmt):
+    """FORMAT_IP / FORMAT_CLF_IP (TokenParser.java:43-52) on non-IPv4 hosts:
+    a host whose IPv6-branch ends cannot be followed by the format's next
+    literal is decided (BAD or the next format), the rest is exact or FALLBACK."""
+    f = {"nginx": NGINX, "common": "common", "mixed": MIXED}[fmt]
+    paths = oracle.possible_paths(f)
+    o = oracle.Oracle(f, paths)
+    e = emu.Emu(f, paths)
+    base = lpa.synth(lpa.SYNTH_MIXED, 20261018, 0, 60).split(b"\n")[:-1]
+    lines = [t.encode() + b" " + l.split(b" ", 1)[1] for l in base for t in IP_TOKENS[:: 1 + len(l) % 3]]
+    s = compare(o, e, lines)
+    assert s["fallback"] < len(lines) // 4, s

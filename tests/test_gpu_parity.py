@@ -247,3 +247,28 @@ def test_authority_variants_gpu(oracle):
     lines = [base.replace(b"%s/p?q=1", (h + t + "/p?q=1").encode()) for h in HOSTS for t in ("", "/x", "#f", "?a")]
     s, _ = gpu_vs_oracle(oracle, "combined", paths(oracle), lines)
     assert s["ok"] > 100, s
+
+
+def test_mixed_config5_gpu(oracle):
+    """BASELINE config 5: the mixed-format corpus (lp_synth workload 5) through
+    one three-format handle, bit-exact against the stateful oracle with no
+    FALLBACK; then the same lines streamed as three batches of one handle
+    (routing state carried across batches, as bench.py --workload 5 does)
+    give the same statuses and records."""
+    fmt = lpa.SYNTH_FORMATS[lpa.SYNTH_MIXED]
+    fields = paths(oracle, fmt)
+    lines = lpa.synth(lpa.SYNTH_MIXED, 20261018, 0, 20000).split(b"\n")[:-1]
+    s, r = gpu_vs_oracle(oracle, fmt, fields, lines, allow_fallback=False)
+    assert s["ok"] == 20000, s
+    whole = [r.record_json(i) for i in range(0, 20000, 97)]
+    p = lpa.HttpdLoglineParser(fmt, fields)
+    got = {}
+    base = 0
+    for part in (lines[:6001], lines[6001:13333], lines[13333:]):
+        rb = p.parse_batch(b"".join(l + b"\n" for l in part))
+        assert rb.n_lines == len(part) and rb.counters["ok"] == len(part)
+        for i in range(len(part)):
+            if (base + i) % 97 == 0:
+                got[base + i] = rb.record_json(i)
+        base += len(part)
+    assert [got[i] for i in range(0, 20000, 97)] == whole
