@@ -41,14 +41,17 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def generate_to_device(lpa, torch, workload, first_line, n_lines, device, chunk=1 << 20, workers=16):
+def generate_to_device(lpa, torch, workload, first_line, n_lines, device, chunk=1 << 20, workers=16, batch_bytes=0):
     """Deterministic synthetic lines [first_line, first_line+n_lines) straight
     into one HBM buffer (host generation in parallel chunks, H2D in order).
-    Returns (buffer, bytes, end offset of every chunk)."""
+    With batch_bytes, consecutive chunks are grouped into batches of about
+    that size, each starting 4 KiB-aligned (as a streaming reader's staging
+    buffers would).  Returns (buffer, bytes of lines, [(offset, bytes)] batches)."""
     upper = n_lines * 320 + (1 << 20)
     dev = torch.empty(upper, dtype=torch.uint8, device=device)
     pos = 0
-    ends = []
+    batches = []
+    bstart = 0
     starts = list(range(first_line, first_line + n_lines, chunk))
     with cf.ThreadPoolExecutor(max_workers=workers) as ex:
         futs = []
@@ -66,27 +69,20 @@ def generate_to_device(lpa, torch, workload, first_line, n_lines, device, chunk=
                 s = starts[nxt]
                 futs.append(ex.submit(lpa.synth, workload, SEEDS[workload], s, min(chunk, first_line + n_lines - s)))
                 nxt += 1
+            if batch_bytes and pos - bstart >= batch_bytes:
+                batches.append((bstart, pos - bstart))
+                pos = bstart = (pos + 4095) & ~4095
             if pos + len(data) > upper:
                 raise RuntimeError("synthetic data larger than the device buffer bound")
             host = torch.frombuffer(bytearray(data), dtype=torch.uint8)
             dev[pos:pos + len(data)].copy_(host)
             pos += len(data)
-            ends.append(pos)
             done += 1
             if done % 16 == 0:
                 log("  generated %d/%d chunks (%.1f GB, %.0f s)" % (done, len(starts), pos / 1e9, time.time() - t0))
     torch.cuda.synchronize()
-    return dev, pos, ends
-
-
-def batch_ranges(ends, target):
-    """Group consecutive newline-aligned chunks into batches of about target bytes."""
-    out, start = [], 0
-    for k, e in enumerate(ends):
-        if e - start >= target or k == len(ends) - 1:
-            out.append((start, e - start))
-            start = e
-    return out
+    batches.append((bstart, pos - bstart))
+    return dev, sum(b[1] for b in batches), batches
 
 
 def pcie_inclusive(torch, parser, buf, batches, max_bytes):
@@ -100,7 +96,10 @@ def pcie_inclusive(torch, parser, buf, batches, max_bytes):
         sel.append((off, nb))
         n += nb
     host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
-    host.copy_(buf[sel[0][0]:sel[0][0] + n])
+    pos = 0
+    for off, nb in sel:
+        host[pos:pos + nb].copy_(buf[off:off + nb])
+        pos += nb
     torch.cuda.synchronize()
     lines = 0
     t0 = time.perf_counter()
@@ -191,10 +190,10 @@ def main():
     fmt = lpa.SYNTH_FORMATS[wl]
     fields = lpa.get_possible_paths(fmt) if args.fields == "all" else args.fields.split(",")
     log("rank %d/%d: generating %d lines (config %d, seed %d) on %s" % (rank, world, args.lines, wl, SEEDS[wl], device))
-    buf, nbytes, ends = generate_to_device(lpa, torch, wl, rank * args.lines, args.lines, device)
-    log("input resident in HBM: %.2f GB" % (nbytes / 1e9))
     batch_mb = args.batch_mb if args.batch_mb is not None else (1024 if wl == 5 else 0)
-    batches = batch_ranges(ends, batch_mb << 20) if batch_mb > 0 else [(0, nbytes)]
+    buf, nbytes, batches = generate_to_device(lpa, torch, wl, rank * args.lines, args.lines, device,
+                                              batch_bytes=batch_mb << 20)
+    log("input resident in HBM: %.2f GB in %d batch(es)" % (nbytes / 1e9, len(batches)))
 
     parser = lpa.HttpdLoglineParser(fmt, fields, device=local)
     counters = torch.zeros(4, dtype=torch.int64, device=device)

@@ -137,6 +137,13 @@ def test_device_tensor_input(oracle):
     recs = [a.record_json(i) for i in range(0, 2000, 97)]
     b = p.parse_batch(lines)
     assert [b.record_json(i) for i in range(0, 2000, 97)] == recs
+    # a line-aligned slice that starts mid-word (a batch of a larger buffer)
+    for skew in (1, 3, 7, 13):
+        u = torch.zeros(len(lines) + 16, dtype=torch.uint8, device="cuda")
+        u[skew:skew + len(lines)].copy_(t)
+        c = p.parse_batch(u[skew:skew + len(lines)])
+        assert c.n_lines == 2000 and c.counters["ok"] == 2000
+        assert [c.record_json(i) for i in range(0, 2000, 97)] == recs
 
 
 def test_large_batch_properties(oracle):
