@@ -375,7 +375,7 @@ __global__ __launch_bounds__(PW) void k_parse_lines(const uint8_t* __restrict__ 
                 if constexpr (MASKS) {
                     uint32_t m0, m1;
                     bcls::classify16(v[j][0], v[j][1], v[j][2], v[j][3], m0, m1);
-                    msk16[4 * mwords * MC_QUOTE + k] = (uint16_t)m0;
+                    if (MC_QUOTE >= 0) msk16[4 * mwords * MC_QUOTE + k] = (uint16_t)m0;
                     msk16[4 * mwords * MC_UEV + k] = (uint16_t)m1;
                 }
             }

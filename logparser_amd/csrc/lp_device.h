@@ -89,11 +89,19 @@ __device__ LP_INLINE uint32_t load_word(const LP_G uint8_t* p) {
 // per-line scanners walk 64 bytes per step instead of 4.  Exact for TAB and
 // printable ASCII (every other byte sends its line to FALLBACK before any
 // scanner runs).
+#if LP_EXP == 4  // experiment: no QUOTE class (less LDS per wave); quotes found by SWAR scans
+enum : int {
+    MC_QUOTE = -1,
+    MC_UEV = 0,
+    MC_N = 1
+};
+#else
 enum : int {
     MC_QUOTE = 0,  // '"'
     MC_UEV = 1,    // URI events: % # & ? ; + A-Z and the bytes URIUtil.encode escapes (not '=')
     MC_N = 2
 };
+#endif
 __host__ __device__ LP_INLINE uint64_t mask_load(const uint64_t* p) { return *p; }
 #if defined(__HIP__)
 typedef const __attribute__((address_space(3))) uint64_t* lds_u64;
@@ -210,7 +218,7 @@ __host__ __device__ LP_INLINE void classify16(uint32_t w0, uint32_t w1, uint32_t
     uev = nib(uev_hb(r0)) | (nib(uev_hb(r1)) << 4) | (nib(uev_hb(r2)) << 8) | (nib(uev_hb(r3)) << 12);
 }
 // mask class whose members are exactly the byte c, -1 none
-__host__ __device__ LP_INLINE int class_of(uint32_t c) { return c == '"' ? MC_QUOTE : -1; }
+__host__ __device__ LP_INLINE int class_of(uint32_t c) { return c == '"' && MC_QUOTE >= 0 ? (int)MC_QUOTE : -1; }
 }  // namespace bcls
 
 // Host builder of the class masks of buf[0, n) (n a multiple of 16), the same
@@ -224,7 +232,7 @@ inline void build_masks(const uint8_t* buf, uint32_t n, uint64_t* masks, uint32_
         uint32_t a, b;
         bcls::classify16(w[0], w[1], w[2], w[3], a, b);
         const int sh = 16 * (k & 3);
-        masks[MC_QUOTE * ms + (k >> 2)] |= (uint64_t)a << sh;
+        if (MC_QUOTE >= 0) masks[MC_QUOTE * ms + (k >> 2)] |= (uint64_t)a << sh;
         masks[MC_UEV * ms + (k >> 2)] |= (uint64_t)b << sh;
     }
 }
@@ -569,7 +577,7 @@ __host__ __device__ LP_INLINE int ipv4_first(const LN& L, int p) {
 template <typename LN>
 __host__ __device__ LP_INLINE int kth_from_end(const LN& L, uint32_t c, int k, int lo) {
     if constexpr (LN::has_masks) {
-        if (c == '"') {  // exact class: count set bits of the QUOTE mask backwards
+        if (MC_QUOTE >= 0 && c == '"') {  // exact class: count set bits of the QUOTE mask backwards
             if (L.n - 1 < lo) return -1;
             const uint32_t A = L.o + (uint32_t)L.n - 1, S = L.o + (uint32_t)lo;
             uint32_t W = A >> 6;
@@ -602,7 +610,7 @@ template <typename LN>
 __host__ __device__ LP_INLINE int anchor_bwd(const LN& L, const Elem& e, int hi, int lo) {
     const uint32_t c0 = e.lit4 & 0xFFu;
     if constexpr (LN::has_masks) {
-        if (e.acls >= 0) {
+        if (MC_QUOTE >= 0 && e.acls >= 0) {
             return mfind_bwd(L, e.acls, hi, lo);  // exact class
         }
     }
@@ -612,7 +620,7 @@ template <typename LN>
 __host__ __device__ LP_INLINE int anchor_fwd(const LN& L, const Elem& e, int lo, int to) {
     const uint32_t c0 = e.lit4 & 0xFFu;
     if constexpr (LN::has_masks) {
-        if (e.acls >= 0) {
+        if (MC_QUOTE >= 0 && e.acls >= 0) {
             return mfind_fwd(L, e.acls, lo, to);  // exact class
         }
     }
