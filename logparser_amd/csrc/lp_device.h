@@ -1400,9 +1400,15 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
     // leaf (each element's first candidate) is tried in lock step with the
     // elements read as wave-uniform values (scalar loads, scalar branches on
     // the element kind); lines it does not match run the backtracking DFS.
+    // Lines the first leaf does not match skip the DFS when the format's
+    // quote count or line tail already rules them out (exact; malformed
+    // lines would otherwise backtrack while the rest of the wave waits).
     int st = P.n_fmt == 1 && match_first_leaf(P, L, o.caps) ? ST_OK : ST_BAD;
-    if (st != ST_OK)
-        st = match_line(P, elems + P.fmt_elem0[fmt], P.fmt_elem0[fmt + 1] - P.fmt_elem0[fmt], L, o.caps, stk);
+    if (st != ST_OK) {
+        const int e0 = P.fmt_elem0[fmt], ne = P.fmt_elem0[fmt + 1] - e0;
+        if (P.n_fmt == 1 && (count_quotes(L) < P.fmt_quotes[fmt] || !fmt_tail_ok(P, elems + e0, ne, L))) st = ST_BAD;
+        else st = match_line(P, elems + e0, ne, L, o.caps, stk);
+    }
     LP_PROF(4);
     if (st != ST_OK) { o.status = st; return; }
     // decodeExtractedValue: "-" -> null (Apache: ApacheHttpdLogFormatDissector.java:169-196,
