@@ -86,8 +86,13 @@ def generate_to_device(lpa, torch, workload, first_line, n_lines, device, chunk=
 
 
 def pcie_inclusive(torch, parser, buf, batches, max_bytes):
-    """Host-resident batches (pinned), each copied H2D inside lp_parse_batch:
-    the rate a caller handing over host buffers sees (never the headline)."""
+    """Host-resident batches (pinned), the rate a caller handing over host
+    buffers sees (never the headline):
+      serial     -- each batch copied H2D inside lp_parse_batch (BUF_HOST);
+      overlapped -- double-buffered: the copy of batch i+1 into one aligned
+                    device staging buffer (copy stream) runs while batch i is
+                    parsed from the other (compute stream), one handle, so
+                    the sticky routing state is carried as in the serial case."""
     n = 0
     sel = []
     for off, nb in batches:
@@ -96,20 +101,41 @@ def pcie_inclusive(torch, parser, buf, batches, max_bytes):
         sel.append((off, nb))
         n += nb
     host = torch.empty(n, dtype=torch.uint8, pin_memory=True)
+    hoff = []
     pos = 0
     for off, nb in sel:
         host[pos:pos + nb].copy_(buf[off:off + nb])
+        hoff.append(pos)
         pos += nb
     torch.cuda.synchronize()
     lines = 0
     t0 = time.perf_counter()
-    pos = 0
-    for _, nb in sel:
-        lines += parser.run(host.data_ptr() + pos, nb, on_device=False)["lines"]
-        pos += nb
-    dt = time.perf_counter() - t0
-    return {"value": round(n / dt / 1e9, 3), "unit": "GB/s", "lines_per_s": round(lines / dt, 1),
-            "sample": "%d host-pinned batches (%.2f GB), H2D copy + newline index + parse per call, serial" % (len(sel), n / 1e9)}
+    for (_, nb), h in zip(sel, hoff):
+        lines += parser.run(host.data_ptr() + h, nb, on_device=False)["lines"]
+    dt_serial = time.perf_counter() - t0
+
+    big = max(nb for _, nb in sel)
+    stage = [torch.empty(big + 4096, dtype=torch.uint8, device=buf.device) for _ in range(2)]
+    cs, xs = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    lines2 = 0
+    t0 = time.perf_counter()
+    with torch.cuda.stream(xs):
+        stage[0][:sel[0][1]].copy_(host[hoff[0]:hoff[0] + sel[0][1]], non_blocking=True)
+    xs.synchronize()
+    for i, (_, nb) in enumerate(sel):
+        if i + 1 < len(sel):
+            nb1, h1 = sel[i + 1][1], hoff[i + 1]
+            with torch.cuda.stream(xs):
+                stage[(i + 1) % 2][:nb1].copy_(host[h1:h1 + nb1], non_blocking=True)
+        lines2 += parser.run(stage[i % 2].data_ptr(), nb, on_device=True, stream=cs.cuda_stream)["lines"]
+        xs.synchronize()
+    dt_over = time.perf_counter() - t0
+    return {"value": round(n / dt_over / 1e9, 3), "unit": "GB/s", "lines_per_s": round(lines2 / dt_over, 1),
+            "serial_value": round(n / dt_serial / 1e9, 3),
+            "sample": "%d host-pinned batches (%.2f GB); value: double-buffered H2D (copy stream) overlapped with "
+                      "index + parse (compute stream), one handle; serial_value: H2D copy inside each call" % (len(sel), n / 1e9),
+            "lines": lines2}
 
 
 def cpu_baseline(lpa, workload, fields, sample_lines, threads):
@@ -278,7 +304,7 @@ def main():
         result["config"]["formats"] = fmt.split("\n")
         result["config"]["corpus_bytes_all_ranks"] = total_bytes
         if rank == 0:
-            result["pcie_inclusive"] = pcie_inclusive(torch, parser, buf, batches, 4 << 30)
+            result["pcie_inclusive"] = pcie_inclusive(torch, parser, buf, batches, 8 << 30)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline (oracle, %d threads) ..." % args.cpu_threads)
         result["cpu_baseline"] = cpu_baseline(lpa, wl, fields, args.cpu_sample_lines, args.cpu_threads)
