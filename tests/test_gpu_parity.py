@@ -279,3 +279,31 @@ def test_mixed_config5_gpu(oracle):
                 got[base + i] = rb.record_json(i)
         base += len(part)
     assert [got[i] for i in range(0, 20000, 97)] == whole
+
+
+@pytest.mark.parametrize("which", ["nginx", "mixed"])
+def test_ip_token_variants_gpu(oracle, which):
+    """Non-IPv4 hosts in FORMAT_IP / FORMAT_CLF_IP tokens: the DFS's exact
+    resolution of the IPv6 branch's other ends (nested DFS) on the device."""
+    from test_emu_parity import IP_TOKENS, MIXED, NGINX
+    fmt = {"nginx": NGINX, "mixed": MIXED}[which]
+    base = lpa.synth(lpa.SYNTH_MIXED, 20261018, 0, 60).split(b"\n")[:-1]
+    lines = [t.encode() + b" " + l.split(b" ", 1)[1] for l in base for t in IP_TOKENS[:: 1 + len(l) % 3]]
+    if which == "nginx":
+        s, _ = gpu_vs_oracle(oracle, fmt, paths(oracle, fmt), lines)
+        assert s["fallback"] < len(lines) // 4 and s["bad"] > len(lines) // 2, s
+    else:  # stateful routing: compare line by line against the sticky oracle
+        fields = paths(oracle, fmt)
+        r = lpa.HttpdLoglineParser(fmt, fields).parse_batch(b"".join(l + b"\n" for l in lines))
+        o = oracle.Oracle(fmt, fields)
+        fb = 0
+        for i, l in enumerate(lines):
+            s1, r1 = o.parse_raw(l)
+            s2 = int(r.status[i])
+            if s2 == lpa.LINE_FALLBACK:
+                fb += 1
+                continue
+            assert s1 == s2, (i, l, s1, s2)
+            if s1 == oracle.OK:
+                assert r1 == r.record_json(i), (i, l)
+        assert fb < len(lines) // 4, fb
