@@ -98,7 +98,7 @@ enum : int {
 #else
 enum : int {
     MC_QUOTE = 0,  // '"'
-    MC_UEV = 1,    // URI events: % # & ? ; + A-Z and the bytes URIUtil.encode escapes (not '=')
+    MC_UEV = 1,    // URI events: % # & ? ; + and the bytes URIUtil.encode escapes (not '=', not A-Z)
     MC_N = 2
 };
 #endif
@@ -168,14 +168,17 @@ __host__ __device__ LP_INLINE int count(uint32_t m) { return __builtin_popcount(
 
 // ---- byte classes through two nibble look-up tables (the SIMD "shuffle"
 // classifier): class bits(b) = LO[b & 15] & HI[b >> 4], one v_perm_b32 per
-// 8-entry table half.  Bits: 0 ' ', 1 TAB, 2 '"', 3 hi 2 x lo {3,5,6,B}
-// (# % & +), 4 hi 3 x lo {B,C,E,F} (; < > ?), 5 hi {4,7} x lo {B,C,D,F}
-// (K L M O { | }), 6 hi {4,5} x lo {1..E} (A-N Q-Z [ \ ] ^), 7 hi {5,6} x
-// lo 0 (P `).  WS = bits 0|1, QUOTE = bit 2, UEV = any bit.
+// 8-entry table half.  Bits (rectangles hi-nibble set x lo-nibble set):
+// 0 hi 2 x lo 0 (' '), 1 hi 0 x lo 9 (TAB), 2 hi 2 x lo 2 ('"'),
+// 3 hi 2 x lo {3,5,6,B} (# % & +), 4 hi 3 x lo {B,C,E,F} (; < > ?),
+// 5 hi {5,7} x lo {B,C,D} ([ \ ] { | }), 6 hi 5 x lo E (^), 7 hi 6 x lo 0 (`).
+// QUOTE = bit 2, UEV = any bit: the URI event bytes % # & ? ; + and every
+// byte URIUtil.encode escapes (upper-case letters are not events: the query
+// stage finds a name's upper-case bytes itself, query_piece).
 namespace bcls {
-constexpr uint32_t LO0 = 0x48444081u, LO1 = 0x40484840u;  // LO[0..3], LO[4..7]
-constexpr uint32_t LO2 = 0x78404240u, LO3 = 0x30506070u;  // LO[8..11], LO[12..15]
-constexpr uint32_t HI0 = 0x100D0002u, HI1 = 0x2080C060u;  // HI[0..3], HI[4..7]
+constexpr uint32_t LO0 = 0x08040081u, LO1 = 0x00080800u;  // LO[0..3], LO[4..7]
+constexpr uint32_t LO2 = 0x38000200u, LO3 = 0x10502030u;  // LO[8..11], LO[12..15]
+constexpr uint32_t HI0 = 0x100D0002u, HI1 = 0x20806000u;  // HI[0..3], HI[4..7]
 // v_perm_b32: byte i of the result = byte sel_i (0..7) of (s0:s1), s1 low
 __host__ __device__ LP_INLINE uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) {
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -328,7 +331,7 @@ __host__ __device__ LP_INLINE int mfind_bwd(const LN& L, int c, int hi, int lo) 
 }
 
 // Calls f(q, c) for every position q in [a, b) whose byte c is a URI event
-// byte (MC_UEV: % # & ? ; + A-Z and the URIUtil-escaped bytes), in order,
+// byte (MC_UEV: % # & ? ; + and the URIUtil-escaped bytes), in order,
 // until f returns false.  Returns false when f stopped the walk.  Lines with
 // masks walk 64 bytes per step and read the next event's byte before f runs
 // on the current one (its LDS latency overlaps f); others classify 4 bytes
@@ -1724,8 +1727,7 @@ __host__ __device__ LP_INLINE uint64_t url_decode_value(const LN& L, int vs, int
 // ---- QueryStringFieldDissector (QueryStringFieldDissector.java:56-108).
 // The URI stage's event pass splits the rawQuery at '&' / '?' into a table of
 // one (name ref, value ref) slot per non-empty piece, noting for each piece
-// its first '=' and whether the name needs rewriting (upper case / URIUtil
-// escapes) or the value decoding ('%' / '+').  A plain piece of a stage that
+// its last '%' / '+' (a value that may need decoding).  A plain piece of a stage that
 // wants every name is final at once (two line refs).  Any other piece is
 // left "pending": slot[0] = start | end << 16 | (eq + 1) << 32 | flags << 48,
 // slot[1] = offset of 3 bytes of the line's arena region per piece byte, and
@@ -1738,22 +1740,19 @@ constexpr uint32_t QP_RW = 1, QP_PV = 2;
 struct QueryTable {
     uint32_t tab = 0, reg = 0, count = 0, maxp = 0;
     int s = 0;
-    int fu = -1;  // first upper-case / URIUtil-escaped byte of the piece (lower-cased / escaped name)
     int lp = -1;  // last '%' / '+' of the piece (a value that needs resilientUrlDecode)
     bool on = false, set = false;  // enumerating now / table laid out
-    // piece [s, e) ends: its slot gets the raw piece (bounds, the two flag
-    // positions, the offset of 3 x its length reserved for rewritten bytes);
+    // piece [s, e) ends: its slot gets the raw piece (bounds, the last '%' /
+    // '+', the offset of 3 x its length reserved for rewritten bytes);
     // query_piece completes every slot afterwards, spread over the wave
     __host__ __device__ LP_INLINE void emit(LP_G uint8_t* region, int e) {
         if (e > s) {
             LP_G uint64_t* t = (LP_G uint64_t*)(region + tab) + 2 * count;
-            t[0] = (uint64_t)(uint32_t)s | ((uint64_t)(uint32_t)e << 16) | ((uint64_t)(uint32_t)(fu + 1) << 32) |
-                   ((uint64_t)(uint32_t)(lp + 1) << 48);
+            t[0] = (uint64_t)(uint32_t)s | ((uint64_t)(uint32_t)e << 16) | ((uint64_t)(uint32_t)(lp + 1) << 48);
             t[1] = reg;
             reg += 3 * (uint32_t)(e - s);
             ++count;
         }
-        fu = -1;
         lp = -1;
     }
 };
@@ -1768,13 +1767,14 @@ __host__ __device__ LP_INLINE uint32_t query_piece(const Program& P, const Query
                                                    LP_G uint8_t* region, LP_G uint64_t* slot) {
     const uint64_t a0 = slot[0], a1 = slot[1];
     const int s = (int)(a0 & 0xFFFFu), e = (int)((a0 >> 16) & 0xFFFFu);
-    const int fu = (int)((a0 >> 32) & 0xFFFFu) - 1, lp = (int)((a0 >> 48) & 0xFFFFu) - 1;
+    const int lp = (int)((a0 >> 48) & 0xFFFFu) - 1;
     // the piece's first '=' splits name and value ('=' is not a URI event byte)
     const int f = find_fwd(L, s, e, [](uint32_t w) { return swar::eq(w, '='); });
     const int eq = f < e ? f : -1;
-    const bool rw = fu >= 0 && (eq < 0 || fu < eq);  // upper-case / escaped bytes in the name
-    const bool pv = eq >= 0 && lp > eq;               // '%' / '+' in the value
     const int ne = eq >= 0 ? eq : e;
+    // upper-case / URIUtil-escaped bytes in the name: it is rewritten
+    const bool rw = find_fwd(L, s, ne, [](uint32_t w) { return swar::upper(w) | swar::needs_encode(w); }) < ne;
+    const bool pv = eq >= 0 && lp > eq;               // '%' / '+' in the value
     Arena A{region, (uint32_t)a1, 0};
     // name [s, ne): URIUtil-escaped and lower-cased as in the rawQuery
     uint64_t nref;
@@ -1831,7 +1831,7 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
     uint32_t rewr = 0;
     int st = ST_OK;
     // Fast walk over the events before the first '#' or ';' (the common
-    // bytes % & ? + A-Z and URIUtil-escaped ones, few branches); it stops
+    // bytes % & ? + and URIUtil-escaped ones, few branches); it stops
     // at the first '#', ';' or invalid escape and the general walk below
     // continues from there with the same state.
     int resume = -1;
@@ -1860,11 +1860,9 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
             fa = fa < 0 ? q : fa;
             return true;
         }
-        // + A-Z and URIUtil-escaped bytes
+        // '+' and URIUtil-escaped bytes
         rewr |= (fa >= 0 && uri_needs_encode(c)) ? 2u : 0u;
-        const bool plus = c == '+';
-        T.lp = plus ? q : T.lp;
-        T.fu = (!plus && T.fu < 0) ? q : T.fu;
+        T.lp = c == '+' ? q : T.lp;
         return true;
     });
     LP_PROF(51 + 4 * u);
@@ -1912,13 +1910,10 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
             }
             if (fa < 0) fa = q;
             rewr |= h >= 0 ? 1u : 0u;
-        } else {  // + A-Z and URIUtil-escaped bytes
+        } else {  // '+' and URIUtil-escaped bytes
             const bool enc = uri_needs_encode(c);
             rewr |= (fa >= 0 && h < 0 && enc) ? 2u : 0u;  // URIUtil escapes it
-            if (T.on) {
-                if (c == '+') T.lp = q;
-                else if (T.fu < 0) T.fu = q;
-            }
+            if (T.on && c == '+') T.lp = q;
         }
         return true;
     });
