@@ -32,6 +32,10 @@
  *   lp_counters       the RecordReader counters "Lines read / Good lines /
  *                     Bad lines" (ApacheHttpdLogfileRecordReader.java:118-120)
  *                     plus the FALLBACK count.
+ *   lp_result_*       the whole batch's SoA results in bulk: what a Java
+ *                     GpuHttpdLogFormatDissector replays into
+ *                     Parsable.addDissection (core/Dissector.java:62-186,
+ *                     core/Parsable.java:77-140), see INTEGRATION.md.
  *
  * Threading: like the reference Parser (not thread-safe), one handle per
  * host thread / GPU.  Ownership: the caller owns the input buffer; the
@@ -81,10 +85,26 @@ void lp_free(lp_handle *h);
  * Returns the number of bytes written (excluding NUL) or a negative error. */
 int64_t lp_possible_paths(const char *logformats, int max_depth, char *out, size_t cap);
 
+/* Options (lp_set_option). */
+#define LP_OPT_FORCE_DIRECT 1  /* 1: every wave reads its lines from HBM (no LDS window);
+                                  diagnostics and tests of the direct path only */
+int lp_set_option(lp_handle *h, int option, int64_t value);
+
+/* Capacity for the coming batches: columns for max_lines lines and
+ * arena_bytes of side arena (0 = estimated).  With it (or after a first
+ * batch, whose line count sizes the buffers) lp_parse_batch enqueues the whole
+ * batch without waiting for the device; a batch that outgrows the buffers is
+ * re-run with exact sizes inside lp_sync. */
+int lp_reserve(lp_handle *h, int64_t max_lines, uint64_t arena_bytes);
+
 /* Parse every '\n'-terminated line of buf[0, nbytes) (a final line without
  * '\n' counts; Hadoop LineRecordReader semantics on '\n').  stream: a
  * hipStream_t (NULL = default stream).  Enqueues all work on the stream and
- * returns without synchronizing; call lp_sync before reading results. */
+ * returns without synchronizing (except a handle's first batch without a
+ * reservation, which waits for its line count); call lp_sync before reading
+ * results.  A batch still pending on the handle is finished first: to overlap
+ * batches, use one handle per stream.  On error the handle holds no batch
+ * (the accessors return LP_E_STATE) until a batch succeeds. */
 int lp_parse_batch(lp_handle *h, const uint8_t *buf, uint64_t nbytes, int buf_flags, void *stream);
 int lp_sync(lp_handle *h);
 
@@ -110,6 +130,57 @@ int lp_last_timing(lp_handle *h, float *out_ms, int n);
 /* Algorithmic bytes of the last batch: [0] input bytes read, [1] bytes of
  * SoA results + arena written (for roofline accounting). */
 int lp_last_bytes(lp_handle *h, uint64_t *out, int n);
+
+/* ---- Bulk results: the SoA the kernels wrote (SURVEY.md §8(b) lp_result). ----
+ * Per line i: status[i] (LP_LINE_*), and for the compiled program's stages
+ * the columns listed in lp_result.column (name, stage index, element size,
+ * byte offset from lp_result.columns), each n_lines elements:
+ *   status (u8), tok_span[k] (u32 start | end << 16, line-relative) and
+ *   tok_flags (u32: bit k value "-" = null, bit 16+k value "0") per captured
+ *   token k; t_epoch[t] (i64 epoch ms), t_local[t] / t_utc[t] (u64 packed
+ *   calendar, lp_program.h pack_cal), t_nano[t] (u32) per timestamp stage;
+ *   fl_kind / fl_method / fl_uri / fl_proto (u32 kind, spans) per first-line
+ *   stage; u_flags (u32 UF_* bits), u_scheme / u_host / u_path / u_query /
+ *   u_frag (u64 refs) and u_port (i32) per URI stage; q_count (u32) and
+ *   q_params (u64 ref of a table of q_count (name ref, value ref) pairs) per
+ *   query stage; arena_base (u64, the line's arena region); fmt_id (u8, the
+ *   routed LogFormat) with several LogFormats.
+ * A ref is off | len << 32 (len 30 bits); bit 63 set: the bytes are in the
+ * line's arena region, else line-relative; bit 62: '&' followed by those line
+ * bytes.  Arena offsets b live in shard s = b / shard_cap, at
+ * arena + shard_off[s] + (b - s * shard_cap). */
+#define LP_ARENA_SHARDS 64
+typedef struct lp_column {
+    char name[16];
+    int32_t index;
+    int32_t elem_size;
+    uint64_t offset;
+} lp_column;
+typedef struct lp_result {
+    int64_t n_lines;
+    uint64_t input_bytes;
+    const uint8_t *input;      /* line i = input[line_off[i], line_off[i+1] - 1); NULL if not copied */
+    const uint64_t *line_off;  /* n_lines + 1 entries */
+    const uint8_t *columns;
+    uint64_t columns_bytes;
+    const uint8_t *arena;
+    uint64_t arena_bytes;
+    uint64_t shard_cap;
+    uint64_t shard_off[LP_ARENA_SHARDS];
+    int32_t n_columns;
+    int32_t on_host;           /* 0: device pointers (lp_result_view), 1: host copy (lp_result_copy) */
+    const lp_column *column;   /* owned by the handle, valid until its next batch */
+} lp_result;
+/* Device pointers of the last batch's results (valid until the next batch). */
+int lp_result_view(lp_handle *h, lp_result *out);
+/* Copy the last batch's results (line index, columns, used arena, and the
+ * input when with_input) into host memory (pinned memory copies fastest) in
+ * one call.  Returns the bytes used, or -(bytes needed) when host is NULL or
+ * cap is too small. */
+int64_t lp_result_copy(lp_handle *h, void *host, uint64_t cap, int with_input, lp_result *out);
+/* The canonical record of line i (as lp_line_record_json) from a host copy
+ * made with the input: no device access. */
+int64_t lp_result_record_json(lp_handle *h, const lp_result *r, int64_t i, char *out, size_t cap);
 
 /* Description of the compiled device program (for logs/tests), NUL-terminated. */
 int64_t lp_describe(lp_handle *h, char *out, size_t cap);

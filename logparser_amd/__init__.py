@@ -29,6 +29,23 @@ LIB_PATH = os.environ.get("LOGPARSER_AMD_LIB") or os.path.join(_HERE, "_lib", "l
 LP_OK, LP_E_INVALID, LP_E_MISSING, LP_E_UNSUPPORTED, LP_E_DEVICE, LP_E_NOMEM, LP_E_STATE = 0, -1, -2, -3, -4, -5, -6
 LINE_OK, LINE_BAD, LINE_FALLBACK = 0, 1, 2
 BUF_HOST, BUF_DEVICE = 0, 1
+OPT_FORCE_DIRECT = 1
+ARENA_SHARDS = 64
+
+
+class LpColumn(ctypes.Structure):
+    """lp_column (include/logparser_amd.h)"""
+    _fields_ = [("name", ctypes.c_char * 16), ("index", ctypes.c_int32), ("elem_size", ctypes.c_int32),
+                ("offset", ctypes.c_uint64)]
+
+
+class LpResult(ctypes.Structure):
+    """lp_result (include/logparser_amd.h): the SoA results of one batch"""
+    _fields_ = [("n_lines", ctypes.c_int64), ("input_bytes", ctypes.c_uint64), ("input", ctypes.c_void_p),
+                ("line_off", ctypes.c_void_p), ("columns", ctypes.c_void_p), ("columns_bytes", ctypes.c_uint64),
+                ("arena", ctypes.c_void_p), ("arena_bytes", ctypes.c_uint64), ("shard_cap", ctypes.c_uint64),
+                ("shard_off", ctypes.c_uint64 * ARENA_SHARDS), ("n_columns", ctypes.c_int32),
+                ("on_host", ctypes.c_int32), ("column", ctypes.POINTER(LpColumn))]
 
 
 class DissectionFailure(Exception):
@@ -89,6 +106,15 @@ def lib():
     L.lp_counters.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
     L.lp_last_timing.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
     L.lp_last_bytes.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
+    L.lp_set_option.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64]
+    L.lp_reserve.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint64]
+    L.lp_result_view.argtypes = [ctypes.c_void_p, ctypes.POINTER(LpResult)]
+    L.lp_result_copy.restype = ctypes.c_int64
+    L.lp_result_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
+                                 ctypes.POINTER(LpResult)]
+    L.lp_result_record_json.restype = ctypes.c_int64
+    L.lp_result_record_json.argtypes = [ctypes.c_void_p, ctypes.POINTER(LpResult), ctypes.c_int64, ctypes.c_char_p,
+                                        ctypes.c_size_t]
     L.lp_describe.restype = ctypes.c_int64
     L.lp_describe.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]
     L.lp_synth_combined.restype = ctypes.c_int64
@@ -151,7 +177,9 @@ class BatchResult:
     def __init__(self, parser):
         self._p = parser
         L = lib()
-        L.lp_sync(parser._h)
+        rc = L.lp_sync(parser._h)
+        if rc != LP_OK:
+            raise EngineUnavailable("lp_sync failed: %d" % rc)
         self.n_lines = L.lp_num_lines(parser._h)
         st = np.zeros(max(1, self.n_lines), dtype=np.uint8)
         if self.n_lines:
@@ -190,15 +218,58 @@ class BatchResult:
     def line_offset(self, i):
         return lib().lp_line_offset(self._p._h, i)
 
+    def copy_to_host(self, with_input=True, buf=None):
+        """lp_result_copy: every result of the batch in one host buffer (a
+        numpy uint8 array, or buf when given and large enough); returns
+        (buffer, LpResult)."""
+        L = lib()
+        need = -L.lp_result_copy(self._p._h, None, 0, 1 if with_input else 0, None)
+        if need <= 0:
+            raise EngineUnavailable("lp_result_copy failed: %d" % need)
+        if buf is None or buf.nbytes < need:
+            buf = np.empty(need, dtype=np.uint8)
+        res = LpResult()
+        rc = L.lp_result_copy(self._p._h, buf.ctypes.data, buf.nbytes, 1 if with_input else 0, ctypes.byref(res))
+        if rc < 0:
+            raise EngineUnavailable("lp_result_copy failed: %d" % rc)
+        return buf, res
+
+    def columns(self, res):
+        """{(name, index): numpy view} of the columns of a host copy."""
+        dt = {1: np.uint8, 2: np.uint16, 4: np.uint32, 8: np.uint64}
+        out = {}
+        for k in range(res.n_columns):
+            c = res.column[k]
+            arr = np.ctypeslib.as_array((ctypes.c_uint8 * (c.elem_size * res.n_lines)).from_address(res.columns + c.offset))
+            out[(c.name.decode(), c.index)] = arr.view(dt[c.elem_size])
+        return out
+
+    def record_json_from(self, res, i):
+        """lp_result_record_json: the record of line i from a host copy."""
+        cap = 1 << 16
+        while True:
+            out = ctypes.create_string_buffer(cap)
+            n = lib().lp_result_record_json(self._p._h, ctypes.byref(res), i, out, cap)
+            if n >= 0:
+                return out.value.decode("utf-8")
+            if n <= -100:
+                cap = int(-n - 100) + 16
+                continue
+            if n == LP_E_STATE:
+                raise ValueError("line %d is not OK" % i)
+            raise EngineUnavailable("lp_result_record_json failed: %d" % n)
+
 
 class HttpdLoglineParser:
     """GPU-backed equivalent of new HttpdLoglineParser<>(RECORD.class, logformat)
     with addParseTarget(...) for each requested "TYPE:path"."""
 
-    def __init__(self, logformat, fields=(), device=0):
+    def __init__(self, logformat, fields=(), device=0, force_direct=False, reserve_lines=0, reserve_arena=0):
         self.logformat = logformat
         self.fields = list(fields)
         self.device = device
+        self.force_direct = force_direct
+        self.reserve = (reserve_lines, reserve_arena)
         self._h = None
         self.device_program_ok = None
         self.unsupported_reason = ""
@@ -230,6 +301,10 @@ class HttpdLoglineParser:
                 raise EngineUnavailable(msg)
             raise InvalidDissectorException(msg)
         self._h = h
+        if self.force_direct:
+            L.lp_set_option(h, OPT_FORCE_DIRECT, 1)
+        if self.reserve[0] or self.reserve[1]:
+            L.lp_reserve(h, self.reserve[0], self.reserve[1])
         self.device_program_ok = st.value == LP_OK
         self.unsupported_reason = msg if st.value == LP_E_UNSUPPORTED else ""
 
@@ -266,7 +341,9 @@ class HttpdLoglineParser:
                               ctypes.c_void_p(stream) if stream is not None else None)
         if rc != LP_OK:
             raise EngineUnavailable("lp_parse_batch failed: %d" % rc)
-        L.lp_sync(self._h)
+        rc = L.lp_sync(self._h)
+        if rc != LP_OK:
+            raise EngineUnavailable("lp_sync failed: %d" % rc)
         c = (ctypes.c_uint64 * 4)()
         L.lp_counters(self._h, c, 4)
         t = (ctypes.c_float * 3)()

@@ -1,6 +1,7 @@
 // C-ABI of the logparser_amd engine (include/logparser_amd.h).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -10,6 +11,8 @@
 #include "../../include/logparser_amd.h"
 #include "kernels.h"
 #include "plan.h"
+
+static_assert(LP_ARENA_SHARDS == lp::ARENA_SHARDS, "arena shard count of the ABI and the kernels");
 
 namespace {
 
@@ -35,6 +38,17 @@ struct DevBuf {
     T* as(size_t off = 0) const { return reinterpret_cast<T*>((char*)p + off); }
 };
 
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// One SoA column of the program: its ABI name, stage index, element size and
+// the Columns field that points at it.
+struct ColSpec {
+    const char* name;
+    int index;
+    int esz;
+    void** field;
+};
+
 }  // namespace
 
 struct lp_handle {
@@ -42,22 +56,36 @@ struct lp_handle {
     int compile_status = LP_OK;
     int device = 0;
     hipStream_t stream = nullptr;
-    DevBuf input, chunk, line_off, cols, arena, misc, waves, args, route;
+    DevBuf input, chunk, line_off, cols, arena, meta, waves, args, route, ovf;
     lp::DeviceArgs host_args{};
     lp::Columns C{};
+    std::vector<ColSpec> specs;
+    std::vector<lp_column> dev_cols, host_cols;
+    // the batch (valid once lp_parse_batch succeeded)
+    bool valid = false, pending = false;
     int64_t n_lines = 0;
     uint64_t nbytes = 0;
     const uint8_t* d_buf = nullptr;
+    // capacities of the column and arena buffers, and what sizes the next batch
+    int64_t cap_lines = 0;
+    uint64_t shard_cap = 0;
+    int64_t reserve_lines = 0;
+    uint64_t reserve_arena = 0;
+    double mean_line = 0;          // input bytes per line of the last batch
+    double arena_per_line = 0;     // arena bytes (largest shard x shards) per line of the last batch
+    bool force_direct = false;
     hipEvent_t ev[4]{};
     bool have_events = false;
-    bool pending = false;
-    uint64_t row_bytes = 0;
     uint64_t counters[4]{};
-    uint64_t arena_used = 0;     // arena bytes allocated (bump pointer)
-    uint64_t arena_written = 0;  // arena bytes actually written
+    uint64_t shard_top[LP_ARENA_SHARDS]{};
+    uint64_t arena_written = 0;
+    int retries = 0;
     float ms[3]{};
+    // host copy for lp_line_record_json / lp_line_status
     bool host_valid = false;
-    lp::HostResults host;
+    std::vector<uint8_t> hostbuf;
+    lp_result host_res{};
+    lp::ResultView view;
     // HttpdLogFormatDissector's active format, carried from batch to batch
     // like the reference parser's (format 0 before the first line)
     uint32_t fmt_state = 0;
@@ -69,120 +97,328 @@ void set_err(char* err, size_t errlen, const std::string& s) {
     if (err && errlen) snprintf(err, errlen, "%s", s.c_str());
 }
 
-size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
-
-// Lay out the result columns for n lines in one allocation.
-bool alloc_columns(lp_handle* h, int64_t n) {
+// The program's SoA columns, in layout order.
+void build_specs(lp_handle* h) {
     const lp::Program& P = h->plan.program();
-    struct Col { void** dst; size_t esz; };
-    std::vector<Col> cols;
     lp::Columns& C = h->C;
-    cols.push_back({(void**)&C.status, 1});
-    for (int k = 0; k < P.n_tok; ++k) cols.push_back({(void**)&C.tok_span[k], 4});
-    cols.push_back({(void**)&C.tok_flags, 4});
+    auto& v = h->specs;
+    v.clear();
+    auto add = [&](const char* nm, int idx, int esz, void* field) { v.push_back({nm, idx, esz, (void**)field}); };
+    add("status", 0, 1, &C.status);
+    for (int k = 0; k < P.n_tok; ++k) add("tok_span", k, 4, &C.tok_span[k]);
+    add("tok_flags", 0, 4, &C.tok_flags);
     for (int t = 0; t < P.n_time; ++t) {
-        cols.push_back({(void**)&C.t_epoch[t], 8});
-        cols.push_back({(void**)&C.t_local[t], 8});
-        cols.push_back({(void**)&C.t_utc[t], 8});
-        if (P.time[t].kind == lp::TK_STRF) cols.push_back({(void**)&C.t_nano[t], 4});  // only strftime has fractions
+        add("t_epoch", t, 8, &C.t_epoch[t]);
+        add("t_local", t, 8, &C.t_local[t]);
+        add("t_utc", t, 8, &C.t_utc[t]);
+        if (P.time[t].kind == lp::TK_STRF) add("t_nano", t, 4, &C.t_nano[t]);  // only strftime has fractions
     }
     for (int f = 0; f < P.n_fl; ++f) {
-        cols.push_back({(void**)&C.fl_kind[f], 4});
-        cols.push_back({(void**)&C.fl_method[f], 4});
-        cols.push_back({(void**)&C.fl_uri[f], 4});
-        cols.push_back({(void**)&C.fl_proto[f], 4});
+        add("fl_kind", f, 4, &C.fl_kind[f]);
+        add("fl_method", f, 4, &C.fl_method[f]);
+        add("fl_uri", f, 4, &C.fl_uri[f]);
+        add("fl_proto", f, 4, &C.fl_proto[f]);
     }
     for (int u = 0; u < P.n_uri; ++u) {
-        cols.push_back({(void**)&C.u_flags[u], 4});
-        cols.push_back({(void**)&C.u_scheme[u], 8});
-        cols.push_back({(void**)&C.u_host[u], 8});
-        cols.push_back({(void**)&C.u_port[u], 4});
-        cols.push_back({(void**)&C.u_path[u], 8});
-        cols.push_back({(void**)&C.u_query[u], 8});
-        cols.push_back({(void**)&C.u_frag[u], 8});
+        add("u_flags", u, 4, &C.u_flags[u]);
+        add("u_scheme", u, 8, &C.u_scheme[u]);
+        add("u_host", u, 8, &C.u_host[u]);
+        add("u_port", u, 4, &C.u_port[u]);
+        add("u_path", u, 8, &C.u_path[u]);
+        add("u_query", u, 8, &C.u_query[u]);
+        add("u_frag", u, 8, &C.u_frag[u]);
     }
     for (int q = 0; q < P.n_query; ++q) {
-        cols.push_back({(void**)&C.q_count[q], 4});
-        cols.push_back({(void**)&C.q_params[q], 8});
+        add("q_count", q, 4, &C.q_count[q]);
+        add("q_params", q, 8, &C.q_params[q]);
     }
-    cols.push_back({(void**)&C.arena_base, 8});
+    add("arena_base", 0, 8, &C.arena_base);
     if (P.n_fmt > 1) {
-        cols.push_back({(void**)&C.fmt_match, 2});
-        cols.push_back({(void**)&C.fmt_id, 1});
+        add("fmt_match", 0, 2, &C.fmt_match);
+        add("fmt_id", 0, 1, &C.fmt_id);
     }
-    size_t total = 0;
-    uint64_t row = 0;
-    for (auto& c : cols) {
-        total += align256(c.esz * (size_t)(n > 0 ? n : 1));
-        row += c.esz;
+}
+
+// column descriptors for columns of `rows` rows
+std::vector<lp_column> layout(const std::vector<ColSpec>& specs, int64_t rows, uint64_t* total) {
+    std::vector<lp_column> out;
+    uint64_t off = 0;
+    for (const auto& c : specs) {
+        lp_column d{};
+        snprintf(d.name, sizeof d.name, "%s", c.name);
+        d.index = c.index;
+        d.elem_size = c.esz;
+        d.offset = off;
+        out.push_back(d);
+        off += align256((size_t)c.esz * (size_t)(rows > 0 ? rows : 1));
     }
+    *total = off;
+    return out;
+}
+
+// Columns for cap lines in one allocation.
+bool alloc_columns(lp_handle* h, int64_t cap) {
+    uint64_t total = 0;
+    h->dev_cols = layout(h->specs, cap, &total);
     if (!h->cols.ensure(total)) return false;
-    size_t off = 0;
-    for (auto& c : cols) {
-        *c.dst = h->cols.as<char>(off);
-        off += align256(c.esz * (size_t)(n > 0 ? n : 1));
-    }
-    h->row_bytes = row;
+    for (size_t k = 0; k < h->specs.size(); ++k) *h->specs[k].field = h->cols.as<char>(h->dev_cols[k].offset);
     return true;
 }
 
-template <typename T>
-void fetch(std::vector<T>& dst, const T* src, int64_t n) {
-    dst.resize((size_t)(n > 0 ? n : 0));
-    if (n > 0 && src) hipMemcpy(dst.data(), src, sizeof(T) * (size_t)n, hipMemcpyDeviceToHost);
+// A view of a result (device or host copy) for the replay.
+void make_view(lp_handle* h, const lp_result& r, lp::ResultView& V) {
+    V = lp::ResultView{};
+    V.n = r.n_lines;
+    V.line_off = r.line_off;
+    V.input = r.input;
+    V.arena = r.arena;
+    V.shard_cap = r.shard_cap;
+    for (int s = 0; s < LP_ARENA_SHARDS; ++s) V.shard_off[s] = r.shard_off[s];
+    for (int k = 0; k < r.n_columns; ++k) {
+        const lp_column& c = r.column[k];
+        const void* p = r.columns + c.offset;
+        const std::string nm = c.name;
+        const int i = c.index;
+        if (nm == "status") V.status = (const uint8_t*)p;
+        else if (nm == "tok_span") V.tok_span[i] = (const uint32_t*)p;
+        else if (nm == "tok_flags") V.tok_flags = (const uint32_t*)p;
+        else if (nm == "t_epoch") V.t_epoch[i] = (const int64_t*)p;
+        else if (nm == "t_local") V.t_local[i] = (const uint64_t*)p;
+        else if (nm == "t_utc") V.t_utc[i] = (const uint64_t*)p;
+        else if (nm == "t_nano") V.t_nano[i] = (const uint32_t*)p;
+        else if (nm == "fl_kind") V.fl_kind[i] = (const uint32_t*)p;
+        else if (nm == "fl_method") V.fl_method[i] = (const uint32_t*)p;
+        else if (nm == "fl_uri") V.fl_uri[i] = (const uint32_t*)p;
+        else if (nm == "fl_proto") V.fl_proto[i] = (const uint32_t*)p;
+        else if (nm == "u_flags") V.u_flags[i] = (const uint32_t*)p;
+        else if (nm == "u_scheme") V.u_scheme[i] = (const uint64_t*)p;
+        else if (nm == "u_host") V.u_host[i] = (const uint64_t*)p;
+        else if (nm == "u_port") V.u_port[i] = (const int32_t*)p;
+        else if (nm == "u_path") V.u_path[i] = (const uint64_t*)p;
+        else if (nm == "u_query") V.u_query[i] = (const uint64_t*)p;
+        else if (nm == "u_frag") V.u_frag[i] = (const uint64_t*)p;
+        else if (nm == "q_count") V.q_count[i] = (const uint32_t*)p;
+        else if (nm == "q_params") V.q_params[i] = (const uint64_t*)p;
+        else if (nm == "arena_base") V.arena_base = (const uint64_t*)p;
+        else if (nm == "fmt_id") V.fmt_id = (const uint8_t*)p;
+    }
+    if (!V.arena) V.arena_base = nullptr;
+}
+
+// Enqueue the whole batch (index, routing, parse) with the current
+// capacities.  sync_count: count the lines first and size the buffers from
+// the exact count (the handle has no estimate yet).
+int enqueue(lp_handle* h, bool sync_count) {
+    hipStream_t s = h->stream;
+    const uint64_t nbytes = h->nbytes;
+    const lp::Program& P = h->plan.program();
+    const int64_t nc = lp::count_chunks(nbytes);
+    const size_t cbytes = align256(sizeof(uint64_t) * (size_t)(nc + 2));
+    if (!h->chunk.ensure(cbytes + 2 * (size_t)lp::nlmask_words(nbytes))) return LP_E_NOMEM;
+    if (!h->meta.ensure(sizeof(lp::Meta))) return LP_E_NOMEM;
+    uint64_t* d_chunk = h->chunk.as<uint64_t>();
+    uint16_t* d_nlmask = h->chunk.as<uint16_t>(cbytes);
+    lp::Meta* d_meta = h->meta.as<lp::Meta>();
+    if (hipMemsetAsync(d_meta, 0, sizeof(lp::Meta), s) != hipSuccess) return LP_E_DEVICE;
+    hipEventRecord(h->ev[0], s);
+    int64_t cap = h->cap_lines;
+    if (sync_count) {
+        // first batch of a handle: the exact line count sizes the columns
+        if (!h->line_off.ensure(16)) return LP_E_NOMEM;
+        if (lp::launch_count(h->d_buf, nbytes, d_chunk, d_nlmask, h->line_off.as<uint64_t>(), -1, d_meta, s) != 0)
+            return LP_E_DEVICE;
+        unsigned long long n = 0;
+        if (hipMemcpyAsync(&n, &d_meta->n_lines, sizeof n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return LP_E_DEVICE;
+        // headroom for the next batches of the stream (sized like the estimate below)
+        cap = std::max<int64_t>((int64_t)(n + n / 4 + 1024), h->reserve_lines);
+    } else {
+        if (!h->line_off.ensure(sizeof(uint64_t) * (size_t)(cap + 2))) return LP_E_NOMEM;
+        if (lp::launch_count(h->d_buf, nbytes, d_chunk, d_nlmask, h->line_off.as<uint64_t>(), cap, d_meta, s) != 0)
+            return LP_E_DEVICE;
+    }
+    if (!h->line_off.ensure(sizeof(uint64_t) * (size_t)(cap + 2))) return LP_E_NOMEM;
+    if (sync_count) {  // the scan ran without the line index buffer: its ends now
+        unsigned long long n = 0;
+        hipMemcpy(&n, &d_meta->n_lines, sizeof n, hipMemcpyDeviceToHost);
+        uint64_t ends[2] = {0, nbytes + 1};
+        hipMemcpy(h->line_off.as<uint64_t>(), &ends[0], 8, hipMemcpyHostToDevice);
+        uint8_t last = '\n';
+        if (nbytes) hipMemcpy(&last, h->d_buf + nbytes - 1, 1, hipMemcpyDeviceToHost);
+        if (nbytes && last != '\n') hipMemcpy(h->line_off.as<uint64_t>() + n, &ends[1], 8, hipMemcpyHostToDevice);
+    }
+    h->cap_lines = cap;
+    if (lp::launch_offsets(d_nlmask, nbytes, d_chunk, h->line_off.as<uint64_t>(), cap, s) != 0) return LP_E_DEVICE;
+    hipEventRecord(h->ev[1], s);
+    if (!alloc_columns(h, cap)) return LP_E_NOMEM;
+    // arena: ARENA_SHARDS shards of shard_cap bytes
+    uint64_t acap = h->reserve_arena;
+    if (!acap) {
+        const double per = h->arena_per_line > 0 ? h->arena_per_line * 1.25 : 64.0;
+        acap = (uint64_t)(per * (double)cap) + (1u << 20);
+    }
+    if (!h->plan.device_ok() || P.n_uri == 0) acap = 4096 * LP_ARENA_SHARDS;
+    h->shard_cap = (acap / LP_ARENA_SHARDS + 255) & ~255ull;
+    if (!h->arena.ensure(h->shard_cap * LP_ARENA_SHARDS)) return LP_E_NOMEM;
+    lp::Columns& C = h->C;
+    C.line_off = h->line_off.as<uint64_t>();
+    C.arena = h->arena.as<uint8_t>();
+    C.shard_cap = h->shard_cap;
+    C.meta = d_meta;
+    C.cap_lines = cap;
+    const int64_t waves = lp::parse_waves(cap);
+    if (!h->waves.ensure(4 * lp::WC_WORDS * (size_t)(waves + 1))) return LP_E_NOMEM;
+    if (!h->ovf.ensure(4 * (size_t)(waves + 1))) return LP_E_NOMEM;
+    C.wave_counts = h->waves.as<uint32_t>();
+    C.ovf_list = h->ovf.as<uint32_t>();
+    if (h->plan.device_ok()) {
+        if (P.n_fmt > 1) {  // sticky multi-format routing scratch
+            if (!h->route.ensure(8 * (size_t)(lp::fmt_chunks(cap) + 1))) return LP_E_NOMEM;
+            C.fmt_chunk = h->route.as<uint64_t>();
+            C.fmt_init = h->fmt_state;
+        }
+        if (!h->args.ensure(sizeof(lp::DeviceArgs))) return LP_E_NOMEM;
+        h->host_args.prog = P;
+        h->host_args.cols = C;
+        if (hipMemcpyAsync(h->args.p, &h->host_args, sizeof(lp::DeviceArgs), hipMemcpyHostToDevice, s) != hipSuccess)
+            return LP_E_DEVICE;
+        lp::ParseLaunch pl{h->d_buf, nbytes, cap, (uint64_t)(h->mean_line > 0 ? h->mean_line + 0.5 : 0),
+                           P.n_elems, P.max_stack, h->force_direct};
+        if (!pl.mean_line && cap > 0) pl.mean_line = (nbytes + cap - 1) / (uint64_t)cap;
+        hipEventRecord(h->ev[2], s);
+        const lp::DeviceArgs* d_args = h->args.as<lp::DeviceArgs>();
+        if (P.n_fmt > 1) {
+            // HttpdLogFormatDissector routing: every format's match per line,
+            // then the scan of the sticky active format
+            if (lp::launch_route_match(pl, d_args, s) != 0 || lp::launch_route(d_args, cap, s) != 0) return LP_E_DEVICE;
+        }
+        if (lp::launch_parse(pl, d_args, C.wave_counts, d_meta, s) != 0) return LP_E_DEVICE;
+    } else {
+        // the requested paths need a dissector that is not on the device:
+        // every line goes back to the reference (FALLBACK)
+        hipEventRecord(h->ev[2], s);
+        if (cap) hipMemsetAsync(C.status, LP_LINE_FALLBACK, (size_t)cap, s);
+    }
+    hipEventRecord(h->ev[3], s);
+    return LP_OK;
+}
+
+// Wait for the batch, read its bookkeeping; when its line count or arena
+// need outgrew the buffers, re-run it with exact sizes.
+int finish(lp_handle* h) {
+    for (;;) {
+        if (hipStreamSynchronize(h->stream) != hipSuccess) return LP_E_DEVICE;
+        lp::Meta m;
+        if (hipMemcpy(&m, h->meta.p, sizeof m, hipMemcpyDeviceToHost) != hipSuccess) return LP_E_DEVICE;
+        uint64_t top_max = 0;
+        for (int s = 0; s < LP_ARENA_SHARDS; ++s) {
+            h->shard_top[s] = m.shard_top[16 * s];
+            top_max = std::max<uint64_t>(top_max, h->shard_top[s]);
+        }
+        const int64_t n = (int64_t)m.n_lines;
+        if (h->plan.device_ok() && (m.cap_ovf || m.arena_ovf) && h->retries < 3) {
+            // exact sizes: the line count, every shard as large as the largest
+            // request (shard tops count what was asked for, also past the end)
+            ++h->retries;
+            h->cap_lines = std::max<int64_t>(n, h->cap_lines);
+            // the next estimate (arena_per_line x 1.25 x capacity) covers the largest shard
+            if (m.arena_ovf && n > 0)
+                h->arena_per_line = std::max(h->arena_per_line, (double)(top_max + 4096) * LP_ARENA_SHARDS / (double)n);
+            const int st = enqueue(h, false);
+            if (st != LP_OK) return st;
+            continue;
+        }
+        if (m.cap_ovf || m.arena_ovf) return LP_E_NOMEM;
+        h->n_lines = n;
+        if (h->plan.device_ok()) {
+            for (int k = 0; k < 4; ++k) h->counters[k] = m.counters[k];
+            h->arena_written = m.counters[4];
+        } else {
+            h->counters[0] = (uint64_t)n;
+            h->counters[1] = h->counters[2] = 0;
+            h->counters[3] = (uint64_t)n;
+            h->arena_written = 0;
+        }
+        for (int s = 0; s < LP_ARENA_SHARDS; ++s) h->shard_top[s] = std::min<uint64_t>(h->shard_top[s], h->shard_cap);
+        const lp::Program& P = h->plan.program();
+        if (h->plan.device_ok() && P.n_fmt > 1 && n > 0) h->fmt_state = (uint32_t)m.fmt_state;
+        if (n > 0) {
+            h->mean_line = (double)h->nbytes / (double)n;
+            h->arena_per_line = (double)top_max * LP_ARENA_SHARDS / (double)n;
+        }
+        float a = 0, b = 0, c = 0;
+        hipEventElapsedTime(&a, h->ev[0], h->ev[3]);
+        hipEventElapsedTime(&b, h->ev[0], h->ev[1]);
+        hipEventElapsedTime(&c, h->ev[2], h->ev[3]);
+        h->ms[0] = a; h->ms[1] = b; h->ms[2] = c;
+        return LP_OK;
+    }
+}
+
+int ensure_synced(lp_handle* h) {
+    if (h->pending) {
+        const int st = lp_sync(h);
+        if (st != LP_OK) return st;
+    }
+    return h->valid ? LP_OK : LP_E_STATE;
+}
+
+// Bytes of a host copy (line index, columns, arena shards, input) and its
+// layout; fills r when dst is non-null.
+int64_t copy_result(lp_handle* h, uint8_t* dst, uint64_t cap, bool with_input, lp_result* r) {
+    const int64_t n = h->n_lines;
+    uint64_t cols_bytes = 0;
+    h->host_cols = layout(h->specs, n, &cols_bytes);
+    uint64_t arena_bytes = 0;
+    uint64_t shard_off[LP_ARENA_SHARDS];
+    for (int s = 0; s < LP_ARENA_SHARDS; ++s) {
+        shard_off[s] = arena_bytes;
+        arena_bytes += (h->shard_top[s] + 15) & ~15ull;
+    }
+    const uint64_t o_lines = 0, o_cols = align256(8 * (uint64_t)(n + 1)), o_arena = o_cols + cols_bytes;
+    const uint64_t o_input = align256(o_arena + arena_bytes);
+    const uint64_t total = with_input ? o_input + h->nbytes + 64 : o_input;
+    if (!dst) return -(int64_t)total;
+    if (cap < total) return -(int64_t)total;
+    auto cp = [&](uint64_t off, const void* src, uint64_t bytes) {
+        return bytes == 0 || hipMemcpy(dst + off, src, bytes, hipMemcpyDeviceToHost) == hipSuccess;
+    };
+    bool ok = cp(o_lines, h->line_off.p, 8 * (uint64_t)(n + 1));
+    for (size_t k = 0; k < h->specs.size() && ok; ++k)
+        ok = cp(o_cols + h->host_cols[k].offset, *h->specs[k].field, (uint64_t)h->specs[k].esz * (uint64_t)n);
+    for (int s = 0; s < LP_ARENA_SHARDS && ok; ++s)
+        ok = cp(o_arena + shard_off[s], h->arena.as<uint8_t>((size_t)s * h->shard_cap), h->shard_top[s]);
+    if (with_input && ok) {
+        ok = cp(o_input, h->d_buf, h->nbytes);
+        memset(dst + o_input + h->nbytes, '\n', 64);
+    }
+    if (!ok) return LP_E_DEVICE;
+    lp_result& R = *r;
+    R = lp_result{};
+    R.n_lines = n;
+    R.input_bytes = h->nbytes;
+    R.input = with_input ? dst + o_input : nullptr;
+    R.line_off = reinterpret_cast<const uint64_t*>(dst + o_lines);
+    R.columns = dst + o_cols;
+    R.columns_bytes = cols_bytes;
+    R.arena = dst + o_arena;
+    R.arena_bytes = arena_bytes;
+    R.shard_cap = h->shard_cap;
+    for (int s = 0; s < LP_ARENA_SHARDS; ++s) R.shard_off[s] = shard_off[s];
+    R.n_columns = (int32_t)h->host_cols.size();
+    R.column = h->host_cols.data();
+    R.on_host = 1;
+    return (int64_t)total;
 }
 
 bool fetch_host(lp_handle* h) {
     if (h->host_valid) return true;
-    if (h->pending) lp_sync(h);
-    const lp::Program& P = h->plan.program();
-    lp::HostResults& R = h->host;
-    const int64_t n = h->n_lines;
-    R.n = n;
-    fetch(R.line_off, h->line_off.as<uint64_t>(), n + 1);
-    fetch(R.status, h->C.status, n);
-    R.input.resize(h->nbytes);
-    if (h->nbytes) hipMemcpy(R.input.data(), h->d_buf, h->nbytes, hipMemcpyDeviceToHost);
-    R.input.push_back('\n');
-    if (!h->plan.device_ok()) { h->host_valid = true; return true; }
-    if (P.n_fmt > 1) fetch(R.fmt_id, h->C.fmt_id, n);
-    R.tok_span.resize(lp::MAX_TOK);
-    for (int k = 0; k < P.n_tok; ++k) fetch(R.tok_span[k], h->C.tok_span[k], n);
-    fetch(R.tok_flags, h->C.tok_flags, n);
-    R.t_epoch.resize(lp::MAX_TIME); R.t_local.resize(lp::MAX_TIME); R.t_utc.resize(lp::MAX_TIME);
-    R.t_nano.resize(lp::MAX_TIME);
-    for (int t = 0; t < P.n_time; ++t) {
-        fetch(R.t_epoch[t], h->C.t_epoch[t], n);
-        fetch(R.t_local[t], h->C.t_local[t], n);
-        fetch(R.t_utc[t], h->C.t_utc[t], n);
-        if (P.time[t].kind == lp::TK_STRF) fetch(R.t_nano[t], h->C.t_nano[t], n);
-    }
-    R.fl_kind.resize(lp::MAX_FL); R.fl_method.resize(lp::MAX_FL); R.fl_uri.resize(lp::MAX_FL); R.fl_proto.resize(lp::MAX_FL);
-    for (int f = 0; f < P.n_fl; ++f) {
-        fetch(R.fl_kind[f], h->C.fl_kind[f], n);
-        fetch(R.fl_method[f], h->C.fl_method[f], n);
-        fetch(R.fl_uri[f], h->C.fl_uri[f], n);
-        fetch(R.fl_proto[f], h->C.fl_proto[f], n);
-    }
-    for (auto* v : {&R.u_scheme, &R.u_host, &R.u_path, &R.u_query, &R.u_frag}) v->resize(lp::MAX_URI);
-    R.u_flags.resize(lp::MAX_URI); R.u_port.resize(lp::MAX_URI);
-    for (int u = 0; u < P.n_uri; ++u) {
-        fetch(R.u_flags[u], h->C.u_flags[u], n);
-        fetch(R.u_scheme[u], h->C.u_scheme[u], n);
-        fetch(R.u_host[u], h->C.u_host[u], n);
-        fetch(R.u_port[u], h->C.u_port[u], n);
-        fetch(R.u_path[u], h->C.u_path[u], n);
-        fetch(R.u_query[u], h->C.u_query[u], n);
-        fetch(R.u_frag[u], h->C.u_frag[u], n);
-    }
-    R.q_count.resize(lp::MAX_QUERY); R.q_params.resize(lp::MAX_QUERY);
-    for (int q = 0; q < P.n_query; ++q) {
-        fetch(R.q_count[q], h->C.q_count[q], n);
-        fetch(R.q_params[q], h->C.q_params[q], n);
-    }
-    fetch(R.arena_base, h->C.arena_base, n);
-    R.arena.resize(h->arena_used + 64);
-    if (h->arena_used) hipMemcpy(R.arena.data(), h->C.arena, h->arena_used, hipMemcpyDeviceToHost);
+    if (ensure_synced(h) != LP_OK) return false;
+    const int64_t need = -copy_result(h, nullptr, 0, true, nullptr);
+    h->hostbuf.resize((size_t)need);
+    if (copy_result(h, h->hostbuf.data(), (uint64_t)need, true, &h->host_res) < 0) return false;
+    make_view(h, h->host_res, h->view);
     h->host_valid = true;
     return true;
 }
@@ -215,10 +451,11 @@ lp_handle* lp_compile(const char* logformats, const char* const* paths, int n_pa
     }
     if (st == LP_E_UNSUPPORTED) set_err(err, errlen, h->plan.unsupported_reason());
     h->compile_status = st;
+    build_specs(h.get());
     if (hipSetDevice(device) != hipSuccess) { if (status) *status = LP_E_DEVICE; return nullptr; }
     for (auto& ev : h->ev) hipEventCreate(&ev);
     h->have_events = true;
-    if (!h->misc.ensure(256)) { if (status) *status = LP_E_NOMEM; return nullptr; }
+    if (!h->meta.ensure(sizeof(lp::Meta))) { if (status) *status = LP_E_NOMEM; return nullptr; }
     if (status) *status = st;
     return h.release();
 }
@@ -227,7 +464,8 @@ void lp_free(lp_handle* h) {
     if (!h) return;
     hipSetDevice(h->device);
     if (h->pending) hipStreamSynchronize(h->stream);
-    for (auto* b : {&h->input, &h->chunk, &h->line_off, &h->cols, &h->arena, &h->misc, &h->waves, &h->args, &h->route})
+    for (auto* b : {&h->input, &h->chunk, &h->line_off, &h->cols, &h->arena, &h->meta, &h->waves, &h->args, &h->route,
+                    &h->ovf})
         b->release();
     if (h->have_events)
         for (auto& ev : h->ev) hipEventDestroy(ev);
@@ -245,13 +483,33 @@ int64_t lp_possible_paths(const char* logformats, int max_depth, char* out, size
     return (int64_t)s.size();
 }
 
+int lp_set_option(lp_handle* h, int option, int64_t value) {
+    if (!h) return LP_E_INVALID;
+    switch (option) {
+    case LP_OPT_FORCE_DIRECT: h->force_direct = value != 0; return LP_OK;
+    default: return LP_E_INVALID;
+    }
+}
+
+int lp_reserve(lp_handle* h, int64_t max_lines, uint64_t arena_bytes) {
+    if (!h || max_lines < 0) return LP_E_INVALID;
+    h->reserve_lines = max_lines;
+    h->reserve_arena = arena_bytes;
+    if (max_lines > h->cap_lines) h->cap_lines = max_lines;
+    return LP_OK;
+}
+
 int lp_parse_batch(lp_handle* h, const uint8_t* buf, uint64_t nbytes, int buf_flags, void* stream) {
     if (!h || (!buf && nbytes)) return LP_E_INVALID;
     if (hipSetDevice(h->device) != hipSuccess) return LP_E_DEVICE;
     if (h->pending) lp_sync(h);
+    // the handle holds no valid batch until this one has been enqueued
+    h->valid = false;
+    h->host_valid = false;
+    h->n_lines = 0;
+    h->retries = 0;
     hipStream_t s = (hipStream_t)stream;
     h->stream = s;
-    h->host_valid = false;
     h->nbytes = nbytes;
     if (buf_flags == LP_BUF_HOST) {
         if (!h->input.ensure(nbytes + 16)) return LP_E_NOMEM;
@@ -268,137 +526,76 @@ int lp_parse_batch(lp_handle* h, const uint8_t* buf, uint64_t nbytes, int buf_fl
     } else {
         h->d_buf = buf;
     }
-    const int64_t nc = lp::count_chunks(nbytes);
-    const size_t cbytes = align256(sizeof(uint64_t) * (size_t)(nc + 2));
-    if (!h->chunk.ensure(cbytes + 2 * (size_t)lp::nlmask_words(nbytes))) return LP_E_NOMEM;
-    uint64_t* d_chunk = h->chunk.as<uint64_t>();
-    uint16_t* d_nlmask = h->chunk.as<uint16_t>(cbytes);
-    hipEventRecord(h->ev[0], s);
-    // index pass 1 (count + scan), then the line count on the host
-    if (lp::launch_count(h->d_buf, nbytes, d_chunk, d_nlmask, s) != 0) return LP_E_DEVICE;
-    uint64_t total = 0;
-    uint8_t last = '\n';
-    if (nc > 0) {
-        hipMemcpyAsync(&total, d_chunk + nc, sizeof total, hipMemcpyDeviceToHost, s);
-        hipMemcpyAsync(&last, h->d_buf + nbytes - 1, 1, hipMemcpyDeviceToHost, s);
-    }
-    if (hipStreamSynchronize(s) != hipSuccess) return LP_E_DEVICE;
-    const int64_t n = (int64_t)total + (nbytes > 0 && last != '\n' ? 1 : 0);
-    h->n_lines = n;
-    if (!h->line_off.ensure(sizeof(uint64_t) * (size_t)(n + 2))) return LP_E_NOMEM;
-    uint64_t* d_off = h->line_off.as<uint64_t>();
-    uint64_t head = 0, tail = nbytes + 1;
-    hipMemcpyAsync(d_off, &head, sizeof head, hipMemcpyHostToDevice, s);
-    if (lp::launch_offsets(d_nlmask, nbytes, d_chunk, d_off, s) != 0) return LP_E_DEVICE;
-    if (nbytes > 0 && last != '\n') hipMemcpyAsync(d_off + n, &tail, sizeof tail, hipMemcpyHostToDevice, s);
-    hipEventRecord(h->ev[1], s);
-    // results
-    if (!alloc_columns(h, n)) return LP_E_NOMEM;
-    const lp::Program& P = h->plan.program();
-    // arena: generous bound (only written bytes cost bandwidth)
-    uint64_t acap = h->plan.device_ok() && P.n_uri > 0 ? 3 * nbytes + 64 * (uint64_t)n + 4096 : 4096;
-    if (!h->arena.ensure(acap)) return LP_E_NOMEM;
-    lp::Columns& C = h->C;
-    C.line_off = d_off;
-    C.arena = h->arena.as<uint8_t>();
-    C.arena_cap = h->arena.cap;
-    if (!h->waves.ensure(4 * lp::WC_WORDS * (size_t)(lp::parse_waves(n) + 1))) return LP_E_NOMEM;
-    C.wave_counts = h->waves.as<uint32_t>();
-    C.arena_top = h->misc.as<unsigned long long>(64);
-    hipMemsetAsync(h->misc.p, 0, 128, s);
-    if (h->plan.device_ok()) {
-        if (P.n_fmt > 1) {  // sticky multi-format routing scratch
-            if (!h->route.ensure(8 * (size_t)(lp::fmt_chunks(n) + 1))) return LP_E_NOMEM;
-            C.fmt_chunk = h->route.as<uint64_t>();
-            C.fmt_init = h->fmt_state;
-        }
-        if (!h->args.ensure(sizeof(lp::DeviceArgs))) return LP_E_NOMEM;
-        h->host_args.prog = P;
-        h->host_args.cols = C;
-        if (hipMemcpyAsync(h->args.p, &h->host_args, sizeof(lp::DeviceArgs), hipMemcpyHostToDevice, s) != hipSuccess)
-            return LP_E_DEVICE;
-        hipEventRecord(h->ev[2], s);
-        if (P.n_fmt > 1) {
-            // HttpdLogFormatDissector routing: every format's match per line,
-            // then the scan of the sticky active format
-            if (lp::launch_parse(h->d_buf, nbytes, n, h->args.as<lp::DeviceArgs>(), P.n_elems, P.max_stack, C.wave_counts,
-                                 h->misc.as<unsigned long long>(), s, lp::PM_MATCH) != 0 ||
-                lp::launch_route(h->args.as<lp::DeviceArgs>(), n, s) != 0)
-                return LP_E_DEVICE;
-        }
-        if (lp::launch_parse(h->d_buf, nbytes, n, h->args.as<lp::DeviceArgs>(), P.n_elems, P.max_stack, C.wave_counts,
-                             h->misc.as<unsigned long long>(), s) != 0)
-            return LP_E_DEVICE;
+    // capacity from the reservation or the previous batch's line length; a
+    // handle without either counts its lines first (one synchronisation)
+    bool sync_count = false;
+    if (h->reserve_lines > 0) {
+        h->cap_lines = std::max<int64_t>(h->cap_lines, h->reserve_lines);
+    } else if (h->mean_line > 0) {
+        const int64_t est = (int64_t)((double)nbytes / h->mean_line * 1.25) + 1024;
+        h->cap_lines = std::max<int64_t>(h->cap_lines, est);
     } else {
-        // the requested paths need a dissector that is not on the device:
-        // every line goes back to the reference (FALLBACK)
-        hipEventRecord(h->ev[2], s);
-        if (n) hipMemsetAsync(C.status, LP_LINE_FALLBACK, (size_t)n, s);
+        sync_count = true;
     }
-    hipEventRecord(h->ev[3], s);
+    const int st = enqueue(h, sync_count);
+    if (st != LP_OK) return st;
     h->pending = true;
+    h->valid = true;
     return LP_OK;
 }
 
 int lp_sync(lp_handle* h) {
     if (!h) return LP_E_INVALID;
-    if (!h->pending) return LP_OK;
+    if (!h->pending) return h->valid ? LP_OK : LP_E_STATE;
     hipSetDevice(h->device);
-    if (hipStreamSynchronize(h->stream) != hipSuccess) return LP_E_DEVICE;
     h->pending = false;
-    unsigned long long m[16];
-    hipMemcpy(m, h->misc.p, sizeof m, hipMemcpyDeviceToHost);
-    if (h->plan.device_ok()) {
-        for (int k = 0; k < 4; ++k) h->counters[k] = m[k];
-    } else {
-        h->counters[0] = (uint64_t)h->n_lines;
-        h->counters[1] = h->counters[2] = 0;
-        h->counters[3] = (uint64_t)h->n_lines;
+    const int st = finish(h);
+    if (st != LP_OK) {
+        h->valid = false;
+        h->n_lines = 0;
     }
-    h->arena_used = m[8];
-    const lp::Program& P = h->plan.program();
-    if (h->plan.device_ok() && P.n_fmt > 1 && h->n_lines > 0) {  // the active format after the batch's last line
-        uint64_t st = 0;
-        hipMemcpy(&st, h->C.fmt_chunk + lp::fmt_chunks(h->n_lines), sizeof st, hipMemcpyDeviceToHost);
-        h->fmt_state = (uint32_t)st;
-    }
-    h->arena_written = h->plan.device_ok() ? m[4] : 0;
-    float a = 0, b = 0, c = 0;
-    hipEventElapsedTime(&a, h->ev[0], h->ev[3]);
-    hipEventElapsedTime(&b, h->ev[0], h->ev[1]);
-    hipEventElapsedTime(&c, h->ev[2], h->ev[3]);
-    h->ms[0] = a; h->ms[1] = b; h->ms[2] = c;
-    return LP_OK;
+    return st;
 }
 
-int64_t lp_num_lines(lp_handle* h) { return h ? h->n_lines : LP_E_INVALID; }
+int64_t lp_num_lines(lp_handle* h) {
+    if (!h) return LP_E_INVALID;
+    const int st = ensure_synced(h);
+    return st == LP_OK ? h->n_lines : st;
+}
 
 int lp_line_status(lp_handle* h, int64_t first, int64_t count, uint8_t* out) {
-    if (!h || first < 0 || count < 0 || first + count > h->n_lines) return LP_E_INVALID;
-    if (h->pending) lp_sync(h);
-    if (count && hipMemcpy(out, h->C.status + first, (size_t)count, hipMemcpyDeviceToHost) != hipSuccess) return LP_E_DEVICE;
+    if (!h) return LP_E_INVALID;
+    const int st = ensure_synced(h);
+    if (st != LP_OK) return st;
+    if (first < 0 || count < 0 || first + count > h->n_lines || (count && !out)) return LP_E_INVALID;
+    if (!count) return LP_OK;
+    if (h->host_valid) {  // served from the host copy
+        memcpy(out, h->view.status + first, (size_t)count);
+        return LP_OK;
+    }
+    if (hipMemcpy(out, h->C.status + first, (size_t)count, hipMemcpyDeviceToHost) != hipSuccess) return LP_E_DEVICE;
     return LP_OK;
 }
 
 int64_t lp_line_offset(lp_handle* h, int64_t i) {
-    if (!h || i < 0 || i > h->n_lines) return LP_E_INVALID;
-    if (h->pending) lp_sync(h);
+    if (!h) return LP_E_INVALID;
+    const int st = ensure_synced(h);
+    if (st != LP_OK) return st;
+    if (i < 0 || i > h->n_lines) return LP_E_INVALID;
+    if (h->host_valid) return (int64_t)h->view.line_off[i];
     uint64_t v = 0;
-    hipMemcpy(&v, h->line_off.as<uint64_t>() + i, sizeof v, hipMemcpyDeviceToHost);
+    if (hipMemcpy(&v, h->line_off.as<uint64_t>() + i, sizeof v, hipMemcpyDeviceToHost) != hipSuccess) return LP_E_DEVICE;
     return (int64_t)v;
 }
 
 int64_t lp_line_record_json(lp_handle* h, int64_t i, char* out, size_t cap) {
-    if (!h || i < 0 || i >= h->n_lines) return LP_E_INVALID;
+    if (!h) return LP_E_INVALID;
+    const int st = ensure_synced(h);
+    if (st != LP_OK) return st;
+    if (i < 0 || i >= h->n_lines) return LP_E_INVALID;
     if (!fetch_host(h)) return LP_E_DEVICE;
-    if (h->host.status[(size_t)i] != LP_LINE_OK) return LP_E_STATE;
-#ifdef LP_DEBUG_HOST
-    for (int u = 0; u < h->plan.program().n_uri; ++u)
-        fprintf(stderr, "host i=%lld u=%d flags=%x query=%llx path=%llx line_off=%llu\n", (long long)i, u,
-                h->host.u_flags[u][i], (unsigned long long)h->host.u_query[u][i], (unsigned long long)h->host.u_path[u][i],
-                (unsigned long long)h->host.line_off[i]);
-#endif
-    std::string js = h->plan.record_json(h->host, i);
+    if (h->view.status[i] != LP_LINE_OK) return LP_E_STATE;
+    std::string js = h->plan.record_json(h->view, i);
     if (!out || js.size() + 1 > cap) return -100 - (int64_t)(js.size() + 1);
     memcpy(out, js.c_str(), js.size() + 1);
     return (int64_t)js.size();
@@ -406,22 +603,27 @@ int64_t lp_line_record_json(lp_handle* h, int64_t i, char* out, size_t cap) {
 
 int lp_counters(lp_handle* h, uint64_t* out, int n) {
     if (!h || !out) return LP_E_INVALID;
-    if (h->pending) lp_sync(h);
+    const int st = ensure_synced(h);
+    if (st != LP_OK) return st;
     for (int k = 0; k < n && k < 4; ++k) out[k] = h->counters[k];
     return n < 4 ? n : 4;
 }
 
 int lp_last_timing(lp_handle* h, float* out, int n) {
     if (!h || !out) return LP_E_INVALID;
-    if (h->pending) lp_sync(h);
+    const int st = ensure_synced(h);
+    if (st != LP_OK) return st;
     for (int k = 0; k < n && k < 3; ++k) out[k] = h->ms[k];
     return n < 3 ? n : 3;
 }
 
 int lp_last_bytes(lp_handle* h, uint64_t* out, int n) {
     if (!h || !out) return LP_E_INVALID;
-    if (h->pending) lp_sync(h);
-    uint64_t v[2] = {h->nbytes, (uint64_t)h->n_lines * (h->row_bytes + 8) + h->arena_written};
+    const int st = ensure_synced(h);
+    if (st != LP_OK) return st;
+    uint64_t row = 8;  // line index entry
+    for (const auto& c : h->specs) row += (uint64_t)c.esz;
+    uint64_t v[2] = {h->nbytes, (uint64_t)h->n_lines * row + h->arena_written};
     for (int k = 0; k < n && k < 2; ++k) out[k] = v[k];
     return n < 2 ? n : 2;
 }
@@ -432,6 +634,47 @@ int64_t lp_describe(lp_handle* h, char* out, size_t cap) {
     if (!out || d.size() + 1 > cap) return -(int64_t)(d.size() + 1);
     memcpy(out, d.c_str(), d.size() + 1);
     return (int64_t)d.size();
+}
+
+int lp_result_view(lp_handle* h, lp_result* out) {
+    if (!h || !out) return LP_E_INVALID;
+    const int st = ensure_synced(h);
+    if (st != LP_OK) return st;
+    lp_result& R = *out;
+    R = lp_result{};
+    R.n_lines = h->n_lines;
+    R.input_bytes = h->nbytes;
+    R.input = h->d_buf;
+    R.line_off = h->line_off.as<uint64_t>();
+    R.columns = h->cols.as<uint8_t>();
+    R.columns_bytes = h->cols.cap;
+    R.arena = h->arena.as<uint8_t>();
+    R.arena_bytes = h->shard_cap * LP_ARENA_SHARDS;
+    R.shard_cap = h->shard_cap;
+    for (int s = 0; s < LP_ARENA_SHARDS; ++s) R.shard_off[s] = (uint64_t)s * h->shard_cap;
+    R.n_columns = (int32_t)h->dev_cols.size();
+    R.column = h->dev_cols.data();
+    R.on_host = 0;
+    return LP_OK;
+}
+
+int64_t lp_result_copy(lp_handle* h, void* host, uint64_t cap, int with_input, lp_result* out) {
+    if (!h || (host && !out)) return LP_E_INVALID;
+    const int st = ensure_synced(h);
+    if (st != LP_OK) return st;
+    return copy_result(h, (uint8_t*)host, host ? cap : 0, with_input != 0, out);
+}
+
+int64_t lp_result_record_json(lp_handle* h, const lp_result* r, int64_t i, char* out, size_t cap) {
+    if (!h || !r || !r->on_host || !r->input) return LP_E_INVALID;
+    if (i < 0 || i >= r->n_lines) return LP_E_INVALID;
+    lp::ResultView V;
+    make_view(h, *r, V);
+    if (!V.status || V.status[i] != LP_LINE_OK) return LP_E_STATE;
+    std::string js = h->plan.record_json(V, i);
+    if (!out || js.size() + 1 > cap) return -100 - (int64_t)(js.size() + 1);
+    memcpy(out, js.c_str(), js.size() + 1);
+    return (int64_t)js.size();
 }
 
 }  // extern "C"

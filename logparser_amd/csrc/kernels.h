@@ -6,7 +6,7 @@
 
 namespace lp {
 
-// Everything the parse kernel reads besides the input: copied to the device
+// Everything the parse kernels read besides the input: copied to the device
 // per batch (stream-ordered), so concurrent handles never share state.
 struct DeviceArgs {
     Program prog;
@@ -14,27 +14,41 @@ struct DeviceArgs {
 };
 
 int64_t count_chunks(uint64_t nbytes);
-// index pass 1: per-chunk '\n' counts, exclusively scanned in place;
-// d_chunk needs count_chunks()+1 entries, d_chunk[nc] = total '\n' count
-// and d_nlmask[i] = '\n' bits of bytes [16 i, 16 i + 16) (nlmask_words() entries)
-int launch_count(const uint8_t* d_buf, uint64_t nbytes, uint64_t* d_chunk, uint16_t* d_nlmask, hipStream_t s);
 inline int64_t nlmask_words(uint64_t nbytes) { return count_chunks(nbytes) * (64 * 1024 / 16); }
-// index pass 2 (from the masks): d_line_off[k] = start of line k for k >= 1 (caller sets [0])
+// line index, pass 1: per-chunk '\n' counts (exclusively scanned in place,
+// d_chunk needs count_chunks()+1 entries) and the '\n' bit mask of every 16
+// input bytes (d_nlmask, nlmask_words() entries); the scan also sets
+// meta->n_lines (Hadoop LineRecordReader count: a final unterminated line
+// counts), line_off[0] and the end sentinel, and meta->cap_ovf when the
+// batch has more lines than the columns hold (cap_lines).
+int launch_count(const uint8_t* d_buf, uint64_t nbytes, uint64_t* d_chunk, uint16_t* d_nlmask, uint64_t* d_line_off,
+                 int64_t cap_lines, Meta* d_meta, hipStream_t s);
+// line index, pass 2 (from the masks): line_off[k] = start of line k (k <= cap_lines)
 int launch_offsets(const uint16_t* d_nlmask, uint64_t nbytes, const uint64_t* d_chunk, uint64_t* d_line_off,
-                   hipStream_t s);
-// parse kernels: number of waves (C.wave_counts needs WC_WORDS u32 per wave)
+                   int64_t cap_lines, hipStream_t s);
+
+// parse kernels: one wave per 64 lines (C.wave_counts needs WC_WORDS u32 per wave)
 constexpr int WC_WORDS = 8;
 int64_t parse_waves(int64_t n_lines);
-// parse every line, then counters[0..4] += lines, ok, bad, fallback, arena bytes written
-// (mode PM_PARSE); mode PM_MATCH only writes C.fmt_match (sticky routing pass 1)
-enum { PM_PARSE = 0, PM_MATCH = 1 };
-int launch_parse(const uint8_t* d_buf, uint64_t nbytes, int64_t n_lines, const DeviceArgs* d_args, int n_elems,
-                 int stack_depth, const uint32_t* d_wave_counts, unsigned long long* counters, hipStream_t s,
-                 int mode = PM_PARSE);
+struct ParseLaunch {
+    const uint8_t* buf;
+    uint64_t nbytes;
+    int64_t cap_lines;      // grid: parse_waves(cap_lines) waves; lines >= meta->n_lines exit
+    uint64_t mean_line;     // expected mean line length (sizes the LDS window)
+    int n_elems, stack_depth;
+    bool force_direct;      // every wave on the direct (HBM) path: tests / diagnostics only
+};
+// parse every line (staged waves, then the waves whose window did not fit
+// LDS on the direct path), then meta->counters[0..4] += lines, ok, bad,
+// fallback, arena bytes written
+int launch_parse(const ParseLaunch& a, const DeviceArgs* d_args, const uint32_t* d_wave_counts, Meta* d_meta,
+                 hipStream_t s);
+// sticky routing pass 1: C.fmt_match of every line
+int launch_route_match(const ParseLaunch& a, const DeviceArgs* d_args, hipStream_t s);
 // sticky routing pass 2: C.fmt_match -> C.fmt_id (C.fmt_chunk: fmt_chunks()+1 words, the
-// state after the last line at [fmt_chunks()])
+// state after the last line at [fmt_chunks(n_lines)])
 constexpr int FMT_CHUNK = 4096;
-inline int64_t fmt_chunks(int64_t n_lines) { return (n_lines + FMT_CHUNK - 1) / FMT_CHUNK; }
-int launch_route(const DeviceArgs* d_args, int64_t n_lines, hipStream_t s);
+__host__ __device__ inline int64_t fmt_chunks(int64_t n_lines) { return (n_lines + FMT_CHUNK - 1) / FMT_CHUNK; }
+int launch_route(const DeviceArgs* d_args, int64_t cap_lines, hipStream_t s);
 
 }  // namespace lp

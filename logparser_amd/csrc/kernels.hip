@@ -1,21 +1,26 @@
 // gfx950 kernels of the logparser_amd engine.
 //
 //   k_count_newlines  per-chunk '\n' count and '\n' bit masks (16-byte loads, SWAR byte compare)
-//   k_scan_counts     exclusive scan of the chunk counts (single workgroup)
+//   k_scan_counts     exclusive scan of the chunk counts (single workgroup); the batch's line
+//                     count, line_off[0] and the end sentinel, written on the device
 //   k_line_offsets    line start offsets from the bit masks (Hadoop LineRecordReader '\n' semantics)
-//   k_parse_lines     one wave per 64 lines, one lane per line: the lines'
-//                     byte window staged in LDS, LogFormat match + token /
-//                     time / first-line stages (phase 1), wave-aggregated
-//                     arena allocation, URI + query-string stages (phase 2)
+//   k_parse_lines     one wave per 64 lines, one lane per line: the lines' byte window and
+//                     its byte-class masks staged in LDS, LogFormat match + token / time /
+//                     first-line stages (phase 1), wave-aggregated arena allocation from a
+//                     sharded bump pointer, URI + query-string stages (phase 2); a wave whose
+//                     window does not fit LDS is queued for k_parse_direct
+//   k_parse_direct    the queued waves, reading the input from HBM (persistent grid)
+//   k_route_match     several LogFormats: which formats match each line (sticky routing pass 1)
+//   k_fmt_*           the sticky active-format scan (routing pass 2)
 //   k_reduce_counts   per-wave status counts -> the batch counters
 //
 // The per-line logic is lp_device.h; this file only adds the data-parallel
-// scaffolding around it.
+// scaffolding around it.  The staged kernel carries exactly one line type
+// (the LDS window with masks): its code is what the hot loop keeps in the
+// instruction cache.
 #include <hip/hip_runtime.h>
 
 #define LP_KERNEL_TU 1  // device column pointers are global-memory pointers (lp_program.h)
-
-#include <cstdlib>
 
 #include "kernels.h"
 #include "lp_device.h"
@@ -98,8 +103,13 @@ __global__ __launch_bounds__(NL_THREADS) void k_count_newlines(const uint8_t* __
     }
 }
 
-// exclusive scan of n counts in place; total written to counts[n]
-__global__ __launch_bounds__(1024) void k_scan_counts(uint64_t* __restrict__ counts, int64_t n) {
+// exclusive scan of n counts in place; total written to counts[n]; then the
+// batch's line count (a final line without '\n' counts), line_off[0] = 0 and
+// the end sentinel of an unterminated last line (line_off[n_lines] = nbytes + 1)
+__global__ __launch_bounds__(1024) void k_scan_counts(uint64_t* __restrict__ counts, int64_t n,
+                                                      const uint8_t* __restrict__ buf, uint64_t nbytes,
+                                                      uint64_t* __restrict__ line_off, int64_t cap_lines,
+                                                      Meta* __restrict__ meta) {
     // one contiguous segment per thread; loads issued 8 at a time so their
     // latencies overlap (a dependent load per element took ~1 ms at 386 K
     // chunks)
@@ -130,7 +140,17 @@ __global__ __launch_bounds__(1024) void k_scan_counts(uint64_t* __restrict__ cou
         uint64_t run = x - t;
 #pragma unroll
         for (int k = 0; k < 16; ++k) { part[threadIdx.x * 16 + k] = run; run += v[k]; }
-        if (threadIdx.x == 63) counts[n] = run;
+        if (threadIdx.x == 63) {
+            counts[n] = run;
+            // Hadoop LineRecordReader: lines = '\n' count, plus a last line without one
+            const bool open_end = nbytes > 0 && buf[nbytes - 1] != '\n';
+            const int64_t lines = (int64_t)run + (open_end ? 1 : 0);
+            meta->n_lines = (unsigned long long)lines;
+            // cap_lines < 0: only count (the host sizes the buffers from the count)
+            meta->cap_ovf = cap_lines >= 0 && lines > cap_lines ? 1ull : 0ull;
+            line_off[0] = 0;
+            if (open_end && cap_lines >= 0 && lines <= cap_lines) line_off[lines] = nbytes + 1;
+        }
     }
     __syncthreads();
     uint64_t run = part[threadIdx.x];
@@ -146,10 +166,11 @@ __global__ __launch_bounds__(1024) void k_scan_counts(uint64_t* __restrict__ cou
 }
 
 // line_off[j] = start of line j.  line_off[0] = 0 and the entry after every
-// '\n' that is not the last byte; line_off[n_lines] = end sentinel.
+// '\n' that is not the last byte; line_off[n_lines] = end sentinel.  Entries
+// past cap_lines are not written (the batch is then re-run with larger columns).
 __global__ __launch_bounds__(NL_THREADS) void k_line_offsets(const uint16_t* __restrict__ nlmask, uint64_t nbytes,
                                                               const uint64_t* __restrict__ chunk_base,
-                                                              uint64_t* __restrict__ line_off) {
+                                                              uint64_t* __restrict__ line_off, int64_t cap_lines) {
     const uint64_t base = (uint64_t)blockIdx.x * CHUNK;
     __shared__ uint32_t wsum[NL_THREADS / 64];
     uint64_t run = chunk_base[blockIdx.x];
@@ -175,7 +196,8 @@ __global__ __launch_bounds__(NL_THREADS) void k_line_offsets(const uint16_t* __r
         while (m) {
             const uint32_t b = (uint32_t)__builtin_ctz(m);
             m &= m - 1;
-            line_off[++k] = pos + b + 1;
+            if ((int64_t)(k + 1) <= cap_lines) line_off[k + 1] = pos + b + 1;
+            ++k;
         }
         run += tot;
         __syncthreads();
@@ -184,9 +206,9 @@ __global__ __launch_bounds__(NL_THREADS) void k_line_offsets(const uint16_t* __r
 
 // ---------------------------------------------------------------- parse
 // One workgroup = one wave = 64 consecutive lines.  The wave copies the byte
-// window holding its lines into LDS with coalesced 16-byte loads, then every
-// lane runs the per-line stages of lp_device.h on its own line out of LDS.
-// Windows larger than the LDS budget (very long lines) read HBM directly.
+// window holding its lines into LDS with coalesced 16-byte loads (classifying
+// every byte into the two mask planes on the way), then every lane runs the
+// per-line stages of lp_device.h on its own line out of LDS.
 constexpr int PW = 64;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -207,20 +229,92 @@ __device__ __forceinline__ LN owner_line(const LN& L, int own) {
     return R;
 }
 
+// Lines [li0, li0 + 64) of a wave: this lane's line [s, e) and the byte
+// window [w0, w1) of all of them (w0 16-byte aligned).
+struct WaveLines {
+    int64_t li0, li, lend;
+    bool active;
+    uint64_t s, e, w0, w1;
+    int n;
+};
+__device__ __forceinline__ WaveLines wave_lines(const Columns& C, int64_t wave, int64_t n_lines, uint64_t nbytes) {
+    WaveLines W;
+    W.li0 = wave * PW;
+    W.li = W.li0 + (int64_t)threadIdx.x;
+    W.active = W.li < n_lines;
+    W.lend = W.li0 + PW < n_lines ? W.li0 + PW : n_lines;
+    W.s = W.e = 0;
+    if (W.active) {
+        W.s = C.line_off[W.li];
+        W.e = C.line_off[W.li + 1] - 1;  // exclude '\n' (or the end sentinel)
+    }
+    W.n = (int)((W.e - W.s) > (uint64_t)0x7FFFFFFF ? 0x7FFFFFFF : (W.e - W.s));
+    W.w0 = C.line_off[W.li0] & ~15ull;
+    W.w1 = C.line_off[W.lend];
+    if (W.w1 > nbytes) W.w1 = nbytes;
+    return W;
+}
+
+// Stage [w0, w1) into win (LDS) and the mask planes into msk16 (two 64-bit
+// planes per 64-byte block, as 16-bit pieces).  Returns whether every byte
+// but '\n' passes the fast-path guard (then no line needs the guard scan).
+__device__ __forceinline__ bool stage_window(const uint8_t* __restrict__ buf, uint64_t nbytes, uint64_t w0, uint64_t w1,
+                                             uint8_t* win, uint16_t* msk16) {
+    const int lane = threadIdx.x;
+    const int nv = (int)((w1 - w0 + 15) >> 4);
+    const int nv4 = (nv + 3) & ~3;  // whole 64-byte mask blocks
+    uint32_t bad = 0;  // guard-failing bytes other than '\n' anywhere in the window
+    // SB loads in flight per lane before the first LDS store (one HBM
+    // round trip per SB x 1 KiB of window instead of one per 1 KiB)
+    constexpr int SB = 20;
+    const uint64_t full_end = nbytes & ~15ull;  // 16-byte pieces wholly inside the buffer
+    for (int k0 = lane; k0 < nv4; k0 += SB * PW) {
+        u32x4 v[SB];
+#pragma unroll
+        for (int j = 0; j < SB; ++j) {
+            const int k = k0 + j * PW;
+            const uint64_t p = w0 + 16ull * k;
+            v[j] = u32x4{0, 0, 0, 0};
+            if (k < nv && p + 16 <= full_end) v[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(buf + p));
+        }
+#pragma unroll
+        for (int j = 0; j < SB; ++j) {
+            const int k = k0 + j * PW;
+            if (k >= nv4) continue;
+            const uint64_t p = w0 + 16ull * k;
+            if (k < nv && p + 16 > full_end) {  // the buffer's last partial piece
+                auto word = [&](uint64_t q) {
+                    uint32_t w = 0;
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) w |= q + b < nbytes ? (uint32_t)buf[q + b] << (8 * b) : 0u;
+                    return w;
+                };
+                v[j] = u32x4{word(p), word(p + 4), word(p + 8), word(p + 12)};
+            }
+            if (k < nv)
+                for (int w = 0; w < 4; ++w) bad |= swar::guard_bad(v[j][w]) & ~swar::eq(v[j][w], '\n');
+            *reinterpret_cast<u32x4*>(win + 16 * k) = v[j];
+            uint32_t m0, m1;
+            bcls::classify16(v[j][0], v[j][1], v[j][2], v[j][3], m0, m1);
+            msk16[8 * (k >> 2) + (k & 3)] = (uint16_t)m0;
+            msk16[8 * (k >> 2) + 4 + (k & 3)] = (uint16_t)m1;
+        }
+    }
+    return !__any(bad != 0);
+}
+
+// Per-line work of one wave: phase 1, arena allocation, phase 2, the wave's
+// query pieces spread over its lanes, the per-wave counts.
 template <typename LN>
 __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, const Columns& C, const LN& L,
-                                           bool active, int64_t li, WaveStack stk, bool clean, int mode) {
-    if (mode == PM_MATCH) {  // sticky routing, pass 1: which formats match each line
-        if (active) C.fmt_match[li] = (uint16_t)fmt_match_word(P, elems, L, stk, clean);
-        return;
-    }
+                                           bool active, int64_t li, WaveStack stk, bool clean, int64_t wave) {
     LineOut o;
     o.status = ST_OK;
     o.arena_need = 0;
     LP_PROF(1);
     if (active) phase1(P, elems, L, o, stk, C, li, clean, P.n_fmt > 1 ? (int)C.fmt_id[li] : 0);
     LP_PROF(9);
-    // wave-aggregated arena allocation (every lane reaches this point)
+    // wave-aggregated arena allocation from the wave's shard (every lane reaches this point)
     const uint32_t need = (active && o.status == ST_OK) ? o.arena_need : 0u;
     const int lane = threadIdx.x;
     uint32_t x = need;
@@ -229,22 +323,23 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
         if (lane >= d) x += y;
     }
     const uint32_t total = __shfl(x, 63);
+    const int shard = (int)(wave % ARENA_SHARDS);
     unsigned long long wbase = 0;
-    if (lane == 63 && total) wbase = atomicAdd(C.arena_top, (unsigned long long)total);
+    if (lane == 63 && total) wbase = atomicAdd(&C.meta->shard_top[16 * shard], (unsigned long long)total);
     wbase = __shfl(wbase, 63);
+    const bool fits = wbase + total <= C.shard_cap;
     uint32_t written = 0;
     if (active) {
-        if (o.status == ST_OK && need) {
-            const unsigned long long mine = wbase + x - need;
-            if (mine + need > C.arena_cap) o.status = ST_FALLBACK;
-            else {
-                C.arena_base[li] = mine;
-                Arena A{C.arena + mine, 0, need};
-                phase2(P, L, o, A, C, li);
-                written = A.used - A.slack;
-            }
+        if (o.status == ST_OK && !fits && need) {
+            // the shard is full: the batch is re-run with a larger arena
+            o.status = ST_FALLBACK;
+            atomicAdd(&C.meta->arena_ovf, 1ull);
         } else if (o.status == ST_OK) {
-            C.arena_base[li] = 0;
+            const unsigned long long mine = (unsigned long long)shard * C.shard_cap + wbase + x - need;
+            C.arena_base[li] = need ? mine : 0ull;
+            Arena A{C.arena + (need ? mine : 0ull), 0, need};
+            phase2(P, L, o, A, C, li);
+            written = A.used - A.slack;
         }
         LP_PROF(20);
         write_line(P, o, C, li);
@@ -265,8 +360,8 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
                 const uint32_t y = __shfl_up(incl, d);
                 if (lane >= d) incl += y;
             }
-            const uint32_t base = incl - np, total = __shfl(incl, 63);
-            for (uint32_t g0 = 0; g0 < total; g0 += PW) {
+            const uint32_t base = incl - np, tot = __shfl(incl, 63);
+            for (uint32_t g0 = 0; g0 < tot; g0 += PW) {
                 const uint32_t g = g0 + (uint32_t)lane;
                 int own = 0;  // last lane whose first pending piece index is <= g
                 for (int st = 32; st; st >>= 1)
@@ -274,7 +369,7 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
                 const uint32_t ob = __shfl(base, own), olist = __shfl(my_list, own);
                 const unsigned long long oab = __shfl(my_ab, own);
                 const auto OL = owner_line(L, own);
-                if (g < total) {
+                if (g < tot) {
                     LP_G uint8_t* region = C.arena + oab;
                     LP_G uint64_t* slot = reinterpret_cast<LP_G uint64_t*>(region + olist + 16 * (g - ob));
                     const uint64_t a0 = slot[0];
@@ -298,112 +393,102 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
         c.w = c.x - c.y - c.z;
         d.x = written;
         d.y = d.z = d.w = 0;
-        uint4* wc = reinterpret_cast<uint4*>(C.wave_counts + WC_WORDS * (size_t)blockIdx.x);
+        uint4* wc = reinterpret_cast<uint4*>(C.wave_counts + WC_WORDS * (size_t)wave);
         wc[0] = c;
         wc[1] = d;
     }
 }
 
-// MASKS: the staging pass also builds the byte-class masks (MC_N bits per
-// window byte) for the 64-bytes-per-step scanners; without them the
-// scanners classify 4 bytes per step and a wave needs less LDS.
-template <bool MASKS>
-__global__ __launch_bounds__(PW) void k_parse_lines(const uint8_t* __restrict__ buf, uint64_t nbytes, int64_t n_lines,
-                                                    const DeviceArgs* __restrict__ args, uint32_t win_cap, int stage,
-                                                    uint32_t stk_words, int mode) {
+// LDS: [elements (n_elems x 16 B)][DFS stack][byte window (win_cap, a multiple of 64)][mask planes (win_cap / 4)]
+__device__ __forceinline__ void load_elems(const Program& P, Elem* s_elems) {
+    for (int k = threadIdx.x; k < P.n_elems; k += PW) s_elems[k] = P.elems[k];
+}
+
+__global__ __launch_bounds__(PW) void k_parse_lines(const uint8_t* __restrict__ buf, uint64_t nbytes,
+                                                    const DeviceArgs* __restrict__ args, uint32_t win_cap,
+                                                    uint32_t stk_words) {
     const Program& P = args->prog;
     const Columns& C = args->cols;
-    // LDS: [elements (n_elems x 16 B)][DFS stack][byte window (win_cap, a multiple of 64)][MC_N class masks]
+    const int64_t n_lines = (int64_t)C.meta->n_lines;
+    const int64_t wave = blockIdx.x;
+    if (wave * PW >= n_lines || C.meta->cap_ovf) return;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     Elem* s_elems = reinterpret_cast<Elem*>(smem);
-    for (int k = threadIdx.x; k < P.n_elems; k += PW) s_elems[k] = P.elems[k];
     WaveStack stk{reinterpret_cast<uint32_t*>(smem + 16 * P.n_elems) + threadIdx.x};
     uint8_t* win = smem + 16 * P.n_elems + stk_words * 4;
-    const uint32_t mwords = win_cap >> 6;
     uint16_t* msk16 = reinterpret_cast<uint16_t*>(win + win_cap);
-    const int lane = threadIdx.x;
-    const int64_t li0 = (int64_t)blockIdx.x * PW;
-    const int64_t li = li0 + lane;
-    const bool active = li < n_lines;
-    const int64_t lend = li0 + PW < n_lines ? li0 + PW : n_lines;
-    uint64_t s = 0, e = 0;
-    if (active) {
-        s = C.line_off[li];
-        e = C.line_off[li + 1] - 1;  // exclude '\n' (or the end sentinel)
+    const WaveLines W = wave_lines(C, wave, n_lines, nbytes);
+    if (W.w1 - W.w0 > win_cap) {  // the window does not fit: k_parse_direct takes the wave
+        if (threadIdx.x == 0) C.ovf_list[atomicAdd(&C.meta->ovf_waves, 1ull)] = (uint32_t)wave;
+        return;
     }
-    const int n = (int)((e - s) > (uint64_t)0x7FFFFFFF ? 0x7FFFFFFF : (e - s));
-    const uint64_t w0 = C.line_off[li0] & ~15ull;
-    uint64_t w1 = C.line_off[lend];
-    if (w1 > nbytes) w1 = nbytes;
+    load_elems(P, s_elems);
     LP_PROF(0);
-    if (stage && w1 - w0 <= win_cap) {
-        // stage the window with coalesced 16-byte loads and classify every
-        // byte once (nibble-LUT classes -> 16 bits per class per 16 bytes)
-        const int nv = (int)((w1 - w0 + 15) >> 4);
-        const int nv4 = (nv + 3) & ~3;  // whole 64-bit mask words
-        uint32_t bad = 0;  // guard-failing bytes other than '\n' anywhere in the window
-        // SB loads in flight per lane before the first LDS store (one HBM
-        // round trip per SB x 1 KiB of window instead of one per 1 KiB)
-        constexpr int SB = 20;
-        const uint64_t full_end = nbytes & ~15ull;  // 16-byte pieces wholly inside the buffer
-        for (int k0 = lane; k0 < nv4; k0 += SB * PW) {
-            u32x4 v[SB];
-#pragma unroll
-            for (int j = 0; j < SB; ++j) {
-                const int k = k0 + j * PW;
-                const uint64_t p = w0 + 16ull * k;
-                v[j] = u32x4{0, 0, 0, 0};
-                if (k < nv && p + 16 <= full_end) v[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(buf + p));
-            }
-#pragma unroll
-            for (int j = 0; j < SB; ++j) {
-                const int k = k0 + j * PW;
-                if (k >= nv4) continue;
-                const uint64_t p = w0 + 16ull * k;
-                if (k < nv && p + 16 > full_end) {  // the buffer's last partial piece
-                    auto word = [&](uint64_t q) {
-                        uint32_t w = 0;
-#pragma unroll
-                        for (int b = 0; b < 4; ++b) w |= q + b < nbytes ? (uint32_t)buf[q + b] << (8 * b) : 0u;
-                        return w;
-                    };
-                    v[j] = u32x4{word(p), word(p + 4), word(p + 8), word(p + 12)};
-                }
-                if (k < nv)
-                    for (int w = 0; w < 4; ++w) bad |= swar::guard_bad(v[j][w]) & ~swar::eq(v[j][w], '\n');
-                *reinterpret_cast<u32x4*>(win + 16 * k) = v[j];
-                if constexpr (MASKS) {
-                    uint32_t m0, m1;
-                    bcls::classify16(v[j][0], v[j][1], v[j][2], v[j][3], m0, m1);
-                    if (MC_QUOTE >= 0) msk16[4 * mwords * MC_QUOTE + k] = (uint16_t)m0;
-                    msk16[4 * mwords * MC_UEV + k] = (uint16_t)m1;
-                }
-            }
-        }
-        const bool clean = !__any(bad != 0);
-        __syncthreads();
-        if constexpr (MASKS) {
-            const LineT<lds_bytes, lds_u64> L{(lds_bytes)win, (uint32_t)(s - w0), n,
-                                              (lds_u64)reinterpret_cast<uint64_t*>(msk16), mwords};
-            parse_wave(P, s_elems, C, L, active, li, stk, clean, mode);
-        } else {
-            const LineT<lds_bytes> L{(lds_bytes)win, (uint32_t)(s - w0), n};
-            parse_wave(P, s_elems, C, L, active, li, stk, clean, mode);
-        }
-    } else {
-        __syncthreads();
+    const bool clean = stage_window(buf, nbytes, W.w0, W.w1, win, msk16);
+    __syncthreads();
+    const LineT<lds_bytes, lds_u64> L{(lds_bytes)win, (uint32_t)(W.s - W.w0), W.n, (lds_u64)reinterpret_cast<uint64_t*>(msk16)};
+    parse_wave(P, s_elems, C, L, W.active, W.li, stk, clean, wave);
+}
+
+// The queued waves of k_parse_lines, lines read from HBM (persistent grid).
+__global__ __launch_bounds__(PW) void k_parse_direct(const uint8_t* __restrict__ buf, uint64_t nbytes,
+                                                     const DeviceArgs* __restrict__ args) {
+    const Program& P = args->prog;
+    const Columns& C = args->cols;
+    const int64_t n_lines = (int64_t)C.meta->n_lines;
+    const uint64_t nq = C.meta->ovf_waves;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    Elem* s_elems = reinterpret_cast<Elem*>(smem);
+    WaveStack stk{reinterpret_cast<uint32_t*>(smem + 16 * P.n_elems) + threadIdx.x};
+    load_elems(P, s_elems);
+    __syncthreads();
+    for (uint64_t q = blockIdx.x; q < nq; q += gridDim.x) {
+        const int64_t wave = C.ovf_list[q];
+        const WaveLines W = wave_lines(C, wave, n_lines, nbytes);
         // base = the line start aligned down to 4 bytes: word reads never
         // leave the 4-byte words holding the line's bytes
-        const LP_G uint8_t* ls = (const LP_G uint8_t*)(buf) + s;
+        const LP_G uint8_t* ls = (const LP_G uint8_t*)(buf) + W.s;
         const uint32_t mis = (uint32_t)((uintptr_t)ls & 3);
-        const LineT<const LP_G uint8_t*> L{ls - mis, mis, n};
-        parse_wave(P, s_elems, C, L, active, li, stk, false, mode);
+        const LineT<const LP_G uint8_t*> L{ls - mis, mis, W.n};
+        parse_wave(P, s_elems, C, L, W.active, W.li, stk, false, wave);
+        __syncthreads();
     }
 }
 
-// counters[0..4] += sum of the per-wave counts (lines ok bad fallback arena-bytes)
-__global__ __launch_bounds__(256) void k_reduce_counts(const uint32_t* __restrict__ wc, int64_t n_waves,
-                                                       unsigned long long* __restrict__ counters) {
+// Sticky routing pass 1: the match word of every line (bit f = format f matches).
+__global__ __launch_bounds__(PW) void k_route_match(const uint8_t* __restrict__ buf, uint64_t nbytes,
+                                                    const DeviceArgs* __restrict__ args, uint32_t win_cap,
+                                                    uint32_t stk_words) {
+    const Program& P = args->prog;
+    const Columns& C = args->cols;
+    const int64_t n_lines = (int64_t)C.meta->n_lines;
+    const int64_t wave = blockIdx.x;
+    if (wave * PW >= n_lines || C.meta->cap_ovf) return;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    Elem* s_elems = reinterpret_cast<Elem*>(smem);
+    WaveStack stk{reinterpret_cast<uint32_t*>(smem + 16 * P.n_elems) + threadIdx.x};
+    uint8_t* win = smem + 16 * P.n_elems + stk_words * 4;
+    uint16_t* msk16 = reinterpret_cast<uint16_t*>(win + win_cap);
+    load_elems(P, s_elems);
+    const WaveLines W = wave_lines(C, wave, n_lines, nbytes);
+    if (W.w1 - W.w0 <= win_cap) {
+        const bool clean = stage_window(buf, nbytes, W.w0, W.w1, win, msk16);
+        __syncthreads();
+        const LineT<lds_bytes, lds_u64> L{(lds_bytes)win, (uint32_t)(W.s - W.w0), W.n, (lds_u64)reinterpret_cast<uint64_t*>(msk16)};
+        if (W.active) C.fmt_match[W.li] = (uint16_t)fmt_match_word(P, s_elems, L, stk, clean);
+    } else {
+        __syncthreads();
+        const LP_G uint8_t* ls = (const LP_G uint8_t*)(buf) + W.s;
+        const uint32_t mis = (uint32_t)((uintptr_t)ls & 3);
+        const LineT<const LP_G uint8_t*> L{ls - mis, mis, W.n};
+        if (W.active) C.fmt_match[W.li] = (uint16_t)fmt_match_word(P, s_elems, L, stk, false);
+    }
+}
+
+// meta->counters[0..4] += sum of the per-wave counts (lines ok bad fallback arena-bytes)
+__global__ __launch_bounds__(256) void k_reduce_counts(const uint32_t* __restrict__ wc, Meta* __restrict__ meta) {
+    const int64_t n_lines = meta->cap_ovf ? 0 : (int64_t)meta->n_lines;
+    const int64_t n_waves = (n_lines + PW - 1) / PW;
     unsigned long long a[5] = {0, 0, 0, 0, 0};
     for (int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x; w < n_waves; w += (int64_t)gridDim.x * 256) {
         const uint4 c = reinterpret_cast<const uint4*>(wc + WC_WORDS * w)[0];
@@ -419,7 +504,7 @@ __global__ __launch_bounds__(256) void k_reduce_counts(const uint32_t* __restric
     __syncthreads();
     if (threadIdx.x < 5) {
         unsigned long long v = red[threadIdx.x][0] + red[threadIdx.x][1] + red[threadIdx.x][2] + red[threadIdx.x][3];
-        if (v) atomicAdd(&counters[threadIdx.x], v);
+        if (v) atomicAdd(&meta->counters[threadIdx.x], v);
     }
 }
 
@@ -449,18 +534,25 @@ __device__ __forceinline__ uint64_t wave_scan_tables(uint64_t t) {
     return t;
 }
 
-__global__ __launch_bounds__(PW) void k_fmt_reduce(const DeviceArgs* __restrict__ args, int64_t n_lines) {
+__device__ __forceinline__ int64_t routed_lines(const Columns& C) {
+    return C.meta->cap_ovf ? 0 : (int64_t)C.meta->n_lines;
+}
+
+__global__ __launch_bounds__(PW) void k_fmt_reduce(const DeviceArgs* __restrict__ args) {
     const Program& P = args->prog;
     const Columns& C = args->cols;
+    const int64_t n_lines = routed_lines(C);
+    if ((int64_t)blockIdx.x * FMT_CHUNK >= n_lines) return;
     const int64_t l0 = (int64_t)blockIdx.x * FMT_CHUNK + (int64_t)threadIdx.x * FMT_LPL;
     const uint64_t t = wave_scan_tables(lane_table(C, P, l0, n_lines));
     if (threadIdx.x == PW - 1) C.fmt_chunk[blockIdx.x] = t;
 }
 
 // one thread: chunk tables -> entry state of every chunk (in place), final
-// state after the last chunk at [n_chunks]
-__global__ void k_fmt_chunks(const DeviceArgs* __restrict__ args, int64_t n_chunks) {
+// state after the last chunk at [n_chunks] and in meta->fmt_state
+__global__ void k_fmt_chunks(const DeviceArgs* __restrict__ args) {
     const Columns& C = args->cols;
+    const int64_t n_chunks = fmt_chunks(routed_lines(C));
     uint32_t s = C.fmt_init;
     for (int64_t c = 0; c < n_chunks; ++c) {
         const uint64_t t = C.fmt_chunk[c];
@@ -468,11 +560,14 @@ __global__ void k_fmt_chunks(const DeviceArgs* __restrict__ args, int64_t n_chun
         s = fmt_apply(t, s);
     }
     C.fmt_chunk[n_chunks] = s;
+    C.meta->fmt_state = s;
 }
 
-__global__ __launch_bounds__(PW) void k_fmt_apply(const DeviceArgs* __restrict__ args, int64_t n_lines) {
+__global__ __launch_bounds__(PW) void k_fmt_apply(const DeviceArgs* __restrict__ args) {
     const Program& P = args->prog;
     const Columns& C = args->cols;
+    const int64_t n_lines = routed_lines(C);
+    if ((int64_t)blockIdx.x * FMT_CHUNK >= n_lines) return;
     const int64_t l0 = (int64_t)blockIdx.x * FMT_CHUNK + (int64_t)threadIdx.x * FMT_LPL;
     const uint64_t incl = wave_scan_tables(lane_table(C, P, l0, n_lines));
     uint64_t excl = __shfl_up(incl, 1);
@@ -486,24 +581,56 @@ __global__ __launch_bounds__(PW) void k_fmt_apply(const DeviceArgs* __restrict__
     }
 }
 
+// LDS window of a wave: sized to the most waves per CU that still leave >= 4 %
+// over the mean 64 lines (the few windows that do not fit go to the direct
+// kernel).  Measured on gfx950: W waves of one 64-thread workgroup each fit
+// when a wave's LDS is at most 160 KiB / W - 640 B.
+struct WindowPlan {
+    uint32_t cap, stk_words;
+    size_t lds;
+};
+WindowPlan window_plan(const ParseLaunch& a) {
+    WindowPlan w;
+    w.stk_words = (uint32_t)(a.stack_depth > 0 ? a.stack_depth : 1) * PW;
+    const uint64_t fixed = 16 * (uint64_t)a.n_elems + 4 * (uint64_t)w.stk_words;
+    const uint64_t per8 = 8 + MC_N;  // LDS bytes per 8 window bytes (window + mask planes)
+    const uint64_t mean = a.mean_line ? a.mean_line : 256;
+    const uint64_t need = PW * mean + PW * mean / 25 + 64;
+    uint64_t cap = 0;
+    for (int k = 8; k >= 2 && !cap; --k) {
+        const uint64_t budget = 160 * 1024 / k - 640;
+        if (budget <= fixed) continue;
+        const uint64_t c = ((budget - fixed) * 8 / per8) & ~63ull;
+        if (c >= need) cap = c;
+    }
+    if (!cap) cap = ((PW * mean * 110) / 100 + 512 + 63) & ~63ull;
+    if (cap > 48 * 1024) cap = 48 * 1024;
+    if (a.force_direct) cap = 0;
+    w.cap = (uint32_t)cap;
+    w.lds = fixed + cap + MC_N * (cap / 8);
+    return w;
+}
+
 }  // namespace
 
 
 int64_t count_chunks(uint64_t nbytes) { return (int64_t)((nbytes + CHUNK - 1) / CHUNK); }
 
-int launch_count(const uint8_t* d_buf, uint64_t nbytes, uint64_t* d_chunk, uint16_t* d_nlmask, hipStream_t s) {
-    int64_t nc = count_chunks(nbytes);
-    if (nc == 0) return 0;
-    hipLaunchKernelGGL(k_count_newlines, dim3((unsigned)nc), dim3(NL_THREADS), 0, s, d_buf, nbytes, d_chunk, d_nlmask);
-    hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, d_chunk, nc);
+int launch_count(const uint8_t* d_buf, uint64_t nbytes, uint64_t* d_chunk, uint16_t* d_nlmask, uint64_t* d_line_off,
+                 int64_t cap_lines, Meta* d_meta, hipStream_t s) {
+    const int64_t nc = count_chunks(nbytes);
+    if (nc > 0)
+        hipLaunchKernelGGL(k_count_newlines, dim3((unsigned)nc), dim3(NL_THREADS), 0, s, d_buf, nbytes, d_chunk, d_nlmask);
+    hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, d_chunk, nc, d_buf, nbytes, d_line_off, cap_lines, d_meta);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int launch_offsets(const uint16_t* d_nlmask, uint64_t nbytes, const uint64_t* d_chunk, uint64_t* d_line_off,
-                   hipStream_t s) {
+                   int64_t cap_lines, hipStream_t s) {
     int64_t nc = count_chunks(nbytes);
     if (nc == 0) return 0;
-    hipLaunchKernelGGL(k_line_offsets, dim3((unsigned)nc), dim3(NL_THREADS), 0, s, d_nlmask, nbytes, d_chunk, d_line_off);
+    hipLaunchKernelGGL(k_line_offsets, dim3((unsigned)nc), dim3(NL_THREADS), 0, s, d_nlmask, nbytes, d_chunk, d_line_off,
+                       cap_lines);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -515,69 +642,45 @@ extern "C" int lp_profile_read(unsigned long long* out, int n) {
     unsigned long long h[64 * 16];
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_prof), sizeof h) != hipSuccess) return -1;
     for (int k = 0; k < n && k < 64; ++k) { out[2 * k] = h[k * 16]; out[2 * k + 1] = h[k * 16 + 1]; }
-    hipMemset(nullptr, 0, 0);
     unsigned long long z[64 * 16] = {};
     hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof z);
     return 0;
 }
 #endif
 
-int launch_route(const DeviceArgs* d_args, int64_t n_lines, hipStream_t s) {
-    if (n_lines == 0) return 0;
-    const int64_t nc = fmt_chunks(n_lines);
-    hipLaunchKernelGGL(k_fmt_reduce, dim3((unsigned)nc), dim3(PW), 0, s, d_args, n_lines);
-    hipLaunchKernelGGL(k_fmt_chunks, dim3(1), dim3(1), 0, s, d_args, nc);
-    hipLaunchKernelGGL(k_fmt_apply, dim3((unsigned)nc), dim3(PW), 0, s, d_args, n_lines);
+int launch_route_match(const ParseLaunch& a, const DeviceArgs* d_args, hipStream_t s) {
+    const int64_t waves = parse_waves(a.cap_lines);
+    if (waves == 0) return 0;
+    const WindowPlan w = window_plan(a);
+    hipLaunchKernelGGL(k_route_match, dim3((unsigned)waves), dim3(PW), w.lds, s, a.buf, a.nbytes, d_args, w.cap,
+                       w.stk_words);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_parse(const uint8_t* d_buf, uint64_t nbytes, int64_t n_lines, const DeviceArgs* d_args, int n_elems,
-                 int stack_depth, const uint32_t* d_wave_counts, unsigned long long* counters, hipStream_t s, int mode) {
-    if (n_lines == 0) return 0;
-    const int64_t waves = parse_waves(n_lines);
-    // LDS window per wave: ~1.1x the mean bytes of 64 lines (+512 B), so
-    // nearly every wave stages; at most 48 KiB (+ 18 KiB of class masks).  A window that does not fit
-    // reads HBM directly.
-    const uint64_t mean = (nbytes + n_lines - 1) / n_lines;
-    // tuning knobs for profiling experiments (defaults are the product setting)
-    const char* e1 = getenv("LP_WIN_PCT");
-    const char* e2 = getenv("LP_NO_STAGE");
-    const char* e4 = getenv("LP_MASKS");
-    const bool masks = e4 ? atoi(e4) != 0 : true;
-    const int force_global = e2 ? atoi(e2) : 0;
-    const uint32_t stk_words = (uint32_t)(stack_depth > 0 ? stack_depth : 1) * PW;
-    const uint64_t fixed = 16 * (uint64_t)n_elems + 4 * (uint64_t)stk_words;
-    const uint64_t per8 = masks ? 8 + MC_N : 8;  // LDS bytes per 8 window bytes
-    // The parse kernel is latency bound: its speed follows the waves a CU
-    // holds, and LDS sets that number.  The window of a wave is sized to the
-    // most waves per CU that still leave >= 4 % over the mean 64 lines (the
-    // few windows that do not fit read HBM directly).  Measured on gfx950:
-    // W waves of one 64-thread workgroup each fit when a wave's LDS is at
-    // most 160 KiB / W - 640 B.
-    const uint64_t need = PW * mean + PW * mean / 25 + 64;
-    uint64_t cap = 0;
-    for (int w = 8; w >= 2 && !cap; --w) {
-        const uint64_t budget = 160 * 1024 / w - 640;
-        if (budget <= fixed) continue;
-        const uint64_t c = ((budget - fixed) * 8 / per8) & ~63ull;
-        if (c >= need) cap = c;
-    }
-    if (!cap || e1) cap = ((PW * mean * (uint64_t)(e1 ? atoi(e1) : 110)) / 100 + 512 + 63) & ~63ull;
-    if (cap > 48 * 1024) cap = 48 * 1024;
-    const int stage = ((uintptr_t)d_buf & 15) == 0 && !force_global;
-    const char* e3 = getenv("LP_LDS_PAD");  // profiling experiments: extra LDS per wave (lower occupancy)
-    const size_t lds = 16 * (size_t)n_elems + stk_words * 4 + cap + (masks ? MC_N * (cap / 8) : 0) +
-                       (e3 ? (size_t)atoi(e3) : 0);
-    if (masks)
-        hipLaunchKernelGGL(k_parse_lines<true>, dim3((unsigned)waves), dim3(PW), lds, s, d_buf, nbytes, n_lines, d_args,
-                           (uint32_t)cap, stage, stk_words, mode);
-    else
-        hipLaunchKernelGGL(k_parse_lines<false>, dim3((unsigned)waves), dim3(PW), lds, s, d_buf, nbytes, n_lines,
-                           d_args, (uint32_t)cap, stage, stk_words, mode);
-    if (mode == PM_MATCH) return hipGetLastError() == hipSuccess ? 0 : -1;
+int launch_route(const DeviceArgs* d_args, int64_t cap_lines, hipStream_t s) {
+    const int64_t nc = fmt_chunks(cap_lines);
+    if (nc == 0) return 0;
+    hipLaunchKernelGGL(k_fmt_reduce, dim3((unsigned)nc), dim3(PW), 0, s, d_args);
+    hipLaunchKernelGGL(k_fmt_chunks, dim3(1), dim3(1), 0, s, d_args);
+    hipLaunchKernelGGL(k_fmt_apply, dim3((unsigned)nc), dim3(PW), 0, s, d_args);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_parse(const ParseLaunch& a, const DeviceArgs* d_args, const uint32_t* d_wave_counts, Meta* d_meta,
+                 hipStream_t s) {
+    const int64_t waves = parse_waves(a.cap_lines);
+    if (waves == 0) return 0;
+    const WindowPlan w = window_plan(a);
+    hipLaunchKernelGGL(k_parse_lines, dim3((unsigned)waves), dim3(PW), w.lds, s, a.buf, a.nbytes, d_args, w.cap,
+                       w.stk_words);
+    // the queued waves (windows larger than LDS): persistent grid, a few
+    // waves per CU, each wave's LDS only the elements and the DFS stack
+    const size_t lds_direct = 16 * (size_t)a.n_elems + 4 * (size_t)w.stk_words;
+    int64_t grid = waves < 2048 ? waves : 2048;
+    hipLaunchKernelGGL(k_parse_direct, dim3((unsigned)grid), dim3(PW), lds_direct, s, a.buf, a.nbytes, d_args);
     int64_t rb = (waves + 255) / 256;
     if (rb > 1024) rb = 1024;
-    hipLaunchKernelGGL(k_reduce_counts, dim3((unsigned)rb), dim3(256), 0, s, d_wave_counts, waves, counters);
+    hipLaunchKernelGGL(k_reduce_counts, dim3((unsigned)rb), dim3(256), 0, s, d_wave_counts, d_meta);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -88,20 +88,16 @@ __device__ LP_INLINE uint32_t load_word(const LP_G uint8_t* p) {
 // built once per LDS window by the staging pass of the parse kernel, so the
 // per-line scanners walk 64 bytes per step instead of 4.  Exact for TAB and
 // printable ASCII (every other byte sends its line to FALLBACK before any
-// scanner runs).
-#if LP_EXP == 4  // experiment: no QUOTE class (less LDS per wave); quotes found by SWAR scans
-enum : int {
-    MC_QUOTE = -1,
-    MC_UEV = 0,
-    MC_N = 1
-};
-#else
+// scanner runs).  Three classes in two bit planes (QUOTE and WS are disjoint
+// subsets of UEV): P0 = UEV minus WS, P1 = UEV minus QUOTE, so QUOTE =
+// P0 & ~P1, WS = P1 & ~P0, UEV = P0 | P1.  The planes of 64-byte block w are
+// the 16 bytes at 16 w (one 128-bit LDS read).
 enum : int {
     MC_QUOTE = 0,  // '"'
     MC_UEV = 1,    // URI events: % # & ? ; + and the bytes URIUtil.encode escapes (not '=', not A-Z)
-    MC_N = 2
+    MC_WS = 2,     // \s of a line that passed the guard: ' ' and TAB
+    MC_N = 2       // bit planes
 };
-#endif
 __host__ __device__ LP_INLINE uint64_t mask_load(const uint64_t* p) { return *p; }
 #if defined(__HIP__)
 typedef const __attribute__((address_space(3))) uint64_t* lds_u64;
@@ -114,8 +110,7 @@ struct LineT {
     Ptr b;
     uint32_t o;
     int n;
-    MPtr m = MPtr{};       // class c, 64-byte block w of b: m[c * ms + w]
-    uint32_t ms = 0;
+    MPtr m = MPtr{};       // planes of the 64-byte block w of b: m[2 w], m[2 w + 1]
     static constexpr bool has_masks = !std::is_same<MPtr, NoMasks>::value;
     __host__ __device__ LP_INLINE uint32_t operator[](int i) const { return b[o + i]; }
     // aligned 32-bit word w of the base (little-endian: byte k at bits 8k..8k+7)
@@ -125,7 +120,10 @@ struct LineT {
     __host__ __device__ LP_INLINE uint32_t word_or0(uint32_t w) const {
         return 4 * w < o + (uint32_t)n ? load_word(b + 4 * w) : 0u;
     }
-    __host__ __device__ LP_INLINE uint64_t mask(int c, uint32_t w) const { return mask_load(m + (c * ms + w)); }
+    __host__ __device__ LP_INLINE uint64_t mask(int c, uint32_t w) const {
+        const uint64_t p0 = mask_load(m + 2 * w), p1 = mask_load(m + 2 * w + 1);
+        return c == MC_QUOTE ? (p0 & ~p1) : c == MC_WS ? (p1 & ~p0) : (p0 | p1);
+    }
 };
 using Line = LineT<const uint8_t*>;
 using MLine = LineT<const uint8_t*, const uint64_t*>;
@@ -211,32 +209,33 @@ __host__ __device__ LP_INLINE uint32_t nonauth_bits(uint32_t w) {
 }
 // bytes with bit 7 set -> 4-bit mask (byte k -> bit k)
 __host__ __device__ LP_INLINE uint32_t nib(uint32_t hb) { return (((hb >> 7) * 0x204081u) >> 21) & 15u; }
-__host__ __device__ LP_INLINE uint32_t quote_hb(uint32_t r) { return (r << 5) & swar::HI; }
 __host__ __device__ LP_INLINE uint32_t uev_hb(uint32_t r) { return (((r & swar::LO7) + swar::LO7) | r) & swar::HI; }
-// 16 bytes (4 little-endian words) -> the 16-bit QUOTE and UEV masks
-__host__ __device__ LP_INLINE void classify16(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t& qt,
-                                              uint32_t& uev) {
+// 16 bytes (4 little-endian words) -> the 16-bit masks of the two planes
+// (P0: a class bit other than ' ' / TAB, P1: a class bit other than '"')
+__host__ __device__ LP_INLINE void classify16(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t& p0,
+                                              uint32_t& p1) {
     const uint32_t r0 = bits(w0), r1 = bits(w1), r2 = bits(w2), r3 = bits(w3);
-    qt = nib(quote_hb(r0)) | (nib(quote_hb(r1)) << 4) | (nib(quote_hb(r2)) << 8) | (nib(quote_hb(r3)) << 12);
-    uev = nib(uev_hb(r0)) | (nib(uev_hb(r1)) << 4) | (nib(uev_hb(r2)) << 8) | (nib(uev_hb(r3)) << 12);
+    constexpr uint32_t NW = 0xFCFCFCFCu, NQ = 0xFBFBFBFBu;
+    p0 = nib(uev_hb(r0 & NW)) | (nib(uev_hb(r1 & NW)) << 4) | (nib(uev_hb(r2 & NW)) << 8) | (nib(uev_hb(r3 & NW)) << 12);
+    p1 = nib(uev_hb(r0 & NQ)) | (nib(uev_hb(r1 & NQ)) << 4) | (nib(uev_hb(r2 & NQ)) << 8) | (nib(uev_hb(r3 & NQ)) << 12);
 }
 // mask class whose members are exactly the byte c, -1 none
-__host__ __device__ LP_INLINE int class_of(uint32_t c) { return c == '"' && MC_QUOTE >= 0 ? (int)MC_QUOTE : -1; }
+__host__ __device__ LP_INLINE int class_of(uint32_t c) { return c == '"' ? (int)MC_QUOTE : -1; }
 }  // namespace bcls
 
-// Host builder of the class masks of buf[0, n) (n a multiple of 16), the same
+// Host builder of the class masks of buf[0, n) (n a multiple of 64), the same
 // computation the kernel's staging pass does; used by the test-only CPU
-// emulation.  masks: MC_N arrays of ms 64-bit words.
-inline void build_masks(const uint8_t* buf, uint32_t n, uint64_t* masks, uint32_t ms) {
-    for (uint32_t i = 0; i < MC_N * ms; ++i) masks[i] = 0;
+// emulation.  masks: 2 x n / 64 words (the planes of each 64-byte block).
+inline void build_masks(const uint8_t* buf, uint32_t n, uint64_t* masks) {
+    for (uint32_t i = 0; i < MC_N * (n / 64); ++i) masks[i] = 0;
     for (uint32_t k = 0; 16 * k < n; ++k) {
         uint32_t w[4];
         for (int j = 0; j < 4; ++j) __builtin_memcpy(&w[j], buf + 16 * k + 4 * j, 4);
         uint32_t a, b;
         bcls::classify16(w[0], w[1], w[2], w[3], a, b);
         const int sh = 16 * (k & 3);
-        if (MC_QUOTE >= 0) masks[MC_QUOTE * ms + (k >> 2)] |= (uint64_t)a << sh;
-        masks[MC_UEV * ms + (k >> 2)] |= (uint64_t)b << sh;
+        masks[2 * (k >> 2)] |= (uint64_t)a << sh;
+        masks[2 * (k >> 2) + 1] |= (uint64_t)b << sh;
     }
 }
 
@@ -450,10 +449,11 @@ __host__ __device__ LP_INLINE uint32_t count_uev(const LN& L, int a, int b) {
     return c;
 }
 
-// First \s in [from, to), else `to`.
+// First \s in [from, to), else `to` (lines with masks: the WS class).
 template <typename LN>
 __host__ __device__ LP_INLINE int find_ws(const LN& L, int from, int to) {
-    return find_fwd(L, from, to, [](uint32_t w) { return swar::ws(w); });
+    if constexpr (LN::has_masks) return mfind_fwd(L, MC_WS, from, to);
+    else return find_fwd(L, from, to, [](uint32_t w) { return swar::ws(w); });
 }
 
 // The 4 bytes at line position p as one little-endian word (bytes past the
@@ -526,7 +526,7 @@ struct RegArr {
 // at pos.  Literals of up to 4 bytes compare against e.lit4 (no Program
 // memory reads inside the scanners).
 template <typename LN>
-__host__ __device__ LP_INLINE bool lit_at(const Program& P, const LN& L, int pos, const Elem& e) {
+__host__ __device__ LP_INLINE bool lit_at(const Program& P, const LN& L, int pos, const ElemV& e) {
     const int len = e.lit_len;
     if (pos + len > L.n) return false;
     if (len <= 4) {
@@ -534,7 +534,7 @@ __host__ __device__ LP_INLINE bool lit_at(const Program& P, const LN& L, int pos
         return ((load_u32_at(L, pos) ^ e.lit4) & keep) == 0;
     }
     for (int k = 0; k < len; ++k)
-        if (L[pos + k] != P.lit[e.lit_off + k]) return false;
+        if (L[pos + k] != P.lit_byte(e.lit_off + k)) return false;
     return true;
 }
 
@@ -580,7 +580,7 @@ __host__ __device__ LP_INLINE int ipv4_first(const LN& L, int p) {
 template <typename LN>
 __host__ __device__ LP_INLINE int kth_from_end(const LN& L, uint32_t c, int k, int lo) {
     if constexpr (LN::has_masks) {
-        if (MC_QUOTE >= 0 && c == '"') {  // exact class: count set bits of the QUOTE mask backwards
+        if (c == '"') {  // exact class: count set bits of the QUOTE mask backwards
             if (L.n - 1 < lo) return -1;
             const uint32_t A = L.o + (uint32_t)L.n - 1, S = L.o + (uint32_t)lo;
             uint32_t W = A >> 6;
@@ -610,20 +610,20 @@ __host__ __device__ LP_INLINE int kth_from_end(const LN& L, uint32_t c, int k, i
 // Candidate starts of e's following literal: positions of its first byte,
 // through the mask class holding that byte (e.acls) when the line has masks.
 template <typename LN>
-__host__ __device__ LP_INLINE int anchor_bwd(const LN& L, const Elem& e, int hi, int lo) {
+__host__ __device__ LP_INLINE int anchor_bwd(const LN& L, const ElemV& e, int hi, int lo) {
     const uint32_t c0 = e.lit4 & 0xFFu;
     if constexpr (LN::has_masks) {
-        if (MC_QUOTE >= 0 && e.acls >= 0) {
+        if (e.acls >= 0) {
             return mfind_bwd(L, e.acls, hi, lo);  // exact class
         }
     }
     return find_bwd(L, hi, lo, [c0](uint32_t w) { return swar::eq(w, c0); });
 }
 template <typename LN>
-__host__ __device__ LP_INLINE int anchor_fwd(const LN& L, const Elem& e, int lo, int to) {
+__host__ __device__ LP_INLINE int anchor_fwd(const LN& L, const ElemV& e, int lo, int to) {
     const uint32_t c0 = e.lit4 & 0xFFu;
     if constexpr (LN::has_masks) {
-        if (MC_QUOTE >= 0 && e.acls >= 0) {
+        if (e.acls >= 0) {
             return mfind_fwd(L, e.acls, lo, to);  // exact class
         }
     }
@@ -633,7 +633,7 @@ __host__ __device__ LP_INLINE int anchor_fwd(const LN& L, const Elem& e, int lo,
 // Occurrence of e's following literal: the last one starting in [lo, hi]
 // (greedy order) or the first one starting in [lo, hi] (lazy order); -1 none.
 template <typename LN>
-__host__ __device__ LP_INLINE int lit_last(const Program& P, const LN& L, const Elem& e, int hi, int lo) {
+__host__ __device__ LP_INLINE int lit_last(const Program& P, const LN& L, const ElemV& e, int hi, int lo) {
     for (int q = hi;;) {
         q = anchor_bwd(L, e, q, lo);
         if (q < 0) return -1;
@@ -642,7 +642,7 @@ __host__ __device__ LP_INLINE int lit_last(const Program& P, const LN& L, const 
     }
 }
 template <typename LN>
-__host__ __device__ LP_INLINE int lit_first(const Program& P, const LN& L, const Elem& e, int lo, int hi) {
+__host__ __device__ LP_INLINE int lit_first(const Program& P, const LN& L, const ElemV& e, int lo, int hi) {
     for (int q = lo;;) {
         q = anchor_fwd(L, e, q, hi + 1);
         if (q > hi) return -1;
@@ -722,7 +722,7 @@ __host__ __device__ LP_INLINE int uplist_prev_end(const LN& L, int p, int cur, b
 // order), -1 = none, -2 = FALLBACK.  '.' runs to the end of the line: the
 // fast-path guard already rejected every line terminator.
 template <typename LN>
-__host__ __device__ LP_INLINE int cand_first(const Program& P, const Elem& e, const LN& L, int p) {
+__host__ __device__ LP_INLINE int cand_first(const Program& P, const ElemV& e, const LN& L, int p) {
     switch (e.kind) {
     case EK_NOSPACE: return find_ws(L, p, L.n);
     case EK_NUMBER: { int q = find_fwd(L, p, L.n, [](uint32_t w) { return ~swar::digit(w) & swar::HI; }); return q > p ? q : -1; }
@@ -795,7 +795,7 @@ __host__ __device__ LP_INLINE int cand_first(const Program& P, const Elem& e, co
 // ip_alt_ends: the same ends as a bit set (bit k = end p + k); returns
 // whether there is any.
 template <typename LN>
-__host__ __device__ LP_INLINE bool ip_alt_ends(const Program& P, const LN& L, const Elem& e, int p, int cur,
+__host__ __device__ LP_INLINE bool ip_alt_ends(const Program& P, const LN& L, const ElemV& e, int p, int cur,
                                                uint32_t* ends) {
     constexpr int W = 96;
     uint32_t cur_set[3] = {1u, 0u, 0u}, all[3];
@@ -842,14 +842,14 @@ __host__ __device__ LP_INLINE bool ip_alt_ends(const Program& P, const LN& L, co
 }
 
 template <typename LN>
-__host__ __device__ LP_INLINE bool ip_alt_end_possible(const Program& P, const LN& L, const Elem& e, int p, int cur) {
+__host__ __device__ LP_INLINE bool ip_alt_end_possible(const Program& P, const LN& L, const ElemV& e, int p, int cur) {
     uint32_t ends[3];
     return ip_alt_ends(P, L, e, p, cur, ends);
 }
 
 // Next candidate after 'cur' (same priority order).
 template <typename LN>
-__host__ __device__ LP_INLINE int cand_next(const Program& P, const Elem& e, const LN& L, int p, int cur) {
+__host__ __device__ LP_INLINE int cand_next(const Program& P, const ElemV& e, const LN& L, int p, int cur) {
     switch (e.kind) {
     case EK_NOSPACE: return cur - 1 >= p ? cur - 1 : -1;
     case EK_NUMBER: case EK_HEXNUMBER: case EK_NONZERO: return cur - 1 >= p + 1 ? cur - 1 : -1;
@@ -922,7 +922,7 @@ __host__ __device__ LP_INLINE int match_line(const Program& P, const EL& elems, 
         if constexpr (Nested) {
             return -2;
         } else {
-            const Elem& e = elems[j];
+            const ElemV e = load_elem(elems + j);
             if (e.kind != EK_IP && e.kind != EK_CLF_IP) return -2;
             uint32_t ends[3];
             ip_alt_ends(P, L, e, p, cur, ends);
@@ -944,7 +944,7 @@ __host__ __device__ LP_INLINE int match_line(const Program& P, const EL& elems, 
             if (pos == L.n) return ST_OK;
             ok = false;
         } else {
-            const Elem e = elems[i];
+            const ElemV e = load_elem(elems + i);
             if (e.kind == EK_LIT) {
                 ok = lit_at(P, L, pos, e);
                 if (ok) { pos += e.lit_len; ++i; continue; }
@@ -970,7 +970,7 @@ __host__ __device__ LP_INLINE int match_line(const Program& P, const EL& elems, 
             if (sp == sp0) return ST_BAD;
             uint32_t top = stk[sp - 1];
             int j = top & 63, p = (top >> 6) & 8191, cur = (top >> 19) & 8191;
-            const Elem e = elems[j];
+            const ElemV e = load_elem(elems + j);
             int c = cand_next(P, e, L, p, cur);
             if (c == -2) c = ip_resolve(j, p, cur, sp);
             if (c == -2) return ST_FALLBACK;
@@ -996,7 +996,7 @@ __host__ __device__ LP_INLINE bool match_first_leaf(const Program& P, const LN& 
     bool ok = true;
     const int ne = P.n_elems;
     for (int i = 0; i < ne; ++i) {
-        const Elem e = P.elems[i];
+        const ElemV e = load_elem(P.elems + i);
         if (e.kind == EK_LIT) {
             ok = ok && lit_at(P, L, pos, e);
             pos += e.lit_len;
@@ -1023,7 +1023,7 @@ __host__ __device__ LP_INLINE int count_quotes(const LN& L) {
     const uint32_t a = L.o, b = L.o + (uint32_t)L.n - 1;
     int cnt = 0;
     if constexpr (LN::has_masks) {
-        if (MC_QUOTE >= 0) {  // popcount of the QUOTE mask, 64 bytes per step
+        {  // popcount of the QUOTE mask, 64 bytes per step
             for (uint32_t W = a >> 6; W <= b >> 6; ++W) {
                 uint64_t m = L.mask(MC_QUOTE, W);
                 if (W == a >> 6) m &= ~0ull << (a & 63);
@@ -1050,7 +1050,7 @@ template <typename LN, typename EL>
 __host__ __device__ LP_INLINE bool fmt_tail_ok(const Program& P, const EL& elems, int ne, const LN& L) {
     int q = L.n;
     for (int i = ne - 1; i >= 0; --i) {
-        const Elem e = elems[i];
+        const ElemV e = load_elem(elems + i);
         if (e.kind == EK_LIT) {
             q -= e.lit_len;
             if (q < 0 || !lit_at(P, L, q, e)) return false;
@@ -1348,10 +1348,16 @@ struct LineOut {
     uint32_t arena_need;
 };
 
-// Last ' ' in [lo, hi], else -1.
+// Last ' ' in [lo, hi], else -1 (lines with masks: the WS class, skipping TABs).
 template <typename LN>
 __host__ __device__ LP_INLINE int find_space_bwd(const LN& L, int hi, int lo) {
-    return find_bwd(L, hi, lo, [](uint32_t w) { return swar::eq(w, ' '); });
+    if constexpr (LN::has_masks) {
+        int q = mfind_bwd(L, MC_WS, hi, lo);
+        while (q >= 0 && L[q] != ' ') q = mfind_bwd(L, MC_WS, q - 1, lo);
+        return q;
+    } else {
+        return find_bwd(L, hi, lo, [](uint32_t w) { return swar::eq(w, ' '); });
+    }
 }
 
 template <typename LN>
@@ -1426,18 +1432,31 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
     LP_PROF(4);
     if (st != ST_OK) { o.status = st; return; }
     // decodeExtractedValue: "-" -> null (Apache: ApacheHttpdLogFormatDissector.java:169-196,
-    // NGINX: NginxHttpdLogFormatDissector.java:107-119)
-    for (int k = 0; k < P.n_tok; ++k) {
-        const uint32_t sp = o.caps.get(k);
-        int a = sp & 0xFFFF, b = sp >> 16;
-        if (b - a == 1 && L[a] == '-') o.tok_flags |= 1u << k;
-        if (b - a == 1 && L[a] == '0') o.tok_flags |= 1u << (16 + k);
-        if (P.fmt_apache[fmt] && b - a >= 15 && value_is_header_name(L, a, b)) {
+    // NGINX: NginxHttpdLogFormatDissector.java:107-119).  Slots unrolled (the
+    // spans stay in registers); only one-byte values are read.
+    {
+        const bool apache = P.fmt_apache[fmt] != 0;
+        bool fb = false;
+        uint32_t flags = 0;
+        o.caps.each([&](int k, uint32_t sp) {
+            if (k >= P.n_tok) return;
+            const int a = sp & 0xFFFF, b = sp >> 16;
+            if (b - a == 1) {
+                const uint32_t c = L[a];
+                flags |= (c == '-' ? 1u << k : 0u) | (c == '0' ? 1u << (16 + k) : 0u);
+            }
             // the reference tests the VALUE (not the token name) against
             // "request.firstline" / "request.header." / "response.header." and
             // then unescapes \xhh sequences (ApacheHttpdLogFormatDissector.java:189-193)
-            if (find_fwd(L, a, b, [](uint32_t w) { return swar::eq(w, '\\'); }) < b) { o.status = ST_FALLBACK; return; }
-        }
+            if (apache && b - a >= 15) {
+                const uint32_t w = load_u32_at(L, a);
+                if ((w == 0x75716572u /* "requ" */ || w == 0x70736572u /* "resp" */) && value_is_header_name(L, a, b) &&
+                    find_fwd(L, a, b, [](uint32_t x) { return swar::eq(x, '\\'); }) < b)
+                    fb = true;
+            }
+        });
+        o.tok_flags = flags;
+        if (fb) { o.status = ST_FALLBACK; return; }
     }
     LP_PROF(5);
     // TimeStampDissector
@@ -1472,8 +1491,12 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
         const uint32_t sp0 = o.caps.get(k);
         int a = sp0 & 0xFFFF, b = sp0 >> 16;
         if (b <= a) continue;                                 // empty
-        int q = a;
-        while (q < b && (is_alpha(L[q]) || L[q] == '-' || L[q] == '_')) ++q;
+        // method [a-zA-Z-_]+ (SWAR scan for the first other byte)
+        const int q = find_fwd(L, a, b, [](uint32_t w) {
+            const uint32_t l = w | 0x20202020u;
+            const uint32_t alpha = swar::ge(l, 'a') & swar::lt(l, 'z' + 1) & ~(w & swar::HI);
+            return ~(alpha | swar::eq(w, '-') | swar::eq(w, '_')) & swar::HI;
+        });
         if (q == a || q >= b || L[q] != ' ') continue;        // neither regex matches
         o.fl_method.set(f, mkspan(a, q));
         int us = q + 1;
@@ -1481,14 +1504,11 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
         int sp = find_space_bwd(L, b - 1, us);
         if (sp < 0) sp = us - 1;
         bool full = false;
-        if (sp >= us && b - sp >= 9 && L[sp + 1] == 'H' && L[sp + 2] == 'T' && L[sp + 3] == 'T' && L[sp + 4] == 'P' &&
-            L[sp + 5] == '/') {
-            int r = sp + 6, d1 = r;
-            while (r < b && is_digit(L[r])) ++r;
+        if (sp >= us && b - sp >= 9 && load_u32_at(L, sp + 1) == 0x50545448u /* "HTTP" */ && L[sp + 5] == '/') {
+            const int d1 = sp + 6, r = digits_end(L, d1);
             if (r > d1 && r < b && L[r] == '.') {
-                int d2 = ++r;
-                while (r < b && is_digit(L[r])) ++r;
-                full = r == b && r > d2;
+                const int d2 = r + 1, r2 = digits_end(L, d2);
+                full = r2 >= b && b > d2;  // digits up to the end of the value
             }
         }
         if (full) {
@@ -1508,10 +1528,12 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
         int a, b;
         if (P.uri[u].fmt != fmt || !uri_source(P, o, u, a, b)) continue;
         // URIUtil-escaped bytes and '&'/'?' separators are both URI event
-        // bytes: their count bounds both
+        // bytes: their count bounds both.  A URI without event bytes writes
+        // nothing to the arena (no query table, no decoded or rewritten part).
         const uint32_t ev = count_uev(L, a, b);
         const uint32_t enc = ev, sep = ev;
         o.usep.set(u, sep);
+        if (ev == 0) continue;
         const UriStage& U = P.uri[u];
         uint32_t ulen = (uint32_t)(b - a), tl = ulen + 2 * enc + 2;
         uint32_t n = 16;
@@ -1798,7 +1820,7 @@ __host__ __device__ LP_INLINE uint32_t query_piece(const Program& P, const Query
         bool same = true;
         for (uint32_t q = 0; q < nlen && same; ++q) {
             const uint32_t c = rw ? (uint32_t)region[ref_off(nref) + q] : L[s + (int)q];
-            same = c == P.lit[Q.name_off[k] + q];
+            same = c == P.lit_byte((int)(Q.name_off[k] + q));
         }
         want = same;
     }

@@ -69,7 +69,7 @@ enum ElemKind : uint8_t {
     EK_UPLIST_NUM,   // X(?: *, *X(?: *: *X)?)*, X = [0-9]+            (upstream byte lists)
 };
 
-struct Elem {
+struct alignas(16) Elem {
     uint8_t kind;
     uint8_t det;       // only the first candidate can lead to an overall match
     int8_t cap;        // captured token slot, -1 = non-capturing (?:...)
@@ -83,6 +83,31 @@ struct Elem {
     uint32_t lit4;     // first (up to) 4 bytes of that literal, little-endian
 };
 
+// An element in registers.  Device code reads an Elem as four dwords (one
+// s_load_dwordx4 / ds_read_b128) and decodes the fields: a byte field read
+// directly would be a per-lane global byte load with a full memory wait.
+struct ElemV {
+    int kind, det, cap, last, lit_off, lit_len, nlit, need, acls;
+    uint32_t lit4;
+};
+template <typename P>
+__host__ __device__ inline ElemV load_elem(P p) {
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(p);
+    const uint32_t a = w[0], b = w[1], c = w[2];
+    ElemV e;
+    e.kind = (int)(a & 0xFFu);
+    e.det = (int)((a >> 8) & 0xFFu);
+    e.cap = (int)(int8_t)(uint8_t)(a >> 16);
+    e.last = (int)(a >> 24);
+    e.lit_off = (int)(b & 0xFFFFu);
+    e.lit_len = (int)(b >> 16);
+    e.nlit = (int)(c & 0xFFu);
+    e.need = (int)((c >> 8) & 0xFFu);
+    e.acls = (int)(int8_t)(uint8_t)(c >> 16);
+    e.lit4 = w[3];
+    return e;
+}
+
 // TimeStampDissector on a TIME.STAMP token (dd/MMM/yyyy:HH:mm:ss ZZ,
 // hp/dissectors/TimeStampDissector.java:46, 404-564).
 // TimeStampDissector on a TIME.STAMP token (TK_APACHE: the fixed
@@ -95,44 +120,44 @@ struct Elem {
 enum : uint8_t { TK_APACHE = 0, TK_STRF = 1 };
 enum : uint8_t { SF_LIT, SF_DAY, SF_MON, SF_MONTXT, SF_YEAR, SF_CLOCKH, SF_HOD, SF_MIN, SF_SEC, SF_MSEC, SF_USEC, SF_OFF };
 constexpr int MAX_SF_OPS = 32;
+// Stage structs hold 32-bit fields only: the kernels read them with scalar
+// (dword) loads.
 struct TimeStage {
-    int8_t tok;
-    int8_t fmt;     // the LogFormat whose token this is
-    uint8_t kind;   // TK_*
-    uint8_t width;  // TK_STRF: exact byte length of the value
-    uint8_t n_ops;
-    uint8_t op[MAX_SF_OPS], off[MAX_SF_OPS], ch[MAX_SF_OPS];  // ch: SF_LIT byte
+    int32_t tok;
+    int32_t fmt;     // the LogFormat whose token this is
+    int32_t kind;    // TK_*
+    int32_t width;   // TK_STRF: exact byte length of the value
+    int32_t n_ops;
+    uint32_t op[MAX_SF_OPS], off[MAX_SF_OPS], ch[MAX_SF_OPS];  // ch: SF_LIT byte
 };
 
 // HttpFirstLineDissector on an HTTP.FIRSTLINE token
 // (hp/dissectors/HttpFirstLineDissector.java:56-134).
 struct FlStage {
-    int8_t tok;
-    int8_t fmt;
-    uint8_t pad[2];
+    int32_t tok;
+    int32_t fmt;
 };
 
 // HttpUriDissector (hp/dissectors/HttpUriDissector.java:130-233) on either a
 // token (e.g. request.referer) or the uri of a first-line stage.
 struct UriStage {
-    int8_t src_tok;     // >= 0: token slot
-    int8_t src_fl;      // >= 0: first-line stage (its uri)
-    uint8_t want_query; // rawQuery needed (delivered or dissected further)
-    uint8_t want_path;
-    uint8_t want_ref;
-    uint8_t want_userinfo;
-    int8_t query_stage; // QueryStringFieldDissector on its query, -1 none
-    int8_t fmt;         // the LogFormat of its source token
+    int32_t src_tok;     // >= 0: token slot
+    int32_t src_fl;      // >= 0: first-line stage (its uri)
+    int32_t want_query;  // rawQuery needed (delivered or dissected further)
+    int32_t want_path;
+    int32_t want_ref;
+    int32_t want_userinfo;
+    int32_t query_stage; // QueryStringFieldDissector on its query, -1 none
+    int32_t fmt;         // the LogFormat of its source token
 };
 
 // QueryStringFieldDissector (hp/dissectors/QueryStringFieldDissector.java:56-108)
 struct QueryStage {
-    int8_t uri;
-    uint8_t want_all;       // "*" requested
-    uint8_t n_names;        // explicitly requested (lower-case) names
-    uint8_t pad;
-    uint16_t name_off[MAX_QNAMES];  // into lit pool
-    uint8_t name_len[MAX_QNAMES];
+    int32_t uri;
+    int32_t want_all;       // "*" requested
+    int32_t n_names;        // explicitly requested (lower-case) names
+    uint32_t name_off[MAX_QNAMES];  // into lit pool
+    uint32_t name_len[MAX_QNAMES];
 };
 
 // Stages (time / first line / URI) belong to one LogFormat: a line runs the
@@ -144,15 +169,20 @@ struct Program {
     int32_t n_time, n_fl, n_uri, n_query;
     int32_t n_fmt;        // LogFormats; > 1: HttpdLogFormatDissector sticky routing
     int32_t max_stack;    // DFS depth bound = number of non-deterministic elements (<= MAX_STACK)
-    uint8_t fmt_elem0[MAX_FMT + 1];  // elements of format f: [fmt_elem0[f], fmt_elem0[f + 1])
-    uint8_t fmt_apache[MAX_FMT];     // 1 = Apache decodeExtractedValue rules, 0 = NGINX
-    uint8_t fmt_quotes[MAX_FMT];     // '"' bytes in format f's literals (a line needs at least as many)
+    int32_t fmt_elem0[MAX_FMT + 1];  // elements of format f: [fmt_elem0[f], fmt_elem0[f + 1])
+    int32_t fmt_apache[MAX_FMT];     // 1 = Apache decodeExtractedValue rules, 0 = NGINX
+    int32_t fmt_quotes[MAX_FMT];     // '"' bytes in format f's literals (a line needs at least as many)
+    int32_t pad_[2];
     Elem elems[MAX_ELEMS];
     TimeStage time[MAX_TIME];
     FlStage fl[MAX_FL];
     UriStage uri[MAX_URI];
     QueryStage query[MAX_QUERY];
-    uint8_t lit[MAX_LIT];
+    alignas(4) uint8_t lit[MAX_LIT];
+    // literal pool byte i, read as a dword (scalar load for a uniform index)
+    __host__ __device__ uint32_t lit_byte(int i) const {
+        return (reinterpret_cast<const uint32_t*>(lit)[i >> 2] >> (8 * (i & 3))) & 0xFFu;
+    }
 };
 
 // Packed calendar fields (TimeStampDissector "as parsed" / "_utc" groups)
@@ -209,6 +239,19 @@ enum : uint32_t {
 #define LP_G
 #endif
 
+// Per-batch device bookkeeping (one block per handle, zeroed before each batch).
+constexpr int ARENA_SHARDS = 64;  // arena bump pointers, each owning 1/64 of the arena
+struct Meta {
+    unsigned long long counters[8];  // lines, ok, bad, fallback, arena bytes written
+    unsigned long long n_lines;      // lines of the batch (the line index's count)
+    unsigned long long cap_ovf;      // 1: more lines than the columns hold (nothing parsed, retry)
+    unsigned long long ovf_waves;    // waves queued for the direct (HBM) parse kernel
+    unsigned long long arena_ovf;    // lines whose arena allocation did not fit its shard (retry)
+    unsigned long long fmt_state;    // routed LogFormat after the batch's last line
+    unsigned long long pad[3];
+    unsigned long long shard_top[ARENA_SHARDS * 16];  // bump pointer of shard s at [16 s] (own 128-B line)
+};
+
 struct Columns {
     LP_G uint8_t* status;          // [n]
     const LP_G uint64_t* line_off; // [n+1]
@@ -238,9 +281,11 @@ struct Columns {
     LP_G uint64_t* fmt_chunk;          // per chunk of FMT_CHUNK lines: composed transition table, then entry state
     uint32_t fmt_init;                 // routing state before the first line (the handle's state)
     LP_G uint8_t* arena;
-    uint64_t arena_cap;
-    LP_G unsigned long long* arena_top;  // bump pointer
-    LP_G uint32_t* wave_counts;          // [n_waves][4] lines ok bad fallback (reduced after the launch)
+    uint64_t shard_cap;                  // arena bytes per shard (ARENA_SHARDS shards)
+    LP_G Meta* meta;
+    LP_G uint32_t* ovf_list;             // waves for the direct parse kernel
+    LP_G uint32_t* wave_counts;          // [n_waves][WC_WORDS] lines ok bad fallback written (reduced after the launch)
+    int64_t cap_lines;                   // lines the columns hold
 };
 
 }  // namespace lp

@@ -1358,7 +1358,7 @@ std::string Plan::describe() const {
 
 // ================================================================ replay
 struct Plan::Ctx {
-    const HostResults& R;
+    const ResultView& R;
     int64_t i;
     const uint8_t* line;
     const uint8_t* arena;
@@ -1415,7 +1415,7 @@ void Plan::emit(Ctx& c, const std::string& base, const std::string& type, const 
 }
 
 void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const MVal& v) const {
-    const HostResults& R = c.R;
+    const ResultView& R = c.R;
     const int64_t i = c.i;
     const int ok = t_origin_kind, oi = t_origin_idx;
     auto has = [&](const char* n) { return in.requested.count(n) > 0; };
@@ -1631,8 +1631,8 @@ void json_str(std::string& o, const uint8_t* p, uint32_t n) {
 }
 }  // namespace
 
-std::string Plan::record_json(const HostResults& R, int64_t i) const {
-    Ctx c{R, i, R.input.data() + R.line_off[i], R.arena.empty() ? nullptr : R.arena.data() + R.arena_base[i], {}};
+std::string Plan::record_json(const ResultView& R, int64_t i) const {
+    Ctx c{R, i, R.input + R.line_off[i], R.region(i), {}};
     // the LogFormat the line was routed to (HttpdLogFormatDissector's active format)
     const int fi = prog_.n_fmt > 1 ? R.fmt_id[i] : 0;
     t_fmt = fi;

@@ -68,26 +68,49 @@ struct MVal {
     int64_t l = 0;
 };
 
-// Host copies of one batch's results (filled by capi.cpp)
-struct HostResults {
+// Read-only view of one batch's results for the replay: the SoA columns,
+// the line index, the input bytes and the side arena, all in host memory
+// (a copy made by lp_result_copy, or the test-only emulation's vectors).
+// Column k of a stage is indexed [k][line].
+struct ResultView {
     int64_t n = 0;
-    std::vector<uint64_t> line_off;
-    std::vector<uint8_t> status;
-    std::vector<uint8_t> input;
-    std::vector<uint8_t> arena;
-    std::vector<uint64_t> arena_base;
-    std::vector<std::vector<uint32_t>> tok_span;
-    std::vector<uint32_t> tok_flags;
-    std::vector<std::vector<int64_t>> t_epoch;
-    std::vector<std::vector<uint64_t>> t_local, t_utc;
-    std::vector<std::vector<uint32_t>> t_nano;
-    std::vector<std::vector<uint32_t>> fl_kind, fl_method, fl_uri, fl_proto;
-    std::vector<std::vector<uint32_t>> u_flags;
-    std::vector<std::vector<uint64_t>> u_scheme, u_host, u_path, u_query, u_frag;
-    std::vector<std::vector<int32_t>> u_port;
-    std::vector<std::vector<uint32_t>> q_count;
-    std::vector<std::vector<uint64_t>> q_params;
-    std::vector<uint8_t> fmt_id;  // multi-format programs: the routed LogFormat per line
+    const uint64_t* line_off = nullptr;   // [n + 1]
+    const uint8_t* status = nullptr;
+    const uint8_t* input = nullptr;       // line i = input[line_off[i], line_off[i + 1] - 1)
+    const uint8_t* arena = nullptr;
+    const uint64_t* arena_base = nullptr; // per line: arena offset of its region
+    // arena offsets b are device offsets of ARENA_SHARDS shards of shard_cap
+    // bytes; shard s starts at arena + shard_off[s] in this view
+    uint64_t shard_cap = 0;
+    uint64_t shard_off[ARENA_SHARDS] = {};
+    const uint32_t* tok_span[MAX_TOK] = {};
+    const uint32_t* tok_flags = nullptr;
+    const int64_t* t_epoch[MAX_TIME] = {};
+    const uint64_t* t_local[MAX_TIME] = {};
+    const uint64_t* t_utc[MAX_TIME] = {};
+    const uint32_t* t_nano[MAX_TIME] = {};
+    const uint32_t* fl_kind[MAX_FL] = {};
+    const uint32_t* fl_method[MAX_FL] = {};
+    const uint32_t* fl_uri[MAX_FL] = {};
+    const uint32_t* fl_proto[MAX_FL] = {};
+    const uint32_t* u_flags[MAX_URI] = {};
+    const uint64_t* u_scheme[MAX_URI] = {};
+    const uint64_t* u_host[MAX_URI] = {};
+    const uint64_t* u_path[MAX_URI] = {};
+    const uint64_t* u_query[MAX_URI] = {};
+    const uint64_t* u_frag[MAX_URI] = {};
+    const int32_t* u_port[MAX_URI] = {};
+    const uint32_t* q_count[MAX_QUERY] = {};
+    const uint64_t* q_params[MAX_QUERY] = {};
+    const uint8_t* fmt_id = nullptr;      // multi-format programs: the routed LogFormat per line
+    // the bytes of line i's arena region
+    const uint8_t* region(int64_t i) const {
+        if (!arena) return nullptr;
+        const uint64_t b = arena_base[i];
+        if (!shard_cap) return arena + b;
+        const uint64_t s = b / shard_cap;
+        return arena + shard_off[s] + (b - s * shard_cap);
+    }
 };
 
 class Plan {
@@ -103,7 +126,7 @@ public:
     std::string describe() const;
 
     // canonical JSON record of line i (status OK)
-    std::string record_json(const HostResults& R, int64_t i) const;
+    std::string record_json(const ResultView& R, int64_t i) const;
 
 private:
     int build_dissectors(const std::string& logformats, std::string& err);

@@ -68,8 +68,20 @@ void emu_set_masks(int on) { g_masks = on; }
 
 }  // extern "C"
 
+// One line's results, stored in vectors (the emulation's columns, one row).
+struct Store {
+    std::vector<uint64_t> line_off;
+    std::vector<uint8_t> status, input, arena, fmt_id;
+    std::vector<uint64_t> arena_base;
+    std::vector<std::vector<uint32_t>> tok_span, t_nano, fl_kind, fl_method, fl_uri, fl_proto, u_flags, q_count;
+    std::vector<uint32_t> tok_flags;
+    std::vector<std::vector<int64_t>> t_epoch;
+    std::vector<std::vector<uint64_t>> t_local, t_utc, u_scheme, u_host, u_path, u_query, u_frag, q_params;
+    std::vector<std::vector<int32_t>> u_port;
+};
+
 template <typename LN>
-static int run_line(const Program& P, const LN& L, LineOut& o, uint32_t* stk, Columns& C, HostResults& R, char* out,
+static int run_line(const Program& P, const LN& L, LineOut& o, uint32_t* stk, Columns& C, Store& R, char* out,
                     int cap, uint32_t& fmt_state) {
     if (P.n_fmt > 1) {  // sticky routing, one line at a time (the kernels do it as a scan)
         const uint32_t m = fmt_match_word(P, P.elems, L, stk, false);
@@ -77,7 +89,7 @@ static int run_line(const Program& P, const LN& L, LineOut& o, uint32_t* stk, Co
         R.fmt_id.assign(1, (uint8_t)fmt_state);
     }
     phase1(P, P.elems, L, o, stk, C, 0, false, P.n_fmt > 1 ? (int)fmt_state : 0);
-    if (o.status == ST_OK && o.arena_need) {
+    if (o.status == ST_OK) {
         R.arena.assign(o.arena_need + 64, 0);
         Arena A{R.arena.data(), 0, o.arena_need};
         phase2(P, L, o, A, C, 0);
@@ -93,8 +105,7 @@ extern "C" {
 static int parse_impl(Emu* e, const char* line, int len, const uint8_t* base, uint32_t base_off, char* out, int cap) {
     if (!e->plan.device_ok()) return 2;
     const Program& P = e->plan.program();
-    HostResults R;
-    R.n = 1;
+    Store R;
     R.input.assign(line, line + len);
     R.input.push_back('\n');
     R.line_off = {0, (uint64_t)len + 1};
@@ -137,10 +148,9 @@ static int parse_impl(Emu* e, const char* line, int len, const uint8_t* base, ui
         const uint32_t wn = ((hi - lo) + 63) & ~63u;
         std::vector<uint64_t> wbuf(wn / 8 + 8, ~0ull);
         memcpy(wbuf.data(), base + lo, hi - lo);
-        const uint32_t ms = wn / 64;
-        std::vector<uint64_t> masks(MC_N * ms);
-        build_masks((const uint8_t*)wbuf.data(), wn, masks.data(), ms);
-        MLine L{(const uint8_t*)wbuf.data(), base_off - lo, len, masks.data(), ms};
+        std::vector<uint64_t> masks(MC_N * (wn / 64));
+        build_masks((const uint8_t*)wbuf.data(), wn, masks.data());
+        MLine L{(const uint8_t*)wbuf.data(), base_off - lo, len, masks.data()};
         st = run_line(P, L, o, stk, C, R, out, cap, e->fmt_state);
     } else {
         Line L{base, base_off, len};
@@ -148,7 +158,25 @@ static int parse_impl(Emu* e, const char* line, int len, const uint8_t* base, ui
     }
     if (st) return st;
     if (o.status != ST_OK) return o.status;
-    std::string js = e->plan.record_json(R, 0);
+    ResultView V;
+    V.n = 1;
+    V.line_off = R.line_off.data();
+    V.status = R.status.data();
+    V.input = R.input.data();
+    V.arena = R.arena.empty() ? nullptr : R.arena.data();
+    V.arena_base = R.arena_base.data();
+    for (int k = 0; k < MAX_TOK; ++k) V.tok_span[k] = R.tok_span[k].data();
+    V.tok_flags = R.tok_flags.data();
+    for (int t = 0; t < MAX_TIME; ++t) { V.t_epoch[t] = R.t_epoch[t].data(); V.t_local[t] = R.t_local[t].data(); V.t_utc[t] = R.t_utc[t].data(); V.t_nano[t] = R.t_nano[t].data(); }
+    for (int f = 0; f < MAX_FL; ++f) { V.fl_kind[f] = R.fl_kind[f].data(); V.fl_method[f] = R.fl_method[f].data(); V.fl_uri[f] = R.fl_uri[f].data(); V.fl_proto[f] = R.fl_proto[f].data(); }
+    for (int u = 0; u < MAX_URI; ++u) {
+        V.u_flags[u] = R.u_flags[u].data(); V.u_scheme[u] = R.u_scheme[u].data(); V.u_host[u] = R.u_host[u].data();
+        V.u_port[u] = R.u_port[u].data(); V.u_path[u] = R.u_path[u].data(); V.u_query[u] = R.u_query[u].data();
+        V.u_frag[u] = R.u_frag[u].data();
+    }
+    for (int q = 0; q < MAX_QUERY; ++q) { V.q_count[q] = R.q_count[q].data(); V.q_params[q] = R.q_params[q].data(); }
+    V.fmt_id = R.fmt_id.empty() ? nullptr : R.fmt_id.data();
+    std::string js = e->plan.record_json(V, 0);
     if ((int)js.size() + 1 > cap) return -1;
     memcpy(out, js.c_str(), js.size() + 1);
     return 0;

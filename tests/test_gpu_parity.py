@@ -167,17 +167,15 @@ def test_large_batch_properties(oracle):
 
 
 @pytest.mark.parametrize("staged", [True, False])
-def test_offsets_beyond_4gb(oracle, staged, monkeypatch):
+def test_offsets_beyond_4gb(oracle, staged):
     """A 4.4 GB batch (a 1 MB block of synthetic lines repeated on the device):
     every line OK, and lines stored past the 4 GiB mark match the oracle --
-    with the LDS-window path and with the direct-HBM path (LP_NO_STAGE=1)."""
+    with the LDS-window path and with the direct-HBM path (LP_OPT_FORCE_DIRECT)."""
     import torch
-    if not staged:
-        monkeypatch.setenv("LP_NO_STAGE", "1")
     block = lpa.synth_combined(31, 0, 4096)
     reps = 4_400_000_000 // len(block) + 1
     dev = torch.frombuffer(bytearray(block), dtype=torch.uint8).cuda().repeat(reps)
-    p = lpa.HttpdLoglineParser("combined", paths(oracle))
+    p = lpa.HttpdLoglineParser("combined", paths(oracle), force_direct=not staged)
     r = p.parse_batch(dev)
     n = 4096 * reps
     assert r.n_lines == n
@@ -307,3 +305,74 @@ def test_ip_token_variants_gpu(oracle, which):
             if s1 == oracle.OK:
                 assert r1 == r.record_json(i), (i, l)
         assert fb < len(lines) // 4, fb
+
+
+def test_bulk_results_rebuild_records(oracle):
+    """lp_result_copy hands the whole batch's SoA to the host in one call;
+    records rebuilt from that copy alone (lp_result_record_json) are byte-
+    identical to lp_line_record_json for every line of a 100 k-line batch, and
+    a 1 M-line batch's copy is consistent (line index, statuses, spans) with
+    the input, with a sample of its records equal to the oracle's."""
+    fields = paths(oracle)
+    p = lpa.HttpdLoglineParser("combined", fields)
+    data = lpa.synth_combined(20261015, 0, 100_000)
+    r = p.parse_batch(data)
+    buf, res = r.copy_to_host()
+    assert res.n_lines == 100_000 and res.on_host == 1
+    for i in range(res.n_lines):
+        assert r.record_json_from(res, i) == r.record_json(i), i
+    # 1 M lines: the bulk copy alone
+    n = 1_000_000
+    data = lpa.synth_combined(77, 0, n)
+    r = p.parse_batch(data)
+    buf, res = r.copy_to_host()
+    cols = r.columns(res)
+    assert res.n_lines == n
+    off = np.ctypeslib.as_array((ctypes_u64 * (n + 1)).from_address(res.line_off))
+    nl = np.flatnonzero(np.frombuffer(data, dtype=np.uint8) == 10)
+    assert np.array_equal(off[1:], nl + 1) and off[0] == 0
+    assert (cols[("status", 0)] == 0).all()
+    lens = (off[1:] - off[:-1] - 1).astype(np.int64)
+    for k in range(9):
+        sp = cols[("tok_span", k)].astype(np.int64)
+        assert ((sp >> 16) <= lens).all() and ((sp & 0xFFFF) <= (sp >> 16)).all()
+    o = oracle.Oracle("combined", fields)
+    lines = data.split(b"\n")
+    rng = random.Random(5)
+    for i in sorted(rng.sample(range(n), 2000)):
+        s1, js = o.parse_raw(lines[i])
+        assert s1 == 0 and js == r.record_json_from(res, i), i
+
+
+ctypes_u64 = __import__("ctypes").c_uint64
+
+
+def test_arena_overflow_retry(oracle):
+    """Query-dense (beacon-style) lines need far more arena than the first
+    batch's estimate: the shards overflow, lp_sync re-runs the batch with an
+    exact arena, and every line matches the oracle."""
+    fields = paths(oracle)
+    q = "&".join("k%d=v%%41%d+x" % (j, j) for j in range(40))
+    lines = [('10.0.0.%d - - [01/Jan/2021:00:00:%02d +0000] "GET /b?%s HTTP/1.1" 200 1 "http://h.nl/r?%s" "u"'
+              % (i % 250, i % 60, q, q)).encode() for i in range(20000)]
+    s, r = gpu_vs_oracle(oracle, "combined", fields, lines, allow_fallback=False)
+    assert s["ok"] == 20000
+
+
+def test_async_batches_and_capacity_retry(oracle):
+    """Later batches of a handle are enqueued without a line count (capacity
+    from the previous batch); a batch of much shorter lines outgrows the
+    columns and is re-run inside lp_sync; a reservation makes even the first
+    batch asynchronous.  Results equal the oracle throughout."""
+    fields = ["IP:connection.client.host", "TIME.EPOCH:request.receive.time.epoch", "HTTP.PATH:request.firstline.uri.path"]
+    o = oracle.Oracle("combined", fields)
+    long_lines = [l + b" " * 0 for l in lpa.synth_combined(3, 0, 5000).split(b"\n")[:-1]]
+    short = [b'1.2.3.4 - - [01/Jan/2021:00:00:00 +0000] "GET /%d HTTP/1.1" 200 1 "-" "u"' % i for i in range(60000)]
+    for reserve in (0, 100000):
+        p = lpa.HttpdLoglineParser("combined", fields, reserve_lines=reserve)
+        for batch in (long_lines, short, long_lines[:10], short):
+            r = p.parse_batch(b"".join(l + b"\n" for l in batch))
+            assert r.n_lines == len(batch) and r.counters["ok"] == len(batch)
+            for i in range(0, len(batch), 997):
+                s1, js = o.parse_raw(batch[i])
+                assert s1 == 0 and js == r.record_json(i)
