@@ -233,6 +233,7 @@ int enqueue(lp_handle* h, bool sync_count) {
             return LP_E_DEVICE;
         // headroom for the next batches of the stream (sized like the estimate below)
         cap = std::max<int64_t>((int64_t)(n + n / 4 + 1024), h->reserve_lines);
+        if (n) h->mean_line = (double)nbytes / (double)n;  // sizes this batch's LDS windows
     } else {
         if (!h->line_off.ensure(sizeof(uint64_t) * (size_t)(cap + 2))) return LP_E_NOMEM;
         if (lp::launch_count(h->d_buf, nbytes, d_chunk, d_nlmask, h->line_off.as<uint64_t>(), cap, d_meta, s) != 0)
@@ -322,6 +323,7 @@ int finish(lp_handle* h) {
             // request (shard tops count what was asked for, also past the end)
             ++h->retries;
             h->cap_lines = std::max<int64_t>(n, h->cap_lines);
+            if (n > 0) h->mean_line = (double)h->nbytes / (double)n;
             // the next estimate (arena_per_line x 1.25 x capacity) covers the largest shard
             if (m.arena_ovf && n > 0)
                 h->arena_per_line = std::max(h->arena_per_line, (double)(top_max + 4096) * LP_ARENA_SHARDS / (double)n);

@@ -8,8 +8,9 @@
 //                     its byte-class masks staged in LDS, LogFormat match + token / time /
 //                     first-line stages (phase 1), wave-aggregated arena allocation from a
 //                     sharded bump pointer, URI + query-string stages (phase 2); a wave whose
-//                     window does not fit LDS is queued for k_parse_direct
-//   k_parse_direct    the queued waves, reading the input from HBM (persistent grid)
+//                     window does not fit LDS is queued for k_parse_overflow
+//   k_parse_overflow  the queued waves: two staged rounds of 32 lines, or the lines read
+//                     from HBM (very long lines), on a persistent grid
 //   k_route_match     several LogFormats: which formats match each line (sticky routing pass 1)
 //   k_fmt_*           the sticky active-format scan (routing pass 2)
 //   k_reduce_counts   per-wave status counts -> the batch counters
@@ -303,17 +304,42 @@ __device__ __forceinline__ bool stage_window(const uint8_t* __restrict__ buf, ui
     return !__any(bad != 0);
 }
 
+// Status counts of a wave's lines (lines, ok, bad, arena bytes written).
+struct WaveCounts {
+    uint32_t act = 0, ok = 0, bad = 0, written = 0;
+    __device__ __forceinline__ void store(const Columns& C, int64_t wave) const {
+        if (threadIdx.x == 0) {
+            uint4 c, d;
+            c.x = act;
+            c.y = ok;
+            c.z = bad;
+            c.w = act - ok - bad;
+            d.x = written;
+            d.y = d.z = d.w = 0;
+            uint4* wc = reinterpret_cast<uint4*>(C.wave_counts + WC_WORDS * (size_t)wave);
+            wc[0] = c;
+            wc[1] = d;
+        }
+    }
+};
+
 // Per-line work of one wave: phase 1, arena allocation, phase 2, the wave's
-// query pieces spread over its lanes, the per-wave counts.
+// query pieces spread over its lanes; adds the lines' counts to WC.
 template <typename LN>
 __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, const Columns& C, const LN& L,
-                                           bool active, int64_t li, WaveStack stk, bool clean, int64_t wave) {
+                                           bool active, int64_t li, WaveStack stk, bool clean, int64_t wave,
+                                           WaveCounts& WC) {
     LineOut o;
     o.status = ST_OK;
     o.arena_need = 0;
     LP_PROF(1);
     if (active) phase1(P, elems, L, o, stk, C, li, clean, P.n_fmt > 1 ? (int)C.fmt_id[li] : 0);
     LP_PROF(9);
+#if LP_EXP == 13 || LP_EXP == 12
+    if (active) write_line(P, o, C, li);  // experiment: stop after phase 1
+    WC.act += (uint32_t)__popcll(__ballot(active));
+    return;
+#endif
     // wave-aggregated arena allocation from the wave's shard (every lane reaches this point)
     const uint32_t need = (active && o.status == ST_OK) ? o.arena_need : 0u;
     const int lane = threadIdx.x;
@@ -348,7 +374,7 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
     // QueryStringFieldDissector pieces of all lines of the wave, spread evenly
     // over the lanes (a line's pieces vary from 0 to dozens; one lane per line
     // would leave most lanes idle while the longest query finishes)
-    if (P.n_query > 0) {
+    if (P.n_query > 0 && LP_EXP != 14) {
         __syncthreads();  // the table slots written in phase 2 are visible to every lane
         const bool has = active && o.status == ST_OK && need != 0;
         const unsigned long long my_ab = has ? C.arena_base[li] : 0ull;
@@ -382,21 +408,10 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
     }
     LP_PROF(22);
     for (int d = 32; d > 0; d >>= 1) written += __shfl_xor(written, d);
-    const uint64_t m_act = __ballot(active);
-    const uint64_t m_ok = __ballot(active && o.status == ST_OK);
-    const uint64_t m_bad = __ballot(active && o.status == ST_BAD);
-    if (lane == 0) {
-        uint4 c, d;
-        c.x = (uint32_t)__popcll(m_act);
-        c.y = (uint32_t)__popcll(m_ok);
-        c.z = (uint32_t)__popcll(m_bad);
-        c.w = c.x - c.y - c.z;
-        d.x = written;
-        d.y = d.z = d.w = 0;
-        uint4* wc = reinterpret_cast<uint4*>(C.wave_counts + WC_WORDS * (size_t)wave);
-        wc[0] = c;
-        wc[1] = d;
-    }
+    WC.act += (uint32_t)__popcll(__ballot(active));
+    WC.ok += (uint32_t)__popcll(__ballot(active && o.status == ST_OK));
+    WC.bad += (uint32_t)__popcll(__ballot(active && o.status == ST_BAD));
+    WC.written += written;
 }
 
 // LDS: [elements (n_elems x 16 B)][DFS stack][byte window (win_cap, a multiple of 64)][mask planes (win_cap / 4)]
@@ -418,7 +433,7 @@ __global__ __launch_bounds__(PW) void k_parse_lines(const uint8_t* __restrict__ 
     uint8_t* win = smem + 16 * P.n_elems + stk_words * 4;
     uint16_t* msk16 = reinterpret_cast<uint16_t*>(win + win_cap);
     const WaveLines W = wave_lines(C, wave, n_lines, nbytes);
-    if (W.w1 - W.w0 > win_cap) {  // the window does not fit: k_parse_direct takes the wave
+    if (W.w1 - W.w0 > win_cap) {  // the window does not fit: k_parse_overflow takes the wave
         if (threadIdx.x == 0) C.ovf_list[atomicAdd(&C.meta->ovf_waves, 1ull)] = (uint32_t)wave;
         return;
     }
@@ -426,13 +441,22 @@ __global__ __launch_bounds__(PW) void k_parse_lines(const uint8_t* __restrict__ 
     LP_PROF(0);
     const bool clean = stage_window(buf, nbytes, W.w0, W.w1, win, msk16);
     __syncthreads();
+#if LP_EXP == 11
+    if (clean) return;  // experiment: stop after staging
+#endif
     const LineT<lds_bytes, lds_u64> L{(lds_bytes)win, (uint32_t)(W.s - W.w0), W.n, (lds_u64)reinterpret_cast<uint64_t*>(msk16)};
-    parse_wave(P, s_elems, C, L, W.active, W.li, stk, clean, wave);
+    WaveCounts WC;
+    parse_wave(P, s_elems, C, L, W.active, W.li, stk, clean, wave, WC);
+    WC.store(C, wave);
 }
 
-// The queued waves of k_parse_lines, lines read from HBM (persistent grid).
-__global__ __launch_bounds__(PW) void k_parse_direct(const uint8_t* __restrict__ buf, uint64_t nbytes,
-                                                     const DeviceArgs* __restrict__ args) {
+// The waves k_parse_lines queued (their 64 lines' window exceeds LDS), on a
+// persistent grid: two staged rounds of 32 lines (lanes 0-31, then 32-63)
+// through the same LDS window when each half fits, else the lines are read
+// from HBM directly (very long lines).
+__global__ __launch_bounds__(PW) void k_parse_overflow(const uint8_t* __restrict__ buf, uint64_t nbytes,
+                                                       const DeviceArgs* __restrict__ args, uint32_t win_cap,
+                                                       uint32_t stk_words) {
     const Program& P = args->prog;
     const Columns& C = args->cols;
     const int64_t n_lines = (int64_t)C.meta->n_lines;
@@ -440,18 +464,39 @@ __global__ __launch_bounds__(PW) void k_parse_direct(const uint8_t* __restrict__
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     Elem* s_elems = reinterpret_cast<Elem*>(smem);
     WaveStack stk{reinterpret_cast<uint32_t*>(smem + 16 * P.n_elems) + threadIdx.x};
+    uint8_t* win = smem + 16 * P.n_elems + stk_words * 4;
+    uint16_t* msk16 = reinterpret_cast<uint16_t*>(win + win_cap);
     load_elems(P, s_elems);
     __syncthreads();
     for (uint64_t q = blockIdx.x; q < nq; q += gridDim.x) {
         const int64_t wave = C.ovf_list[q];
         const WaveLines W = wave_lines(C, wave, n_lines, nbytes);
-        // base = the line start aligned down to 4 bytes: word reads never
-        // leave the 4-byte words holding the line's bytes
-        const LP_G uint8_t* ls = (const LP_G uint8_t*)(buf) + W.s;
-        const uint32_t mis = (uint32_t)((uintptr_t)ls & 3);
-        const LineT<const LP_G uint8_t*> L{ls - mis, mis, W.n};
-        parse_wave(P, s_elems, C, L, W.active, W.li, stk, false, wave);
-        __syncthreads();
+        const int64_t mid = W.li0 + PW / 2 < W.lend ? W.li0 + PW / 2 : W.lend;
+        const uint64_t lm = C.line_off[mid];
+        const uint64_t a0 = W.w0, b0 = lm < nbytes ? lm : nbytes, a1 = lm & ~15ull, b1 = W.w1;
+        const bool two = mid < W.lend;
+        WaveCounts WC;
+        if (b0 - a0 <= win_cap && (!two || b1 - a1 <= win_cap)) {
+            for (int r = 0; r < (two ? 2 : 1); ++r) {
+                const uint64_t a = r ? a1 : a0, b = r ? b1 : b0;
+                const bool clean = stage_window(buf, nbytes, a, b, win, msk16);
+                __syncthreads();
+                const bool mine = W.active && ((int)threadIdx.x >= PW / 2) == (r != 0);
+                const LineT<lds_bytes, lds_u64> L{(lds_bytes)win, mine ? (uint32_t)(W.s - a) : 0u, mine ? W.n : 0,
+                                                  (lds_u64)reinterpret_cast<uint64_t*>(msk16)};
+                parse_wave(P, s_elems, C, L, mine, W.li, stk, clean, wave, WC);
+                __syncthreads();  // this round's LDS reads are done before the next staging
+            }
+        } else {
+            // base = the line start aligned down to 4 bytes: word reads never
+            // leave the 4-byte words holding the line's bytes
+            const LP_G uint8_t* ls = (const LP_G uint8_t*)(buf) + W.s;
+            const uint32_t mis = (uint32_t)((uintptr_t)ls & 3);
+            const LineT<const LP_G uint8_t*> L{ls - mis, mis, W.n};
+            parse_wave(P, s_elems, C, L, W.active, W.li, stk, false, wave, WC);
+            __syncthreads();
+        }
+        WC.store(C, wave);
     }
 }
 
@@ -643,7 +688,16 @@ extern "C" int lp_profile_read(unsigned long long* out, int n) {
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_prof), sizeof h) != hipSuccess) return -1;
     for (int k = 0; k < n && k < 64; ++k) { out[2 * k] = h[k * 16]; out[2 * k + 1] = h[k * 16 + 1]; }
     unsigned long long z[64 * 16] = {};
-    hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof z);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof z);
+    return 0;
+}
+// per first-leaf element: cycles, visits (and clear)
+extern "C" int lp_profile_read_elems(unsigned long long* out, int n) {
+    unsigned long long h[64 * 2];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_prof_el), sizeof h) != hipSuccess) return -1;
+    for (int k = 0; k < 2 * n && k < 128; ++k) out[k] = h[k];
+    unsigned long long z[64 * 2] = {};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_prof_el), z, sizeof z);
     return 0;
 }
 #endif
@@ -674,10 +728,10 @@ int launch_parse(const ParseLaunch& a, const DeviceArgs* d_args, const uint32_t*
     hipLaunchKernelGGL(k_parse_lines, dim3((unsigned)waves), dim3(PW), w.lds, s, a.buf, a.nbytes, d_args, w.cap,
                        w.stk_words);
     // the queued waves (windows larger than LDS): persistent grid, a few
-    // waves per CU, each wave's LDS only the elements and the DFS stack
-    const size_t lds_direct = 16 * (size_t)a.n_elems + 4 * (size_t)w.stk_words;
-    int64_t grid = waves < 2048 ? waves : 2048;
-    hipLaunchKernelGGL(k_parse_direct, dim3((unsigned)grid), dim3(PW), lds_direct, s, a.buf, a.nbytes, d_args);
+    // waves per CU (the same LDS layout as k_parse_lines)
+    const int64_t grid = waves < 1024 ? waves : 1024;
+    hipLaunchKernelGGL(k_parse_overflow, dim3((unsigned)grid), dim3(PW), w.lds, s, a.buf, a.nbytes, d_args, w.cap,
+                       w.stk_words);
     int64_t rb = (waves + 255) / 256;
     if (rb > 1024) rb = 1024;
     hipLaunchKernelGGL(k_reduce_counts, dim3((unsigned)rb), dim3(256), 0, s, d_wave_counts, d_meta);

@@ -24,6 +24,7 @@ enum : int { ST_OK = 0, ST_BAD = 1, ST_FALLBACK = 2 };
 // summed per point; differences of the sums = cycles spent between points.
 #if defined(LP_PROFILE) && defined(__HIP__)
 __device__ unsigned long long g_prof[64 * 16];
+__device__ unsigned long long g_prof_el[64 * 2];  // per first-leaf element: cycles, visits
 #endif
 #if defined(LP_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
 __device__ __forceinline__ void lp_prof_mark(int k) {
@@ -33,8 +34,20 @@ __device__ __forceinline__ void lp_prof_mark(int k) {
     if ((int)threadIdx.x % 64 == (int)__builtin_ctzll(act)) atomicAdd(&g_prof[k * 16 + 1], 1ull);
 }
 #define LP_PROF(k) lp_prof_mark(k)
+#define LP_PROF_EL_BEGIN() const unsigned long long lp_t0 = clock64()
+#define LP_PROF_EL_END(i)                                                                  \
+    do {                                                                                   \
+        const unsigned long long lp_dt = clock64() - lp_t0;                                \
+        const uint64_t lp_act = __ballot(1);                                               \
+        if ((int)threadIdx.x % 64 == (int)__builtin_ctzll(lp_act)) {                       \
+            atomicAdd(&g_prof_el[2 * (i)], lp_dt);                                         \
+            atomicAdd(&g_prof_el[2 * (i) + 1], 1ull);                                      \
+        }                                                                                  \
+    } while (0)
 #else
 #define LP_PROF(k)
+#define LP_PROF_EL_BEGIN()
+#define LP_PROF_EL_END(i)
 #endif
 // profiling experiments only (tools/build_exp.sh): 0 = the product
 #ifndef LP_EXP
@@ -794,56 +807,73 @@ __host__ __device__ LP_INLINE int cand_first(const Program& P, const ElemV& e, c
 // simulated as bit sets over the <= 83 bytes it can span.
 // ip_alt_ends: the same ends as a bit set (bit k = end p + k); returns
 // whether there is any.
+// 128-bit set in two registers (no arrays: dynamically indexed arrays go to
+// scratch memory on the GPU)
+struct Set128 {
+    uint64_t lo = 0, hi = 0;
+    __host__ __device__ LP_INLINE void add(int k) {
+        if (k < 64) lo |= 1ull << k;
+        else if (k < 128) hi |= 1ull << (k - 64);
+    }
+    __host__ __device__ LP_INLINE bool any() const { return (lo | hi) != 0; }
+    // f(k) for every member k, ascending
+    template <typename F>
+    __host__ __device__ LP_INLINE void each(F&& f) const {
+        for (uint64_t m = lo; m; m &= m - 1) f(__builtin_ctzll(m));
+        for (uint64_t m = hi; m; m &= m - 1) f(64 + __builtin_ctzll(m));
+    }
+};
+
 template <typename LN>
 __host__ __device__ LP_INLINE bool ip_alt_ends(const Program& P, const LN& L, const ElemV& e, int p, int cur,
-                                               uint32_t* ends) {
+                                               Set128& ends) {
     constexpr int W = 96;
-    uint32_t cur_set[3] = {1u, 0u, 0u}, all[3];
-    auto add = [](uint32_t* m, int k) { if (k < W) m[k >> 5] |= 1u << (k & 31); };
-    auto has = [](const uint32_t* m, int k) { return (m[k >> 5] >> (k & 31)) & 1u; };
     auto hexat = [&](int q) {
         if (q >= L.n) return false;
         const uint32_t c = L[q];
         return (c - '0' < 10u) || ((c | 32u) - 'a' < 6u);
     };
-    if (p < L.n && L[p] == ':') add(cur_set, 1);
-    // one (H{1,4}(?::|.)?) group from every position of m
-    auto groups = [&](uint32_t* m, uint32_t* acc) {
+    Set128 cur_set;
+    cur_set.add(0);
+    if (p < L.n && L[p] == ':') cur_set.add(1);
+    // one (H{1,4}(?::|.)?) group from every position of m, up to 8 times
+    auto groups = [&](Set128 m, Set128& acc) {
         for (int it = 0; it < 8; ++it) {
-            uint32_t nx[3] = {0u, 0u, 0u};
-            for (int k = 0; k < W; ++k) {
-                if (!has(m, k)) continue;
+            Set128 nx;
+            m.each([&](int k) {
                 for (int h = 1; h <= 4 && hexat(p + k + h - 1); ++h) {
-                    add(nx, k + h);
-                    if (p + k + h < L.n) add(nx, k + h + 1);  // (?::|.): any byte but a line terminator
+                    if (k + h < W) nx.add(k + h);
+                    if (p + k + h < L.n && k + h + 1 < W) nx.add(k + h + 1);  // (?::|.): any byte but a line terminator
                 }
-            }
-            if (!(nx[0] | nx[1] | nx[2])) break;
-            for (int w = 0; w < 3; ++w) { acc[w] |= nx[w]; m[w] = nx[w]; }
+            });
+            if (!nx.any()) break;
+            acc.lo |= nx.lo;
+            acc.hi |= nx.hi;
+            m = nx;
         }
     };
-    for (int w = 0; w < 3; ++w) all[w] = cur_set[w];
+    Set128 all = cur_set;
     groups(cur_set, all);
-    uint32_t mid[3] = {all[0], all[1], all[2]};
-    for (int k = 0; k < W; ++k) {
-        if (!has(all, k) || p + k >= L.n || L[p + k] != ':') continue;
-        add(mid, k + 1);
-        if (p + k + 1 < L.n && L[p + k + 1] == ':') add(mid, k + 2);
-    }
-    uint32_t fin[3] = {mid[0], mid[1], mid[2]};
+    Set128 mid = all;
+    all.each([&](int k) {
+        if (p + k >= L.n || L[p + k] != ':') return;
+        if (k + 1 < W) mid.add(k + 1);
+        if (p + k + 1 < L.n && L[p + k + 1] == ':' && k + 2 < W) mid.add(k + 2);
+    });
+    Set128 fin = mid;
     groups(mid, fin);
     bool any = false;
-    ends[0] = ends[1] = ends[2] = 0u;
-    for (int k = 0; k < W; ++k) {
-        if (!has(fin, k) || p + k == cur || p + k > L.n) continue;
-        if (e.last ? p + k == L.n : (!e.nlit || lit_at(P, L, p + k, e))) { add(ends, k); any = true; }
-    }
+    ends = Set128{};
+    fin.each([&](int k) {
+        if (p + k == cur || p + k > L.n) return;
+        if (e.last ? p + k == L.n : (!e.nlit || lit_at(P, L, p + k, e))) { ends.add(k); any = true; }
+    });
     return any;
 }
 
 template <typename LN>
 __host__ __device__ LP_INLINE bool ip_alt_end_possible(const Program& P, const LN& L, const ElemV& e, int p, int cur) {
-    uint32_t ends[3];
+    Set128 ends;
     return ip_alt_ends(P, L, e, p, cur, ends);
 }
 
@@ -924,17 +954,15 @@ __host__ __device__ LP_INLINE int match_line(const Program& P, const EL& elems, 
         } else {
             const ElemV e = load_elem(elems + j);
             if (e.kind != EK_IP && e.kind != EK_CLF_IP) return -2;
-            uint32_t ends[3];
+            Set128 ends;
             ip_alt_ends(P, L, e, p, cur, ends);
-            if (e.kind == EK_CLF_IP && p < L.n && L[p] == '-' && p + 1 != cur) ends[0] |= 2u;  // the '-' alternative
+            if (e.kind == EK_CLF_IP && p < L.n && L[p] == '-' && p + 1 != cur) ends.add(1);  // the '-' alternative
             NoCapsDfs nc;
-            for (int w = 0; w < 3; ++w) {
-                for (uint32_t m = ends[w]; m; m &= m - 1) {
-                    const int k = 32 * w + __builtin_ctz(m);
-                    if (match_line<true>(P, elems + j + 1, ne - j - 1, L, nc, stk, p + k, spn) != ST_BAD) return -2;
-                }
-            }
-            return -1;
+            bool hit = false;
+            ends.each([&](int k) {
+                if (!hit && match_line<true>(P, elems + j + 1, ne - j - 1, L, nc, stk, p + k, spn) != ST_BAD) hit = true;
+            });
+            return hit ? -2 : -1;
         }
     };
     for (;;) {
@@ -996,6 +1024,7 @@ __host__ __device__ LP_INLINE bool match_first_leaf(const Program& P, const LN& 
     bool ok = true;
     const int ne = P.n_elems;
     for (int i = 0; i < ne; ++i) {
+        LP_PROF_EL_BEGIN();
         const ElemV e = load_elem(P.elems + i);
         if (e.kind == EK_LIT) {
             ok = ok && lit_at(P, L, pos, e);
@@ -1008,6 +1037,7 @@ __host__ __device__ LP_INLINE bool match_first_leaf(const Program& P, const LN& 
                 pos = c;
             }
         }
+        LP_PROF_EL_END(i);
     }
     return ok && pos == L.n;
 }
@@ -1431,6 +1461,9 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
     }
     LP_PROF(4);
     if (st != ST_OK) { o.status = st; return; }
+#if LP_EXP == 12
+    return;  // experiment: stop after the match
+#endif
     // decodeExtractedValue: "-" -> null (Apache: ApacheHttpdLogFormatDissector.java:169-196,
     // NGINX: NginxHttpdLogFormatDissector.java:107-119).  Slots unrolled (the
     // spans stay in registers); only one-byte values are read.

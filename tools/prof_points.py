@@ -17,11 +17,15 @@ t = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
 p = lpa.HttpdLoglineParser("combined", fields)
 L = lpa.lib()
 L.lp_profile_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+L.lp_profile_read_elems.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
 buf = (ctypes.c_ulonglong * 128)()
+el = (ctypes.c_ulonglong * 128)()
 p.run(t.data_ptr(), len(data))
 L.lp_profile_read(buf, 64)  # clear after warm-up
+L.lp_profile_read_elems(el, 64)
 st = p.run(t.data_ptr(), len(data))
 L.lp_profile_read(buf, 64)
+L.lp_profile_read_elems(el, 64)
 names = {0: "start", 1: "staged", 2: "phase1 entry", 3: "guard", 4: "match", 5: "tok flags", 6: "time",
          7: "first line", 8: "arena need", 9: "phase1 exit", 10: "uri0 in", 11: "uri0 out", 12: "uri1 in",
          13: "uri1 out", 20: "phase2 exit", 21: "rows written", 22: "query pieces"}
@@ -46,3 +50,8 @@ for k in pts:
         else:
             print("  %-14s -> %-14s (mark counts differ %d vs %d)" % (names[prev], names[k], pc, c))
     prev = k
+print("first-leaf elements (cycles per visit):")
+print(p.describe())
+for i in range(64):
+    if el[2 * i + 1]:
+        print("  elem %2d %10.0f" % (i, el[2 * i] / el[2 * i + 1]))

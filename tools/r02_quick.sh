@@ -1,0 +1,19 @@
+#!/bin/bash
+# quick GPU check: parity tests, then a 20M-line bench with a kernel trace
+set -uo pipefail
+TAG=${1:-r02_quick}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/$TAG
+mkdir -p "$O"
+cd "$R"
+if [ "${SKIP_TESTS:-0}" = "0" ]; then
+  timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$O/gpu_tests.log" 2>&1
+  rc=$?
+  echo "tests rc=$rc"
+  [ $rc -ne 0 ] && exit $rc
+fi
+cd /tmp
+export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$O/trace" -o run -- \
+    python3 "$R/bench.py" --lines 20000000 --steps 3 --warmup 2 --no-cpu-baseline > "$O/bench20m.json" 2> "$O/bench20m.err" || exit 1
+echo done
