@@ -138,9 +138,10 @@ def pcie_inclusive(torch, parser, buf, batches, max_bytes):
             "lines": lines2}
 
 
-def cpu_baseline(lpa, workload, fields, sample_lines, threads):
+def cpu_baseline(lpa, workload, fields, sample_lines, threads, repeats=3):
     """The oracle (C restatement of the reference semantics) on the GPU box's
-    host cores, on the first sample_lines lines of the same workload."""
+    host cores, on the first sample_lines lines of the same workload: the
+    median of `repeats` timed runs (spread reported)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
     oracle_lib.lib()
@@ -148,21 +149,62 @@ def cpu_baseline(lpa, workload, fields, sample_lines, threads):
     probe = lpa.synth(workload, SEEDS[workload], 0, 2000)
     secs, _ = oracle_lib.bench(fmt, fields, probe, 1)
     rate1 = 2000 / max(secs, 1e-6)
-    # aim at ~15 s of work on `threads` threads
-    n = int(min(sample_lines, max(20000, rate1 * threads * 15)))
+    # aim at ~5 s of work per run on `threads` threads (~15 s in all)
+    n = int(min(sample_lines, max(20000, rate1 * threads * 5)))
     data = lpa.synth(workload, SEEDS[workload], 0, n)
-    secs, counts = oracle_lib.bench(fmt, fields, data, threads)
+    runs = []
+    for _ in range(repeats):
+        secs, counts = oracle_lib.bench(fmt, fields, data, threads)
+        runs.append(secs)
+    runs.sort()
+    secs = runs[len(runs) // 2]
     return {
         "value": round(len(data) / secs / 1e9, 6),
         "unit": "GB/s",
         "lines_per_s": round(counts[0] / secs, 1),
         "cores": threads,
+        "host_cpus": os.cpu_count(),
         "kind": "port",
         "sample": "first %d lines (%.1f MB) of the config-%d workload, all %d paths, oracle/ C restatement, "
-                  "%d threads, one parser per thread; ok=%d bad=%d unsupported=%d" % (
-                      counts[0], len(data) / 1e6, workload, len(fields), threads, counts[1], counts[2], counts[3]),
+                  "%d threads (the GPU box's CPU share; os.cpu_count() = %s), one parser per thread, median of %d "
+                  "runs; ok=%d bad=%d unsupported=%d" % (
+                      counts[0], len(data) / 1e6, workload, len(fields), threads, os.cpu_count(), repeats,
+                      counts[1], counts[2], counts[3]),
         "seconds": round(secs, 2),
+        "spread_gbs": [round(len(data) / t / 1e9, 6) for t in reversed(runs)],
     }
+
+
+def host_delivery(lpa, torch, parser, n_lines, workload, sample=20000):
+    """Rate at which the finished batch reaches the caller: one
+    lp_result_copy of the batch's SoA results (line index, columns, arena)
+    into pinned host memory; then the host-side record rebuild
+    (lp_result_record_json, one thread) from a copy of a small batch."""
+    import ctypes
+    L = lpa.lib()
+    need = -L.lp_result_copy(parser._h, None, 0, 0, None)
+    host = torch.empty(need, dtype=torch.uint8, pin_memory=True)
+    res = lpa.LpResult()
+    t0 = time.perf_counter()
+    rc = L.lp_result_copy(parser._h, ctypes.c_void_p(host.data_ptr()), need, 0, ctypes.byref(res))
+    dt = time.perf_counter() - t0
+    del host
+    if rc < 0:
+        return None
+    data = lpa.synth(workload, SEEDS[workload], 0, sample)
+    r = parser.parse_batch(data)
+    _, res2 = r.copy_to_host()
+    out = ctypes.create_string_buffer(1 << 16)
+    ok = [i for i in range(r.n_lines) if r.status[i] == lpa.LINE_OK]
+    t1 = time.perf_counter()
+    for i in ok:
+        L.lp_result_record_json(parser._h, ctypes.byref(res2), i, out, 1 << 16)
+    dt2 = time.perf_counter() - t1
+    return {"soa_copy_lines_per_s": round(n_lines / dt, 1), "soa_copy_gbs": round(need / dt / 1e9, 3),
+            "soa_bytes": int(need), "records_json_per_s_1thread": round(len(ok) / dt2, 1),
+            "sample": "lp_result_copy of the timed batch's SoA (%d lines) into pinned host memory; "
+                      "lp_result_record_json of the %d OK lines of a %d-line batch, one host thread"
+                      % (n_lines, len(ok), sample)}
 
 
 def pmc_traffic(path, n_lines, lib_path):
@@ -185,7 +227,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--lines", type=int, default=100_000_000, help="lines per GPU")
     ap.add_argument("--cpu-sample-lines", type=int, default=2_000_000)
-    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-threads", type=int, default=16, help="the GPU box's CPU share per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--workload", type=int, default=2, choices=(2, 3, 4, 5), help="BASELINE.json config")
     ap.add_argument("--batch-mb", type=int, default=None,
@@ -305,6 +347,8 @@ def main():
         result["config"]["corpus_bytes_all_ranks"] = total_bytes
         if rank == 0:
             result["pcie_inclusive"] = pcie_inclusive(torch, parser, buf, batches, 8 << 30)
+    if rank == 0 and wl != 5:
+        result["delivery"] = host_delivery(lpa, torch, parser, stats["lines"], wl)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline (oracle, %d threads) ..." % args.cpu_threads)
         result["cpu_baseline"] = cpu_baseline(lpa, wl, fields, args.cpu_sample_lines, args.cpu_threads)

@@ -682,22 +682,14 @@ int launch_offsets(const uint16_t* d_nlmask, uint64_t nbytes, const uint64_t* d_
 int64_t parse_waves(int64_t n_lines) { return (n_lines + PW - 1) / PW; }
 
 #if defined(LP_PROFILE)
-// profiling build: copy out (and clear) the per-point timestamp sums
+// profiling build: copy out (and clear) the per-wave timestamps
+// (PROF_WAVES x PROF_POINTS u64)
 extern "C" int lp_profile_read(unsigned long long* out, int n) {
-    unsigned long long h[64 * 16];
-    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_prof), sizeof h) != hipSuccess) return -1;
-    for (int k = 0; k < n && k < 64; ++k) { out[2 * k] = h[k * 16]; out[2 * k + 1] = h[k * 16 + 1]; }
-    unsigned long long z[64 * 16] = {};
+    if (n < PROF_WAVES * PROF_POINTS) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * PROF_WAVES * PROF_POINTS) != hipSuccess)
+        return -1;
+    static unsigned long long z[PROF_WAVES * PROF_POINTS];
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof z);
-    return 0;
-}
-// per first-leaf element: cycles, visits (and clear)
-extern "C" int lp_profile_read_elems(unsigned long long* out, int n) {
-    unsigned long long h[64 * 2];
-    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_prof_el), sizeof h) != hipSuccess) return -1;
-    for (int k = 0; k < 2 * n && k < 128; ++k) out[k] = h[k];
-    unsigned long long z[64 * 2] = {};
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_prof_el), z, sizeof z);
     return 0;
 }
 #endif

@@ -21,34 +21,26 @@ namespace lp {
 enum : int { ST_OK = 0, ST_BAD = 1, ST_FALLBACK = 2 };
 
 // Profiling build only (-DLP_PROFILE): wave timestamps at fixed points,
-// summed per point; differences of the sums = cycles spent between points.
+// stored per wave (the waves of blocks [PROF_W0, PROF_W0 + PROF_WAVES)),
+// no atomics: the host averages the cycles between consecutive points.
+constexpr int PROF_WAVES = 16384, PROF_W0 = 1024, PROF_POINTS = 64;
 #if defined(LP_PROFILE) && defined(__HIP__)
-__device__ unsigned long long g_prof[64 * 16];
-__device__ unsigned long long g_prof_el[64 * 2];  // per first-leaf element: cycles, visits
+__device__ unsigned long long g_prof[PROF_WAVES * PROF_POINTS];
 #endif
 #if defined(LP_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
 __device__ __forceinline__ void lp_prof_mark(int k) {
     const unsigned long long t = clock64();
+    const unsigned w = blockIdx.x - PROF_W0;
     const uint64_t act = __ballot(1);
-    if ((int)threadIdx.x % 64 == (int)__builtin_ctzll(act)) atomicAdd(&g_prof[k * 16], t);
-    if ((int)threadIdx.x % 64 == (int)__builtin_ctzll(act)) atomicAdd(&g_prof[k * 16 + 1], 1ull);
+    if (w < (unsigned)PROF_WAVES && (int)threadIdx.x % 64 == (int)__builtin_ctzll(act))
+        __builtin_nontemporal_store(t, &g_prof[w * PROF_POINTS + k]);
 }
 #define LP_PROF(k) lp_prof_mark(k)
-#define LP_PROF_EL_BEGIN() const unsigned long long lp_t0 = clock64()
-#define LP_PROF_EL_END(i)                                                                  \
-    do {                                                                                   \
-        const unsigned long long lp_dt = clock64() - lp_t0;                                \
-        const uint64_t lp_act = __ballot(1);                                               \
-        if ((int)threadIdx.x % 64 == (int)__builtin_ctzll(lp_act)) {                       \
-            atomicAdd(&g_prof_el[2 * (i)], lp_dt);                                         \
-            atomicAdd(&g_prof_el[2 * (i) + 1], 1ull);                                      \
-        }                                                                                  \
-    } while (0)
 #else
 #define LP_PROF(k)
+#endif
 #define LP_PROF_EL_BEGIN()
 #define LP_PROF_EL_END(i)
-#endif
 // profiling experiments only (tools/build_exp.sh): 0 = the product
 #ifndef LP_EXP
 #define LP_EXP 0
@@ -526,6 +518,18 @@ struct RegArr {
         (f((int)J, v[J]), ...);
     }
     __host__ __device__ LP_INLINE uint32_t get(int k) const { return get_(k, std::make_index_sequence<N>{}); }
+    // set with a wave-uniform index: a scalar branch to one register write
+    // (the select chain of set() rewrites every element)
+    __host__ __device__ LP_INLINE void set_u(int k, uint32_t x) {
+        switch (k) {
+#define LP_RA_CASE(J) case J: if constexpr (J < N) v[J] = x; break;
+            LP_RA_CASE(0) LP_RA_CASE(1) LP_RA_CASE(2) LP_RA_CASE(3) LP_RA_CASE(4) LP_RA_CASE(5) LP_RA_CASE(6)
+            LP_RA_CASE(7) LP_RA_CASE(8) LP_RA_CASE(9) LP_RA_CASE(10) LP_RA_CASE(11) LP_RA_CASE(12) LP_RA_CASE(13)
+            LP_RA_CASE(14) LP_RA_CASE(15)
+#undef LP_RA_CASE
+        default: break;
+        }
+    }
     __host__ __device__ LP_INLINE void set(int k, uint32_t x) { set_(k, x, std::make_index_sequence<N>{}); }
     __host__ __device__ LP_INLINE void fill(uint32_t x) { set_all(x, std::make_index_sequence<N>{}); }
     template <size_t... J>
@@ -1032,10 +1036,8 @@ __host__ __device__ LP_INLINE bool match_first_leaf(const Program& P, const LN& 
         } else if (ok) {
             const int c = cand_first(P, e, L, pos);
             ok = c >= 0;
-            if (ok) {
-                if (e.cap >= 0) caps.set(e.cap, mkspan(pos, c));
-                pos = c;
-            }
+            if (e.cap >= 0) caps.set_u(e.cap, mkspan(pos, c));  // e.cap is uniform
+            pos = ok ? c : pos;
         }
         LP_PROF_EL_END(i);
     }
