@@ -182,6 +182,19 @@ int64_t lp_result_copy(lp_handle *h, void *host, uint64_t cap, int with_input, l
  * made with the input: no device access. */
 int64_t lp_result_record_json(lp_handle *h, const lp_result *r, int64_t i, char *out, size_t cap);
 
+/* The reference's Parsable.addDissection(base, type, name, value) calls
+ * that deliver line i's requested values (core/Parsable.java:77-193), from a
+ * host copy made with the input, in the reference's emission order: what a
+ * Java GpuHttpdLogFormatDissector.dissect replays.  kind:
+ * LP_VALUE_STRING (bytes p[0, len), UTF-8), LP_VALUE_NULL, LP_VALUE_LONG (l).
+ * Returns the number of calls, or LP_E_STATE when line i is not OK. */
+#define LP_VALUE_STRING 0
+#define LP_VALUE_NULL 1
+#define LP_VALUE_LONG 2
+typedef void (*lp_emit_fn)(void *ctx, const char *base, const char *type, const char *name, int kind,
+                           const uint8_t *p, uint32_t len, int64_t l);
+int lp_result_emit(lp_handle *h, const lp_result *r, int64_t i, lp_emit_fn fn, void *ctx);
+
 /* Description of the compiled device program (for logs/tests), NUL-terminated. */
 int64_t lp_describe(lp_handle *h, char *out, size_t cap);
 

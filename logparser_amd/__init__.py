@@ -39,6 +39,11 @@ class LpColumn(ctypes.Structure):
                 ("offset", ctypes.c_uint64)]
 
 
+EMIT_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
+                           ctypes.POINTER(ctypes.c_uint8), ctypes.c_uint32, ctypes.c_int64)
+VALUE_STRING, VALUE_NULL, VALUE_LONG = 0, 1, 2
+
+
 class LpResult(ctypes.Structure):
     """lp_result (include/logparser_amd.h): the SoA results of one batch"""
     _fields_ = [("n_lines", ctypes.c_int64), ("input_bytes", ctypes.c_uint64), ("input", ctypes.c_void_p),
@@ -115,6 +120,7 @@ def lib():
     L.lp_result_record_json.restype = ctypes.c_int64
     L.lp_result_record_json.argtypes = [ctypes.c_void_p, ctypes.POINTER(LpResult), ctypes.c_int64, ctypes.c_char_p,
                                         ctypes.c_size_t]
+    L.lp_result_emit.argtypes = [ctypes.c_void_p, ctypes.POINTER(LpResult), ctypes.c_int64, EMIT_FN, ctypes.c_void_p]
     L.lp_describe.restype = ctypes.c_int64
     L.lp_describe.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]
     L.lp_synth_combined.restype = ctypes.c_int64
@@ -242,6 +248,22 @@ class BatchResult:
             c = res.column[k]
             arr = np.ctypeslib.as_array((ctypes.c_uint8 * (c.elem_size * res.n_lines)).from_address(res.columns + c.offset))
             out[(c.name.decode(), c.index)] = arr.view(dt[c.elem_size])
+        return out
+
+    def emissions_from(self, res, i):
+        """lp_result_emit: the Parsable.addDissection(base, type, name, value)
+        calls delivering line i's values, from a host copy with the input;
+        value = str | None | int."""
+        out = []
+
+        def cb(_ctx, base, typ, name, kind, p, n, l):
+            v = None if kind == VALUE_NULL else l if kind == VALUE_LONG else ctypes.string_at(p, n).decode("utf-8")
+            out.append((base.decode(), typ.decode(), name.decode(), v))
+
+        fn = EMIT_FN(cb)
+        rc = lib().lp_result_emit(self._p._h, ctypes.byref(res), i, fn, None)
+        if rc < 0:
+            raise ValueError("lp_result_emit(%d) failed: %d" % (i, rc))
         return out
 
     def record_json_from(self, res, i):

@@ -679,4 +679,13 @@ int64_t lp_result_record_json(lp_handle* h, const lp_result* r, int64_t i, char*
     return (int64_t)js.size();
 }
 
+int lp_result_emit(lp_handle* h, const lp_result* r, int64_t i, lp_emit_fn fn, void* ctx) {
+    if (!h || !r || !fn || !r->on_host || !r->input) return LP_E_INVALID;
+    if (i < 0 || i >= r->n_lines) return LP_E_INVALID;
+    lp::ResultView V;
+    make_view(h, *r, V);
+    if (!V.status || V.status[i] != LP_LINE_OK) return LP_E_STATE;
+    return h->plan.emit_row(V, i, fn, ctx);
+}
+
 }  // extern "C"

@@ -1357,12 +1357,17 @@ std::string Plan::describe() const {
 }
 
 // ================================================================ replay
+struct Emission {
+    std::string base, type, name;
+    MVal v;
+};
 struct Plan::Ctx {
     const ResultView& R;
     int64_t i;
     const uint8_t* line;
     const uint8_t* arena;
-    std::vector<std::pair<std::string, MVal>> rec;
+    std::vector<std::pair<std::string, MVal>> rec;  // (TYPE:path, value) per setter call
+    std::vector<Emission> em;                        // the delivering addDissection calls
     std::deque<std::string> pool;  // formatted date/time strings
 };
 
@@ -1410,8 +1415,10 @@ void Plan::emit(Ctx& c, const std::string& base, const std::string& type, const 
                 run_phase(c, in, complete, v);
             }
     }
-    if (needed_.count(needed)) c.rec.emplace_back(needed, v);
-    if (needed_.count(wild)) c.rec.emplace_back(needed, v);
+    const bool exact = needed_.count(needed) > 0, wildcard = needed_.count(wild) > 0;
+    if (exact) c.rec.emplace_back(needed, v);
+    if (wildcard) c.rec.emplace_back(needed, v);
+    if (exact || wildcard) c.em.push_back(Emission{base, type, name, v});
 }
 
 void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const MVal& v) const {
@@ -1631,8 +1638,10 @@ void json_str(std::string& o, const uint8_t* p, uint32_t n) {
 }
 }  // namespace
 
-std::string Plan::record_json(const ResultView& R, int64_t i) const {
-    Ctx c{R, i, R.input + R.line_off[i], R.region(i), {}};
+// Replays line c.i: every root token value through the dissector tree.
+void Plan::replay(Ctx& c) const {
+    const ResultView& R = c.R;
+    const int64_t i = c.i;
     // the LogFormat the line was routed to (HttpdLogFormatDissector's active format)
     const int fi = prog_.n_fmt > 1 ? R.fmt_id[i] : 0;
     t_fmt = fi;
@@ -1649,6 +1658,21 @@ std::string Plan::record_json(const ResultView& R, int64_t i) const {
             emit(c, "", o.type, o.name, v);
         }
     }
+}
+
+int Plan::emit_row(const ResultView& R, int64_t i, EmitFn fn, void* ctx) const {
+    Ctx c{R, i, R.input + R.line_off[i], R.region(i), {}, {}, {}};
+    replay(c);
+    for (const auto& e : c.em) {
+        const int kind = e.v.is_long ? 2 : e.v.null ? 1 : 0;
+        fn(ctx, e.base.c_str(), e.type.c_str(), e.name.c_str(), kind, e.v.p, e.v.len, e.v.l);
+    }
+    return (int)c.em.size();
+}
+
+std::string Plan::record_json(const ResultView& R, int64_t i) const {
+    Ctx c{R, i, R.input + R.line_off[i], R.region(i), {}, {}, {}};
+    replay(c);
     std::stable_sort(c.rec.begin(), c.rec.end(),
                      [](const std::pair<std::string, MVal>& a, const std::pair<std::string, MVal>& b) {
                          return a.first < b.first;

@@ -127,6 +127,12 @@ public:
 
     // canonical JSON record of line i (status OK)
     std::string record_json(const ResultView& R, int64_t i) const;
+    // the reference's Parsable.addDissection(base, type, name, value) calls that
+    // deliver line i's requested values (core/Parsable.java:142-193), in
+    // emission order: kind 0 string (p, len), 1 null, 2 long (l)
+    using EmitFn = void (*)(void* ctx, const char* base, const char* type, const char* name, int kind,
+                            const uint8_t* p, uint32_t len, int64_t l);
+    int emit_row(const ResultView& R, int64_t i, EmitFn fn, void* ctx) const;
 
 private:
     int build_dissectors(const std::string& logformats, std::string& err);
@@ -136,6 +142,7 @@ private:
 
     // replay
     struct Ctx;
+    void replay(Ctx& c) const;
     void emit(Ctx& c, const std::string& base, const std::string& type, const std::string& name, const MVal& v) const;
     void run_phase(Ctx& c, const Instance& in, const std::string& name, const MVal& v) const;
 

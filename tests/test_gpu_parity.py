@@ -376,3 +376,29 @@ def test_async_batches_and_capacity_retry(oracle):
             for i in range(0, len(batch), 997):
                 s1, js = o.parse_raw(batch[i])
                 assert s1 == 0 and js == r.record_json(i)
+
+
+def test_result_emit_replays_setter_calls(oracle):
+    """lp_result_emit gives, per line, the (base, type, name, value)
+    addDissection calls a Java GpuHttpdLogFormatDissector replays
+    (core/Parsable.java:142-193): rebuilding the record from them with the
+    reference's exact / wildcard rule gives the record of lp_line_record_json."""
+    import json
+    for fmt in ("combined", lpa.SYNTH_FORMATS[lpa.SYNTH_NGINX]):
+        fields = paths(oracle, fmt)
+        wl = lpa.SYNTH_COMBINED if fmt == "combined" else lpa.SYNTH_NGINX
+        p = lpa.HttpdLoglineParser(fmt, fields)
+        r = p.parse_batch(lpa.synth(wl, 9, 0, 3000))
+        _, res = r.copy_to_host()
+        need = set(fields)
+        for i in range(0, 3000, 7):
+            rec = {}
+            for base, typ, name, v in r.emissions_from(res, i):
+                complete = name if not base else (base if not name else base + "." + name)
+                key = typ + ":" + complete
+                wild = typ + ":" + (base + ".*" if base else "*")
+                val = {"l": v} if isinstance(v, int) else v
+                for hit in (key in need, wild in need):
+                    if hit:
+                        rec.setdefault(key, []).append(val)
+            assert rec == json.loads(r.record_json(i)), i
