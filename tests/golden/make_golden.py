@@ -24,9 +24,19 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CASES = []
 
 
+# Reference tests written with DissectorTester
+# (parser-core/src/test/java/nl/basjes/parse/core/test/DissectorTester.java):
+# their .expect(field, (String) null) means "present AND null" (EdgeCasesTest.java:37-46);
+# the Map-based record tests (ApacheHttpdLogParserTest, MultiLine, Jetty,
+# Flink TestCase) read null for an absent field too.
+DISSECTOR_TESTER_SOURCES = ("EdgeCasesTest", "NginxLogFormatTest", "NginxUpstreamTest", "dissectors/Test",
+                            "TestTranslators", "AllFieldsTest")
+
+
 def case(source, logformat, line, fields, expect=None, absent=(), bad=False, skipped=(), note=""):
     CASES.append({
         "source": source,
+        "null_present": any(k in source for k in DISSECTOR_TESTER_SOURCES),
         "logformat": logformat,
         "line": line,
         "fields": list(fields),
@@ -577,8 +587,24 @@ URLDECODE = [
     ["x%u", "x"], ["x%", "x"], ["%20 %20%u0020%20 %20%2", "       "],
 ]
 
+# Setup-time failures (the parser refuses the requested paths before any line
+# is parsed): MissingDissectorsException with the offending path, lower-cased
+# as the reference reports it.
+SETUP = [
+    {"source": "hpt/ApacheHttpdLogParserTest.java:242-259 (testMissing)", "logformat": FULLCOMBINED,
+     "fields": ["STRING:request.firstline.uri.query.ThisShouldNOTBeMissing",
+                "HEADER:response.header.Etag.ThisShouldBeMissing"],
+     "error": "MissingDissectorsException", "message_contains": "HEADER:response.header.etag.thisshouldbemissing"},
+    {"source": "hpt/ApacheHttpdLogParserTest.java:263-279 (testMissing2)", "logformat": FULLCOMBINED,
+     "fields": ["BLURP:request.firstline.uri.query.ThisShouldBeMissing", "HTTP.HEADER:response.header.etag"],
+     "error": "MissingDissectorsException", "message_contains": "BLURP:request.firstline.uri.query.thisshouldbemissing"},
+    {"source": "hpt/ApacheHttpdLogParserTest.java:472-485 (testFailOnMissingDissectors)", "logformat": "%t",
+     "fields": ["STRING:request.firstline.uri.query.foo", "TIME.EPOCH:request.receive.time.epoch"],
+     "error": "MissingDissectorsException", "message_contains": "STRING:request.firstline.uri.query.foo"},
+]
+
 if __name__ == "__main__":
-    out = {"generated_by": "tests/golden/make_golden.py", "cases": CASES,
+    out = {"generated_by": "tests/golden/make_golden.py", "cases": CASES, "setup_cases": SETUP,
            "url_decode": {"source": "hpt/UtilsTest.java:27-49", "vectors": URLDECODE}}
     with open(os.path.join(HERE, "reference_vectors.json"), "w", encoding="utf-8") as f:
         json.dump(out, f, indent=1, ensure_ascii=False)

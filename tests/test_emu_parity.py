@@ -369,3 +369,12 @@ def test_ip_token_variants_emulated(oracle, emu, fmt):
     lines = [t.encode() + b" " + l.split(b" ", 1)[1] for l in base for t in IP_TOKENS[:: 1 + len(l) % 3]]
     s = compare(o, e, lines)
     assert s["fallback"] < len(lines) // 4, s
+
+
+def test_setup_vectors_planner(emu, vectors):
+    """The device planner (plan.cpp, the code lp_compile runs) refuses the
+    same requests as the reference: MissingDissectorsException with the path."""
+    for c in vectors["setup_cases"]:
+        with pytest.raises(RuntimeError) as ei:
+            emu.Emu(c["logformat"], c["fields"])
+        assert "failed -2" in str(ei.value) and c["message_contains"] in str(ei.value), c["source"]

@@ -140,3 +140,12 @@ def test_nginx_equals_apache(oracle):
         assert (f in ra) == (f in rn), f
         if f in ra:
             assert as_str(ra[f]) == as_str(rn[f]), f
+
+
+def test_setup_vectors_oracle(oracle, vectors):
+    """Setup-time failures transcribed from the reference (MissingDissectorsException)."""
+    assert len(vectors["setup_cases"]) >= 3
+    for c in vectors["setup_cases"]:
+        with pytest.raises(Exception) as ei:
+            oracle.Oracle(c["logformat"], c["fields"])
+        assert c["error"] in str(ei.value) and c["message_contains"] in str(ei.value), c["source"]
