@@ -1636,7 +1636,66 @@ void json_str(std::string& o, const uint8_t* p, uint32_t n) {
     }
     o += '"';
 }
+void json_s(std::string& o, const std::string& s) { json_str(o, (const uint8_t*)s.data(), (uint32_t)s.size()); }
 }  // namespace
+
+// The token table in the canonical form tests/golden/extract_token_tables.py
+// derives from the reference's Java sources: one entry per TokenParser in
+// table order; "token" is the literal token or, for Named/Parameterized
+// parsers, the Java regex they match the LogFormat with.
+std::string token_table_json(bool nginx) {
+    const TokenTable& T = nginx ? nginx_table() : apache_table();
+    std::string o = "[";
+    for (size_t k = 0; k < T.v.size(); ++k) {
+        const TParser& t = T.v[k];
+        std::string kind = "plain", tok = t.tok, custom;
+        if (t.kind == TP_FIXED) kind = "fixed";
+        if (t.kind == TP_NAMED) {
+            kind = "named";
+            tok = std::string("\\%\\{([a-z0-9\\-") + (t.underscore ? "_" : "") + "]*)\\}";
+            for (char c : t.suffix) {
+                if (c == '^') tok += '\\';
+                tok += c;
+            }
+        }
+        if (t.kind == TP_DOLLAR) kind = "named";
+        if (t.kind == TP_PARAM) {
+            kind = "param";
+            tok = "\\%\\{" + t.pprefix + "([^\\}]*%[^\\}]*)\\}t";
+        }
+        if (t.strftime) custom = "StrfTimeStampDissector";
+        o += k ? ",\n{" : "{";
+        o += "\"kind\":";
+        json_s(o, kind);
+        o += ",\"token\":";
+        json_s(o, tok);
+        o += ",\"regex\":";
+        json_s(o, t.regex);
+        o += ",\"prio\":" + std::to_string(t.prio) + ",\"custom\":";
+        if (custom.empty()) o += "null";
+        else json_s(o, custom);
+        o += ",\"outs\":[";
+        for (size_t j = 0; j < t.outs.size(); ++j) {
+            const TokOut& u = t.outs[j];
+            o += j ? ",[" : "[";
+            json_s(o, u.type);
+            o += ',';
+            json_s(o, u.name);
+            o += ",[";
+            bool first = true;
+            for (auto [bit, nm] : {std::pair<int, const char*>{CAST_S, "STRING"}, {CAST_L, "LONG"}, {CAST_D, "DOUBLE"}})
+                if (u.casts & bit) {
+                    o += first ? "\"" : ",\"";
+                    o += nm;
+                    o += '"';
+                    first = false;
+                }
+            o += "]]";
+        }
+        o += "]}";
+    }
+    return o + "]";
+}
 
 // Replays line c.i: every root token value through the dissector tree.
 void Plan::replay(Ctx& c) const {

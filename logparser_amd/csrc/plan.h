@@ -113,6 +113,10 @@ struct ResultView {
     }
 };
 
+// the Apache or NGINX token table as canonical JSON (checked against the
+// tables extracted from the reference's sources by the CPU tests)
+std::string token_table_json(bool nginx);
+
 class Plan {
 public:
     // returns LP_OK / LP_E_UNSUPPORTED / error; err filled on error

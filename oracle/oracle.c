@@ -2615,6 +2615,45 @@ static void ob_json_str(ob *o, const char *s, int n) {
     ob_put(o, "\"", 1);
 }
 
+int orc_token_table(int nginx, char *out, int out_cap) {
+    pthread_once(&g_tps_once, init_tps);
+    const tplist *l = nginx ? &g_nginx_tps : &g_apache_tps;
+    ob o = {out, 0, out_cap, 0};
+    if (out_cap > 0) out[0] = 0;
+    ob_s(&o, "[");
+    for (int k = 0; k < l->n; k++) {
+        const tparser *t = &l->v[k];
+        const char *kind = t->kind == TP_FIXED ? "fixed" : t->kind == TP_NAMED ? "named" : t->kind == TP_PARAM ? "param" : "plain";
+        ob_s(&o, k ? ",\n{\"kind\":" : "{\"kind\":");
+        ob_json_str(&o, kind, (int)strlen(kind));
+        ob_s(&o, ",\"token\":");
+        ob_json_str(&o, t->tok, (int)strlen(t->tok));
+        ob_s(&o, ",\"regex\":");
+        ob_json_str(&o, t->regex, (int)strlen(t->regex));
+        char b[64];
+        snprintf(b, sizeof b, ",\"prio\":%d,\"custom\":", t->prio);
+        ob_s(&o, b);
+        ob_s(&o, t->custom == CUSTOM_STRFTIME ? "\"StrfTimeStampDissector\"" : "null");
+        ob_s(&o, ",\"outs\":[");
+        for (int j = 0; j < t->nouts; j++) {
+            const ofield *u = &t->outs[j];
+            ob_s(&o, j ? ",[" : "[");
+            ob_json_str(&o, u->type, (int)strlen(u->type));
+            ob_s(&o, ",");
+            ob_json_str(&o, u->name, (int)strlen(u->name));
+            int first = 1;
+            ob_s(&o, ",[");
+            if (u->casts & C_S) { ob_s(&o, "\"STRING\""); first = 0; }
+            if (u->casts & C_L) { ob_s(&o, first ? "\"LONG\"" : ",\"LONG\""); first = 0; }
+            if (u->casts & C_D) ob_s(&o, first ? "\"DOUBLE\"" : ",\"DOUBLE\"");
+            ob_s(&o, "]]");
+        }
+        ob_s(&o, "]}");
+    }
+    ob_s(&o, "]");
+    return o.overflow ? -1 : o.n;
+}
+
 static int rcmp(const void *a, const void *b) {
     const rentry *x = (const rentry *)a, *y = (const rentry *)b;
     int c = strcmp(x->name, y->name);

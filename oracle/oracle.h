@@ -74,6 +74,11 @@ double orc_bench(const char *logformat, const char *const *fields, int nfields,
 /* Individual component restatements, exposed for unit tests. */
 int orc_resilient_url_decode(const char *in, int len, char *out, int out_cap);
 
+/* The Apache (nginx=0) or NGINX token table as canonical JSON (the form
+ * tests/golden/extract_token_tables.py derives from the reference's Java
+ * sources).  Returns bytes written or -1 when out_cap is too small. */
+int orc_token_table(int nginx, char *out, int out_cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -66,6 +66,13 @@ static int g_masks = 1;  // 1: lines carry byte-class masks (the kernel's LDS pa
 
 void emu_set_masks(int on) { g_masks = on; }
 
+// the planner's token table (plan.cpp) as canonical JSON; returns its length
+int emu_token_table(int nginx, char* out, int cap) {
+    const std::string j = lp::token_table_json(nginx != 0);
+    if (out && cap > 0) snprintf(out, cap, "%s", j.c_str());
+    return (int)j.size();
+}
+
 }  // extern "C"
 
 // One line's results, stored in vectors (the emulation's columns, one row).

@@ -40,6 +40,8 @@ def lib():
         L.emu_describe.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]
         L.emu_set_masks.argtypes = [ctypes.c_int]
         L.emu_possible_paths.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        L.emu_token_table.restype = ctypes.c_int
+        L.emu_token_table.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -104,3 +106,11 @@ def possible_paths(logformat, depth=15):
     b = ctypes.create_string_buffer(1 << 20)
     lib().emu_possible_paths(logformat.encode(), depth, b, len(b))
     return [p for p in b.value.decode().split("\n") if p]
+
+
+def token_table(nginx):
+    """plan.cpp's Apache (False) / NGINX (True) token table, canonical form"""
+    n = lib().emu_token_table(1 if nginx else 0, None, 0)
+    b = ctypes.create_string_buffer(n + 1)
+    lib().emu_token_table(1 if nginx else 0, b, len(b))
+    return json.loads(b.value.decode("utf-8"))

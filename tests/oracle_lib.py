@@ -41,6 +41,8 @@ def lib():
                                 ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_int64)]
         L.orc_resilient_url_decode.restype = ctypes.c_int
         L.orc_resilient_url_decode.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        L.orc_token_table.restype = ctypes.c_int
+        L.orc_token_table.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -117,3 +119,12 @@ def bench(logformat, fields, data, threads):
     f = _fields(fields)
     secs = lib().orc_bench(logformat.encode(), f, len(fields), data, len(data), threads, out)
     return secs, list(out)
+
+
+def token_table(nginx):
+    """oracle.c's Apache (False) / NGINX (True) token table, canonical form"""
+    out = ctypes.create_string_buffer(1 << 20)
+    n = lib().orc_token_table(1 if nginx else 0, out, len(out))
+    if n < 0:
+        raise OracleError("token table buffer too small")
+    return json.loads(out.value.decode("utf-8"))
