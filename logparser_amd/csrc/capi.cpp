@@ -247,7 +247,7 @@ int enqueue(lp_handle* h, bool sync_count) {
         hipMemcpy(h->line_off.as<uint64_t>(), &ends[0], 8, hipMemcpyHostToDevice);
         uint8_t last = '\n';
         if (nbytes) hipMemcpy(&last, h->d_buf + nbytes - 1, 1, hipMemcpyDeviceToHost);
-        if (nbytes && last != '\n') hipMemcpy(h->line_off.as<uint64_t>() + n, &ends[1], 8, hipMemcpyHostToDevice);
+        if (nbytes && last != '\n' && last != '\r') hipMemcpy(h->line_off.as<uint64_t>() + n, &ends[1], 8, hipMemcpyHostToDevice);
     }
     h->cap_lines = cap;
     if (lp::launch_offsets(d_nlmask, nbytes, d_chunk, h->line_off.as<uint64_t>(), cap, s) != 0) return LP_E_DEVICE;

@@ -1,6 +1,7 @@
 // gfx950 kernels of the logparser_amd engine.
 //
-//   k_count_newlines  per-chunk '\n' count and '\n' bit masks (16-byte loads, SWAR byte compare)
+//   k_count_newlines  per-chunk line terminator count and terminator bit masks ('\n', lone '\r',
+//                     the '\n' of "\r\n"; 16-byte loads, SWAR byte compare)
 //   k_scan_counts     exclusive scan of the chunk counts (single workgroup); the batch's line
 //                     count, line_off[0] and the end sentinel, written on the device
 //   k_line_offsets    line start offsets from the bit masks (Hadoop LineRecordReader '\n' semantics)
@@ -33,21 +34,22 @@ namespace {
 constexpr int CHUNK = 64 * 1024;  // bytes per workgroup in the newline passes
 constexpr int NL_THREADS = 256;   // 256 threads x 16 B x 16 iterations = 64 KiB
 
-// exact per-byte "== '\n'" mask of a 32-bit word (high bit of each byte)
-__device__ __forceinline__ uint32_t nl_mask(uint32_t w) {
-    uint32_t x = w ^ 0x0A0A0A0Au;
+// exact per-byte "== c" mask of a 32-bit word (high bit of each byte)
+__device__ __forceinline__ uint32_t byte_eq(uint32_t w, uint32_t c4) {
+    uint32_t x = w ^ c4;
     return ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x | 0x7F7F7F7Fu);
 }
+__device__ __forceinline__ uint32_t bits16(uint32_t m0, uint32_t m1, uint32_t m2, uint32_t m3) {
+    return bcls::nib(m0) | (bcls::nib(m1) << 4) | (bcls::nib(m2) << 8) | (bcls::nib(m3) << 12);
+}
 
-// the 16 bytes at pos (zero past nbytes) and their '\n' masks (bit 7 of
-// each byte, one 32-bit mask per word)
-struct Piece16 {
-    uint32_t m[4];
-    __device__ __forceinline__ uint32_t count() const {
-        return __popc(m[0]) + __popc(m[1]) + __popc(m[2]) + __popc(m[3]);
-    }
-};
-__device__ __forceinline__ Piece16 nl16(const uint8_t* p, uint64_t pos, uint64_t nbytes) {
+// Line terminators of the 16 bytes at pos as a 16-bit mask (bit k = byte k),
+// Hadoop LineReader.readDefaultLine semantics (the reader behind
+// LineRecordReader, ApacheHttpdLogfileRecordReader.java:57, 115): '\n', a
+// '\r' not followed by '\n', and of "\r\n" the '\n' (the '\r' is then the
+// last byte of the line's bytes and the parse kernels drop it).  Bytes at or
+// past nbytes are not terminators; a '\r' as the buffer's last byte is.
+__device__ __forceinline__ uint32_t term16(const uint8_t* p, uint64_t pos, uint64_t nbytes) {
     uint4 v = make_uint4(0, 0, 0, 0);
     if (pos + 16 <= nbytes && ((uintptr_t)(p + pos) & 15) == 0) {
         v = *reinterpret_cast<const uint4*>(p + pos);
@@ -56,27 +58,26 @@ __device__ __forceinline__ Piece16 nl16(const uint8_t* p, uint64_t pos, uint64_t
         for (uint64_t k = pos; k < pos + 16 && k < nbytes; ++k) w[(k - pos) >> 2] |= (uint32_t)p[k] << (8 * ((k - pos) & 3));
         v = make_uint4(w[0], w[1], w[2], w[3]);
     }
-    Piece16 r;
-    r.m[0] = nl_mask(v.x);
-    r.m[1] = nl_mask(v.y);
-    r.m[2] = nl_mask(v.z);
-    r.m[3] = nl_mask(v.w);
-    if (pos + 16 > nbytes) {  // zero bytes past the end are not newlines anyway
-        for (int j = 0; j < 4; ++j)
-            for (int b = 0; b < 4; ++b)
-                if (pos + 4 * j + b >= nbytes) r.m[j] &= ~(0x80u << (8 * b));
+    uint32_t lf = bits16(byte_eq(v.x, 0x0A0A0A0Au), byte_eq(v.y, 0x0A0A0A0Au), byte_eq(v.z, 0x0A0A0A0Au),
+                         byte_eq(v.w, 0x0A0A0A0Au));
+    uint32_t cr = bits16(byte_eq(v.x, 0x0D0D0D0Du), byte_eq(v.y, 0x0D0D0D0Du), byte_eq(v.z, 0x0D0D0D0Du),
+                         byte_eq(v.w, 0x0D0D0D0Du));
+    if (pos + 16 > nbytes) {  // zero bytes past the end match neither
+        const uint32_t live = nbytes > pos ? (1u << (uint32_t)(nbytes - pos)) - 1u : 0u;
+        lf &= live;
+        cr &= live;
     }
-    return r;
+    if (cr) {
+        uint32_t next_lf = lf >> 1;  // byte k + 1 is '\n'
+        if ((cr & 0x8000u) && pos + 16 < nbytes && p[pos + 16] == '\n') next_lf |= 0x8000u;
+        cr &= ~next_lf;
+    }
+    return lf | cr;
 }
 
-// '\n' bits of a 16-byte piece as a 16-bit mask (bit k = byte k)
-__device__ __forceinline__ uint32_t piece_bits(const Piece16& pc) {
-    return bcls::nib(pc.m[0]) | (bcls::nib(pc.m[1]) << 4) | (bcls::nib(pc.m[2]) << 8) | (bcls::nib(pc.m[3]) << 12);
-}
-
-// Pass 1 of the line index: '\n' count per 64 KiB chunk, and the '\n' bit
-// mask of every 16-byte piece (1 bit per input byte) so that pass 2 reads
-// nbytes / 8 bytes instead of the input again.
+// Pass 1 of the line index: line terminators per 64 KiB chunk, and the
+// terminator bit mask of every 16-byte piece (1 bit per input byte) so that
+// pass 2 reads nbytes / 8 bytes instead of the input again.
 __global__ __launch_bounds__(NL_THREADS) void k_count_newlines(const uint8_t* __restrict__ buf, uint64_t nbytes,
                                                                 uint64_t* __restrict__ counts,
                                                                 uint16_t* __restrict__ nlmask) {
@@ -86,9 +87,8 @@ __global__ __launch_bounds__(NL_THREADS) void k_count_newlines(const uint8_t* __
         uint64_t pos = base + ((uint64_t)it * NL_THREADS + threadIdx.x) * 16;
         uint32_t m = 0;
         if (pos < nbytes) {
-            const Piece16 pc = nl16(buf, pos, nbytes);
-            c += pc.count();
-            m = piece_bits(pc);
+            m = term16(buf, pos, nbytes);
+            c += (uint32_t)__popc(m);
         }
         nlmask[pos >> 4] = (uint16_t)m;
     }
@@ -143,8 +143,8 @@ __global__ __launch_bounds__(1024) void k_scan_counts(uint64_t* __restrict__ cou
         for (int k = 0; k < 16; ++k) { part[threadIdx.x * 16 + k] = run; run += v[k]; }
         if (threadIdx.x == 63) {
             counts[n] = run;
-            // Hadoop LineRecordReader: lines = '\n' count, plus a last line without one
-            const bool open_end = nbytes > 0 && buf[nbytes - 1] != '\n';
+            // Hadoop LineRecordReader: lines = terminator count, plus a last line without one
+            const bool open_end = nbytes > 0 && buf[nbytes - 1] != '\n' && buf[nbytes - 1] != '\r';
             const int64_t lines = (int64_t)run + (open_end ? 1 : 0);
             meta->n_lines = (unsigned long long)lines;
             // cap_lines < 0: only count (the host sizes the buffers from the count)
@@ -247,7 +247,7 @@ __device__ __forceinline__ WaveLines wave_lines(const Columns& C, int64_t wave, 
     W.s = W.e = 0;
     if (W.active) {
         W.s = C.line_off[W.li];
-        W.e = C.line_off[W.li + 1] - 1;  // exclude '\n' (or the end sentinel)
+        W.e = C.line_off[W.li + 1] - 1;  // exclude the terminator (or the end sentinel); see crlf_len
     }
     W.n = (int)((W.e - W.s) > (uint64_t)0x7FFFFFFF ? 0x7FFFFFFF : (W.e - W.s));
     W.w0 = C.line_off[W.li0] & ~15ull;
@@ -256,9 +256,18 @@ __device__ __forceinline__ WaveLines wave_lines(const Columns& C, int64_t wave, 
     return W;
 }
 
+// Length of a line whose last byte (before its terminator) is `last`: the
+// '\r' of a "\r\n" terminator is not part of the line.  (A '\r' never is
+// line content: not followed by '\n' it is itself a terminator, term16.)
+__device__ __forceinline__ int crlf_len(int n, uint32_t last) { return n - (n > 0 && last == '\r' ? 1 : 0); }
+__device__ __forceinline__ int crlf_len_hbm(const uint8_t* buf, const WaveLines& W) {
+    return W.active ? crlf_len(W.n, W.n > 0 ? buf[W.e - 1] : 0u) : W.n;
+}
+
 // Stage [w0, w1) into win (LDS) and the mask planes into msk16 (two 64-bit
 // planes per 64-byte block, as 16-bit pieces).  Returns whether every byte
-// but '\n' passes the fast-path guard (then no line needs the guard scan).
+// but the terminators is TAB or printable ASCII (then no line needs the
+// guard scan of phase 1).
 __device__ __forceinline__ bool stage_window(const uint8_t* __restrict__ buf, uint64_t nbytes, uint64_t w0, uint64_t w1,
                                              uint8_t* win, uint16_t* msk16) {
     const int lane = threadIdx.x;
@@ -293,7 +302,8 @@ __device__ __forceinline__ bool stage_window(const uint8_t* __restrict__ buf, ui
                 v[j] = u32x4{word(p), word(p + 4), word(p + 8), word(p + 12)};
             }
             if (k < nv)
-                for (int w = 0; w < 4; ++w) bad |= swar::guard_bad(v[j][w]) & ~swar::eq(v[j][w], '\n');
+                for (int w = 0; w < 4; ++w)
+                    bad |= swar::guard_bad(v[j][w]) & ~swar::eq(v[j][w], '\n') & ~swar::eq(v[j][w], '\r');
             *reinterpret_cast<u32x4*>(win + 16 * k) = v[j];
             uint32_t m0, m1;
             bcls::classify16(v[j][0], v[j][1], v[j][2], v[j][3], m0, m1);
@@ -444,7 +454,8 @@ __global__ __launch_bounds__(PW) void k_parse_lines(const uint8_t* __restrict__ 
 #if LP_EXP == 11
     if (clean) return;  // experiment: stop after staging
 #endif
-    const LineT<lds_bytes, lds_u64> L{(lds_bytes)win, (uint32_t)(W.s - W.w0), W.n, (lds_u64)reinterpret_cast<uint64_t*>(msk16)};
+    const int n = W.active ? crlf_len(W.n, W.n > 0 ? win[W.e - 1 - W.w0] : 0u) : W.n;
+    const LineT<lds_bytes, lds_u64> L{(lds_bytes)win, (uint32_t)(W.s - W.w0), n, (lds_u64)reinterpret_cast<uint64_t*>(msk16)};
     WaveCounts WC;
     parse_wave(P, s_elems, C, L, W.active, W.li, stk, clean, wave, WC);
     WC.store(C, wave);
@@ -482,7 +493,8 @@ __global__ __launch_bounds__(PW) void k_parse_overflow(const uint8_t* __restrict
                 const bool clean = stage_window(buf, nbytes, a, b, win, msk16);
                 __syncthreads();
                 const bool mine = W.active && ((int)threadIdx.x >= PW / 2) == (r != 0);
-                const LineT<lds_bytes, lds_u64> L{(lds_bytes)win, mine ? (uint32_t)(W.s - a) : 0u, mine ? W.n : 0,
+                const int n = mine ? crlf_len(W.n, W.n > 0 ? win[W.e - 1 - a] : 0u) : 0;
+                const LineT<lds_bytes, lds_u64> L{(lds_bytes)win, mine ? (uint32_t)(W.s - a) : 0u, n,
                                                   (lds_u64)reinterpret_cast<uint64_t*>(msk16)};
                 parse_wave(P, s_elems, C, L, mine, W.li, stk, clean, wave, WC);
                 __syncthreads();  // this round's LDS reads are done before the next staging
@@ -492,7 +504,7 @@ __global__ __launch_bounds__(PW) void k_parse_overflow(const uint8_t* __restrict
             // leave the 4-byte words holding the line's bytes
             const LP_G uint8_t* ls = (const LP_G uint8_t*)(buf) + W.s;
             const uint32_t mis = (uint32_t)((uintptr_t)ls & 3);
-            const LineT<const LP_G uint8_t*> L{ls - mis, mis, W.n};
+            const LineT<const LP_G uint8_t*> L{ls - mis, mis, crlf_len_hbm(buf, W)};
             parse_wave(P, s_elems, C, L, W.active, W.li, stk, false, wave, WC);
             __syncthreads();
         }
@@ -519,13 +531,14 @@ __global__ __launch_bounds__(PW) void k_route_match(const uint8_t* __restrict__ 
     if (W.w1 - W.w0 <= win_cap) {
         const bool clean = stage_window(buf, nbytes, W.w0, W.w1, win, msk16);
         __syncthreads();
-        const LineT<lds_bytes, lds_u64> L{(lds_bytes)win, (uint32_t)(W.s - W.w0), W.n, (lds_u64)reinterpret_cast<uint64_t*>(msk16)};
+        const int n = W.active ? crlf_len(W.n, W.n > 0 ? win[W.e - 1 - W.w0] : 0u) : W.n;
+        const LineT<lds_bytes, lds_u64> L{(lds_bytes)win, (uint32_t)(W.s - W.w0), n, (lds_u64)reinterpret_cast<uint64_t*>(msk16)};
         if (W.active) C.fmt_match[W.li] = (uint16_t)fmt_match_word(P, s_elems, L, stk, clean);
     } else {
         __syncthreads();
         const LP_G uint8_t* ls = (const LP_G uint8_t*)(buf) + W.s;
         const uint32_t mis = (uint32_t)((uintptr_t)ls & 3);
-        const LineT<const LP_G uint8_t*> L{ls - mis, mis, W.n};
+        const LineT<const LP_G uint8_t*> L{ls - mis, mis, crlf_len_hbm(buf, W)};
         if (W.active) C.fmt_match[W.li] = (uint16_t)fmt_match_word(P, s_elems, L, stk, false);
     }
 }

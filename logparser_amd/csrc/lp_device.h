@@ -53,6 +53,8 @@ __host__ __device__ LP_INLINE bool is_hex(uint32_t c) { return is_digit(c) || ((
 __host__ __device__ LP_INLINE bool is_alpha(uint32_t c) { return ((c | 32u) - 'a') < 26u; }
 __host__ __device__ LP_INLINE bool is_alnum(uint32_t c) { return is_alpha(c) || is_digit(c); }
 __host__ __device__ LP_INLINE uint32_t hexv(uint32_t c) { return c <= '9' ? c - '0' : (c | 32u) - 'a' + 10; }
+// bytes of the UTF-8 char whose lead byte is c (lines are validated first)
+__host__ __device__ LP_INLINE int utf8_len(uint32_t c) { return c < 0x80 ? 1 : c < 0xE0 ? 2 : c < 0xF0 ? 3 : 4; }
 // chars commons-httpclient URIUtil.encode escapes with the HttpUriDissector
 // "badUriChars" set (HttpUriDissector.java:111-120): control, space, unwise
 // {}|\^[]` and <>"  (ASCII only; non-ASCII lines never reach this point)
@@ -153,6 +155,9 @@ __host__ __device__ LP_INLINE uint32_t hex(uint32_t w) {
 __host__ __device__ LP_INLINE uint32_t upper(uint32_t w) { return ge(w, 'A') & lt(w, 'Z' + 1); }
 // not printable ASCII and not TAB: the fast-path guard
 __host__ __device__ LP_INLINE uint32_t guard_bad(uint32_t w) { return (lt(w, 0x20) & ~eq(w, '\t')) | ge(w, 0x7F); }
+// controls other than TAB, and DEL: never on the fast path (bytes >= 0x80
+// are, in valid UTF-8 outside the URI stages)
+__host__ __device__ LP_INLINE uint32_t guard_ctl(uint32_t w) { return (lt(w, 0x20) & ~eq(w, '\t')) | eq(w, 0x7F); }
 // URIUtil "badUriChars" (see uri_needs_encode below), ASCII part
 __host__ __device__ LP_INLINE uint32_t needs_encode(uint32_t w) {
     return lt(w, 0x21) | ge(w, 0x7F) | (ge(w, '{') & lt(w, '~')) | (ge(w, '[') & lt(w, '_')) | eq(w, '`') |
@@ -193,13 +198,16 @@ __host__ __device__ LP_INLINE uint32_t perm(uint32_t s0, uint32_t s1, uint32_t s
     return r;
 #endif
 }
-// class bits of the 4 bytes of w (bytes >= 0x80: unspecified)
+// class bits of the 4 bytes of w; bytes >= 0x80 (UTF-8) get bit 3 only: a
+// URI event (URIUtil leaves them raw, the URI stage sends them to FALLBACK),
+// neither '"' nor \s
 __host__ __device__ LP_INLINE uint32_t bits(uint32_t w) {
     const uint32_t s = w & 0x07070707u;
     const uint32_t p1 = perm(LO1, LO0, s), p2 = perm(LO3, LO2, s);
     const uint32_t m8 = ((w >> 3) & 0x01010101u) * 0xFFu;
     const uint32_t rl = (p2 & m8) | (p1 & ~m8);
-    return rl & perm(HI1, HI0, (w >> 4) & 0x07070707u);
+    const uint32_t hb = ((w >> 7) & 0x01010101u) * 0xFFu;
+    return (rl & perm(HI1, HI0, (w >> 4) & 0x07070707u) & ~hb) | (hb & 0x08080808u);
 }
 // java.net.URI authority bytes: a second table pair whose class is the
 // bytes outside L_SERVER and L_REG_NAME (controls, space, " # % & / < > ? @
@@ -781,7 +789,7 @@ __host__ __device__ LP_INLINE int cand_first(const Program& P, const ElemV& e, c
         if (e.kind == EK_CLF_IP && p < L.n && L[p] == '-' && e.nlit && (e.lit4 & 0xFFu) != '-') return p + 1;
         return -2;  // resolved by match_line (ip_resolve)
     }
-    case EK_ANYCHAR: return p < L.n ? p + 1 : -1;  // '.': the guard already rejected line terminators
+    case EK_ANYCHAR: return p < L.n ? p + utf8_len(L[p]) : -1;  // '.': one char (the guard rejected line terminators)
     case EK_DECIMAL: return decimal_at(L, p);
     case EK_MSEC: {
         const int d = digits_end(L, p);
@@ -847,7 +855,10 @@ __host__ __device__ LP_INLINE bool ip_alt_ends(const Program& P, const LN& L, co
             m.each([&](int k) {
                 for (int h = 1; h <= 4 && hexat(p + k + h - 1); ++h) {
                     if (k + h < W) nx.add(k + h);
-                    if (p + k + h < L.n && k + h + 1 < W) nx.add(k + h + 1);  // (?::|.): any byte but a line terminator
+                    if (p + k + h < L.n) {  // (?::|.): any char but a line terminator (1-4 UTF-8 bytes)
+                        const int cl = utf8_len(L[p + k + h]);
+                        if (k + h + cl < W) nx.add(k + h + cl);
+                    }
                 }
             });
             if (!nx.any()) break;
@@ -1106,6 +1117,38 @@ __host__ __device__ LP_INLINE bool fmt_tail_ok(const Program& P, const EL& elems
     return q == 0;
 }
 
+// The line as the reference sees it after Hadoop's Text -> String decode:
+// no controls but TAB (a line never holds its terminators), no DEL, and any
+// bytes >= 0x80 are strict UTF-8 (else the decoder's U+FFFD replacements
+// would change the values) other than U+0085, U+2028 and U+2029, which
+// java.util.regex '.' does not match.  Lines with such bytes go to FALLBACK.
+template <typename LN>
+__host__ __device__ LP_INLINE bool line_text_ok(const LN& L) {
+    if (find_fwd(L, 0, L.n, [](uint32_t w) { return swar::guard_ctl(w); }) < L.n) return false;
+    int i = find_fwd(L, 0, L.n, [](uint32_t w) { return w & swar::HI; });
+    while (i < L.n) {
+        const uint32_t c = L[i];
+        if (c < 0x80) { ++i; continue; }
+        int need;
+        uint32_t cp;
+        if (c >= 0xC2 && c <= 0xDF) { need = 1; cp = c & 0x1F; }
+        else if (c >= 0xE0 && c <= 0xEF) { need = 2; cp = c & 0x0F; }
+        else if (c >= 0xF0 && c <= 0xF4) { need = 3; cp = c & 0x07; }
+        else return false;
+        if (i + need >= L.n) return false;
+        for (int r = 1; r <= need; ++r) {
+            const uint32_t d = L[i + r];
+            if ((d & 0xC0) != 0x80) return false;
+            cp = (cp << 6) | (d & 0x3F);
+        }
+        if (need == 2 && (cp < 0x800 || (cp >= 0xD800 && cp <= 0xDFFF))) return false;
+        if (need == 3 && (cp < 0x10000 || cp > 0x10FFFF)) return false;
+        if (cp == 0x85 || cp == 0x2028 || cp == 0x2029) return false;
+        i += need + 1;
+    }
+    return true;
+}
+
 // The match word of a line for sticky routing: bit f = format f matches,
 // bit 8+f = undecided on the device (FALLBACK).  Formats whose literal '"'
 // count or line tail rule them out skip the DFS.
@@ -1114,7 +1157,7 @@ __host__ __device__ LP_INLINE uint32_t fmt_match_word(const Program& P, const EL
                                                       bool clean) {
     const uint32_t all = (1u << P.n_fmt) - 1u;
     if (L.n > MAX_LINE) return all << 8;
-    if (!clean && find_fwd(L, 0, L.n, [](uint32_t w) { return swar::guard_bad(w); }) < L.n) return all << 8;
+    if (!clean && !line_text_ok(L)) return all << 8;
     uint32_t m = 0;
     NoCaps nc;
     const int quotes = count_quotes(L);
@@ -1440,10 +1483,10 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
     o.qlist.fill(0);
     o.qpend.fill(0);
     if (L.n > MAX_LINE || fmt >= P.n_fmt) { o.status = ST_FALLBACK; return; }  // too long / routing undecided
-    // fast-path guard: printable ASCII + TAB only (no \r, no line
-    // terminators, no bytes that need UTF-8 decoding or URIUtil UTF-8 bytes)
+    // fast-path guard: TAB, printable ASCII and valid UTF-8 without the
+    // chars java.util.regex '.' does not match (line_text_ok)
     LP_PROF(2);
-    if (!clean && find_fwd(L, 0, L.n, [](uint32_t w) { return swar::guard_bad(w); }) < L.n) {
+    if (!clean && !line_text_ok(L)) {
         o.status = ST_FALLBACK;
         return;
     }
@@ -1895,7 +1938,7 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
     LP_PROF(50 + 4 * u);
     for_uev_w(L, a, b, [&](int q, uint32_t w) {
         const uint32_t c = w & 0xFFu;
-        if (c == '#' || c == ';') { resume = q; return false; }
+        if (c == '#' || c == ';' || c >= 0x80) { resume = q; return false; }
         if (c == '%') {
             if (q + 2 >= b || !is_hex((w >> 8) & 0xFFu) || !is_hex((w >> 16) & 0xFFu)) { resume = q; return false; }
             first_pct = first_pct < 0 ? q : first_pct;
@@ -1930,6 +1973,9 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
 #if LP_EXP == 1
         return true;
 #endif
+        // non-ASCII: URIUtil.encode keeps the UTF-8 bytes raw and the
+        // dissector reads them back as US-ASCII (U+FFFD each); not on the device
+        if (c >= 0x80) { st = ST_FALLBACK; return false; }
         if (c == '%') {
             if (q + 2 >= b || !is_hex(L[q + 1]) || !is_hex(L[q + 2])) { st = ST_FALLBACK; return false; }  // BAD_EXCAPE_PATTERN
             if (first_pct < 0) first_pct = q;

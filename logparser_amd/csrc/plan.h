@@ -76,7 +76,7 @@ struct ResultView {
     int64_t n = 0;
     const uint64_t* line_off = nullptr;   // [n + 1]
     const uint8_t* status = nullptr;
-    const uint8_t* input = nullptr;       // line i = input[line_off[i], line_off[i + 1] - 1)
+    const uint8_t* input = nullptr;       // line i = input[line_off[i], line_off[i + 1] - 1) minus a "\r\n"'s '\r'
     const uint8_t* arena = nullptr;
     const uint64_t* arena_base = nullptr; // per line: arena offset of its region
     // arena offsets b are device offsets of ARENA_SHARDS shards of shard_cap

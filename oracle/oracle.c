@@ -2676,7 +2676,14 @@ int orc_parse(orc_parser *p, const char *line, int len, char *out, int out_cap) 
             unsigned c = u[i];
             int need = c < 0x80 ? 0 : (c >= 0xC2 && c <= 0xDF) ? 1 : (c >= 0xE0 && c <= 0xEF) ? 2 : (c >= 0xF0 && c <= 0xF4) ? 3 : -1;
             if (need < 0) return ORC_UNSUPPORTED;
-            for (int k = 1; k <= need; k++) if (i + k >= len || (u[i + k] & 0xC0) != 0x80) return ORC_UNSUPPORTED;
+            unsigned cp = need == 1 ? (c & 0x1F) : need == 2 ? (c & 0x0F) : (c & 0x07);
+            for (int k = 1; k <= need; k++) {
+                if (i + k >= len || (u[i + k] & 0xC0) != 0x80) return ORC_UNSUPPORTED;
+                cp = (cp << 6) | (u[i + k] & 0x3F);
+            }
+            /* overlong forms, surrogates and code points past U+10FFFF decode to U+FFFD */
+            if ((need == 2 && (cp < 0x800 || (cp >= 0xD800 && cp <= 0xDFFF))) || (need == 3 && (cp < 0x10000 || cp > 0x10FFFF)))
+                return ORC_UNSUPPORTED;
             i += need + 1;
         }
     }

@@ -378,3 +378,30 @@ def test_setup_vectors_planner(emu, vectors):
         with pytest.raises(RuntimeError) as ei:
             emu.Emu(c["logformat"], c["fields"])
         assert "failed -2" in str(ei.value) and c["message_contains"] in str(ei.value), c["source"]
+
+
+def test_utf8_user_agents_emulated(oracle, emu):
+    """UTF-8 user agents / users stay on the device path with exact records;
+    UTF-8 in URIs, U+0085/U+2028/U+2029 and invalid sequences go to FALLBACK"""
+    import corpora
+    base = lpa.synth_combined(20261016, 0, 1500).split(b"\n")[:-1]
+    o = oracle.Oracle("combined", all_paths(oracle))
+    e = emu.Emu("combined", all_paths(oracle))
+    s = compare(o, e, corpora.utf8_ua_lines(base, 5), allow_fallback=False)
+    assert s["ok"] == 1500, s
+    hard = corpora.utf8_hard_lines(base, 6)
+    s = compare(o, e, hard)
+    assert s["fallback"] > 500 and s["ok"] > 200, s
+    # NGINX: CLF_IP tokens (the IPv6 '.' consumes one char, not one byte)
+    paths = oracle.possible_paths(NGINX)
+    o = oracle.Oracle(NGINX, paths)
+    e = emu.Emu(NGINX, paths)
+    lines = lpa.synth(lpa.SYNTH_NGINX, 20261018, 0, 800).split(b"\n")[:-1]
+    rng = random.Random(3)
+    u8 = []
+    for l in lines:
+        i = l.index(b" - ")
+        u8.append(l[:i] + b" - " + rng.choice(corpora.USERS).encode() + l[l.index(b" ", i + 3):])
+    s = compare(o, e, u8)
+    assert s["ok"] > 700, s
+    compare(o, e, [b"1:2\xc3\xa9 - - [" + l.split(b"[", 1)[1] for l in lines[:50]])

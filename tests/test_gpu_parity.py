@@ -22,9 +22,11 @@ def paths(oracle, fmt="combined"):
     return _PATHS[fmt]
 
 
-def gpu_vs_oracle(oracle, fmt, fields, lines, allow_fallback=True):
+def gpu_vs_oracle(oracle, fmt, fields, lines, allow_fallback=True, data=None):
+    """lines: the expected lines; data: the batch buffer (default: the lines + '\n')"""
     p = lpa.HttpdLoglineParser(fmt, fields)
-    data = b"".join(l + b"\n" for l in lines)
+    if data is None:
+        data = b"".join(l + b"\n" for l in lines)
     r = p.parse_batch(data)
     assert r.n_lines == len(lines)
     o = oracle.Oracle(fmt, fields)
@@ -418,3 +420,45 @@ def test_result_emit_replays_setter_calls(oracle):
                     if hit:
                         rec.setdefault(key, []).append(val)
             assert rec == json.loads(r.record_json(i)), i
+
+
+def test_crlf_terminators_gpu(oracle):
+    """Hadoop LineRecordReader terminators: "\\r\\n", lone '\\r' and '\\n' end a
+    line and are not part of it (ApacheHttpdLogfileRecordReader.java:57, 115)"""
+    import corpora
+    lines = lpa.synth_combined(20261019, 0, 20000).split(b"\n")[:-1]
+    data = corpora.crlf_join(lines, 9)
+    assert corpora.split_hadoop(data) == lines
+    s, r = gpu_vs_oracle(oracle, "combined", paths(oracle), lines, allow_fallback=False, data=data)
+    assert s["ok"] == 20000, s
+    # terminator corners: counts and per-line status against the reference split
+    rng = random.Random(4)
+    pieces = [b"\r", b"\n", b"\r\n", b"\r\r", b"\n\r", b"\r\n\r\n", b"-", b"x", lines[0], lines[1]]
+    o = oracle.Oracle("combined", paths(oracle))
+    p = lpa.HttpdLoglineParser("combined", paths(oracle))
+    for t in range(40):
+        buf = b"".join(rng.choice(pieces) for _ in range(rng.randrange(1, 30)))
+        want = corpora.split_hadoop(buf)
+        r = p.parse_batch(buf)
+        assert r.n_lines == len(want), (buf, r.n_lines, len(want))
+        for i, l in enumerate(want):
+            s1, r1 = o.parse_raw(l)
+            assert int(r.status[i]) == s1, (buf, i, l)
+            if s1 == oracle.OK:
+                assert r.record_json(i) == r1
+
+
+def test_utf8_text_gpu(oracle):
+    """UTF-8 user agents and users stay on the device with exact records;
+    UTF-8 in URIs, U+0085/U+2028/U+2029 and invalid sequences go to FALLBACK"""
+    import corpora
+    base = lpa.synth_combined(20261016, 0, 20000).split(b"\n")[:-1]
+    s, _ = gpu_vs_oracle(oracle, "combined", paths(oracle), corpora.utf8_ua_lines(base, 5), allow_fallback=False)
+    assert s["ok"] == 20000, s
+    s, _ = gpu_vs_oracle(oracle, "combined", paths(oracle), corpora.utf8_hard_lines(base[:5000], 6))
+    assert s["fallback"] > 1500 and s["ok"] > 1000, s
+    # both at once: UTF-8 user agents in a CRLF file
+    lines = corpora.utf8_ua_lines(base, 8)
+    s, _ = gpu_vs_oracle(oracle, "combined", paths(oracle), lines, allow_fallback=False,
+                         data=corpora.crlf_join(lines, 10))
+    assert s["ok"] == 20000, s

@@ -83,3 +83,102 @@ def test_two_rank_gloo_counters(oracle):
     assert out[0][:4] == ref and out[1][:4] == ref
     assert ref[2] == 2
     assert out[0][4] == out[1][4] == 2.0
+
+
+def test_line_aligned_ranges_cr_terminators():
+    import corpora
+    lines = lpa.synth_combined(7, 0, 3000).split(b"\n")[:-1]
+    data = corpora.crlf_join(lines, 3)
+    for parts in (2, 3, 7):
+        got = []
+        for a, b in line_aligned_ranges(data, parts):
+            got += corpora.split_hadoop(data[a:b])
+        assert got == lines
+    from logparser_amd.shard import count_terminators
+    assert count_terminators(np.frombuffer(b"a\r\nb\rc\n\r\r\n", dtype=np.uint8)) == 5
+
+
+def _stream_split_local(chunks, rank, world, group=None):
+    """stream_split over numpy home chunks (the CPU stand-in of device buffers)"""
+    from logparser_amd.shard import count_terminators, stream_split
+    import corpora
+    mine = np.frombuffer(chunks[rank], dtype=np.uint8)
+    n_lines = len(corpora.split_hadoop(chunks[rank]))
+    return stream_split(len(mine), n_lines, lambda off, n: mine[off:off + n],
+                        lambda a, b: count_terminators(mine[a:b]), group=group)
+
+
+def test_stream_split_matches_line_aligned_ranges_single_process():
+    """stream_split's cuts == line_aligned_ranges on the concatenated stream
+    (the collectives replaced by the loop over ranks the all-reduce merges)"""
+    import corpora
+    lines = lpa.synth_combined(8, 0, 4000).split(b"\n")[:-1]
+    for world, sizes in ((2, [2100, 1900]), (3, [1000, 1500, 1500]), (4, [50, 3000, 900, 50])):
+        data_lines, chunks, k = lines, [], 0
+        for sz in sizes:
+            part = data_lines[k:k + sz]
+            k += sz
+            chunks.append(corpora.crlf_join(part, k) + (b"\r\n" if k < len(lines) else b""))
+        stream = b"".join(chunks)
+        want = line_aligned_ranges(stream, world)
+        # emulate the all-gather / all-reduce: every rank resolves its own cuts
+        g = np.cumsum([0] + [len(c) for c in chunks])
+        gl = np.cumsum([0] + [len(corpora.split_hadoop(c)) for c in chunks])
+        pos = [0] * (world + 1)
+        first = [0] * (world + 1)
+        for r in range(world):
+            f, p = _split_as_rank(chunks, r, world)
+            for j in range(1, world):
+                s = (j * len(stream)) // world
+                if g[r] <= s < g[r + 1]:
+                    pos[j], first[j] = p[j], f[j]
+        pos[world], first[world] = len(stream), int(gl[-1])
+        assert [(pos[j], max(pos[j], pos[j + 1])) for j in range(world)] == want
+        for j in range(world):
+            assert first[j] == len(corpora.split_hadoop(stream[:pos[j]]))
+
+
+def _split_as_rank(chunks, rank, world):
+    """one rank's view of stream_split without a process group: the all_gather
+    and the all-reduce are replaced by their results over the given chunks"""
+    import corpora
+    from unittest import mock
+    import torch.distributed as dist
+    sizes = [torch.tensor([len(c), len(corpora.split_hadoop(c))]) for c in chunks]
+
+    def all_gather(out, t, group=None):
+        for i, v in enumerate(sizes):
+            out[i].copy_(v)
+
+    with mock.patch.object(dist, "is_initialized", return_value=True), \
+            mock.patch.object(dist, "get_world_size", return_value=world), \
+            mock.patch.object(dist, "get_rank", return_value=rank), \
+            mock.patch.object(dist, "all_gather", side_effect=all_gather), \
+            mock.patch.object(dist, "all_reduce", side_effect=lambda *a, **k: None):
+        return _stream_split_local(chunks, rank, world)
+
+
+def _split_worker(rank, world, port, chunks, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out[rank] = _stream_split_local(chunks, rank, world)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_two_rank_gloo_stream_split():
+    """world-size-2 gloo: all_gather of chunk sizes / line counts, all-reduce of
+    the cuts; both ranks agree, and the splits are line_aligned_ranges' with
+    global line numbers"""
+    import corpora
+    lines = lpa.synth_combined(9, 0, 3000).split(b"\n")[:-1]
+    chunks = [corpora.crlf_join(lines[:1700], 1) + b"\r\n", corpora.crlf_join(lines[1700:], 2)]
+    stream = b"".join(chunks)
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_split_worker, args=(2, _free_port(), chunks, out), nprocs=2, join=True)
+    assert out[0] == out[1]
+    first, pos = out[0]
+    assert [(pos[0], pos[1]), (pos[1], pos[2])] == line_aligned_ranges(stream, 2)
+    assert first == [0, len(corpora.split_hadoop(stream[:pos[1]])), 3000]
