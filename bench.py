@@ -41,17 +41,19 @@ def log(*a):
         print(*a, file=sys.stderr, flush=True)
 
 
-def generate_to_device(lpa, torch, workload, first_line, n_lines, device, chunk=1 << 20, workers=16, batch_bytes=0):
+def generate_to_device(lpa, torch, workload, first_line, n_lines, device, chunk=1 << 20, workers=16, batch_bytes=0,
+                       front=0):
     """Deterministic synthetic lines [first_line, first_line+n_lines) straight
-    into one HBM buffer (host generation in parallel chunks, H2D in order).
-    With batch_bytes, consecutive chunks are grouped into batches of about
-    that size, each starting 4 KiB-aligned (as a streaming reader's staging
-    buffers would).  Returns (buffer, bytes of lines, [(offset, bytes)] batches)."""
-    upper = n_lines * 320 + (1 << 20)
+    into one HBM buffer at offset `front` (host generation in parallel chunks,
+    H2D in order).  With batch_bytes, consecutive chunks are grouped into
+    batches of about that size, each starting 4 KiB-aligned (as a streaming
+    reader's staging buffers would).  Returns (buffer, bytes of lines,
+    [(offset, bytes)] batches)."""
+    upper = front + n_lines * 320 + (1 << 20)
     dev = torch.empty(upper, dtype=torch.uint8, device=device)
-    pos = 0
+    pos = front
     batches = []
-    bstart = 0
+    bstart = front
     starts = list(range(first_line, first_line + n_lines, chunk))
     with cf.ThreadPoolExecutor(max_workers=workers) as ex:
         futs = []
@@ -83,6 +85,61 @@ def generate_to_device(lpa, torch, workload, first_line, n_lines, device, chunk=
     torch.cuda.synchronize()
     batches.append((bstart, pos - bstart))
     return dev, sum(b[1] for b in batches), batches
+
+
+def device_terminators(torch, x, piece=1 << 30):
+    """Hadoop line terminators in the device bytes x ('\n' + lone '\r'), in 1 GiB pieces"""
+    n, lf, cr, crlf = x.numel(), 0, 0, 0
+    for a in range(0, n, piece):
+        v = x[a:min(n, a + piece + 1)]  # one byte of overlap: a "\r\n" across pieces
+        body = v[:min(piece, n - a)]
+        lf += int((body == 10).sum())
+        c = body == 13
+        cr += int(c.sum())
+        if len(v) > 1:
+            crlf += int(((v[:-1] == 13) & (v[1:] == 10))[:len(body)].sum())
+    return lf + cr - crlf
+
+
+def split_stream(lpa, torch, buf, front, nbytes, workload, lines_per_rank, rank, device):
+    """This rank's Hadoop split of ONE stream: the ranks' home chunks (lines
+    [r L, (r+1) L) of the deterministic synthetic stream) are consecutive
+    pieces of it; logparser_amd.shard.stream_split places the cuts at equal
+    byte offsets (all_gather of the chunk sizes / line counts, all-reduce of
+    the cuts, which also gives each split's global first line number).  The
+    lines of this split outside the home chunk (next to a neighbour's) are
+    produced the way a split reader reads past its end: from the stream
+    itself (here, the deterministic generator) -- never moved between GPUs.
+    Returns ((offset, bytes) of the split in buf, first lines, byte cuts)."""
+    from logparser_amd.shard import stream_split
+    home = buf[front:front + nbytes]
+    first, pos = stream_split(nbytes, lines_per_rank,
+                              lambda off, n: home[off:off + n].cpu().numpy(),
+                              lambda a, b: device_terminators(torch, home[a:b]), device=device)
+    h0, h1 = rank * lines_per_rank, (rank + 1) * lines_per_rank
+    f0, f1 = first[rank], first[rank + 1]
+    seed = SEEDS[workload]
+    start, end = front, front + nbytes
+    if f0 < h0:    # the split starts in the previous rank's chunk
+        pre = lpa.synth(workload, seed, f0, h0 - f0)
+        if len(pre) > front:
+            raise RuntimeError("split prefix larger than the reserved front")
+        buf[front - len(pre):front].copy_(torch.frombuffer(bytearray(pre), dtype=torch.uint8))
+        start = front - len(pre)
+    elif f0 > h0:
+        start = front + len(lpa.synth(workload, seed, h0, min(f0, h1) - h0))
+    if f1 > h1:    # the split ends in the next rank's chunk
+        post = lpa.synth(workload, seed, h1, f1 - h1)
+        if end + len(post) > buf.numel():
+            raise RuntimeError("split suffix past the device buffer")
+        buf[end:end + len(post)].copy_(torch.frombuffer(bytearray(post), dtype=torch.uint8))
+        end += len(post)
+    elif f1 < h1:
+        end = front + nbytes - len(lpa.synth(workload, seed, max(f1, h0), h1 - max(f1, h0)))
+    end = max(end, start)
+    if buf.is_cuda:
+        torch.cuda.synchronize()
+    return (start, end - start), first, pos
 
 
 def pcie_inclusive(torch, parser, buf, batches, max_bytes):
@@ -259,8 +316,20 @@ def main():
     fields = lpa.get_possible_paths(fmt) if args.fields == "all" else args.fields.split(",")
     log("rank %d/%d: generating %d lines (config %d, seed %d) on %s" % (rank, world, args.lines, wl, SEEDS[wl], device))
     batch_mb = args.batch_mb if args.batch_mb is not None else (1024 if wl == 5 else 0)
+    front = (256 << 20) if (world > 1 and wl != 5) else 0
     buf, nbytes, batches = generate_to_device(lpa, torch, wl, rank * args.lines, args.lines, device,
-                                              batch_bytes=batch_mb << 20)
+                                              batch_bytes=batch_mb << 20, front=front)
+    split = None
+    if world > 1 and wl != 5 and not batch_mb:
+        # one stream, newline-aligned Hadoop splits (config 5 keeps one corpus
+        # per rank: its sticky format state would need the k-state scan of
+        # SURVEY.md 8(e) across the splits)
+        (soff, sbytes), first, cuts = split_stream(lpa, torch, buf, front, nbytes, wl, args.lines, rank, device)
+        batches = [(soff, sbytes)]
+        nbytes = sbytes
+        split = {"first_line": first, "byte_cuts": cuts}
+        log("rank %d split: lines [%d, %d), bytes [%d, %d)" % (rank, first[rank], first[rank + 1], cuts[rank],
+                                                                cuts[rank + 1]))
     log("input resident in HBM: %.2f GB in %d batch(es)" % (nbytes / 1e9, len(batches)))
 
     parser = lpa.HttpdLoglineParser(fmt, fields, device=local)
@@ -298,8 +367,14 @@ def main():
     torch.cuda.synchronize()
     elapsed = max_over_ranks(time.perf_counter() - t0, device=device)
 
-    total_bytes = nbytes * world * args.steps
-    total_lines = stats["lines"] * world * args.steps
+    if split is not None:  # the whole stream, every split once per step
+        total_bytes = split["byte_cuts"][-1] * args.steps
+        total_lines = split["first_line"][-1] * args.steps
+        if int(counters[0]) != split["first_line"][-1]:
+            raise RuntimeError("all-reduced line count %d != the stream's %d" % (int(counters[0]), split["first_line"][-1]))
+    else:
+        total_bytes = nbytes * world * args.steps
+        total_lines = stats["lines"] * world * args.steps
     avg_parse = sum(parse_ms) / len(parse_ms)
     algo_bytes = stats["bytes_in"] + stats["bytes_out"]
     achieved = algo_bytes / (avg_parse / 1e3) / 1e9
@@ -324,7 +399,9 @@ def main():
             "logformat": fmt,
             "lines_per_gpu": stats["lines"],
             "bytes_per_gpu": nbytes,
-            "parallelism": "dp%d (newline-aligned shards, RCCL counter all-reduce)" % world,
+            "parallelism": ("dp%d (one stream in Hadoop newline-aligned splits: all_gather of chunk sizes, "
+                            "all-reduce of the cuts; RCCL counter all-reduce)" % world) if split is not None else
+                           "dp%d (one corpus per rank; RCCL counter all-reduce)" % world,
             "batches_per_step": len(batches),
         },
         "status_counts": {k: int(stats[k]) for k in ("lines", "ok", "bad", "fallback")},

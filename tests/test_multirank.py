@@ -182,3 +182,38 @@ def test_two_rank_gloo_stream_split():
     first, pos = out[0]
     assert [(pos[0], pos[1]), (pos[1], pos[2])] == line_aligned_ranges(stream, 2)
     assert first == [0, len(corpora.split_hadoop(stream[:pos[1]])), 3000]
+
+
+def _bench_split_worker(rank, world, port, L, out):
+    """bench.py's split of one synthetic stream (CPU tensors for the HBM buffer)"""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    home = lpa.synth(2, bench.SEEDS[2], rank * L, L)
+    front = 1 << 20
+    buf = torch.zeros(front + len(home) + (1 << 20), dtype=torch.uint8)
+    buf[front:front + len(home)] = torch.frombuffer(bytearray(home), dtype=torch.uint8)
+    (off, nb), first, cuts = bench.split_stream(lpa, torch, buf, front, len(home), 2, L, rank, None)
+    out[rank] = (bytes(buf[off:off + nb].numpy()), first, cuts)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_bench_stream_split_gloo():
+    """bench.py --gpus N on one stream: each rank's batch is exactly its
+    Hadoop split of the concatenated stream, and the splits tile it"""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    L, world = 1500, 3
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_bench_split_worker, args=(world, _free_port(), L, out), nprocs=world, join=True)
+    stream = lpa.synth(2, 20261015, 0, world * L)
+    want = line_aligned_ranges(stream, world)
+    assert out[0][1] == out[1][1] == out[2][1]
+    for r in range(world):
+        a, b = want[r]
+        assert out[r][0] == stream[a:b], r
+        assert out[r][2][r] == a
+    assert out[0][1][-1] == world * L
