@@ -419,6 +419,17 @@ def main():
         },
         "cpu_baseline": None,
     }
+    # run histograms of the last step's batch (device kernel), all-reduced over the ranks
+    # (outside the timed region)
+    hist = torch.zeros(lpa.HIST_WORDS, dtype=torch.int64, device=device)
+    if len(batches) == 1:
+        parser.histograms(device_ptr=hist.data_ptr())
+        reduce_counters(hist)
+        hd = lpa.decode_histograms(hist.cpu().tolist())
+        top = sorted(hd["status"].items(), key=lambda kv: -kv[1])[:6]
+        result["histograms"] = {"lines": hd["lines"], "ok": hd["ok"], "bad": hd["bad"], "fallback": hd["fallback"],
+                                "status_top": {str(c): v for c, v in top}, "methods": hd["methods"],
+                                "note": "lp_histograms of the last step (all ranks, RCCL all-reduce), untimed"}
     if wl == 5:
         result["config"]["formats"] = fmt.split("\n")
         result["config"]["corpus_bytes_all_ranks"] = total_bytes

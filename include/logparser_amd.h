@@ -127,6 +127,35 @@ int lp_counters(lp_handle *h, uint64_t *out, int n);
  * [2] parse kernel.  Returns the number of values written. */
 int lp_last_timing(lp_handle *h, float *out_ms, int n);
 
+/* Run histograms of the last batch, computed on the device (SURVEY.md §5
+ * counters; multi-GPU callers all-reduce them, e.g. over RCCL).  out: 1024
+ * u64 words, host memory, or device memory on the handle's device when
+ * out_on_device (then usable directly as an all-reduce buffer).  The batch's
+ * input must still be valid.  Layout (word: count):
+ *   0 lines, 1 OK, 2 BAD, 3 FALLBACK lines
+ *   16 + k: OK lines whose captured token slot k is "-" (null)
+ *   32 + k: OK lines whose token slot k is present and non-empty
+ *   48: OK lines whose status value (token request.status.last, else
+ *       request.status, if requested) is not a code 100..599
+ *   64 + m: OK lines by request method (first-line dissector, if requested):
+ *       m = 0 GET 1 POST 2 HEAD 3 PUT 4 DELETE 5 OPTIONS 6 PATCH 7 CONNECT
+ *       8 TRACE 9 PROPFIND 10 MKCOL 11 COPY 12 MOVE 13 LOCK 14 UNLOCK
+ *       15 other, 16 no method
+ *   100 + c: OK lines with status code c (100 <= c <= 599)
+ * Replaces the reference's Hadoop counters (ApacheHttpdLogfileRecordReader.java:118-120)
+ * for a batch; returns LP_OK or an error. */
+#define LP_HIST_WORDS 1024
+#define LP_HIST_LINES 0
+#define LP_HIST_OK 1
+#define LP_HIST_BAD 2
+#define LP_HIST_FALLBACK 3
+#define LP_HIST_TOK_NULL 16
+#define LP_HIST_TOK_PRESENT 32
+#define LP_HIST_STATUS_OTHER 48
+#define LP_HIST_METHOD 64
+#define LP_HIST_STATUS 100
+int lp_histograms(lp_handle *h, uint64_t *out, int out_on_device);
+
 /* Algorithmic bytes of the last batch: [0] input bytes read, [1] bytes of
  * SoA results + arena written (for roofline accounting). */
 int lp_last_bytes(lp_handle *h, uint64_t *out, int n);

@@ -110,6 +110,7 @@ def lib():
     L.lp_line_record_json.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_char_p, ctypes.c_size_t]
     L.lp_counters.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
     L.lp_last_timing.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.c_int]
+    L.lp_histograms.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
     L.lp_last_bytes.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]
     L.lp_set_option.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int64]
     L.lp_reserve.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint64]
@@ -223,6 +224,10 @@ class BatchResult:
 
     def line_offset(self, i):
         return lib().lp_line_offset(self._p._h, i)
+
+    def histograms(self):
+        """lp_histograms into host memory: a dict view of the run counters"""
+        return decode_histograms(self._p.histograms())
 
     def copy_to_host(self, with_input=True, buf=None):
         """lp_result_copy: every result of the batch in one host buffer (a
@@ -352,6 +357,22 @@ class HttpdLoglineParser:
             raise EngineUnavailable("lp_parse_batch failed: %d" % rc)
         return BatchResult(self)
 
+    def histograms(self, device_ptr=None):
+        """lp_histograms of the last batch: the 1024 u64 words (numpy) in host
+        memory, or written to device_ptr (a device buffer of 8 KiB on the
+        handle's device, e.g. a torch tensor to all-reduce) when given"""
+        self._ensure()
+        if device_ptr is not None:
+            rc = lib().lp_histograms(self._h, ctypes.c_void_p(device_ptr), 1)
+            if rc != LP_OK:
+                raise EngineUnavailable("lp_histograms failed: %d" % rc)
+            return None
+        out = np.zeros(HIST_WORDS, dtype=np.uint64)
+        rc = lib().lp_histograms(self._h, out.ctypes.data, 0)
+        if rc != LP_OK:
+            raise EngineUnavailable("lp_histograms failed: %d" % rc)
+        return out
+
     def run(self, data_ptr, nbytes, on_device=True, stream=None):
         """Lean batch call for benchmarks/pipelines: parse nbytes at data_ptr
         (a device pointer when on_device), wait, and return the device
@@ -408,3 +429,21 @@ class HttpdLoglineParser:
             self._close()
         except Exception:
             pass
+
+
+# lp_histograms layout (include/logparser_amd.h)
+HIST_WORDS = 1024
+HIST_METHODS = ["GET", "POST", "HEAD", "PUT", "DELETE", "OPTIONS", "PATCH", "CONNECT", "TRACE", "PROPFIND", "MKCOL",
+                "COPY", "MOVE", "LOCK", "UNLOCK", "(other)", "(none)"]
+
+
+def decode_histograms(h):
+    """the words of lp_histograms (or their all-reduced sum) as a dict"""
+    h = [int(x) for x in h]
+    return {
+        "lines": h[0], "ok": h[1], "bad": h[2], "fallback": h[3],
+        "token_null": h[16:32], "token_present": h[32:48],
+        "status_other": h[48],
+        "methods": {m: h[64 + i] for i, m in enumerate(HIST_METHODS) if h[64 + i]},
+        "status": {c: h[100 + c] for c in range(100, 600) if h[100 + c]},
+    }

@@ -56,7 +56,7 @@ struct lp_handle {
     int compile_status = LP_OK;
     int device = 0;
     hipStream_t stream = nullptr;
-    DevBuf input, chunk, line_off, cols, arena, meta, waves, args, route, ovf;
+    DevBuf input, chunk, line_off, cols, arena, meta, waves, args, route, ovf, hist;
     lp::DeviceArgs host_args{};
     lp::Columns C{};
     std::vector<ColSpec> specs;
@@ -609,6 +609,31 @@ int lp_counters(lp_handle* h, uint64_t* out, int n) {
     if (st != LP_OK) return st;
     for (int k = 0; k < n && k < 4; ++k) out[k] = h->counters[k];
     return n < 4 ? n : 4;
+}
+
+int lp_histograms(lp_handle* h, uint64_t* out, int out_on_device) {
+    if (!h || !out) return LP_E_INVALID;
+    const int st = ensure_synced(h);
+    if (st != LP_OK) return st;
+    if (!h->valid) return LP_E_INVALID;
+    static_assert(lp::HIST_WORDS == LP_HIST_WORDS, "histogram layout");
+    if (!h->plan.device_ok()) {  // every line FALLBACK
+        std::vector<uint64_t> v(LP_HIST_WORDS, 0);
+        v[LP_HIST_LINES] = h->counters[0];
+        v[LP_HIST_FALLBACK] = h->counters[3];
+        if (!out_on_device) memcpy(out, v.data(), 8 * v.size());
+        else if (hipMemcpy(out, v.data(), 8 * v.size(), hipMemcpyHostToDevice) != hipSuccess) return LP_E_DEVICE;
+        return LP_OK;
+    }
+    uint64_t* d = out;
+    if (!out_on_device) {
+        if (!h->hist.ensure(8 * (size_t)LP_HIST_WORDS)) return LP_E_NOMEM;
+        d = h->hist.as<uint64_t>();
+    }
+    if (lp::launch_histograms(h->args.as<lp::DeviceArgs>(), h->d_buf, h->n_lines, d, h->stream) != 0) return LP_E_DEVICE;
+    if (!out_on_device && hipMemcpyAsync(out, d, 8 * (size_t)LP_HIST_WORDS, hipMemcpyDeviceToHost, h->stream) != hipSuccess)
+        return LP_E_DEVICE;
+    return hipStreamSynchronize(h->stream) == hipSuccess ? LP_OK : LP_E_DEVICE;
 }
 
 int lp_last_timing(lp_handle* h, float* out, int n) {

@@ -51,4 +51,9 @@ constexpr int FMT_CHUNK = 4096;
 __host__ __device__ inline int64_t fmt_chunks(int64_t n_lines) { return (n_lines + FMT_CHUNK - 1) / FMT_CHUNK; }
 int launch_route(const DeviceArgs* d_args, int64_t cap_lines, hipStream_t s);
 
+// run histograms of the parsed batch (buf: its input) into hist
+// (HIST_WORDS u64, zeroed here): layout in include/logparser_amd.h
+constexpr int HIST_WORDS = 1024;
+int launch_histograms(const DeviceArgs* d_args, const uint8_t* buf, int64_t cap_lines, uint64_t* hist, hipStream_t s);
+
 }  // namespace lp

@@ -24,6 +24,8 @@
 
 #define LP_KERNEL_TU 1  // device column pointers are global-memory pointers (lp_program.h)
 
+#include <algorithm>
+
 #include "kernels.h"
 #include "lp_device.h"
 
@@ -639,6 +641,71 @@ __global__ __launch_bounds__(PW) void k_fmt_apply(const DeviceArgs* __restrict__
     }
 }
 
+// ------------------------------------------------------------- histograms
+// Run counters of a parsed batch (device counters all-reduced
+// over RCCL by multi-GPU callers): per-status line counts, per-token null /
+// present counts, response status codes and request methods of the OK lines.
+// Grid-stride over lines, one LDS histogram per block, flushed with global
+// atomics (a few thousand per launch).
+__device__ __constant__ const char HIST_METHODS[15][10] = {
+    "GET", "POST", "HEAD", "PUT", "DELETE", "OPTIONS", "PATCH", "CONNECT", "TRACE",
+    "PROPFIND", "MKCOL", "COPY", "MOVE", "LOCK", "UNLOCK"};
+
+__global__ __launch_bounds__(256) void k_histograms(const DeviceArgs* __restrict__ args, const uint8_t* __restrict__ buf,
+                                                    unsigned long long* __restrict__ hist) {
+    const Program& P = args->prog;
+    const Columns& C = args->cols;
+    __shared__ unsigned long long h[HIST_WORDS];
+    for (int k = threadIdx.x; k < HIST_WORDS; k += blockDim.x) h[k] = 0;
+    __syncthreads();
+    const int64_t n = C.meta->cap_ovf ? 0 : (int64_t)C.meta->n_lines;
+    for (int64_t li = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; li < n; li += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t st = C.status[li] < 3 ? C.status[li] : 2u;
+        atomicAdd(&h[0], 1ull);
+        atomicAdd(&h[1 + st], 1ull);
+        if (st != ST_OK) continue;
+        const int fmt = P.n_fmt > 1 ? (int)C.fmt_id[li] : 0;
+        if (fmt >= P.n_fmt) continue;
+        const uint8_t* line = buf + C.line_off[li];
+        const uint32_t flags = C.tok_flags[li];
+        for (int k = 0; k < P.n_tok; ++k) {
+            const uint32_t sp = C.tok_span[k][li];
+            if ((flags >> k) & 1u) atomicAdd(&h[16 + k], 1ull);
+            else if ((sp >> 16) > (sp & 0xFFFFu)) atomicAdd(&h[32 + k], 1ull);
+        }
+        const int sk = P.hist_status[fmt];
+        if (sk >= 0) {
+            const uint32_t sp = C.tok_span[sk][li];
+            const uint32_t a = sp & 0xFFFFu, b = sp >> 16;
+            int code = -1;
+            if (b - a == 3 && !((flags >> sk) & 1u)) {
+                const uint32_t d0 = line[a] - '0', d1 = line[a + 1] - '0', d2 = line[a + 2] - '0';
+                if (d0 < 10 && d1 < 10 && d2 < 10) code = (int)(d0 * 100 + d1 * 10 + d2);
+            }
+            if (code >= 100 && code <= 599) atomicAdd(&h[100 + code], 1ull);
+            else atomicAdd(&h[48], 1ull);
+        }
+        const int f = P.hist_fl[fmt];
+        if (f >= 0) {
+            const uint32_t sp = C.fl_method[f][li];
+            const uint32_t a = sp & 0xFFFFu, b = sp >> 16;
+            int m = 15;
+            if (b <= a) m = 16;  // no method (null or empty first line, or neither regex matched)
+            else if (b - a <= 9) {
+                for (int t = 0; t < 15 && m == 15; ++t) {
+                    uint32_t q = 0;
+                    while (q < b - a && HIST_METHODS[t][q] == (char)line[a + q]) ++q;
+                    if (q == b - a && HIST_METHODS[t][q] == 0) m = t;
+                }
+            }
+            atomicAdd(&h[64 + m], 1ull);
+        }
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < HIST_WORDS; k += blockDim.x)
+        if (h[k]) atomicAdd(&hist[k], h[k]);
+}
+
 // LDS window of a wave: sized to the most waves per CU that still leave >= 4 %
 // over the mean 64 lines (the few windows that do not fit go to the direct
 // kernel).  Measured on gfx950: W waves of one 64-thread workgroup each fit
@@ -722,6 +789,15 @@ int launch_route(const DeviceArgs* d_args, int64_t cap_lines, hipStream_t s) {
     hipLaunchKernelGGL(k_fmt_reduce, dim3((unsigned)nc), dim3(PW), 0, s, d_args);
     hipLaunchKernelGGL(k_fmt_chunks, dim3(1), dim3(1), 0, s, d_args);
     hipLaunchKernelGGL(k_fmt_apply, dim3((unsigned)nc), dim3(PW), 0, s, d_args);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_histograms(const DeviceArgs* d_args, const uint8_t* buf, int64_t cap_lines, uint64_t* hist, hipStream_t s) {
+    if (hipMemsetAsync(hist, 0, sizeof(uint64_t) * HIST_WORDS, s) != hipSuccess) return -1;
+    if (cap_lines <= 0) return 0;
+    const int64_t blocks = std::min<int64_t>(2048, (cap_lines + 255) / 256);
+    hipLaunchKernelGGL(k_histograms, dim3((unsigned)blocks), dim3(256), 0, s, d_args, buf,
+                       reinterpret_cast<unsigned long long*>(hist));
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

@@ -172,6 +172,11 @@ struct Program {
     int32_t fmt_elem0[MAX_FMT + 1];  // elements of format f: [fmt_elem0[f], fmt_elem0[f + 1])
     int32_t fmt_apache[MAX_FMT];     // 1 = Apache decodeExtractedValue rules, 0 = NGINX
     int32_t fmt_quotes[MAX_FMT];     // '"' bytes in format f's literals (a line needs at least as many)
+    // run histograms (lp_histograms): format f's token slot of the response
+    // status (request.status.last, else request.status), and its first-line
+    // stage (the method); -1 none
+    int32_t hist_status[MAX_FMT];
+    int32_t hist_fl[MAX_FMT];
     int32_t pad_[2];
     Elem elems[MAX_ELEMS];
     TimeStage time[MAX_TIME];

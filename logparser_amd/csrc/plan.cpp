@@ -1333,6 +1333,22 @@ void Plan::compile_program() {
             for (const auto& o : f.tokens[i].outs) walk(O_TOKEN, it->second, o.type, o.name);
         }
     }
+    // histogram sources: the captured status token and the first first-line stage of each format
+    for (int fi = 0; fi < P.n_fmt; ++fi) {
+        P.hist_status[fi] = P.hist_fl[fi] = -1;
+        int rank = 0;  // 2: request.status.last, 1: request.status
+        const Format& f = *formats_[fi];
+        for (int i = 0; i < (int)f.tokens.size(); ++i) {
+            auto it = tok_slot_.find(fi * 256 + i);
+            if (it == tok_slot_.end()) continue;
+            for (const auto& o : f.tokens[i].outs) {
+                const int r = o.name == "request.status.last" ? 2 : o.name == "request.status" ? 1 : 0;
+                if (r > rank) { rank = r; P.hist_status[fi] = it->second; }
+            }
+        }
+        for (int s = P.n_fl - 1; s >= 0; --s)
+            if (P.fl[s].fmt == fi) P.hist_fl[fi] = s;
+    }
 }
 
 std::string Plan::describe() const {

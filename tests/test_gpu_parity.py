@@ -462,3 +462,62 @@ def test_utf8_text_gpu(oracle):
     s, _ = gpu_vs_oracle(oracle, "combined", paths(oracle), lines, allow_fallback=False,
                          data=corpora.crlf_join(lines, 10))
     assert s["ok"] == 20000, s
+
+
+def expected_histograms(p, r, lines, oracle_fields_rec):
+    """the lp_histograms words restated from the per-line results: statuses,
+    the token columns of a host copy, and the records' status / method"""
+    h = np.zeros(lpa.HIST_WORDS, dtype=np.int64)
+    st = r.status
+    h[0] = len(st)
+    for s in (0, 1, 2):
+        h[1 + s] = int((st == s).sum())
+    buf, res = r.copy_to_host(with_input=False)
+    cols = r.columns(res)
+    ok = st == 0
+    flags = cols[("tok_flags", 0)]
+    k = 0
+    while ("tok_span", k) in cols:
+        sp = cols[("tok_span", k)].astype(np.int64)
+        null = ok & (((flags >> k) & 1) == 1)
+        h[16 + k] = int(null.sum())
+        h[32 + k] = int((ok & ~null & ((sp >> 16) > (sp & 0xFFFF))).sum())
+        k += 1
+    for i in np.flatnonzero(ok):
+        rec = oracle_fields_rec(i)
+        s = rec.get("STRING:request.status.last", [None])[0]
+        if s is not None and len(s) == 3 and s.isdigit() and 100 <= int(s) <= 599:
+            h[100 + int(s)] += 1
+        else:
+            h[48] += 1
+        m = rec.get("HTTP.METHOD:request.firstline.method", [None])[0]
+        if m is None or m == "":
+            h[64 + 16] += 1
+        else:
+            h[64 + (lpa.HIST_METHODS.index(m) if m in lpa.HIST_METHODS[:15] else 15)] += 1
+    return h
+
+
+def test_histograms_gpu(oracle):
+    """lp_histograms (device run counters) against the same counts restated
+    from the records and the token columns"""
+    from test_emu_parity import mutate
+    rng = random.Random(12)
+    lines = lpa.synth_combined(20261020, 0, 6000).split(b"\n")[:-1]
+    lines = [mutate(rng, l) if i % 3 == 0 else l for i, l in enumerate(lines)]
+    for i in range(0, 6000, 97):  # other methods / status values
+        lines[i] = lines[i].replace(b'"GET ', b'"PROPFIND ', 1).replace(b'" 200 ', b'" 999 ', 1)
+    p = lpa.HttpdLoglineParser("combined", paths(oracle))
+    r = p.parse_batch(b"".join(l + b"\n" for l in lines))
+    got = np.array(p.histograms(), dtype=np.int64)
+    want = expected_histograms(p, r, lines, lambda i: r.record(i))
+    bad = np.flatnonzero(got != want)
+    assert bad.size == 0, [(int(w), int(got[w]), int(want[w])) for w in bad[:20]]
+    d = lpa.decode_histograms(got)
+    assert d["lines"] == 6000 and d["bad"] > 100 and d["methods"].get("PROPFIND", 0) > 10
+    assert sum(d["status"].values()) > 3000
+    # into a device buffer (the RCCL all-reduce operand)
+    import torch
+    t = torch.zeros(lpa.HIST_WORDS, dtype=torch.int64, device="cuda")
+    p.histograms(device_ptr=t.data_ptr())
+    assert (t.cpu().numpy() == got).all()
