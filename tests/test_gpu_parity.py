@@ -456,7 +456,7 @@ def test_utf8_text_gpu(oracle):
     s, _ = gpu_vs_oracle(oracle, "combined", paths(oracle), corpora.utf8_ua_lines(base, 5), allow_fallback=False)
     assert s["ok"] == 20000, s
     s, _ = gpu_vs_oracle(oracle, "combined", paths(oracle), corpora.utf8_hard_lines(base[:5000], 6))
-    assert s["fallback"] > 1500 and s["ok"] > 1000, s
+    assert s["fallback"] > 1500 and s["ok"] > 900, s
     # both at once: UTF-8 user agents in a CRLF file
     lines = corpora.utf8_ua_lines(base, 8)
     s, _ = gpu_vs_oracle(oracle, "combined", paths(oracle), lines, allow_fallback=False,
