@@ -332,6 +332,8 @@ def main():
                                                                 cuts[rank + 1]))
     log("input resident in HBM: %.2f GB in %d batch(es)" % (nbytes / 1e9, len(batches)))
 
+    torch.cuda.synchronize()
+    free0 = torch.cuda.mem_get_info(device)[0]
     parser = lpa.HttpdLoglineParser(fmt, fields, device=local)
     counters = torch.zeros(4, dtype=torch.int64, device=device)
 
@@ -352,6 +354,7 @@ def main():
     for _ in range(args.warmup):
         st = step()
     torch.cuda.synchronize()
+    engine_hbm = free0 - torch.cuda.mem_get_info(device)[0]  # the handle's buffers after the warmup batches
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -405,6 +408,10 @@ def main():
             "batches_per_step": len(batches),
         },
         "status_counts": {k: int(stats[k]) for k in ("lines", "ok", "bad", "fallback")},
+        "hbm_footprint": {"input_bytes": int(nbytes), "engine_bytes": int(engine_hbm),
+                          "engine_bytes_per_line": round(engine_hbm / max(1, stats["lines"]), 1),
+                          "note": "device memory the handle holds after the warmup (columns, line index, arena, "
+                                  "scratch), measured with hipMemGetInfo; the input is the caller's"},
         "kernel_ms": {"parse_avg": round(avg_parse, 3), "index_avg": round(sum(index_ms) / len(index_ms), 3)},
         "roofline": {
             "bound": "hbm",

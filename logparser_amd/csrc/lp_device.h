@@ -743,6 +743,48 @@ __host__ __device__ LP_INLINE int uplist_prev_end(const LN& L, int p, int cur, b
     return best;
 }
 
+// EK_UPLIST_NS, UpstreamModule.upstreamListOf(FORMAT_NO_SPACE_STRING)
+// (nginxmodules/UpstreamModule.java:42-44, 139-199): X(?: *, *X(?: *: *X)?)*
+// with X = [^\s]*.  X also eats ',' and ':', so the regex's ends in priority
+// order are not simple; instead every end of it from p is found (an NFA over
+// the positions) and kept if the next literal (or the line end) follows.  A
+// single such end is exact whatever the priority order (the others fail at
+// the literal); several -> FALLBACK.  Also FALLBACK: a server piece of the
+// value that UpstreamListDissector would split into no parts (a piece of
+// ": " pairs: ArrayIndexOutOfBoundsException in the reference).
+template <typename LN>
+__host__ __device__ LP_INLINE int uplist_ns_end(const Program& P, const ElemV& e, const LN& L, int p) {
+    // state bits: X0 1 (the first X), X1 2 (X after S), X2 4 (X after C),
+    // S_pre 8, S_post 16 (implies X1), C_pre 32, C_post 64 (implies X2)
+    constexpr uint32_t XS = 1 | 2 | 4 | 16 | 64;
+    uint32_t s = 1;
+    int found = -1;
+    for (int q = p;; ++q) {
+        if (s & XS) {
+            const bool ok = e.last ? q == L.n : (!e.nlit || lit_at(P, L, q, e));
+            if (ok) {
+                if (found >= 0 || (!e.nlit && !e.last)) return -2;
+                found = q;
+            }
+        }
+        if (q >= L.n || !s) break;
+        const uint32_t c = L[q];
+        uint32_t t = 0;
+        if (c == ' ') {
+            t = (s & XS ? 8u : 0u) | (s & (2 | 16 | 32) ? 32u : 0u) | (s & 8) | (s & 16) | (s & 64);
+        } else if (!is_ws(c)) {
+            t = (s & 1) | (s & (2 | 16) ? 2u : 0u) | (s & (4 | 64) ? 4u : 0u);
+            if (c == ',' && (s & (XS | 8))) t |= 16;
+            if (c == ':' && (s & (2 | 16 | 32))) t |= 64;
+        }
+        s = t;
+    }
+    if (found < 0) return -1;
+    for (int q = p; q + 1 < found; ++q)  // ": " opening a server piece
+        if (L[q] == ':' && L[q + 1] == ' ' && (q == p || (q >= p + 2 && L[q - 2] == ',' && L[q - 1] == ' '))) return -2;
+    return found;
+}
+
 // First candidate end of element e at position p (exact leftmost-first
 // order), -1 = none, -2 = FALLBACK.  '.' runs to the end of the line: the
 // fast-path guard already rejected every line terminator.
@@ -807,6 +849,13 @@ __host__ __device__ LP_INLINE int cand_first(const Program& P, const ElemV& e, c
     }
     case EK_UPLIST_DEC: return uplist_at(L, p, true);
     case EK_UPLIST_NUM: return uplist_at(L, p, false);
+    case EK_UPLIST_NS: return uplist_ns_end(P, e, L, p);
+    case EK_BINIP: {
+        if (p + 16 > L.n) return -1;
+        for (int k = p; k < p + 16; k += 4)
+            if (L[k] != '\\' || L[k + 1] != 'x' || !is_hex(L[k + 2]) || !is_hex(L[k + 3])) return -1;
+        return p + 16;
+    }
     }
     return -2;
 }
@@ -916,7 +965,7 @@ __host__ __device__ LP_INLINE int cand_next(const Program& P, const ElemV& e, co
         // shorter IPv4 / IPv6 alternatives: exact only when none of them can
         // be followed by the rest of the format
         return ip_alt_end_possible(P, L, e, p, cur) ? -2 : -1;
-    case EK_ANYCHAR: case EK_MSEC: return -1;
+    case EK_ANYCHAR: case EK_MSEC: case EK_UPLIST_NS: case EK_BINIP: return -1;
     case EK_DECIMAL: {  // a shorter fraction
         const int d = digits_end(L, p);
         return cur - 1 >= d + 2 ? cur - 1 : -1;

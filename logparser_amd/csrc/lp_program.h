@@ -67,6 +67,8 @@ enum ElemKind : uint8_t {
     EK_NOSPACE3,     // [^\s]* [^\s]* [^\s]*                ($request)
     EK_UPLIST_DEC,   // X(?: *, *X(?: *: *X)?)*, X = [0-9]+\.[0-9]+   (upstream time lists)
     EK_UPLIST_NUM,   // X(?: *, *X(?: *: *X)?)*, X = [0-9]+            (upstream byte lists)
+    EK_UPLIST_NS,    // X(?: *, *X(?: *: *X)?)*, X = [^\s]*           (upstream address / status lists)
+    EK_BINIP,        // (\\x[0-9a-fA-F]{2}){4}                         ($binary_remote_addr)
 };
 
 struct alignas(16) Elem {

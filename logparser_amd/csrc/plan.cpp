@@ -54,6 +54,9 @@ const std::string R_NUMBER_DECIMAL = R_NUMBER + "\\." + R_NUMBER;
 const std::string R_NUMBER_OPT_DECIMAL = R_NUMBER + "(?:\\." + R_NUMBER + ")?";
 const std::string R_MSEC = "[0-9]+\\.[0-9][0-9][0-9]";      // nginxmodules/CoreLogModule.java:56-58
 const std::string R_NOSPACE3 = R_NO_SPACE + " " + R_NO_SPACE + " " + R_NO_SPACE;  // $request (CoreLogModule.java:296-300)
+// $binary_remote_addr (CoreLogModule.java): four "\\x" + 2 hex digits
+const std::string R_BINIP = "\\\\x" + R_HEXDIGIT + R_HEXDIGIT + "\\\\x" + R_HEXDIGIT + R_HEXDIGIT + "\\\\x" + R_HEXDIGIT +
+                            R_HEXDIGIT + "\\\\x" + R_HEXDIGIT + R_HEXDIGIT;
 // UpstreamModule.upstreamListOf (nginxmodules/UpstreamModule.java:42-44)
 std::string upstream_list(const std::string& x) { return x + "(?: *, *" + x + "(?: *: *" + x + ")?)*"; }
 
@@ -75,6 +78,8 @@ int elem_kind_of(const std::string& r) {
     if (r == R_NOSPACE3) return EK_NOSPACE3;
     if (r == upstream_list(R_NUMBER_DECIMAL)) return EK_UPLIST_DEC;
     if (r == upstream_list(R_NUMBER)) return EK_UPLIST_NUM;
+    if (r == upstream_list(R_NO_SPACE)) return EK_UPLIST_NS;
+    if (r == R_BINIP) return EK_BINIP;
     return -1;
 }
 
@@ -1163,7 +1168,7 @@ void Plan::compile_program() {
         case EK_NUMBER: case EK_CLFNUMBER: case EK_NONZERO: e.det = (e.nlit && !dig0) || e.last; break;
         case EK_HEXNUMBER: case EK_CLFHEXNUMBER: e.det = (e.nlit && !hex0) || e.last; break;
         case EK_ANY_GREEDY: case EK_ANY_LAZY: e.det = e.last; break;
-        case EK_TIME_US: case EK_ANYCHAR: case EK_MSEC: e.det = 1; break;
+        case EK_TIME_US: case EK_ANYCHAR: case EK_MSEC: case EK_BINIP: case EK_UPLIST_NS: e.det = 1; break;
         case EK_DECIMAL: e.det = (e.nlit && !dig0) || e.last; break;
         case EK_NOSPACE3: e.det = (e.nlit && ws0) || e.last; break;
         default: e.det = 0; break;
@@ -1252,7 +1257,9 @@ void Plan::compile_program() {
                     break;
                 }
                 case D_PROTOCOL:
-                    if (ok != O_FL_PROTO) { device_ok_ = false; why_ = "protocol from a non first-line value"; return; }
+                    // the replay splits the value (first-line protocol, or a
+                    // HTTP.PROTOCOL_VERSION token such as NGINX $server_protocol)
+                    if (ok != O_FL_PROTO && ok != O_TOKEN) { device_ok_ = false; why_ = "protocol from a derived value"; return; }
                     break;
                 case D_URI: {
                     std::map<int, int>& m = ok == O_TOKEN ? uri_of_tok_ : uri_of_fl_;
@@ -1304,7 +1311,7 @@ void Plan::compile_program() {
                     }
                     break;
                 }
-                case D_CLF2NUM: case D_NUM2CLF: case D_SECMILLIS: case D_MS2US:
+                case D_CLF2NUM: case D_NUM2CLF: case D_SECMILLIS: case D_MS2US: case D_BINIP:
                     // value-level conversions, done in the replay from the token / list item
                     if (ok != O_TOKEN && ok != O_CONV) { device_ok_ = false; why_ = "converter on a derived value"; return; }
                     walk(O_CONV, oi, in.d->out_type, complete);
@@ -1593,9 +1600,12 @@ void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const 
         return;
     }
     case D_UPSTREAM: {
-        // UpstreamListDissector.dissect (nginxmodules/UpstreamListDissector.java:79-125): split(", "),
-        // each split(": "), trimmed.  EK_UPLIST_* accepted only lists whose ','
-        // and ':' are all followed by ' ', so every piece is a clean item.
+        // UpstreamListDissector.dissect (nginxmodules/UpstreamListDissector.java:79-125):
+        // servers = value.split(", "); parts = server.split(": "); outputs
+        // parts[0].trim() and (parts.length == 1 ? parts[0] : parts[1]).trim().
+        // String.split drops trailing empty pieces (an all-empty split is
+        // empty); the device sends a server whose parts would be empty (an
+        // ArrayIndexOutOfBoundsException in the reference) to FALLBACK.
         if (v.null) return;
         auto trim = [](const uint8_t* p, uint32_t n) {
             uint32_t a = 0, b = n;
@@ -1603,25 +1613,53 @@ void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const 
             while (b > a && p[b - 1] <= ' ') --b;
             return mstr(p + a, b - a);
         };
-        uint32_t s0 = 0;
+        // Java String.split(two-char literal), limit 0: pieces as (offset, length)
+        auto split2 = [](const uint8_t* p, uint32_t n, uint8_t c0, uint8_t c1) {
+            std::vector<std::pair<uint32_t, uint32_t>> out;
+            uint32_t from = 0;
+            for (uint32_t q = 0; q + 1 < n; ++q)
+                if (p[q] == c0 && p[q + 1] == c1) {
+                    out.emplace_back(from, q - from);
+                    from = q + 2;
+                    ++q;
+                }
+            out.emplace_back(from, n - from);
+            if (out.size() > 1)  // no separator: the input itself, even when empty
+                while (!out.empty() && out.back().second == 0) out.pop_back();
+            return out;
+        };
         int k = 0;
-        for (uint32_t q = 0; q <= v.len; ++q) {
-            if (q < v.len && !(v.p[q] == ',' && q + 1 < v.len && v.p[q + 1] == ' ')) continue;
-            const uint8_t* sp = v.p + s0;
-            const uint32_t sn = q - s0;
-            uint32_t colon = sn;
-            for (uint32_t r = 0; r + 1 < sn; ++r)
-                if (sp[r] == ':' && sp[r + 1] == ' ') { colon = r; break; }
-            MVal orig = trim(sp, colon);
-            MVal redir = colon < sn ? trim(sp + colon + 2, sn - colon - 2) : orig;
+        for (const auto& sv : split2(v.p, v.len, ',', ' ')) {
+            const uint8_t* sp = v.p + sv.first;
+            const auto parts = split2(sp, sv.second, ':', ' ');
+            if (parts.empty()) return;  // not reached: the device sent the line to FALLBACK
+            MVal orig = trim(sp + parts[0].first, parts[0].second);
+            MVal redir = parts.size() == 1 ? orig : trim(sp + parts[1].first, parts[1].second);
             set_origin(O_CONV, oi);
             emit(c, name, in.d->out_type, std::to_string(k) + ".value", orig);
             set_origin(O_CONV, oi);
             emit(c, name, in.d->out_type, std::to_string(k) + ".redirected", redir);
             ++k;
-            s0 = q + 2;
-            ++q;
         }
+        return;
+    }
+    case D_BINIP: {
+        // NginxHttpdLogFormatDissector.BinaryIPDissector (:151-178): "\\xHH" x 4
+        // (the token kind proves the shape) -> the four bytes as Java (signed)
+        // bytes joined by '.'
+        if (v.null || v.len != 16) return;
+        char ip[32];
+        int b[4];
+        for (int k = 0; k < 4; ++k) {
+            const uint8_t* h = v.p + 4 * k + 2;
+            auto hv = [](uint8_t ch) { return ch <= '9' ? ch - '0' : (ch | 32) - 'a' + 10; };
+            const int x = hv(h[0]) * 16 + hv(h[1]);
+            b[k] = x >= 128 ? x - 256 : x;
+        }
+        const int n = snprintf(ip, sizeof ip, "%d.%d.%d.%d", b[0], b[1], b[2], b[3]);
+        set_origin(O_CONV, oi);
+        c.pool.emplace_back(ip, (size_t)n);
+        emit(c, name, in.d->out_type, "", mstr((const uint8_t*)c.pool.back().data(), (uint32_t)n));
         return;
     }
     case D_NUM2CLF: {

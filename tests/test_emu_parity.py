@@ -405,3 +405,41 @@ def test_utf8_user_agents_emulated(oracle, emu):
     s = compare(o, e, u8)
     assert s["ok"] > 700, s
     compare(o, e, [b"1:2\xc3\xa9 - - [" + l.split(b"[", 1)[1] for l in lines[:50]])
+
+
+def upstream_lines(n, seed):
+    """NGINX lines with $upstream_addr / $upstream_status lists ([^\\s]* items),
+    quoted and unquoted, and $binary_remote_addr"""
+    rng = random.Random(seed)
+    out = []
+    for _ in range(n):
+        k = rng.choice([1, 1, 1, 2, 3])
+        addrs = [rng.choice(["10.0.%d.%d:80" % (rng.randrange(256), rng.randrange(256)), "unix:/tmp/sock",
+                             "backend_%d" % rng.randrange(9), "[::1]:8080"]) for _ in range(k)]
+        st = [str(rng.choice([200, 502, 504, 404])) for _ in range(k)]
+        sep = [rng.choice([", ", ", ", " : "]) for _ in range(k - 1)]
+        addr = addrs[0] + "".join(s + a for s, a in zip(sep, addrs[1:]))
+        stat = st[0] + "".join(s + a for s, a in zip(sep, st[1:]))
+        ip = "".join("\\x%02X" % rng.randrange(256) for _ in range(4))
+        if rng.random() < 0.1:
+            addr = addr.replace(", ", ", : ", 1)  # a server piece the reference cannot split
+        out.append(('%s "%s" %s %s "GET /x HTTP/1.1"' % (rng.choice(["1.2.3.4", "-"]), addr, stat, ip)).encode())
+    return out
+
+
+UPSTREAM_FMT = '$remote_addr "$upstream_addr" $upstream_status $binary_remote_addr "$request"'
+
+
+def test_upstream_lists_and_binary_ip_emulated(oracle, emu):
+    """UpstreamModule [^\\s]* lists (UpstreamListDissector split) and
+    BinaryIPDissector (signed bytes) on the device"""
+    paths = oracle.possible_paths(UPSTREAM_FMT)
+    o = oracle.Oracle(UPSTREAM_FMT, paths)
+    e = emu.Emu(UPSTREAM_FMT, paths)
+    assert e.status == 0, e.err
+    s = compare(o, e, upstream_lines(3000, 5))
+    assert s["ok"] > 1500, s
+    st, rec = e.parse(b'- "a:1, b:2 : c:3" 504 \\xC0\\xA8\\x01\\xFF "GET / HTTP/1.1"')
+    assert st == 0
+    assert "-64.-88.1.-1" in rec["IP:connection.client.host"]  # ($remote_addr "-" adds a null)
+    assert rec["UPSTREAM_ADDR:nginxmodule.upstream.addr.1.redirected"] == ["c:3"]
