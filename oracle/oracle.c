@@ -2708,7 +2708,7 @@ int orc_parse(orc_parser *p, const char *line, int len, char *out, int out_cap) 
     }
     int status = ps.unsupported ? ORC_UNSUPPORTED : ps.failed ? ORC_BAD : ORC_OK;
     if (status == ORC_OK && out) {
-        qsort(ps.rec, (size_t)ps.nrec, sizeof(rentry), rcmp);
+        if (ps.nrec > 1) qsort(ps.rec, (size_t)ps.nrec, sizeof(rentry), rcmp);
         ob o = {out, 0, out_cap, 0};
         out[0] = 0;
         ob_s(&o, "{");

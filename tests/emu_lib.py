@@ -9,6 +9,11 @@ import subprocess
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB = os.path.join(ROOT, "tests", "emu", "_build", "libemu.so")
+# ASan/UBSan build of the same sources (tools/asan_check.sh sets LP_EMU_ASAN=1)
+ASAN = os.environ.get("LP_EMU_ASAN") == "1"
+SAN_FLAGS = ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined", "-fno-omit-frame-pointer"]
+if ASAN:
+    LIB = os.path.join(ROOT, "tests", "emu", "_build", "libemu_asan.so")
 SRCS = [os.path.join(ROOT, "tests", "emu", "emu.cpp"), os.path.join(ROOT, "logparser_amd", "csrc", "plan.cpp")]
 HDRS = [os.path.join(ROOT, "logparser_amd", "csrc", h) for h in ("lp_device.h", "lp_program.h", "plan.h")]
 
@@ -20,7 +25,8 @@ def build(force=False):
     if not force and os.path.exists(LIB) and os.path.getmtime(LIB) >= newest:
         return
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
-    subprocess.run(["g++", "-std=c++17", "-O2", "-g", "-fPIC", "-shared", "-o", LIB] + SRCS, check=True)
+    flags = ["-O1"] + SAN_FLAGS if ASAN else ["-O2"]
+    subprocess.run(["g++", "-std=c++17", "-g", "-fPIC", "-shared", "-o", LIB] + flags + SRCS, check=True)
 
 
 def lib():

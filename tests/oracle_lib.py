@@ -9,7 +9,8 @@ import os
 import subprocess
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+# LP_ORACLE_LIB: another build of the same sources (the ASan/UBSan one, tools/asan_check.sh)
+LIB = os.environ.get("LP_ORACLE_LIB") or os.path.join(ROOT, "oracle", "_build", "liboracle.so")
 
 OK, BAD, UNSUPPORTED = 0, 1, 2
 
