@@ -93,6 +93,11 @@ struct lp_handle {
 
 namespace {
 
+// column capacity for n (expected) lines: 25 % more for the next batches of
+// a stream, at most 4 M lines more (a huge batch keeps its footprint close to
+// its size; a larger next batch re-runs once with exact capacity)
+int64_t headroom(int64_t n) { return n + std::min<int64_t>(n / 4, 1 << 22) + 1024; }
+
 void set_err(char* err, size_t errlen, const std::string& s) {
     if (err && errlen) snprintf(err, errlen, "%s", s.c_str());
 }
@@ -232,7 +237,7 @@ int enqueue(lp_handle* h, bool sync_count) {
             hipStreamSynchronize(s) != hipSuccess)
             return LP_E_DEVICE;
         // headroom for the next batches of the stream (sized like the estimate below)
-        cap = std::max<int64_t>((int64_t)(n + n / 4 + 1024), h->reserve_lines);
+        cap = std::max<int64_t>(headroom((int64_t)n), h->reserve_lines);
         if (n) h->mean_line = (double)nbytes / (double)n;  // sizes this batch's LDS windows
     } else {
         if (!h->line_off.ensure(sizeof(uint64_t) * (size_t)(cap + 2))) return LP_E_NOMEM;
@@ -534,7 +539,7 @@ int lp_parse_batch(lp_handle* h, const uint8_t* buf, uint64_t nbytes, int buf_fl
     if (h->reserve_lines > 0) {
         h->cap_lines = std::max<int64_t>(h->cap_lines, h->reserve_lines);
     } else if (h->mean_line > 0) {
-        const int64_t est = (int64_t)((double)nbytes / h->mean_line * 1.25) + 1024;
+        const int64_t est = headroom((int64_t)((double)nbytes / h->mean_line));
         h->cap_lines = std::max<int64_t>(h->cap_lines, est);
     } else {
         sync_count = true;

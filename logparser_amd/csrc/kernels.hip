@@ -376,8 +376,17 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
             const unsigned long long mine = (unsigned long long)shard * C.shard_cap + wbase + x - need;
             C.arena_base[li] = need ? mine : 0ull;
             Arena A{C.arena + (need ? mine : 0ull), 0, need};
+            if (need) {  // spills come from the same shard (lines without a region never spill)
+                A.top = &C.meta->shard_top[16 * shard];
+                A.base = wbase + x - need;
+                A.limit = C.shard_cap;
+            }
             phase2(P, L, o, A, C, li);
-            written = A.used - A.slack;
+            if (A.ovf) {
+                o.status = ST_FALLBACK;
+                atomicAdd(&C.meta->arena_ovf, 1ull);
+            }
+            written = A.used - A.slack + A.extra;
         }
         LP_PROF(20);
         write_line(P, o, C, li);
@@ -408,12 +417,13 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
                 const unsigned long long oab = __shfl(my_ab, own);
                 const auto OL = owner_line(L, own);
                 if (g < tot) {
-                    LP_G uint8_t* region = C.arena + oab;
-                    LP_G uint64_t* slot = reinterpret_cast<LP_G uint64_t*>(region + olist + 16 * (g - ob));
-                    const uint64_t a0 = slot[0];
-                    const uint32_t reserved = 3u * (uint32_t)(((a0 >> 16) & 0xFFFFu) - (a0 & 0xFFFFu));
-                    const uint32_t used = query_piece(P, P.query[qs], OL, region, slot);
-                    written += used - reserved;  // modulo 2^32: the wave sum is exact
+                    Arena R{C.arena + oab, 0, 0};
+                    R.top = &C.meta->shard_top[16 * shard];  // the owner is a line of this wave: same shard
+                    R.base = oab - (unsigned long long)shard * C.shard_cap;
+                    R.limit = C.shard_cap;
+                    LP_G uint64_t* slot = reinterpret_cast<LP_G uint64_t*>(R.p + olist + 16 * (g - ob));
+                    written += query_piece(P, P.query[qs], OL, R, slot);
+                    if (R.ovf) atomicAdd(&C.meta->arena_ovf, 1ull);  // the batch is re-run with a larger arena
                 }
             }
         }

@@ -1649,7 +1649,7 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
         }
     }
     LP_PROF(7);
-    // arena need of the URI / query stages (upper bound of phase-2 writes)
+    // arena need of the URI / query stages: their query tables
     uint32_t need = 0;
     for (int u = 0; u < P.n_uri; ++u) {
         int a, b;
@@ -1657,31 +1657,57 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
         // URIUtil-escaped bytes and '&'/'?' separators are both URI event
         // bytes: their count bounds both.  A URI without event bytes writes
         // nothing to the arena (no query table, no decoded or rewritten part).
+        // (separators are URI event bytes: their count bounds the pieces).  A
+        // URI without event bytes writes nothing to the arena; rewritten or
+        // decoded parts and query values are spilled when they occur.
         const uint32_t ev = count_uev(L, a, b);
-        const uint32_t enc = ev, sep = ev;
+        const uint32_t sep = ev;
         o.usep.set(u, sep);
         if (ev == 0) continue;
         const UriStage& U = P.uri[u];
-        uint32_t ulen = (uint32_t)(b - a), tl = ulen + 2 * enc + 2;
-        uint32_t n = 16;
-        if (U.want_query) n += tl;
-        if (U.want_path) n += ulen;
-        if (U.want_ref) n += tl;
-        if (U.query_stage >= 0) n += 16 + 20 * (sep + 1) + 3 * ulen;  // slots, pending list, piece regions
-        need += n;
+        if (U.query_stage >= 0) need += 16 + 16 * (sep + 1);  // alignment, one slot per piece
     }
     o.arena_need = (need + 15) & ~15u;
     LP_PROF(8);
 }
 
 // ------------------------------------------------------------ URI stage
+// A line's arena region: the reserved part (phase 1 bounds the query table
+// there) written from offset 0 up, plus pieces spilled further on into the
+// same shard for the rare rewritten / decoded URI parts and query values
+// (sized then, exactly; refs stay region-relative: spills are allocated after
+// the region, in the same shard).
 struct Arena {
     LP_G uint8_t* p;  // this line's region
     uint32_t used;
     uint32_t cap;
     uint32_t slack = 0;  // reserved, never written
+    uint32_t extra = 0;  // bytes written in spilled pieces
+    // spill allocator: the shard's bump pointer (a device atomic; the CPU
+    // emulation's counter), the region's offset in the shard, the shard size
+    LP_G unsigned long long* top = nullptr;
+    uint64_t base = 0, limit = 0;
+    bool ovf = false;    // a spill did not fit (the batch is re-run with a larger arena)
     __host__ __device__ uint32_t put(uint32_t c) { p[used] = (uint8_t)c; return used++; }
 };
+
+// X = a fresh piece of n bytes of A's shard, written like a region (region-
+// relative offsets).  false: the shard is full (A.ovf set).
+__host__ __device__ LP_INLINE bool spill(Arena& A, uint32_t n, Arena& X) {
+    X = A;
+    if (!A.top || n == 0) { A.ovf = A.top == nullptr; X.cap = X.used; return n == 0; }
+#if defined(__HIP_DEVICE_COMPILE__)
+    const unsigned long long x = __hip_atomic_fetch_add(A.top, (unsigned long long)n, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+#else
+    const unsigned long long x = *A.top;
+    *A.top += n;
+#endif
+    if (x < A.base || x + n > A.limit || x - A.base + n > 0x7FFFFFFFull) { A.ovf = true; return false; }
+    X.used = (uint32_t)(x - A.base);
+    X.cap = X.used + n;
+    return true;
+}
 
 // Forward byte reader over a line: 8 bytes in registers, one aligned word
 // read per 4 bytes for increasing positions (any position < n works).
@@ -1898,8 +1924,7 @@ struct QueryTable {
         if (e > s) {
             LP_G uint64_t* t = (LP_G uint64_t*)(region + tab) + 2 * count;
             t[0] = (uint64_t)(uint32_t)s | ((uint64_t)(uint32_t)e << 16) | ((uint64_t)(uint32_t)(lp + 1) << 48);
-            t[1] = reg;
-            reg += 3 * (uint32_t)(e - s);
+            t[1] = 0;
             ++count;
         }
         lp = -1;
@@ -1909,12 +1934,13 @@ struct QueryTable {
 // Completes a query piece (QueryStringFieldDissector.java:75-104): the name
 // is lower-cased and keeps URIUtil's escapes, never decoded; a piece without
 // '=' has value ""; else the value goes through Utils.resilientUrlDecode.
-// region: the owning line's arena region; slot: its table slot.  Returns the
-// region bytes written.
+// R: the owning line's arena region (its spill allocator); slot: the piece's
+// table slot.  Returns the arena bytes written; R.ovf when a spill did not fit.
 template <typename LN>
-__host__ __device__ LP_INLINE uint32_t query_piece(const Program& P, const QueryStage& Q, const LN& L,
-                                                   LP_G uint8_t* region, LP_G uint64_t* slot) {
-    const uint64_t a0 = slot[0], a1 = slot[1];
+__host__ __device__ LP_INLINE uint32_t query_piece(const Program& P, const QueryStage& Q, const LN& L, Arena& R,
+                                                   LP_G uint64_t* slot) {
+    LP_G uint8_t* region = R.p;
+    const uint64_t a0 = slot[0];
     const int s = (int)(a0 & 0xFFFFu), e = (int)((a0 >> 16) & 0xFFFFu);
     const int lp = (int)((a0 >> 48) & 0xFFFFu) - 1;
     // the piece's first '=' splits name and value ('=' is not a URI event byte)
@@ -1924,7 +1950,14 @@ __host__ __device__ LP_INLINE uint32_t query_piece(const Program& P, const Query
     // upper-case / URIUtil-escaped bytes in the name: it is rewritten
     const bool rw = find_fwd(L, s, ne, [](uint32_t w) { return swar::upper(w) | swar::needs_encode(w); }) < ne;
     const bool pv = eq >= 0 && lp > eq;               // '%' / '+' in the value
-    Arena A{region, (uint32_t)a1, 0};
+    // rewritten name / decoded value: 3 bytes per piece byte at most
+    Arena A;
+    if (!spill(R, (rw || pv) ? 3u * (uint32_t)(e - s) : 0u, A)) {
+        slot[0] = REF_SKIP;
+        slot[1] = 0;
+        return 0;
+    }
+    const uint32_t a1 = A.used;
     // name [s, ne): URIUtil-escaped and lower-cased as in the rawQuery
     uint64_t nref;
     if (rw) {
@@ -1954,7 +1987,7 @@ __host__ __device__ LP_INLINE uint32_t query_piece(const Program& P, const Query
     if (!want) {
         slot[0] = REF_SKIP;
         slot[1] = 0;
-        return A.used - (uint32_t)a1;
+        return A.used - a1;
     }
     uint64_t vref;
     if (eq < 0) vref = mkref(0, 0, false);  // no '=' -> ""
@@ -1962,7 +1995,7 @@ __host__ __device__ LP_INLINE uint32_t query_piece(const Program& P, const Query
     else vref = url_decode_value(L, eq + 1, e, A);
     slot[0] = nref;
     slot[1] = vref;
-    return A.used - (uint32_t)a1;
+    return A.used - a1;
 }
 
 // HttpUriDissector fast path on the line bytes [a,b).  Returns status.
@@ -2158,7 +2191,14 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
     C.u_host[u][li] = (uint64_t)host_ref;
     C.u_port[u][li] = port;
     if (U.want_path) {
-        uint64_t r = (first_pct >= 0 && first_pct < pend) ? decode_span(L, ps, pend, A) : mkref(ps, pend - ps, false);
+        uint64_t r = mkref(ps, pend - ps, false);
+        if (first_pct >= 0 && first_pct < pend) {  // decoded: at most the escaped length
+            Arena X;
+            if (!spill(A, (uint32_t)(pend - ps), X)) return ST_FALLBACK;
+            const uint32_t x0 = X.used;
+            r = decode_span(L, ps, pend, X);
+            A.extra += X.used - x0;
+        }
         if (r == ~0ull) return ST_FALLBACK;
         C.u_path[u][li] = r;
     }
@@ -2175,15 +2215,18 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
             if (!(rewr & 2u)) {
                 C.u_query[u][li] = amp_ref;
             } else {
-                uint32_t st = A.used;
-                A.put('&');
+                Arena X;  // '&' + the query, URIUtil-escaped bytes tripled
+                if (!spill(A, 1u + 3u * (uint32_t)(qe - qs0), X)) return ST_FALLBACK;
+                const uint32_t st = X.used;
+                X.put('&');
                 for (int q = fa + 1; q < qe; ++q) {
                     uint32_t c = L[q];
-                    if (c == '?') A.put('&');
-                    else if (uri_needs_encode(c)) put_encoded(A, c);
-                    else A.put(c);
+                    if (c == '?') X.put('&');
+                    else if (uri_needs_encode(c)) put_encoded(X, c);
+                    else X.put(c);
                 }
-                C.u_query[u][li] = mkref(st, A.used - st, true);
+                A.extra += X.used - st;
+                C.u_query[u][li] = mkref(st, X.used - st, true);
             }
         } else {
             C.u_query[u][li] = mkref(0, 0, true);
@@ -2196,16 +2239,19 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
         // fragment = decode(normalized text after '#')
         if (!(rewr & 1u)) C.u_frag[u][li] = mkref(h + 1, b - h - 1, false);
         else {
-            uint32_t st = A.used;
+            Arena X;  // the decoded fragment: at most one byte more than its text
+            if (!spill(A, (uint32_t)(b - h), X)) return ST_FALLBACK;
+            const uint32_t st = X.used;
             for (int q = h + 1; q < b;) {
                 uint32_t c = L[q];
-                if (q == fa) { A.put('?'); A.put('&'); ++q; }
-                else if (c == '?') { A.put('&'); ++q; }
-                else if (c == '%') { A.put(hexv(L[q + 1]) * 16 + hexv(L[q + 2])); q += 3; }
-                else { A.put(c); ++q; }
+                if (q == fa) { X.put('?'); X.put('&'); ++q; }
+                else if (c == '?') { X.put('&'); ++q; }
+                else if (c == '%') { X.put(hexv(L[q + 1]) * 16 + hexv(L[q + 2])); q += 3; }
+                else { X.put(c); ++q; }
             }
-            if (!utf8_ok(A.p + st, A.used - st)) return ST_FALLBACK;
-            C.u_frag[u][li] = mkref(st, A.used - st, true);
+            A.extra += X.used - st;
+            if (!utf8_ok(X.p + st, X.used - st)) return ST_FALLBACK;
+            C.u_frag[u][li] = mkref(st, X.used - st, true);
         }
     }
     LP_PROF(34 + 8 * u);
@@ -2216,10 +2262,10 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
 // The pending query pieces of one line, one after the other (the test-only
 // CPU emulation; the kernel spreads them over the wave).
 template <typename LN>
-__host__ __device__ LP_INLINE void query_pieces_serial(const Program& P, const LN& L, const LineOut& o, LP_G uint8_t* region) {
+__host__ __device__ LP_INLINE void query_pieces_serial(const Program& P, const LN& L, const LineOut& o, Arena& A) {
     for (int qs = 0; qs < P.n_query; ++qs) {
         for (uint32_t k = 0; k < o.qpend.get(qs); ++k)
-            query_piece(P, P.query[qs], L, region, (LP_G uint64_t*)(region + o.qlist.get(qs) + 16 * k));
+            A.extra += query_piece(P, P.query[qs], L, A, (LP_G uint64_t*)(A.p + o.qlist.get(qs) + 16 * k));
     }
 }
 

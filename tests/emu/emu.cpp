@@ -97,11 +97,19 @@ static int run_line(const Program& P, const LN& L, LineOut& o, uint32_t* stk, Co
     }
     phase1(P, P.elems, L, o, stk, C, 0, false, P.n_fmt > 1 ? (int)fmt_state : 0);
     if (o.status == ST_OK) {
-        R.arena.assign(o.arena_need + 64, 0);
+        // the region, then room for spills (a shard of its own: bump counter
+        // after the region, as the kernel's shard_top)
+        const uint64_t room = o.arena_need + 16ull * (uint64_t)L.n + 4096;
+        R.arena.assign(room + 64, 0);
+        unsigned long long top = o.arena_need;
         Arena A{R.arena.data(), 0, o.arena_need};
+        A.top = &top;
+        A.base = 0;
+        A.limit = room;
         phase2(P, L, o, A, C, 0);
-        if (o.status == ST_OK) query_pieces_serial(P, L, o, A.p);
+        if (o.status == ST_OK) query_pieces_serial(P, L, o, A);
         if (A.used > o.arena_need) { snprintf(out, cap, "ARENA OVERFLOW %u > %u", A.used, o.arena_need); return 3; }
+        if (A.ovf) { snprintf(out, cap, "ARENA SPILL OVERFLOW"); return 3; }
     }
     write_line(P, o, C, 0);
     return 0;
