@@ -374,13 +374,11 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
             atomicAdd(&C.meta->arena_ovf, 1ull);
         } else if (o.status == ST_OK) {
             const unsigned long long mine = (unsigned long long)shard * C.shard_cap + wbase + x - need;
-            C.arena_base[li] = need ? mine : 0ull;
-            Arena A{C.arena + (need ? mine : 0ull), 0, need};
-            if (need) {  // spills come from the same shard (lines without a region never spill)
-                A.top = &C.meta->shard_top[16 * shard];
-                A.base = wbase + x - need;
-                A.limit = C.shard_cap;
-            }
+            C.arena_base[li] = mine;  // also for an empty region: spills are region-relative
+            Arena A{C.arena + mine, 0, need};
+            A.top = &C.meta->shard_top[16 * shard];  // spills come from the same shard
+            A.base = wbase + x - need;
+            A.limit = C.shard_cap;
             phase2(P, L, o, A, C, li);
             if (A.ovf) {
                 o.status = ST_FALLBACK;
