@@ -188,7 +188,8 @@ typedef struct lp_column {
 typedef struct lp_result {
     int64_t n_lines;
     uint64_t input_bytes;
-    const uint8_t *input;      /* line i = input[line_off[i], line_off[i+1] - 1); NULL if not copied */
+    const uint8_t *input;      /* line i = input[line_off[i], line_off[i+1] - 1), less the '\r' of a
+                                  "\r\n" terminator; NULL if not copied */
     const uint64_t *line_off;  /* n_lines + 1 entries */
     const uint8_t *columns;
     uint64_t columns_bytes;
@@ -198,7 +199,8 @@ typedef struct lp_result {
     uint64_t shard_off[LP_ARENA_SHARDS];
     int32_t n_columns;
     int32_t on_host;           /* 0: device pointers (lp_result_view), 1: host copy (lp_result_copy) */
-    const lp_column *column;   /* owned by the handle, valid until its next batch */
+    const lp_column *column;   /* view: owned by the handle, valid until its next batch;
+                                  host copy: inside the copy's buffer */
 } lp_result;
 /* Device pointers of the last batch's results (valid until the next batch). */
 int lp_result_view(lp_handle *h, lp_result *out);

@@ -60,7 +60,7 @@ struct lp_handle {
     lp::DeviceArgs host_args{};
     lp::Columns C{};
     std::vector<ColSpec> specs;
-    std::vector<lp_column> dev_cols, host_cols;
+    std::vector<lp_column> dev_cols;
     // the batch (valid once lp_parse_batch succeeded)
     bool valid = false, pending = false;
     int64_t n_lines = 0;
@@ -376,14 +376,18 @@ int ensure_synced(lp_handle* h) {
 int64_t copy_result(lp_handle* h, uint8_t* dst, uint64_t cap, bool with_input, lp_result* r) {
     const int64_t n = h->n_lines;
     uint64_t cols_bytes = 0;
-    h->host_cols = layout(h->specs, n, &cols_bytes);
+    // the column table travels in the copy: the result never points into the
+    // handle (a later copy or batch must not invalidate an earlier copy)
+    const std::vector<lp_column> cols = layout(h->specs, n, &cols_bytes);
+    const uint64_t tab_bytes = sizeof(lp_column) * cols.size();
     uint64_t arena_bytes = 0;
     uint64_t shard_off[LP_ARENA_SHARDS];
     for (int s = 0; s < LP_ARENA_SHARDS; ++s) {
         shard_off[s] = arena_bytes;
         arena_bytes += (h->shard_top[s] + 15) & ~15ull;
     }
-    const uint64_t o_lines = 0, o_cols = align256(8 * (uint64_t)(n + 1)), o_arena = o_cols + cols_bytes;
+    const uint64_t o_tab = 0, o_lines = align256(tab_bytes), o_cols = o_lines + align256(8 * (uint64_t)(n + 1));
+    const uint64_t o_arena = o_cols + cols_bytes;
     const uint64_t o_input = align256(o_arena + arena_bytes);
     const uint64_t total = with_input ? o_input + h->nbytes + 64 : o_input;
     if (!dst) return -(int64_t)total;
@@ -391,9 +395,10 @@ int64_t copy_result(lp_handle* h, uint8_t* dst, uint64_t cap, bool with_input, l
     auto cp = [&](uint64_t off, const void* src, uint64_t bytes) {
         return bytes == 0 || hipMemcpy(dst + off, src, bytes, hipMemcpyDeviceToHost) == hipSuccess;
     };
+    if (tab_bytes) memcpy(dst + o_tab, cols.data(), tab_bytes);
     bool ok = cp(o_lines, h->line_off.p, 8 * (uint64_t)(n + 1));
     for (size_t k = 0; k < h->specs.size() && ok; ++k)
-        ok = cp(o_cols + h->host_cols[k].offset, *h->specs[k].field, (uint64_t)h->specs[k].esz * (uint64_t)n);
+        ok = cp(o_cols + cols[k].offset, *h->specs[k].field, (uint64_t)h->specs[k].esz * (uint64_t)n);
     for (int s = 0; s < LP_ARENA_SHARDS && ok; ++s)
         ok = cp(o_arena + shard_off[s], h->arena.as<uint8_t>((size_t)s * h->shard_cap), h->shard_top[s]);
     if (with_input && ok) {
@@ -413,8 +418,8 @@ int64_t copy_result(lp_handle* h, uint8_t* dst, uint64_t cap, bool with_input, l
     R.arena_bytes = arena_bytes;
     R.shard_cap = h->shard_cap;
     for (int s = 0; s < LP_ARENA_SHARDS; ++s) R.shard_off[s] = shard_off[s];
-    R.n_columns = (int32_t)h->host_cols.size();
-    R.column = h->host_cols.data();
+    R.n_columns = (int32_t)cols.size();
+    R.column = reinterpret_cast<const lp_column*>(dst + o_tab);
     R.on_host = 1;
     return (int64_t)total;
 }
