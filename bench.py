@@ -286,6 +286,7 @@ def main():
     ap.add_argument("--cpu-sample-lines", type=int, default=2_000_000)
     ap.add_argument("--cpu-threads", type=int, default=16, help="the GPU box's CPU share per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-delivery", action="store_true", help="skip the host delivery measurement (huge batches)")
     ap.add_argument("--workload", type=int, default=2, choices=(2, 3, 4, 5), help="BASELINE.json config")
     ap.add_argument("--batch-mb", type=int, default=None,
                     help="split the resident input into newline-aligned batches of about this size "
@@ -442,7 +443,7 @@ def main():
         result["config"]["corpus_bytes_all_ranks"] = total_bytes
         if rank == 0:
             result["pcie_inclusive"] = pcie_inclusive(torch, parser, buf, batches, 8 << 30)
-    if rank == 0 and wl != 5:
+    if rank == 0 and wl != 5 and not args.no_delivery:
         result["delivery"] = host_delivery(lpa, torch, parser, stats["lines"], wl)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         log("cpu baseline (oracle, %d threads) ..." % args.cpu_threads)
