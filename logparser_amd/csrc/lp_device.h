@@ -1585,6 +1585,16 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
         o.tok_flags = flags;
         if (fb) { o.status = ST_FALLBACK; return; }
     }
+    // values the replay URL-decodes (request cookies, Utils.resilientUrlDecode):
+    // ASCII, and every '%' followed by two hex digits, else FALLBACK
+    for (uint32_t gm = (uint32_t)P.guard_pct[fmt]; gm; gm &= gm - 1) {
+        const uint32_t sp = o.caps.get(__builtin_ctz(gm));
+        const int a = sp & 0xFFFF, b = sp >> 16;
+        if (find_fwd(L, a, b, [](uint32_t w) { return w & swar::HI; }) < b) { o.status = ST_FALLBACK; return; }
+        for (int q = find_fwd(L, a, b, [](uint32_t w) { return swar::eq(w, '%'); }); q < b;
+             q = find_fwd(L, q + 1, b, [](uint32_t w) { return swar::eq(w, '%'); }))
+            if (q + 2 >= b || !is_hex(L[q + 1]) || !is_hex(L[q + 2])) { o.status = ST_FALLBACK; return; }
+    }
     LP_PROF(5);
     // TimeStampDissector
     for (int t = 0; t < P.n_time; ++t) {

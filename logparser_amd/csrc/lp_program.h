@@ -179,6 +179,10 @@ struct Program {
     // stage (the method); -1 none
     int32_t hist_status[MAX_FMT];
     int32_t hist_fl[MAX_FMT];
+    // token slots of format f whose value the replay URL-decodes (request
+    // cookies): bit k -> phase 1 sends the line to FALLBACK unless every '%'
+    // is followed by two hex digits and the value is ASCII
+    int32_t guard_pct[MAX_FMT];
     int32_t pad_[2];
     Elem elems[MAX_ELEMS];
     TimeStage time[MAX_TIME];

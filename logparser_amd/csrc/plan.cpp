@@ -1241,6 +1241,12 @@ void Plan::compile_program() {
                 case D_LOCALIZED:
                     if (ok != O_TOKEN) { device_ok_ = false; why_ = "localized time from a derived value"; return; }
                     break;
+                case D_COOKIES:
+                    // RequestCookieListDissector: split and decoded in the replay;
+                    // the device proves the decode cannot fail (guard_pct)
+                    if (ok != O_TOKEN) { device_ok_ = false; why_ = "cookies from a derived value"; return; }
+                    P.guard_pct[cur_fmt] |= 1 << oi;
+                    break;
                 case D_FIRSTLINE: {
                     if (ok != O_TOKEN) { device_ok_ = false; why_ = "first line from a derived value"; return; }
                     int fidx;
@@ -1640,6 +1646,61 @@ void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const 
             set_origin(O_CONV, oi);
             emit(c, name, in.d->out_type, std::to_string(k) + ".redirected", redir);
             ++k;
+        }
+        return;
+    }
+    case D_COOKIES: {
+        // RequestCookieListDissector.dissect (dissectors/RequestCookieListDissector.java:79-110):
+        // Pattern("; ").split (trailing empty pieces dropped), name = the part
+        // before the first '=' trimmed and lower-cased (just a name: value ""),
+        // value = Utils.resilientUrlDecode of the trimmed rest.  The device's
+        // guard proved the header ASCII with every '%' followed by two hex
+        // digits: each %XX is the Latin-1 char U+00XX, '+' a space.
+        if (v.null || v.len == 0) return;
+        const bool all = has("*");
+        auto trim = [](const uint8_t* p, uint32_t& a, uint32_t& b) {
+            while (a < b && p[a] <= ' ') ++a;
+            while (b > a && p[b - 1] <= ' ') --b;
+        };
+        std::vector<std::pair<uint32_t, uint32_t>> parts;
+        uint32_t from = 0;
+        for (uint32_t q = 0; q + 1 < v.len; ++q)
+            if (v.p[q] == ';' && v.p[q + 1] == ' ') { parts.emplace_back(from, q); from = q + 2; ++q; }
+        parts.emplace_back(from, v.len);
+        if (parts.size() > 1)
+            while (!parts.empty() && parts.back().second == parts.back().first) parts.pop_back();
+        set_origin(O_NONE, 0);
+        for (const auto& pr : parts) {
+            const uint8_t* s = v.p + pr.first;
+            const uint32_t n = pr.second - pr.first;
+            uint32_t eq = 0;
+            while (eq < n && s[eq] != '=') ++eq;
+            uint32_t na = 0, nb = eq;
+            if (eq == n && n == 0) continue;
+            trim(s, na, nb);
+            std::string nm((const char*)s + na, nb - na);
+            for (auto& ch : nm) if (ch >= 'A' && ch <= 'Z') ch = char(ch + 32);
+            if (!all && !has(nm.c_str())) continue;
+            std::string val;
+            if (eq < n) {
+                uint32_t va = eq + 1, vb = n;
+                trim(s, va, vb);
+                for (uint32_t q = va; q < vb;) {
+                    const uint8_t ch = s[q];
+                    if (ch == '%' && q + 2 < vb) {  // the guard proved two hex digits follow
+                        auto hv = [](uint8_t x) { return x <= '9' ? x - '0' : (x | 32) - 'a' + 10; };
+                        const int x = hv(s[q + 1]) * 16 + hv(s[q + 2]);
+                        if (x < 0x80) val += char(x);
+                        else { val += char(0xC0 | (x >> 6)); val += char(0x80 | (x & 0x3F)); }
+                        q += 3;
+                    } else {
+                        val += ch == '+' ? ' ' : char(ch);
+                        ++q;
+                    }
+                }
+            }
+            c.pool.emplace_back(std::move(val));
+            emit(c, name, "HTTP.COOKIE", nm, mstr((const uint8_t*)c.pool.back().data(), (uint32_t)c.pool.back().size()));
         }
         return;
     }

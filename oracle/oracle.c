@@ -1083,7 +1083,7 @@ static void inst_prepare(orc_parser *p, instance *in, const char *subroot, const
         break;
     }
     case D_LOCALIZED: break;
-    case D_TIMESTAMP_ISO: case D_COOKIES: case D_SETCOOKIES:
+    case D_TIMESTAMP_ISO: case D_SETCOOKIES:
     case D_SETCOOKIE: case D_UNIQUEID:
         if (!p->unsupported) {
             p->unsupported = 1;
@@ -2447,6 +2447,41 @@ static js js_trim(js s, int a, int b) {
     return js_sub(s, a, b);
 }
 
+/* RequestCookieListDissector.dissect (dissectors/RequestCookieListDissector.java:79-110):
+ * Pattern("; ").split (trailing empty pieces dropped); a piece without '='
+ * (and not empty) is a name with value ""; else name = trim + lower-case of
+ * the part before the first '=', value = Utils.resilientUrlDecode of the
+ * trimmed rest (IllegalArgumentException -> DissectionFailure).  Only
+ * requested names ("*" = all) are delivered, as HTTP.COOKIE:<name>. */
+static void d_cookies(parsable *ps, instance *in, const char *inputname) {
+    val *vp = cache_get(ps, "HTTP.COOKIES", inputname);
+    js s = v_getstring(ps->a, *vp);
+    if (s.null || s.n == 0) return;
+    const int want_all = has_req(in, "*");
+    int st[512], en[512];
+    const int np = java_split2(s, 0, s.n, ';', ' ', st, en, 512);
+    if (np < 0) { ps->unsupported = 1; return; }
+    for (int k = 0; k < np; k++) {
+        js v = js_sub(s, st[k], en[k]);
+        const int eq = js_index_of_char(v, '=', 0);
+        if (eq == -1) {
+            if (v.n == 0) continue;
+            js name = js_lower(ps->a, js_trim(v, 0, v.n));
+            char *nm = js_cstr(ps, name);
+            if (want_all || has_req(in, nm)) add_str(ps, inputname, "HTTP.COOKIE", nm, js_lit(ps->a, ""));
+        } else {
+            js name = js_lower(ps->a, js_trim(v, 0, eq));
+            char *nm = js_cstr(ps, name);
+            if (!(want_all || has_req(in, nm))) continue;
+            js dec;
+            const int r = resilient_url_decode(ps, js_trim(v, eq + 1, v.n), &dec);
+            if (r == 1) { ps->failed = 1; return; }
+            if (r == 2) { ps->unsupported = 1; return; }
+            add_str(ps, inputname, "HTTP.COOKIE", nm, dec);
+        }
+    }
+}
+
 /* UpstreamListDissector.dissect (nginxmodules/UpstreamListDissector.java:79-125):
  * split(", ") into servers, each split(": ") into original / redirected,
  * both trimmed; N.value and N.redirected per server. */
@@ -2487,6 +2522,7 @@ static void run_instance(parsable *ps, instance *in, const char *name) {
     case D_SECMILLIS: d_secmillis(ps, in, name); break;
     case D_MS2US: d_ms2us(ps, in, name); break;
     case D_UPSTREAM: d_upstream(ps, in, name); break;
+    case D_COOKIES: d_cookies(ps, in, name); break;
     default: ps->unsupported = 1; break;
     }
 }

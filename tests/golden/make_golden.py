@@ -103,6 +103,45 @@ case("hpt/ApacheHttpdLogParserTest.java:104-163", FULLCOMBINED,
      absent=["STRING:request.firstline.uri.query.foo", "STRING:request.querystring.aap"],
      skipped=APACHE_SKIPPED)
 
+# the same line's request cookie (RequestCookieListDissector; the Set-Cookie
+# dissectors stay off the device and out of the oracle)
+case("hpt/ApacheHttpdLogParserTest.java:104-163 (cookies)", FULLCOMBINED,
+     "%127.0.0.1 127.0.0.1 127.0.0.1 - - [31/Dec/2012:23:49:40 +0100] "
+     "\"GET /icons/powered_by_rh.png?aap=noot&res=1024x768 HTTP/1.1\" 200 1213 "
+     "80 \"\" \"http://localhost/index.php?mies=wim\" 351 "
+     "\"Mozilla/5.0 (X11; Linux i686 on x86_64; rv:11.0) Gecko/20100101 Firefox/11.0\" "
+     "\"jquery-ui-theme=Eggplant\" \"Apache=127.0.0.1.1344635380111339; path=/; domain=.basjes.nl\" \"-\" "
+     "\"\\\"3780ff-4bd-4c1ce3df91380\\\"\"",
+     ["HTTP.COOKIES:request.cookies", "HTTP.COOKIE:request.cookies.jquery-ui-theme"],
+     expect={"HTTP.COOKIES:request.cookies": "jquery-ui-theme=Eggplant",
+             "HTTP.COOKIE:request.cookies.jquery-ui-theme": "Eggplant"})
+
+# hpt/CookiesTest.java:110-127,157-218 (cookiesTest): the request cookies of COOKIES_LINE
+COOKIES_FMT = ("%h %a %A %l %u %t \"%r\" %>s %b %p \"%q\" \"%{Referer}i\" %D \"%{User-agent}i\" "
+               "\"%{Cookie}i\" \"%{Set-Cookie}o\" \"%{If-None-Match}i\" \"%{Etag}o\"")
+case("hpt/CookiesTest.java:110-127,157-218", COOKIES_FMT,
+     "127.0.0.1 127.0.0.1 127.0.0.1 - - [31/Dec/2012:23:00:44 -0700] \"GET /index.php HTTP/1.1\" "
+     "200 - 80 \"\" \"-\" 80991 \"Mozilla/5.0 (X11; Linux i686 on x86_64; rv:11.0) Gecko/20100101 Firefox/11.0\" "
+     "\"jquery-ui-theme=Eggplant; Apache=127.0.0.1.1351111543699529\" "
+     "\"NBA-0=, NBA-1=1234, NBA-2=1234; expires=Wed, 01-Jan-2020 00:00:10 GMT, "
+     "NBA-3=1234; expires=Wed, 01-Jan-2020 00:00:10 GMT; path=/, "
+     "NBA-4=1234; expires=Wed, 01-Jan-2020 00:00:10 GMT; path=/; domain=.basj.es\" \"-\" \"-\"",
+     ["HTTP.COOKIES:request.cookies", "HTTP.COOKIE:request.cookies.*", "STRING:request.status.last",
+      "HTTP.URI:request.firstline.uri"],
+     expect={"HTTP.COOKIE:request.cookies.jquery-ui-theme": "Eggplant",
+             "HTTP.COOKIE:request.cookies.apache": "127.0.0.1.1351111543699529",
+             "STRING:request.status.last": "200", "HTTP.URI:request.firstline.uri": "/index.php"},
+     skipped=["HTTP.SETCOOKIES / HTTP.SETCOOKIE fields (ResponseSetCookieDissector: not restated)"])
+
+# hpt/dissectors/TestCookieDissector.java:26-40 (testRequestCookies), as the
+# %{Cookie}i token of a one-token LogFormat
+case("hpt/dissectors/TestCookieDissector.java:26-40", "%{Cookie}i", "NBA-0; NBA-1=; NBA-2=1234; ",
+     ["HTTP.COOKIES:request.cookies", "HTTP.COOKIE:request.cookies.nba-0", "HTTP.COOKIE:request.cookies.nba-1",
+      "HTTP.COOKIE:request.cookies.nba-2"],
+     expect={"HTTP.COOKIES:request.cookies": "NBA-0; NBA-1=; NBA-2=1234; ",
+             "HTTP.COOKIE:request.cookies.nba-0": "", "HTTP.COOKIE:request.cookies.nba-1": "",
+             "HTTP.COOKIE:request.cookies.nba-2": "1234"})
+
 case("hpt/ApacheHttpdLogParserTest.java:168-200", FULLCOMBINED,
      "%127.0.0.1 127.0.0.1 127.0.0.1 - - [10/Aug/2012:23:55:11 +0200] \"GET /icons/powered_by_rh.png HTTP/1.1\" 200 1213 80"
      " \"\" \"http://localhost/\" 1306 \"Mozilla/5.0 (X11; Linux i686 on x86_64; rv:11.0) Gecko/20100101 Firefox/11.0\""
@@ -417,14 +456,16 @@ if FLINK_LINE:
     case("examples/apache-flink/src/test/java/nl/basjes/parse/httpdlog/flink/TestCase.java:37-43,86-94",
          "%h %l %u %t \"%r\" %>s %b \"%{Referer}i\" \"%{User-Agent}i\" \"%{Cookie}i\"", FLINK_LINE,
          ["IP:connection.client.host", "TIME.STAMP:request.receive.time", "TIME.EPOCH:request.receive.time.epoch",
-          "HTTP.USERAGENT:request.user-agent", "STRING:request.firstline.uri.query.g", "STRING:request.firstline.uri.query.s"],
+          "HTTP.USERAGENT:request.user-agent", "STRING:request.firstline.uri.query.g", "STRING:request.firstline.uri.query.s",
+          "HTTP.COOKIE:request.cookies.bui"],
          expect={"IP:connection.client.host": "2001:980:91c0:1:8d31:a232:25e5:85d",
                  "TIME.STAMP:request.receive.time": "05/Sep/2010:11:27:50 +0200",
                  "TIME.EPOCH:request.receive.time.epoch": {"l": 1283678870000},
                  "STRING:request.firstline.uri.query.s": "1280x800",
                  "HTTP.USERAGENT:request.user-agent": "Mozilla/5.0 (Macintosh; U; Intel Mac OS X 10_6_4; nl-nl) "
-                                                      "AppleWebKit/533.17.8 (KHTML, like Gecko) Version/5.0.1 Safari/533.17.8"},
-         skipped=["STRING:request.firstline.uri.query.g.query.promo (type remapping)", "GeoIP fields", "HTTP.COOKIE:request.cookies.bui"])
+                                                      "AppleWebKit/533.17.8 (KHTML, like Gecko) Version/5.0.1 Safari/533.17.8",
+                 "HTTP.COOKIE:request.cookies.bui": "SomeThing"},
+         skipped=["STRING:request.firstline.uri.query.g.query.promo (type remapping)", "GeoIP fields"])
 
 # --------------------------------------------------------------------- NGINX
 # hpt/nginxmodules/NginxUpstreamTest.java:49-90 (testBasicLogFormat)

@@ -443,3 +443,42 @@ def test_upstream_lists_and_binary_ip_emulated(oracle, emu):
     assert st == 0
     assert "-64.-88.1.-1" in rec["IP:connection.client.host"]  # ($remote_addr "-" adds a null)
     assert rec["UPSTREAM_ADDR:nginxmodule.upstream.addr.1.redirected"] == ["c:3"]
+
+
+COOKIE_FMT = '%h %l %u %t "%r" %>s %b "%{Cookie}i"'
+
+
+def cookie_lines(n, seed):
+    """'combined'-like lines with a request Cookie header: upper-case names,
+    blanks around names and values, empty pieces, names without '=',
+    %XX / '+' values, and a few invalid escapes / non-ASCII bytes (FALLBACK)"""
+    rng = random.Random(seed)
+    base = lpa.synth_combined(seed, 0, n).split(b"\n")[:-1]
+    out = []
+    for l in base:
+        head = l.rsplit(b' "', 2)[0]
+        pieces = []
+        for _ in range(rng.randrange(0, 7)):
+            name = rng.choice(["session", "JSESSIONID", "_ga", "Theme", "a b", " pad", "x-Y_z", ""])
+            val = rng.choice(["abc", "1234", "%41%42", "a+b", "%C3%A9t%C3%A9", " spaced ", "", "x=y", "%7E%2F"])
+            form = rng.random()
+            pieces.append(name if form < 0.15 else name + "=" + val)
+        hdr = "; ".join(pieces) + ("; " if rng.random() < 0.2 else "")
+        if rng.random() < 0.05:
+            hdr += "; bad=%zz"
+        if rng.random() < 0.03:
+            hdr += "; u=é"
+        out.append(head + b' "' + hdr.encode() + b'"')
+    return out
+
+
+@pytest.mark.parametrize("fields", [["HTTP.COOKIE:request.cookies.*"],
+                                    ["HTTP.COOKIE:request.cookies.session", "HTTP.COOKIE:request.cookies.theme",
+                                     "HTTP.COOKIES:request.cookies", "STRING:request.status.last"]])
+def test_request_cookies_emulated(oracle, emu, fields):
+    """RequestCookieListDissector: split / trim / lower-case / resilientUrlDecode"""
+    o = oracle.Oracle(COOKIE_FMT, fields)
+    e = emu.Emu(COOKIE_FMT, fields)
+    assert e.status == 0, e.err
+    s = compare(o, e, cookie_lines(3000, 11))
+    assert s["ok"] > 2500 and s["fallback"] < 300, s

@@ -77,7 +77,7 @@ def test_golden_vectors_gpu(oracle, vectors):
           "dissector not on the device)" % (checked, n, len(fallback), unsupported))
     for src in sorted(set(fallback)):
         print("  FALLBACK:", src)
-    assert checked >= 143, (checked, n)  # 145 of 160 in the CPU emulation of the same device code
+    assert checked >= 146, (checked, n)  # 148 of 163 in the CPU emulation of the same device code
 
 
 def test_setup_vectors_gpu(vectors):
@@ -528,3 +528,13 @@ def test_upstream_lists_and_binary_ip_gpu(oracle):
     fields = oracle.possible_paths(UPSTREAM_FMT)
     s, _ = gpu_vs_oracle(oracle, UPSTREAM_FMT, fields, upstream_lines(20000, 5))
     assert s["ok"] > 10000, s
+
+
+@pytest.mark.parametrize("which", [0, 1])
+def test_request_cookies_gpu(oracle, which):
+    from test_emu_parity import COOKIE_FMT, cookie_lines
+    fields = [["HTTP.COOKIE:request.cookies.*"],
+              ["HTTP.COOKIE:request.cookies.session", "HTTP.COOKIE:request.cookies.theme",
+               "HTTP.COOKIES:request.cookies", "STRING:request.status.last"]][which]
+    s, _ = gpu_vs_oracle(oracle, COOKIE_FMT, fields, cookie_lines(20000, 11 + which))
+    assert s["ok"] > 17000 and s["fallback"] < 2000, s
