@@ -345,7 +345,8 @@ def main():
             if st is None:
                 st = r
             else:
-                for k in ("lines", "ok", "bad", "fallback", "ms_total", "ms_index", "ms_parse", "bytes_in", "bytes_out"):
+                for k in ("lines", "ok", "bad", "fallback", "ms_total", "ms_index", "ms_parse", "bytes_in", "bytes_out",
+                          "overflow_waves", "retries"):
                     st[k] += r[k]
         if world > 1:
             counters.copy_(torch.tensor([st["lines"], st["ok"], st["bad"], st["fallback"]], dtype=torch.int64))
@@ -409,6 +410,8 @@ def main():
             "batches_per_step": len(batches),
         },
         "status_counts": {k: int(stats[k]) for k in ("lines", "ok", "bad", "fallback")},
+        "parse_diag": {"overflow_waves": int(stats.get("overflow_waves", 0)), "retries": int(stats.get("retries", 0)),
+                       "waves": (int(stats["lines"]) + 63) // 64},
         "hbm_footprint": {"input_bytes": int(nbytes), "engine_bytes": int(engine_hbm),
                           "engine_bytes_per_line": round(engine_hbm / max(1, stats["lines"]), 1),
                           "note": "device memory the handle holds after the warmup (columns, line index, arena, "

@@ -119,7 +119,10 @@ int64_t lp_line_offset(lp_handle *h, int64_t i);
  * returns bytes written (excluding NUL) or negative (LP_E_STATE if the line
  * is not OK, -100 - needed if cap is too small). */
 int64_t lp_line_record_json(lp_handle *h, int64_t i, char *out, size_t cap);
-/* out[0..3] = lines, ok, bad, fallback of the last batch (device counters) */
+/* out[0..3] = lines, ok, bad, fallback of the last batch (device counters);
+ * diagnostics: out[4] = waves parsed by the overflow kernel (their lines'
+ * window exceeded the main kernel's LDS window), out[5] = re-runs of the
+ * batch (capacity / arena estimates exceeded).  Returns the words written. */
 int lp_counters(lp_handle *h, uint64_t *out, int n);
 
 /* Device-side timing of the last batch, in milliseconds, measured with HIP

@@ -387,13 +387,13 @@ class HttpdLoglineParser:
         rc = L.lp_sync(self._h)
         if rc != LP_OK:
             raise EngineUnavailable("lp_sync failed: %d" % rc)
-        c = (ctypes.c_uint64 * 4)()
-        L.lp_counters(self._h, c, 4)
+        c = (ctypes.c_uint64 * 6)()
+        L.lp_counters(self._h, c, 6)
         t = (ctypes.c_float * 3)()
         L.lp_last_timing(self._h, t, 3)
         b = (ctypes.c_uint64 * 2)()
         L.lp_last_bytes(self._h, b, 2)
-        return {"lines": c[0], "ok": c[1], "bad": c[2], "fallback": c[3],
+        return {"lines": c[0], "ok": c[1], "bad": c[2], "fallback": c[3], "overflow_waves": c[4], "retries": c[5],
                 "ms_total": t[0], "ms_index": t[1], "ms_parse": t[2], "bytes_in": b[0], "bytes_out": b[1]}
 
     def parse(self, line):

@@ -77,6 +77,7 @@ struct lp_handle {
     hipEvent_t ev[4]{};
     bool have_events = false;
     uint64_t counters[4]{};
+    uint64_t ovf_waves = 0;        // waves of the last batch parsed by k_parse_overflow
     uint64_t shard_top[LP_ARENA_SHARDS]{};
     uint64_t arena_written = 0;
     int retries = 0;
@@ -341,6 +342,7 @@ int finish(lp_handle* h) {
         if (h->plan.device_ok()) {
             for (int k = 0; k < 4; ++k) h->counters[k] = m.counters[k];
             h->arena_written = m.counters[4];
+            h->ovf_waves = m.ovf_waves;
         } else {
             h->counters[0] = (uint64_t)n;
             h->counters[1] = h->counters[2] = 0;
@@ -617,8 +619,10 @@ int lp_counters(lp_handle* h, uint64_t* out, int n) {
     if (!h || !out) return LP_E_INVALID;
     const int st = ensure_synced(h);
     if (st != LP_OK) return st;
-    for (int k = 0; k < n && k < 4; ++k) out[k] = h->counters[k];
-    return n < 4 ? n : 4;
+    const uint64_t v[6] = {h->counters[0], h->counters[1], h->counters[2], h->counters[3], h->ovf_waves,
+                           (uint64_t)h->retries};
+    for (int k = 0; k < n && k < 6; ++k) out[k] = v[k];
+    return n < 6 ? n : 6;
 }
 
 int lp_histograms(lp_handle* h, uint64_t* out, int out_on_device) {

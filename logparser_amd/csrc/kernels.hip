@@ -51,15 +51,7 @@ __device__ __forceinline__ uint32_t bits16(uint32_t m0, uint32_t m1, uint32_t m2
 // '\r' not followed by '\n', and of "\r\n" the '\n' (the '\r' is then the
 // last byte of the line's bytes and the parse kernels drop it).  Bytes at or
 // past nbytes are not terminators; a '\r' as the buffer's last byte is.
-__device__ __forceinline__ uint32_t term16(const uint8_t* p, uint64_t pos, uint64_t nbytes) {
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (pos + 16 <= nbytes && ((uintptr_t)(p + pos) & 15) == 0) {
-        v = *reinterpret_cast<const uint4*>(p + pos);
-    } else {
-        uint32_t w[4] = {0, 0, 0, 0};
-        for (uint64_t k = pos; k < pos + 16 && k < nbytes; ++k) w[(k - pos) >> 2] |= (uint32_t)p[k] << (8 * ((k - pos) & 3));
-        v = make_uint4(w[0], w[1], w[2], w[3]);
-    }
+__device__ __forceinline__ uint32_t term_bits(uint4 v, const uint8_t* p, uint64_t pos, uint64_t nbytes) {
     uint32_t lf = bits16(byte_eq(v.x, 0x0A0A0A0Au), byte_eq(v.y, 0x0A0A0A0Au), byte_eq(v.z, 0x0A0A0A0Au),
                          byte_eq(v.w, 0x0A0A0A0Au));
     uint32_t cr = bits16(byte_eq(v.x, 0x0D0D0D0Du), byte_eq(v.y, 0x0D0D0D0Du), byte_eq(v.z, 0x0D0D0D0Du),
@@ -76,6 +68,17 @@ __device__ __forceinline__ uint32_t term16(const uint8_t* p, uint64_t pos, uint6
     }
     return lf | cr;
 }
+__device__ __forceinline__ uint32_t term16(const uint8_t* p, uint64_t pos, uint64_t nbytes) {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (pos + 16 <= nbytes && ((uintptr_t)(p + pos) & 15) == 0) {
+        v = *reinterpret_cast<const uint4*>(p + pos);
+    } else {
+        uint32_t w[4] = {0, 0, 0, 0};
+        for (uint64_t k = pos; k < pos + 16 && k < nbytes; ++k) w[(k - pos) >> 2] |= (uint32_t)p[k] << (8 * ((k - pos) & 3));
+        v = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+    return term_bits(v, p, pos, nbytes);
+}
 
 // Pass 1 of the line index: line terminators per 64 KiB chunk, and the
 // terminator bit mask of every 16-byte piece (1 bit per input byte) so that
@@ -84,15 +87,33 @@ __global__ __launch_bounds__(NL_THREADS) void k_count_newlines(const uint8_t* __
                                                                 uint64_t* __restrict__ counts,
                                                                 uint16_t* __restrict__ nlmask) {
     const uint64_t base = (uint64_t)blockIdx.x * CHUNK;
+    constexpr int IT = CHUNK / (NL_THREADS * 16);
     uint32_t c = 0;
-    for (int it = 0; it < CHUNK / (NL_THREADS * 16); ++it) {
-        uint64_t pos = base + ((uint64_t)it * NL_THREADS + threadIdx.x) * 16;
-        uint32_t m = 0;
-        if (pos < nbytes) {
-            m = term16(buf, pos, nbytes);
+    if (base + CHUNK <= nbytes && ((uintptr_t)(buf + base) & 15) == 0) {
+        // a whole chunk: every load in flight before the first use
+        typedef uint32_t w4 __attribute__((ext_vector_type(4)));
+        w4 v[IT];
+#pragma unroll
+        for (int it = 0; it < IT; ++it)
+            v[it] = __builtin_nontemporal_load(
+                reinterpret_cast<const w4*>(buf + base + ((uint64_t)it * NL_THREADS + threadIdx.x) * 16));
+#pragma unroll
+        for (int it = 0; it < IT; ++it) {
+            const uint64_t pos = base + ((uint64_t)it * NL_THREADS + threadIdx.x) * 16;
+            const uint32_t m = term_bits(make_uint4(v[it][0], v[it][1], v[it][2], v[it][3]), buf, pos, nbytes);
             c += (uint32_t)__popc(m);
+            nlmask[pos >> 4] = (uint16_t)m;
         }
-        nlmask[pos >> 4] = (uint16_t)m;
+    } else {
+        for (int it = 0; it < IT; ++it) {
+            uint64_t pos = base + ((uint64_t)it * NL_THREADS + threadIdx.x) * 16;
+            uint32_t m = 0;
+            if (pos < nbytes) {
+                m = term16(buf, pos, nbytes);
+                c += (uint32_t)__popc(m);
+            }
+            nlmask[pos >> 4] = (uint16_t)m;
+        }
     }
     // block reduction
     __shared__ uint32_t red[NL_THREADS / 64];
@@ -169,41 +190,56 @@ __global__ __launch_bounds__(1024) void k_scan_counts(uint64_t* __restrict__ cou
 }
 
 // line_off[j] = start of line j.  line_off[0] = 0 and the entry after every
-// '\n' that is not the last byte; line_off[n_lines] = end sentinel.  Entries
-// past cap_lines are not written (the batch is then re-run with larger columns).
+// terminator that is not the last byte; line_off[n_lines] = end sentinel.
+// Entries past cap_lines are not written (the batch is then re-run with
+// larger columns).  Thread t of a chunk takes 16 consecutive mask words (256
+// input bytes): one block scan of the per-thread counts, then each thread
+// writes its lines' starts.
 __global__ __launch_bounds__(NL_THREADS) void k_line_offsets(const uint16_t* __restrict__ nlmask, uint64_t nbytes,
                                                               const uint64_t* __restrict__ chunk_base,
                                                               uint64_t* __restrict__ line_off, int64_t cap_lines) {
+    constexpr int WPT = CHUNK / 16 / NL_THREADS;  // mask words per thread (16)
     const uint64_t base = (uint64_t)blockIdx.x * CHUNK;
+    const uint64_t pos0 = base + (uint64_t)threadIdx.x * WPT * 16;  // first input byte of this thread
     __shared__ uint32_t wsum[NL_THREADS / 64];
-    uint64_t run = chunk_base[blockIdx.x];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    for (int it = 0; it < CHUNK / (NL_THREADS * 16); ++it) {
-        uint64_t pos = base + ((uint64_t)it * NL_THREADS + threadIdx.x) * 16;
-        uint32_t m = pos < nbytes ? (uint32_t)nlmask[pos >> 4] : 0u;
-        const uint32_t c = (uint32_t)__popc(m);
-        // block exclusive scan of c
-        uint32_t x = c;
-        for (int d = 1; d < 64; d <<= 1) {
-            uint32_t y = __shfl_up(x, d);
-            if (lane >= d) x += y;
-        }
-        if (lane == 63) wsum[wave] = x;
-        __syncthreads();
-        uint32_t wpre = 0, tot = 0;
-        for (int w = 0; w < NL_THREADS / 64; ++w) {
-            if (w < wave) wpre += wsum[w];
-            tot += wsum[w];
-        }
-        uint64_t k = run + wpre + x - c;  // index of this thread's first '\n'
-        while (m) {
-            const uint32_t b = (uint32_t)__builtin_ctz(m);
-            m &= m - 1;
-            if ((int64_t)(k + 1) <= cap_lines) line_off[k + 1] = pos + b + 1;
+    uint32_t m[WPT];
+    const uint64_t nwords = (nbytes + 15) >> 4;
+    const uint64_t w0 = pos0 >> 4;
+    if (w0 + WPT <= nwords) {
+        const uint4* q = reinterpret_cast<const uint4*>(nlmask + w0);  // 32-byte aligned
+        const uint4 a = q[0], b = q[1];
+        const uint32_t x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { m[2 * k] = x[k] & 0xFFFFu; m[2 * k + 1] = x[k] >> 16; }
+    } else {
+#pragma unroll
+        for (int k = 0; k < WPT; ++k) m[k] = w0 + k < nwords ? (uint32_t)nlmask[w0 + k] : 0u;
+    }
+    uint32_t c = 0;
+#pragma unroll
+    for (int k = 0; k < WPT; ++k) c += (uint32_t)__popc(m[k]);
+    // block exclusive scan of c
+    uint32_t x = c;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+    }
+    if (lane == 63) wsum[wave] = x;
+    __syncthreads();
+    uint32_t wpre = 0;
+    for (int w = 0; w < NL_THREADS / 64; ++w)
+        if (w < wave) wpre += wsum[w];
+    uint64_t k = chunk_base[blockIdx.x] + wpre + x - c;  // index of this thread's first terminator
+#pragma unroll
+    for (int j = 0; j < WPT; ++j) {
+        uint32_t mm = m[j];
+        while (mm) {
+            const uint32_t b = (uint32_t)__builtin_ctz(mm);
+            mm &= mm - 1;
+            if ((int64_t)(k + 1) <= cap_lines) line_off[k + 1] = pos0 + 16ull * j + b + 1;
             ++k;
         }
-        run += tot;
-        __syncthreads();
     }
 }
 
@@ -439,7 +475,7 @@ __device__ __forceinline__ void load_elems(const Program& P, Elem* s_elems) {
     for (int k = threadIdx.x; k < P.n_elems; k += PW) s_elems[k] = P.elems[k];
 }
 
-__global__ __launch_bounds__(PW) void k_parse_lines(const uint8_t* __restrict__ buf, uint64_t nbytes,
+__global__ __launch_bounds__(PW, 2) void k_parse_lines(const uint8_t* __restrict__ buf, uint64_t nbytes,
                                                     const DeviceArgs* __restrict__ args, uint32_t win_cap,
                                                     uint32_t stk_words) {
     const Program& P = args->prog;
@@ -453,31 +489,48 @@ __global__ __launch_bounds__(PW) void k_parse_lines(const uint8_t* __restrict__ 
     uint8_t* win = smem + 16 * P.n_elems + stk_words * 4;
     uint16_t* msk16 = reinterpret_cast<uint16_t*>(win + win_cap);
     const WaveLines W = wave_lines(C, wave, n_lines, nbytes);
-    if (W.w1 - W.w0 > win_cap) {  // the window does not fit: k_parse_overflow takes the wave
-        if (threadIdx.x == 0) C.ovf_list[atomicAdd(&C.meta->ovf_waves, 1ull)] = (uint32_t)wave;
-        return;
+    // the lines' window in one staged round; a window larger than LDS in two
+    // rounds of 32 lines (lanes 0-31, then 32-63) when each half fits, else
+    // the wave is queued for k_parse_overflow (lines read from HBM)
+    uint64_t a0 = W.w0, b0 = W.w1, a1 = 0, b1 = 0;
+    int rounds = 1;
+    if (W.w1 - W.w0 > win_cap) {
+        const int64_t mid = W.li0 + PW / 2 < W.lend ? W.li0 + PW / 2 : W.lend;
+        const uint64_t lm = C.line_off[mid];
+        b0 = lm < nbytes ? lm : nbytes;
+        a1 = lm & ~15ull;
+        b1 = W.w1;
+        rounds = mid < W.lend ? 2 : 1;
+        if (b0 - a0 > win_cap || (rounds == 2 && b1 - a1 > win_cap)) {
+            if (threadIdx.x == 0) C.ovf_list[atomicAdd(&C.meta->ovf_waves, 1ull)] = (uint32_t)wave;
+            return;
+        }
     }
     load_elems(P, s_elems);
     LP_PROF(0);
-    const bool clean = stage_window(buf, nbytes, W.w0, W.w1, win, msk16);
-    __syncthreads();
-#if LP_EXP == 11
-    if (clean) return;  // experiment: stop after staging
-#endif
-    const int n = W.active ? crlf_len(W.n, W.n > 0 ? win[W.e - 1 - W.w0] : 0u) : W.n;
-    const LineT<lds_bytes, lds_u64> L{(lds_bytes)win, (uint32_t)(W.s - W.w0), n, (lds_u64)reinterpret_cast<uint64_t*>(msk16)};
     WaveCounts WC;
-    parse_wave(P, s_elems, C, L, W.active, W.li, stk, clean, wave, WC);
+#pragma nounroll
+    for (int r = 0; r < rounds; ++r) {
+        const uint64_t a = r ? a1 : a0, b = r ? b1 : b0;
+        const bool clean = stage_window(buf, nbytes, a, b, win, msk16);
+        __syncthreads();
+#if LP_EXP == 11
+        if (clean) return;  // experiment: stop after staging
+#endif
+        const bool mine = W.active && (rounds == 1 || ((int)threadIdx.x >= PW / 2) == (r != 0));
+        const int n = mine ? crlf_len(W.n, W.n > 0 ? win[W.e - 1 - a] : 0u) : 0;
+        const LineT<lds_bytes, lds_u64> L{(lds_bytes)win, mine ? (uint32_t)(W.s - a) : 0u, n,
+                                          (lds_u64)reinterpret_cast<uint64_t*>(msk16)};
+        parse_wave(P, s_elems, C, L, mine, W.li, stk, clean, wave, WC);
+        if (r + 1 < rounds) __syncthreads();  // this round's LDS reads are done before the next staging
+    }
     WC.store(C, wave);
 }
 
-// The waves k_parse_lines queued (their 64 lines' window exceeds LDS), on a
-// persistent grid: two staged rounds of 32 lines (lanes 0-31, then 32-63)
-// through the same LDS window when each half fits, else the lines are read
-// from HBM directly (very long lines).
+// The waves k_parse_lines queued (even half their window exceeds LDS: very
+// long lines), on a persistent grid: the lines are read from HBM directly.
 __global__ __launch_bounds__(PW) void k_parse_overflow(const uint8_t* __restrict__ buf, uint64_t nbytes,
-                                                       const DeviceArgs* __restrict__ args, uint32_t win_cap,
-                                                       uint32_t stk_words) {
+                                                       const DeviceArgs* __restrict__ args, uint32_t stk_words) {
     const Program& P = args->prog;
     const Columns& C = args->cols;
     const int64_t n_lines = (int64_t)C.meta->n_lines;
@@ -485,39 +538,19 @@ __global__ __launch_bounds__(PW) void k_parse_overflow(const uint8_t* __restrict
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     Elem* s_elems = reinterpret_cast<Elem*>(smem);
     WaveStack stk{reinterpret_cast<uint32_t*>(smem + 16 * P.n_elems) + threadIdx.x};
-    uint8_t* win = smem + 16 * P.n_elems + stk_words * 4;
-    uint16_t* msk16 = reinterpret_cast<uint16_t*>(win + win_cap);
     load_elems(P, s_elems);
     __syncthreads();
     for (uint64_t q = blockIdx.x; q < nq; q += gridDim.x) {
         const int64_t wave = C.ovf_list[q];
         const WaveLines W = wave_lines(C, wave, n_lines, nbytes);
-        const int64_t mid = W.li0 + PW / 2 < W.lend ? W.li0 + PW / 2 : W.lend;
-        const uint64_t lm = C.line_off[mid];
-        const uint64_t a0 = W.w0, b0 = lm < nbytes ? lm : nbytes, a1 = lm & ~15ull, b1 = W.w1;
-        const bool two = mid < W.lend;
         WaveCounts WC;
-        if (b0 - a0 <= win_cap && (!two || b1 - a1 <= win_cap)) {
-            for (int r = 0; r < (two ? 2 : 1); ++r) {
-                const uint64_t a = r ? a1 : a0, b = r ? b1 : b0;
-                const bool clean = stage_window(buf, nbytes, a, b, win, msk16);
-                __syncthreads();
-                const bool mine = W.active && ((int)threadIdx.x >= PW / 2) == (r != 0);
-                const int n = mine ? crlf_len(W.n, W.n > 0 ? win[W.e - 1 - a] : 0u) : 0;
-                const LineT<lds_bytes, lds_u64> L{(lds_bytes)win, mine ? (uint32_t)(W.s - a) : 0u, n,
-                                                  (lds_u64)reinterpret_cast<uint64_t*>(msk16)};
-                parse_wave(P, s_elems, C, L, mine, W.li, stk, clean, wave, WC);
-                __syncthreads();  // this round's LDS reads are done before the next staging
-            }
-        } else {
-            // base = the line start aligned down to 4 bytes: word reads never
-            // leave the 4-byte words holding the line's bytes
-            const LP_G uint8_t* ls = (const LP_G uint8_t*)(buf) + W.s;
-            const uint32_t mis = (uint32_t)((uintptr_t)ls & 3);
-            const LineT<const LP_G uint8_t*> L{ls - mis, mis, crlf_len_hbm(buf, W)};
-            parse_wave(P, s_elems, C, L, W.active, W.li, stk, false, wave, WC);
-            __syncthreads();
-        }
+        // base = the line start aligned down to 4 bytes: word reads never
+        // leave the 4-byte words holding the line's bytes
+        const LP_G uint8_t* ls = (const LP_G uint8_t*)(buf) + W.s;
+        const uint32_t mis = (uint32_t)((uintptr_t)ls & 3);
+        const LineT<const LP_G uint8_t*> L{ls - mis, mis, crlf_len_hbm(buf, W)};
+        parse_wave(P, s_elems, C, L, W.active, W.li, stk, false, wave, WC);
+        __syncthreads();
         WC.store(C, wave);
     }
 }
@@ -816,10 +849,11 @@ int launch_parse(const ParseLaunch& a, const DeviceArgs* d_args, const uint32_t*
     const WindowPlan w = window_plan(a);
     hipLaunchKernelGGL(k_parse_lines, dim3((unsigned)waves), dim3(PW), w.lds, s, a.buf, a.nbytes, d_args, w.cap,
                        w.stk_words);
-    // the queued waves (windows larger than LDS): persistent grid, a few
-    // waves per CU (the same LDS layout as k_parse_lines)
+    // the queued waves (even half the window exceeds LDS): persistent grid,
+    // lines read from HBM (LDS: the elements and the DFS stack only)
     const int64_t grid = waves < 1024 ? waves : 1024;
-    hipLaunchKernelGGL(k_parse_overflow, dim3((unsigned)grid), dim3(PW), w.lds, s, a.buf, a.nbytes, d_args, w.cap,
+    const size_t lds_ovf = 16 * (size_t)a.n_elems + 4 * (size_t)w.stk_words;
+    hipLaunchKernelGGL(k_parse_overflow, dim3((unsigned)grid), dim3(PW), lds_ovf, s, a.buf, a.nbytes, d_args,
                        w.stk_words);
     int64_t rb = (waves + 255) / 256;
     if (rb > 1024) rb = 1024;

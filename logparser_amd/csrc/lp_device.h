@@ -510,7 +510,14 @@ __host__ __device__ LP_INLINE Bytes28 load28(const LN& L, int p) {
 // any pass could turn it into a dynamically indexed scratch-memory array.
 template <int N>
 struct RegArr {
+#if defined(__HIP_DEVICE_COMPILE__)
+    // a vector value: an element write with a wave-uniform index is one
+    // VGPR-indexed move (s_set_gpr_idx), not a branch or a select chain
+    typedef uint32_t vec_t __attribute__((ext_vector_type(N)));
+    vec_t v;
+#else
     uint32_t v[N];
+#endif
     template <size_t... J>
     __host__ __device__ LP_INLINE uint32_t get_(int k, std::index_sequence<J...>) const {
         uint32_t r = 0;
@@ -526,9 +533,13 @@ struct RegArr {
         (f((int)J, v[J]), ...);
     }
     __host__ __device__ LP_INLINE uint32_t get(int k) const { return get_(k, std::make_index_sequence<N>{}); }
-    // set with a wave-uniform index: a scalar branch to one register write
+    // set with a wave-uniform index: one indexed register write on the device
     // (the select chain of set() rewrites every element)
     __host__ __device__ LP_INLINE void set_u(int k, uint32_t x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        if ((unsigned)k < (unsigned)N) v[k] = x;
+        return;
+#endif
         switch (k) {
 #define LP_RA_CASE(J) case J: if constexpr (J < N) v[J] = x; break;
             LP_RA_CASE(0) LP_RA_CASE(1) LP_RA_CASE(2) LP_RA_CASE(3) LP_RA_CASE(4) LP_RA_CASE(5) LP_RA_CASE(6)
