@@ -807,6 +807,28 @@ std::unique_ptr<Dissector> mkdis(int cls, const std::string& in) {
     return d;
 }
 
+// Utils.resilientUrlDecode (hp/Utils.java:27-65) of a value whose every '%'
+// is followed by two hex digits (the device's guard_pct proved it): each %XX
+// is the Latin-1 char U+00XX (VALID_STANDARD -> %00%XX, a UTF-16 decode), '+'
+// a space; UTF-8 out
+std::string latin1_url_decode(const uint8_t* s, uint32_t n) {
+    std::string val;
+    auto hv = [](uint8_t x) { return x <= '9' ? x - '0' : (x | 32) - 'a' + 10; };
+    for (uint32_t q = 0; q < n;) {
+        const uint8_t ch = s[q];
+        if (ch == '%' && q + 2 < n) {
+            const int x = hv(s[q + 1]) * 16 + hv(s[q + 2]);
+            if (x < 0x80) val += char(x);
+            else { val += char(0xC0 | (x >> 6)); val += char(0x80 | (x & 0x3F)); }
+            q += 3;
+        } else {
+            val += ch == '+' ? ' ' : char(ch);
+            ++q;
+        }
+    }
+    return val;
+}
+
 std::string extract_field_name(const std::string& in, const std::string& out) {
     if (in == out) return "";
     if (!in.empty()) return out.substr(in.size() + 1);
@@ -1291,7 +1313,14 @@ void Plan::compile_program() {
                     break;
                 }
                 case D_QUERY: {
-                    if (ok != O_URI_QUERY) { device_ok_ = false; why_ = "query string from a raw token"; return; }
+                    if (ok == O_TOKEN) {
+                        // a HTTP.QUERYSTRING token (%q, $args, $query_string):
+                        // split / decoded in the replay, the device proves the
+                        // decode cannot fail (guard_pct, as for cookies)
+                        P.guard_pct[cur_fmt] |= 1 << oi;
+                        break;
+                    }
+                    if (ok != O_URI_QUERY) { device_ok_ = false; why_ = "query string from a derived value"; return; }
                     UriStage& U = P.uri[oi];
                     U.want_query = 1;
                     if (U.query_stage < 0) {
@@ -1565,6 +1594,34 @@ void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const 
     }
     case D_QUERY: {
         if (v.null || v.len == 0) return;
+        if (ok == O_TOKEN) {
+            // QueryStringFieldDissector.dissect (dissectors/QueryStringFieldDissector.java:75-104)
+            // on a raw token: split("&") (trailing empty pieces dropped), names
+            // lower-cased (not trimmed), values resilientUrlDecode'd (the
+            // device's guard: ASCII, every '%' followed by two hex digits)
+            const bool all = has("*");
+            std::vector<std::pair<uint32_t, uint32_t>> parts;
+            uint32_t from = 0;
+            for (uint32_t q = 0; q < v.len; ++q)
+                if (v.p[q] == '&') { parts.emplace_back(from, q); from = q + 1; }
+            parts.emplace_back(from, v.len);
+            if (parts.size() > 1)
+                while (!parts.empty() && parts.back().second == parts.back().first) parts.pop_back();
+            set_origin(O_NONE, 0);
+            for (const auto& pr : parts) {
+                const uint8_t* sp = v.p + pr.first;
+                const uint32_t n = pr.second - pr.first;
+                if (n == 0) continue;
+                uint32_t eq = 0;
+                while (eq < n && sp[eq] != '=') ++eq;
+                std::string nm((const char*)sp, eq);
+                for (auto& ch : nm) if (ch >= 'A' && ch <= 'Z') ch = char(ch + 32);
+                if (!all && !has(nm.c_str())) continue;
+                c.pool.emplace_back(eq < n ? latin1_url_decode(sp + eq + 1, n - eq - 1) : std::string());
+                emit(c, name, "STRING", nm, mstr((const uint8_t*)c.pool.back().data(), (uint32_t)c.pool.back().size()));
+            }
+            return;
+        }
         int q = query_of_uri_.at(oi);
         uint32_t cnt = R.q_count[q][i];
         uint64_t tab = R.q_params[q][i];
@@ -1685,19 +1742,7 @@ void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const 
             if (eq < n) {
                 uint32_t va = eq + 1, vb = n;
                 trim(s, va, vb);
-                for (uint32_t q = va; q < vb;) {
-                    const uint8_t ch = s[q];
-                    if (ch == '%' && q + 2 < vb) {  // the guard proved two hex digits follow
-                        auto hv = [](uint8_t x) { return x <= '9' ? x - '0' : (x | 32) - 'a' + 10; };
-                        const int x = hv(s[q + 1]) * 16 + hv(s[q + 2]);
-                        if (x < 0x80) val += char(x);
-                        else { val += char(0xC0 | (x >> 6)); val += char(0x80 | (x & 0x3F)); }
-                        q += 3;
-                    } else {
-                        val += ch == '+' ? ' ' : char(ch);
-                        ++q;
-                    }
-                }
+                val = latin1_url_decode(s + va, vb - va);
             }
             c.pool.emplace_back(std::move(val));
             emit(c, name, "HTTP.COOKIE", nm, mstr((const uint8_t*)c.pool.back().data(), (uint32_t)c.pool.back().size()));

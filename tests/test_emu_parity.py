@@ -482,3 +482,40 @@ def test_request_cookies_emulated(oracle, emu, fields):
     assert e.status == 0, e.err
     s = compare(o, e, cookie_lines(3000, 11))
     assert s["ok"] > 2500 and s["fallback"] < 300, s
+
+
+QS_FMT = '%h %l %u %t "%r" %>s %b "%q"'
+
+
+def querystring_lines(n, seed):
+    """lines with a raw %q query string token: '?'-prefixed or empty, upper-case
+    names, empty pieces, %XX / '+' values, a few invalid escapes (FALLBACK)"""
+    rng = random.Random(seed)
+    base = lpa.synth_combined(seed, 0, n).split(b"\n")[:-1]
+    out = []
+    for l in base:
+        head = l.rsplit(b' "', 2)[0]
+        pieces = []
+        for _ in range(rng.randrange(0, 6)):
+            name = rng.choice(["aap", "Res", "q", "", "x%41", "utm_source"])
+            val = rng.choice(["noot", "1024x768", "%41%42", "a+b", "%C3%A9", "", "x=y"])
+            pieces.append(name if rng.random() < 0.15 else name + "=" + val)
+        q = "&".join(pieces) + ("&" if rng.random() < 0.2 else "")
+        if q and rng.random() < 0.7:
+            q = "?" + q
+        if rng.random() < 0.04:
+            q += "&bad=%g1"
+        out.append(head + b' "' + q.encode() + b'"')
+    return out
+
+
+@pytest.mark.parametrize("fields", [["STRING:request.querystring.*"],
+                                    ["STRING:request.querystring.aap", "STRING:request.querystring.res",
+                                     "HTTP.QUERYSTRING:request.querystring"]])
+def test_querystring_token_emulated(oracle, emu, fields):
+    """QueryStringFieldDissector on a raw %q token"""
+    o = oracle.Oracle(QS_FMT, fields)
+    e = emu.Emu(QS_FMT, fields)
+    assert e.status == 0, e.err
+    s = compare(o, e, querystring_lines(3000, 13))
+    assert s["ok"] > 2600 and s["fallback"] < 250, s

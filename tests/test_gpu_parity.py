@@ -77,7 +77,7 @@ def test_golden_vectors_gpu(oracle, vectors):
           "dissector not on the device)" % (checked, n, len(fallback), unsupported))
     for src in sorted(set(fallback)):
         print("  FALLBACK:", src)
-    assert checked >= 146, (checked, n)  # 148 of 163 in the CPU emulation of the same device code
+    assert checked >= 152, (checked, n)  # 154 of 163 in the CPU emulation of the same device code
 
 
 def test_setup_vectors_gpu(vectors):
@@ -538,3 +538,9 @@ def test_request_cookies_gpu(oracle, which):
                "HTTP.COOKIES:request.cookies", "STRING:request.status.last"]][which]
     s, _ = gpu_vs_oracle(oracle, COOKIE_FMT, fields, cookie_lines(20000, 11 + which))
     assert s["ok"] > 17000 and s["fallback"] < 2000, s
+
+
+def test_querystring_token_gpu(oracle):
+    from test_emu_parity import QS_FMT, querystring_lines
+    s, _ = gpu_vs_oracle(oracle, QS_FMT, ["STRING:request.querystring.*"], querystring_lines(20000, 13))
+    assert s["ok"] > 18000 and s["fallback"] < 1500, s
