@@ -861,6 +861,27 @@ __host__ __device__ LP_INLINE int cand_first(const Program& P, const ElemV& e, c
     case EK_UPLIST_DEC: return uplist_at(L, p, true);
     case EK_UPLIST_NUM: return uplist_at(L, p, false);
     case EK_UPLIST_NS: return uplist_ns_end(P, e, L, p);
+    case EK_CACHE_STATUS: {
+        // the alternatives in order; their first letters differ, so at most
+        // one matches at p (the element has a single candidate)
+        const char* alt[7] = {"MISS", "BYPASS", "EXPIRED", "STALE", "UPDATING", "REVALIDATED", "HIT"};
+        for (int k = 0; k < 7; ++k) {
+            int q = 0;
+            while (alt[k][q] && p + q < L.n && L[p + q] == (uint32_t)(uint8_t)alt[k][q]) ++q;
+            if (!alt[k][q]) return p + q;
+        }
+        return -1;
+    }
+    case EK_TIME_ISO: {  // [1-9]ddd-[01]d-[0-3]dTdd:dd:dd[+|-]dd:dd
+        if (p + 25 > L.n) return -1;
+        const uint32_t c0 = L[p], s = L[p + 19];
+        bool ok = c0 >= '1' && c0 <= '9' && L[p + 4] == '-' && L[p + 7] == '-' && L[p + 10] == 'T' &&
+                  L[p + 13] == ':' && L[p + 16] == ':' && L[p + 22] == ':' && (s == '+' || s == '|' || s == '-') &&
+                  L[p + 5] <= '1' && L[p + 8] <= '3';
+        const int dg[] = {1, 2, 3, 5, 6, 8, 9, 11, 12, 14, 15, 17, 18, 20, 21, 23, 24};
+        for (int k = 0; k < 17 && ok; ++k) ok = is_digit(L[p + dg[k]]);
+        return ok ? p + 25 : -1;
+    }
     case EK_BINIP: {
         if (p + 16 > L.n) return -1;
         for (int k = p; k < p + 16; k += 4)
@@ -976,7 +997,8 @@ __host__ __device__ LP_INLINE int cand_next(const Program& P, const ElemV& e, co
         // shorter IPv4 / IPv6 alternatives: exact only when none of them can
         // be followed by the rest of the format
         return ip_alt_end_possible(P, L, e, p, cur) ? -2 : -1;
-    case EK_ANYCHAR: case EK_MSEC: case EK_UPLIST_NS: case EK_BINIP: return -1;
+    case EK_ANYCHAR: case EK_MSEC: case EK_UPLIST_NS: case EK_BINIP: case EK_TIME_ISO: case EK_CACHE_STATUS:
+        return -1;
     case EK_DECIMAL: {  // a shorter fraction
         const int d = digits_end(L, p);
         return cur - 1 >= d + 2 ? cur - 1 : -1;
@@ -1385,6 +1407,39 @@ __host__ __device__ LP_INLINE bool parse_apache_time(const LN& L, int a, int64_t
     return true;
 }
 
+// TimeStampDissector("TIME.ISO8601", "yyyy-MM-dd'T'HH:mm:ssXXX")
+// (hp/HttpdLoglineParser.java:110, TimeStampDissector.java:100-108) on the
+// 25 bytes at a (the token kind proved the digit / separator layout):
+// SMART resolution as parse_apache_time, numeric month 1..12, offset
+// "+HH:MM" (numbers <= 59, total within +-18:00; '|' fails).
+template <typename LN>
+__host__ __device__ LP_INLINE bool parse_iso_time(const LN& L, int a, int64_t& epoch_s, uint64_t& local, uint64_t& utc) {
+    const Bytes28 c = load28(L, a);
+    auto d2 = [&](int k) { return (int)(c[k] - '0') * 10 + (int)(c[k + 1] - '0'); };
+    const int32_t year = (int32_t)((c[0] - '0') * 1000 + (c[1] - '0') * 100 + (c[2] - '0') * 10 + (c[3] - '0'));
+    int month = d2(5), day = d2(8), hh = d2(11), mi = d2(14), ss = d2(17);
+    if (c[19] == '|') return false;
+    const int oh = d2(20), om = d2(23);
+    if (oh > 59 || om > 59) return false;
+    const int off = (c[19] == '-' ? -1 : 1) * (oh * 3600 + om * 60);
+    if (off > 64800 || off < -64800) return false;
+    if (month < 1 || month > 12 || day < 1 || day > 31) return false;
+    const int ml = month_len(year, month);
+    if (day > ml) day = ml;
+    if (mi > 59) return false;
+    int32_t y = year;
+    int32_t days = days_from_civil(y, month, day);
+    if (hh == 24 && mi == 0 && ss == 0) {
+        hh = 0;
+        ++days;
+        civil_from_days(days, y, month, day);
+    } else if (hh > 23 || ss > 59) {
+        return false;
+    }
+    time_fields(y, month, day, hh, mi, ss, off, days, epoch_s, local, utc);
+    return true;
+}
+
 // StrfTimeStampDissector with a fixed-width converted formatter
 // (StrfTimeToDateTimeFormatter: appendValue(DAY_OF_MONTH, 2), appendText(
 // MONTH_OF_YEAR, SHORT) in the default locale en_US, appendValue(YEAR, 4),
@@ -1618,6 +1673,9 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
         uint32_t ns = 0;
         if (T.kind == TK_APACHE) {
             if (!parse_apache_time(L, a, ep, lo, ut)) { o.status = ST_BAD; return; }
+            ep *= 1000;
+        } else if (T.kind == TK_ISO) {
+            if (!parse_iso_time(L, a, ep, lo, ut)) { o.status = ST_BAD; return; }
             ep *= 1000;
         } else {
             // an empty or "-" (null) value has no outputs (TimeStampDissector.java:412-415)

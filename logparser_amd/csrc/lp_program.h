@@ -69,6 +69,8 @@ enum ElemKind : uint8_t {
     EK_UPLIST_NUM,   // X(?: *, *X(?: *: *X)?)*, X = [0-9]+            (upstream byte lists)
     EK_UPLIST_NS,    // X(?: *, *X(?: *: *X)?)*, X = [^\s]*           (upstream address / status lists)
     EK_BINIP,        // (\\x[0-9a-fA-F]{2}){4}                         ($binary_remote_addr)
+    EK_TIME_ISO,     // [1-9][0-9]{3}-[0-1][0-9]-[0-3][0-9]T[0-9]{2}:[0-9]{2}:[0-9]{2}[\+|\-][0-9]{2}:[0-9]{2}
+    EK_CACHE_STATUS, // (?:MISS|BYPASS|EXPIRED|STALE|UPDATING|REVALIDATED|HIT)  ($upstream_cache_status)
 };
 
 struct alignas(16) Elem {
@@ -119,7 +121,7 @@ __host__ __device__ inline ElemV load_elem(P p) {
 // converts to fixed-width DateTimeFormatter fields
 // (hp/dissectors/StrfTimeToDateTimeFormatter.java): the value must be exactly
 // `width` bytes, op k reads its field at byte off[k].
-enum : uint8_t { TK_APACHE = 0, TK_STRF = 1 };
+enum : uint8_t { TK_APACHE = 0, TK_STRF = 1, TK_ISO = 2 };  // TK_ISO: TIME.ISO8601 ($time_iso8601)
 enum : uint8_t { SF_LIT, SF_DAY, SF_MON, SF_MONTXT, SF_YEAR, SF_CLOCKH, SF_HOD, SF_MIN, SF_SEC, SF_MSEC, SF_USEC, SF_OFF };
 constexpr int MAX_SF_OPS = 32;
 // Stage structs hold 32-bit fields only: the kernels read them with scalar

@@ -80,6 +80,8 @@ int elem_kind_of(const std::string& r) {
     if (r == upstream_list(R_NUMBER)) return EK_UPLIST_NUM;
     if (r == upstream_list(R_NO_SPACE)) return EK_UPLIST_NS;
     if (r == R_BINIP) return EK_BINIP;
+    if (r == R_TIME_ISO8601) return EK_TIME_ISO;
+    if (r == "(?:MISS|BYPASS|EXPIRED|STALE|UPDATING|REVALIDATED|HIT)") return EK_CACHE_STATUS;  // UpstreamModule.java
     return -1;
 }
 
@@ -1190,7 +1192,10 @@ void Plan::compile_program() {
         case EK_NUMBER: case EK_CLFNUMBER: case EK_NONZERO: e.det = (e.nlit && !dig0) || e.last; break;
         case EK_HEXNUMBER: case EK_CLFHEXNUMBER: e.det = (e.nlit && !hex0) || e.last; break;
         case EK_ANY_GREEDY: case EK_ANY_LAZY: e.det = e.last; break;
-        case EK_TIME_US: case EK_ANYCHAR: case EK_MSEC: case EK_BINIP: case EK_UPLIST_NS: e.det = 1; break;
+        case EK_TIME_US: case EK_ANYCHAR: case EK_MSEC: case EK_BINIP: case EK_UPLIST_NS: case EK_TIME_ISO:
+        case EK_CACHE_STATUS:
+            e.det = 1;
+            break;
         case EK_DECIMAL: e.det = (e.nlit && !dig0) || e.last; break;
         case EK_NOSPACE3: e.det = (e.nlit && ws0) || e.last; break;
         default: e.det = 0; break;
@@ -1228,12 +1233,13 @@ void Plan::compile_program() {
             if (it == compiled_.end()) return;
             for (const auto& in : it->second) {
                 switch (in.cls) {
-                case D_TIMESTAMP: {
+                case D_TIMESTAMP: case D_TIMESTAMP_ISO: {
                     if (ok != O_TOKEN) { device_ok_ = false; why_ = "timestamp from a derived value"; return; }
                     if (!time_of_tok_.count(tk(oi))) {
                         if (P.n_time == MAX_TIME) { device_ok_ = false; why_ = "too many timestamps"; return; }
                         P.time[P.n_time].tok = (int8_t)oi;
                         P.time[P.n_time].fmt = (int8_t)cur_fmt;
+                        P.time[P.n_time].kind = in.cls == D_TIMESTAMP_ISO ? TK_ISO : TK_APACHE;
                         time_of_tok_[tk(oi)] = P.n_time++;
                     }
                     break;
@@ -1496,7 +1502,7 @@ void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const 
     case D_LOCALIZED:  // StrfTimeStampDissector.LocalizedTimeDissector (:117-120): the raw value
         if (has("")) emit(c, name, "TIME.LOCALIZEDSTRING", "", v);
         return;
-    case D_TIMESTAMP: case D_STRFTIME: {
+    case D_TIMESTAMP: case D_TIMESTAMP_ISO: case D_STRFTIME: {
         if (v.null || v.len == 0) return;
         int t = time_of_tok_.at(t_fmt * 64 + oi);
         int64_t epoch = R.t_epoch[t][i];

@@ -1083,7 +1083,7 @@ static void inst_prepare(orc_parser *p, instance *in, const char *subroot, const
         break;
     }
     case D_LOCALIZED: break;
-    case D_TIMESTAMP_ISO: case D_SETCOOKIES:
+    case D_SETCOOKIES:
     case D_SETCOOKIE: case D_UNIQUEID:
         if (!p->unsupported) {
             p->unsupported = 1;
@@ -1532,6 +1532,50 @@ static int parse_apache_time(js s, int64_t *ly, int *lm, int *ld, int *lh, int *
     return 0;
 }
 
+/* TimeStampDissector("TIME.ISO8601", "yyyy-MM-dd'T'HH:mm:ssXXX") (hp/HttpdLoglineParser.java:110,
+ * TimeStampDissector.java:100-108): parseCaseInsensitive + appendPattern, SMART
+ * resolver.  YEAR_OF_ERA 4+ digits (the token regex gives exactly 4),
+ * MONTH_OF_YEAR / DAY_OF_MONTH / HOUR_OF_DAY / MINUTE / SECOND two digits,
+ * appendOffset("+HH:MM", "Z") (each number <= 59, total within +-18:00);
+ * resolution as in parse_apache_time (month 1..12, day 1..31 clamped to the
+ * month, 24:00:00 = next day). */
+static int parse_iso_time(js s, int64_t *ly, int *lm, int *ld, int *lh, int *lmi, int *ls, int *offset_secs) {
+    if (s.n != 25) return 1;
+    const int *c = s.c;
+    int64_t year = 0;
+    for (int k = 0; k < 4; k++) { int v = dig(c[k]); if (v < 0) return 1; year = year * 10 + v; }
+    if (c[4] != '-' || c[7] != '-' || c[10] != 'T' || c[13] != ':' || c[16] != ':' || c[22] != ':') return 1;
+    const int idx[] = {5, 8, 11, 14, 17, 20, 23};
+    int v[7];
+    for (int k = 0; k < 7; k++) {
+        int a = dig(c[idx[k]]), b = dig(c[idx[k] + 1]);
+        if (a < 0 || b < 0) return 1;
+        v[k] = a * 10 + b;
+    }
+    if (c[19] != '+' && c[19] != '-') return 1;
+    if (v[5] > 59 || v[6] > 59) return 1;
+    int off = (c[19] == '-' ? -1 : 1) * (v[5] * 3600 + v[6] * 60);
+    if (off > 18 * 3600 || off < -18 * 3600) return 1;
+    int month = v[0], day = v[1], hh = v[2], mi = v[3], ss = v[4];
+    if (month < 1 || month > 12) return 1;
+    if (day < 1 || day > 31) return 1;
+    int ml = month_len(year, month);
+    if (day > ml) day = ml;
+    if (mi > 59) return 1;
+    int plus_day = 0;
+    if (hh == 24 && mi == 0 && ss == 0) { hh = 0; plus_day = 1; }
+    else {
+        if (hh > 23) return 1;
+        if (ss > 59) return 1;
+    }
+    if (plus_day) {
+        int64_t days = days_from_civil(year, month, day) + 1;
+        civil_from_days(days, &year, &month, &day);
+    }
+    *ly = year; *lm = month; *ld = day; *lh = hh; *lmi = mi; *ls = ss; *offset_secs = off;
+    return 0;
+}
+
 static int has_req(instance *in, const char *n) { return sl_has(&in->requested, n); }
 
 static js fmt2(parsable *ps, const char *f, int64_t a, int b, int c) {
@@ -1641,7 +1685,9 @@ static void d_timestamp(parsable *ps, instance *in, const char *inputname) {
     js s = v_getstring(ps->a, *vp);
     if (s.null || s.n == 0) return;
     int64_t y; int m, d, h, mi, sec, off;
-    if (parse_apache_time(s, &y, &m, &d, &h, &mi, &sec, &off)) { ps->failed = 1; return; }
+    const int bad = in->d->cls == D_TIMESTAMP_ISO ? parse_iso_time(s, &y, &m, &d, &h, &mi, &sec, &off)
+                                                  : parse_apache_time(s, &y, &m, &d, &h, &mi, &sec, &off);
+    if (bad) { ps->failed = 1; return; }
     emit_time(ps, in, inputname, y, m, d, h, mi, sec, 0, off);
 }
 
@@ -2509,7 +2555,7 @@ static void d_upstream(parsable *ps, instance *in, const char *inputname) {
 static void run_instance(parsable *ps, instance *in, const char *name) {
     switch (in->d->cls) {
     case D_ROOT: d_root(ps, in, name); break;
-    case D_TIMESTAMP: d_timestamp(ps, in, name); break;
+    case D_TIMESTAMP: case D_TIMESTAMP_ISO: d_timestamp(ps, in, name); break;
     case D_STRFTIME: d_strftime(ps, in, name); break;
     case D_LOCALIZED: d_localized(ps, in, name); break;
     case D_FIRSTLINE: d_firstline(ps, in, name); break;

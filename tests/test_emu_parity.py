@@ -445,6 +445,34 @@ def test_upstream_lists_and_binary_ip_emulated(oracle, emu):
     assert rec["UPSTREAM_ADDR:nginxmodule.upstream.addr.1.redirected"] == ["c:3"]
 
 
+CACHE_FMT = '$remote_addr $upstream_cache_status [$time_local] "$request" $status'
+
+
+def cache_status_lines(n, seed):
+    """$upstream_cache_status: the seven words of UpstreamModule's alternation
+    plus near misses (BAD lines)"""
+    rng = random.Random(seed)
+    words = ["MISS", "BYPASS", "EXPIRED", "STALE", "UPDATING", "REVALIDATED", "HIT",
+             "MISSING", "HITS", "-", "miss", "", "REVALIDATE", "STALE STALE"]
+    out = []
+    for i in range(n):
+        w = rng.choice(words[:7]) if rng.random() < 0.8 else rng.choice(words[7:])
+        out.append(('10.1.%d.%d %s [%02d/Mar/2024:10:%02d:%02d +0100] "GET /p?x=%d HTTP/1.1" %d' % (
+            rng.randrange(256), rng.randrange(256), w, 1 + i % 28, i % 60, (i * 7) % 60, i,
+            rng.choice([200, 304, 404]))).encode())
+    return out
+
+
+def test_upstream_cache_status_emulated(oracle, emu):
+    """$upstream_cache_status (?:MISS|BYPASS|...|HIT) on the device"""
+    paths = oracle.possible_paths(CACHE_FMT)
+    o = oracle.Oracle(CACHE_FMT, paths)
+    e = emu.Emu(CACHE_FMT, paths)
+    assert e.status == 0, e.err
+    s = compare(o, e, cache_status_lines(3000, 8))
+    assert s["ok"] > 2000 and s["bad"] > 300 and s["fallback"] == 0, s
+
+
 COOKIE_FMT = '%h %l %u %t "%r" %>s %b "%{Cookie}i"'
 
 
@@ -519,3 +547,39 @@ def test_querystring_token_emulated(oracle, emu, fields):
     assert e.status == 0, e.err
     s = compare(o, e, querystring_lines(3000, 13))
     assert s["ok"] > 2600 and s["fallback"] < 250, s
+
+
+ISO_FMT = '$remote_addr - - [$time_iso8601] "$request" $status'
+
+
+def iso_lines(n, seed):
+    """NGINX $time_iso8601 lines: valid stamps and the resolver corners
+    (day clamp, 24:00:00, offsets up to +-18:00, invalid month / day /
+    offset / sign -> BAD)"""
+    rng = random.Random(seed)
+    out = []
+    for _ in range(n):
+        y = rng.choice([2000, 2012, 2015, 2016, 2019, 2024, 1999, 9999, 1000])
+        mo = rng.choice(list(range(1, 13)) + [0, 13])
+        d = rng.choice(list(range(1, 29)) + [29, 30, 31, 0, 32])
+        h = rng.choice(list(range(0, 24)) + [24])
+        mi = rng.choice([0, 1, 30, 59, 60])
+        s = rng.choice([0, 5, 59, 60])
+        sign = rng.choice("++--|")
+        oh, om = rng.choice([(0, 0), (1, 0), (5, 30), (14, 0), (18, 0), (19, 0), (2, 60)])
+        if rng.random() < 0.7:  # mostly valid
+            mo, d, h, mi, s, oh, om, sign = rng.randrange(1, 13), rng.randrange(1, 29), rng.randrange(24), \
+                rng.randrange(60), rng.randrange(60), rng.randrange(15), rng.choice([0, 30, 45]), rng.choice("+-")
+        ts = "%04d-%02d-%02dT%02d:%02d:%02d%s%02d:%02d" % (y, mo, d, h, mi, s, sign, oh, om)
+        out.append(('10.0.0.%d - - [%s] "GET /x?a=%d HTTP/1.1" 200' % (rng.randrange(256), ts, rng.randrange(99))).encode())
+    return out
+
+
+def test_iso8601_timestamps_emulated(oracle, emu):
+    """TimeStampDissector("TIME.ISO8601", "yyyy-MM-dd'T'HH:mm:ssXXX") on the device"""
+    paths = oracle.possible_paths(ISO_FMT)
+    o = oracle.Oracle(ISO_FMT, paths)
+    e = emu.Emu(ISO_FMT, paths)
+    assert e.status == 0, e.err
+    s = compare(o, e, iso_lines(4000, 21), allow_fallback=False)
+    assert s["ok"] > 2500 and s["bad"] > 300, s

@@ -77,7 +77,7 @@ def test_golden_vectors_gpu(oracle, vectors):
           "dissector not on the device)" % (checked, n, len(fallback), unsupported))
     for src in sorted(set(fallback)):
         print("  FALLBACK:", src)
-    assert checked >= 152, (checked, n)  # 154 of 163 in the CPU emulation of the same device code
+    assert checked >= 154, (checked, n)  # 156 of 163 in the CPU emulation of the same device code
 
 
 def test_setup_vectors_gpu(vectors):
@@ -544,3 +544,17 @@ def test_querystring_token_gpu(oracle):
     from test_emu_parity import QS_FMT, querystring_lines
     s, _ = gpu_vs_oracle(oracle, QS_FMT, ["STRING:request.querystring.*"], querystring_lines(20000, 13))
     assert s["ok"] > 18000 and s["fallback"] < 1500, s
+
+
+def test_iso8601_timestamps_gpu(oracle):
+    from test_emu_parity import ISO_FMT, iso_lines
+    fields = oracle.possible_paths(ISO_FMT)
+    s, _ = gpu_vs_oracle(oracle, ISO_FMT, fields, iso_lines(20000, 21), allow_fallback=False)
+    assert s["ok"] > 12000 and s["bad"] > 1500, s
+
+
+def test_upstream_cache_status_gpu(oracle):
+    from test_emu_parity import CACHE_FMT, cache_status_lines
+    fields = oracle.possible_paths(CACHE_FMT)
+    s, _ = gpu_vs_oracle(oracle, CACHE_FMT, fields, cache_status_lines(20000, 9), allow_fallback=False)
+    assert s["ok"] > 14000 and s["bad"] > 2000, s
