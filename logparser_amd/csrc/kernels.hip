@@ -399,10 +399,13 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
     const uint32_t total = __shfl(x, 63);
     const int shard = (int)(wave % ARENA_SHARDS);
     unsigned long long wbase = 0;
-    if (lane == 63 && total) wbase = atomicAdd(&C.meta->shard_top[16 * shard], (unsigned long long)total);
-    wbase = __shfl(wbase, 63);
+    // regions start 16-byte aligned (their query tables take 16-byte slot
+    // stores; spills keep the bump pointer only 4-byte aligned)
+    if (lane == 63 && total) wbase = atomicAdd(&C.meta->shard_top[16 * shard], (unsigned long long)total + 12ull);
+    wbase = (__shfl(wbase, 63) + 15) & ~15ull;
     const bool fits = wbase + total <= C.shard_cap;
     uint32_t written = 0;
+    unsigned long long my_region = 0;
     if (active) {
         if (o.status == ST_OK && !fits && need) {
             // the shard is full: the batch is re-run with a larger arena
@@ -410,6 +413,7 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
             atomicAdd(&C.meta->arena_ovf, 1ull);
         } else if (o.status == ST_OK) {
             const unsigned long long mine = (unsigned long long)shard * C.shard_cap + wbase + x - need;
+            my_region = mine;
             C.arena_base[li] = mine;  // also for an empty region: spills are region-relative
             Arena A{C.arena + mine, 0, need};
             A.top = &C.meta->shard_top[16 * shard];  // spills come from the same shard
@@ -432,7 +436,7 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
     if (P.n_query > 0 && LP_EXP != 14) {
         __syncthreads();  // the table slots written in phase 2 are visible to every lane
         const bool has = active && o.status == ST_OK && need != 0;
-        const unsigned long long my_ab = has ? C.arena_base[li] : 0ull;
+        const unsigned long long my_ab = has ? my_region : 0ull;
         for (int qs = 0; qs < P.n_query; ++qs) {
             const uint32_t np = has ? o.qpend.get(qs) : 0u;
             const uint32_t my_list = o.qlist.get(qs);
@@ -450,14 +454,32 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
                 const uint32_t ob = __shfl(base, own), olist = __shfl(my_list, own);
                 const unsigned long long oab = __shfl(my_ab, own);
                 const auto OL = owner_line(L, own);
+                LP_G uint64_t* slot = reinterpret_cast<LP_G uint64_t*>(C.arena + oab + olist + 16 * (g - ob));
+                QPrep qp;
+                if (g < tot) qp = query_prep(OL, slot);
+                // the round's spilled bytes in one allocation from the wave's
+                // shard (every owner is a line of this wave)
+                uint32_t x = qp.need;
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t y = __shfl_up(x, d);
+                    if (lane >= d) x += y;
+                }
+                const uint32_t rtot = __shfl(x, 63);
+                unsigned long long rbase = 0;
+                if (lane == 63 && rtot)
+                    rbase = atomicAdd(&C.meta->shard_top[16 * shard], (unsigned long long)rtot);
+                rbase = __shfl(rbase, 63);
                 if (g < tot) {
-                    Arena R{C.arena + oab, 0, 0};
-                    R.top = &C.meta->shard_top[16 * shard];  // the owner is a line of this wave: same shard
-                    R.base = oab - (unsigned long long)shard * C.shard_cap;
-                    R.limit = C.shard_cap;
-                    LP_G uint64_t* slot = reinterpret_cast<LP_G uint64_t*>(R.p + olist + 16 * (g - ob));
-                    written += query_piece(P, P.query[qs], OL, R, slot);
-                    if (R.ovf) atomicAdd(&C.meta->arena_ovf, 1ull);  // the batch is re-run with a larger arena
+                    const unsigned long long rel = oab - (unsigned long long)shard * C.shard_cap;  // region in the shard
+                    const unsigned long long at = rbase + x - qp.need;                          // piece in the shard
+                    if (qp.need && (at + qp.need > C.shard_cap || at - rel + qp.need > 0x7FFFFFFFull)) {
+                        slot[0] = REF_SKIP;
+                        slot[1] = 0;
+                        atomicAdd(&C.meta->arena_ovf, 1ull);  // the batch is re-run with a larger arena
+                    } else {
+                        Arena A{C.arena + oab, (uint32_t)(at - rel), (uint32_t)(at - rel + qp.need)};
+                        written += query_finish(P, P.query[qs], OL, A, C.arena + oab, slot, qp);
+                    }
                 }
             }
         }

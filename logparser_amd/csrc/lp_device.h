@@ -35,9 +35,22 @@ __device__ __forceinline__ void lp_prof_mark(int k) {
     if (w < (unsigned)PROF_WAVES && (int)threadIdx.x % 64 == (int)__builtin_ctzll(act))
         __builtin_nontemporal_store(t, &g_prof[w * PROF_POINTS + k]);
 }
+// accumulating points (inside loops): slot k += cycles since the lane's last LP_PACC
+__device__ __forceinline__ void lp_prof_acc(int k, unsigned long long& t0) {
+    const unsigned long long t = clock64();
+    const unsigned w = blockIdx.x - PROF_W0;
+    const uint64_t act = __ballot(1);
+    if (w < (unsigned)PROF_WAVES && (int)threadIdx.x % 64 == (int)__builtin_ctzll(act))
+        g_prof[w * PROF_POINTS + k] += t - t0;
+    t0 = t;
+}
 #define LP_PROF(k) lp_prof_mark(k)
+#define LP_PT_DECL unsigned long long lp_pt = clock64();
+#define LP_PACC(k) lp_prof_acc(k, lp_pt)
 #else
 #define LP_PROF(k)
+#define LP_PT_DECL
+#define LP_PACC(k)
 #endif
 #define LP_PROF_EL_BEGIN()
 #define LP_PROF_EL_END(i)
@@ -1773,6 +1786,7 @@ struct Arena {
 // X = a fresh piece of n bytes of A's shard, written like a region (region-
 // relative offsets).  false: the shard is full (A.ovf set).
 __host__ __device__ LP_INLINE bool spill(Arena& A, uint32_t n, Arena& X) {
+    n = (n + 3) & ~3u;  // every spilled piece starts 4-byte aligned (word stores)
     X = A;
     if (!A.top || n == 0) { A.ovf = A.top == nullptr; X.cap = X.used; return n == 0; }
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -1953,28 +1967,51 @@ __host__ __device__ LP_INLINE void put_encoded(Arena& A, uint32_t c) {
 // Latin-1 char U+00XX (VALID_STANDARD -> %00%XX, UTF-16 decode), '+' is a
 // space, and URIUtil escapes decode back to their byte.  Output UTF-8.
 // Bytes come from a two-word register window (one LDS read per 4 bytes).
+// Output is gathered into 32-bit words, one aligned word store per 4 bytes
+// (A.used is 4-byte aligned: spilled pieces are; the last word's padding
+// bytes lie inside the spilled piece).  Each outer step produces at least 4
+// bytes on every lane still decoding, so the lanes of a wave issue their word
+// stores together instead of one byte store per lane and byte.
+__host__ __device__ LP_INLINE void store_word(LP_G uint8_t* p, uint32_t v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    *reinterpret_cast<LP_G uint32_t*>(p) = v;
+#else
+    __builtin_memcpy(p, &v, 4);
+#endif
+}
 template <typename LN>
 __host__ __device__ LP_INLINE uint64_t url_decode_value(const LN& L, int vs, int e, Arena& A) {
     const uint32_t st = A.used;
     uint32_t W = (L.o + (uint32_t)vs) >> 2;
     uint64_t ww = (uint64_t)L.word(W) | ((uint64_t)L.word_or0(W + 1) << 32);
+    uint64_t acc = 0;  // pending output bytes (na of them)
+    uint32_t na = 0, out = st;
     for (int q = vs; q < e;) {
-        const uint32_t k = L.o + (uint32_t)q - 4 * W;  // 0..3
-        const uint32_t c = (uint32_t)(ww >> (8 * k)) & 0xFFu;
-        if (c == '%') {
-            const uint32_t v = hexv((uint32_t)(ww >> (8 * k + 8)) & 0xFFu) * 16 + hexv((uint32_t)(ww >> (8 * k + 16)) & 0xFFu);
-            if (v < 0x80) A.put(v);
-            else { A.put(0xC0 | (v >> 6)); A.put(0x80 | (v & 0x3F)); }
-            q += 3;
-        } else {
-            A.put(c == '+' ? ' ' : c);
-            ++q;
+        while (na < 4 && q < e) {
+            const uint32_t k = L.o + (uint32_t)q - 4 * W;  // 0..3
+            const uint32_t c = (uint32_t)(ww >> (8 * k)) & 0xFFu;
+            if (c == '%') {
+                const uint32_t v =
+                    hexv((uint32_t)(ww >> (8 * k + 8)) & 0xFFu) * 16 + hexv((uint32_t)(ww >> (8 * k + 16)) & 0xFFu);
+                if (v < 0x80) { acc |= (uint64_t)v << (8 * na); na += 1; }
+                else { acc |= (uint64_t)((0xC0 | (v >> 6)) | ((0x80 | (v & 0x3F)) << 8)) << (8 * na); na += 2; }
+                q += 3;
+            } else {
+                acc |= (uint64_t)(c == '+' ? ' ' : c) << (8 * na);
+                na += 1;
+                ++q;
+            }
+            if (L.o + (uint32_t)q >= 4 * (W + 1)) {
+                ++W;
+                ww = (ww >> 32) | ((uint64_t)L.word_or0(W + 1) << 32);
+            }
         }
-        if (L.o + (uint32_t)q >= 4 * (W + 1)) {
-            ++W;
-            ww = (ww >> 32) | ((uint64_t)L.word_or0(W + 1) << 32);
-        }
+        store_word(A.p + out, (uint32_t)acc);
+        if (na >= 4) { out += 4; na -= 4; acc >>= 32; }
+        else { out += na; na = 0; acc = 0; }
     }
+    if (na) { store_word(A.p + out, (uint32_t)acc); out += na; }
+    A.used = out;
     return mkref(st, A.used - st, true);
 }
 
@@ -2001,45 +2038,87 @@ struct QueryTable {
     // query_piece completes every slot afterwards, spread over the wave
     __host__ __device__ LP_INLINE void emit(LP_G uint8_t* region, int e) {
         if (e > s) {
+            // one 16-byte store per slot (tables are 16-byte aligned: regions are)
+            const uint64_t t0 = (uint64_t)(uint32_t)s | ((uint64_t)(uint32_t)e << 16) | ((uint64_t)(uint32_t)(lp + 1) << 48);
+#if defined(__HIP_DEVICE_COMPILE__)
+            typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+            *reinterpret_cast<LP_G u32x4_t*>(region + tab + 16 * count) = u32x4_t{(uint32_t)t0, (uint32_t)(t0 >> 32), 0u, 0u};
+#else
             LP_G uint64_t* t = (LP_G uint64_t*)(region + tab) + 2 * count;
-            t[0] = (uint64_t)(uint32_t)s | ((uint64_t)(uint32_t)e << 16) | ((uint64_t)(uint32_t)(lp + 1) << 48);
+            t[0] = t0;
             t[1] = 0;
+#endif
             ++count;
         }
         lp = -1;
     }
 };
 
-// Completes a query piece (QueryStringFieldDissector.java:75-104): the name
-// is lower-cased and keeps URIUtil's escapes, never decoded; a piece without
-// '=' has value ""; else the value goes through Utils.resilientUrlDecode.
-// R: the owning line's arena region (its spill allocator); slot: the piece's
-// table slot.  Returns the arena bytes written; R.ovf when a spill did not fit.
+// First '=' of [s, e) (-1 if none) and whether the name before it (the
+// whole piece without one) holds upper-case or URIUtil-escaped bytes: one
+// pass over the piece's words.
 template <typename LN>
-__host__ __device__ LP_INLINE uint32_t query_piece(const Program& P, const QueryStage& Q, const LN& L, Arena& R,
-                                                   LP_G uint64_t* slot) {
-    LP_G uint8_t* region = R.p;
-    const uint64_t a0 = slot[0];
-    const int s = (int)(a0 & 0xFFFFu), e = (int)((a0 >> 16) & 0xFFFFu);
-    const int lp = (int)((a0 >> 48) & 0xFFFFu) - 1;
-    // the piece's first '=' splits name and value ('=' is not a URI event byte)
-    const int f = find_fwd(L, s, e, [](uint32_t w) { return swar::eq(w, '='); });
-    const int eq = f < e ? f : -1;
-    const int ne = eq >= 0 ? eq : e;
-    // upper-case / URIUtil-escaped bytes in the name: it is rewritten
-    const bool rw = find_fwd(L, s, ne, [](uint32_t w) { return swar::upper(w) | swar::needs_encode(w); }) < ne;
-    const bool pv = eq >= 0 && lp > eq;               // '%' / '+' in the value
-    // rewritten name / decoded value: 3 bytes per piece byte at most
-    Arena A;
-    if (!spill(R, (rw || pv) ? 3u * (uint32_t)(e - s) : 0u, A)) {
-        slot[0] = REF_SKIP;
-        slot[1] = 0;
-        return 0;
+__host__ __device__ LP_INLINE int piece_eq_rw(const LN& L, int s, int e, bool& rw) {
+    rw = false;
+    if (s >= e) return -1;
+    const uint32_t A = L.o + (uint32_t)s, E = L.o + (uint32_t)e;
+    uint32_t W = A >> 2;
+    uint32_t valid = swar::HI << (8 * (A & 3));
+    for (;;) {
+        const uint32_t w = L.word(W);
+        const uint32_t r = E - 4 * W;  // bytes of this word before E (>= 1)
+        if (r < 4) valid &= swar::HI >> (8 * (4 - r));
+        const uint32_t meq = swar::eq(w, '=') & valid;
+        const uint32_t mrw = (swar::upper(w) | swar::needs_encode(w)) & valid;
+        if (meq) {
+            rw = rw || (mrw & ((meq & (0u - meq)) - 1u)) != 0;  // name bytes before the '='
+            return (int)(4 * W + (uint32_t)swar::first(meq) - L.o);
+        }
+        rw = rw || mrw != 0;
+        ++W;
+        if (4 * W >= E) return -1;
+        valid = swar::HI;
     }
+}
+
+// A query piece's split (QueryStringFieldDissector.java:75-104): bounds from
+// its table slot, the first '=', and the arena bytes its completion may write
+// (rewritten name: 3 per name byte; decoded value: at most its length).
+struct QPrep {
+    int s = 0, e = 0, eq = -1;
+    bool rw = false, pv = false;
+    uint32_t need = 0;
+};
+template <typename LN>
+__host__ __device__ LP_INLINE QPrep query_prep(const LN& L, const LP_G uint64_t* slot) {
+    QPrep q;
+    const uint64_t a0 = slot[0];
+    q.s = (int)(a0 & 0xFFFFu);
+    q.e = (int)((a0 >> 16) & 0xFFFFu);
+    const int lp = (int)((a0 >> 48) & 0xFFFFu) - 1;  // the piece's last '%' / '+'
+    q.eq = piece_eq_rw(L, q.s, q.e, q.rw);
+    q.pv = q.eq >= 0 && lp > q.eq;  // '%' / '+' in the value
+    const int ne = q.eq >= 0 ? q.eq : q.e;
+    // (whole words: the decoder's last word store pads up to 3 bytes)
+    q.need = (q.rw ? (3u * (uint32_t)(ne - q.s) + 3u) & ~3u : 0u) + (q.pv ? ((uint32_t)(q.e - q.eq - 1) + 3u) & ~3u : 0u);
+    return q;
+}
+
+// Completes a query piece: the name is lower-cased and keeps URIUtil's
+// escapes, never decoded; a piece without '=' has value ""; else the value
+// goes through Utils.resilientUrlDecode.  A: the piece's spilled bytes
+// (q.need of them, A.used 4-byte aligned, offsets relative to the owning
+// line's region `region`); slot: the piece's table slot.  Returns the arena
+// bytes written.
+template <typename LN>
+__host__ __device__ LP_INLINE uint32_t query_finish(const Program& P, const QueryStage& Q, const LN& L, Arena& A,
+                                                    const LP_G uint8_t* region, LP_G uint64_t* slot, const QPrep& qp) {
+    const int s = qp.s, e = qp.e, eq = qp.eq;
+    const int ne = eq >= 0 ? eq : e;
     const uint32_t a1 = A.used;
     // name [s, ne): URIUtil-escaped and lower-cased as in the rawQuery
     uint64_t nref;
-    if (rw) {
+    if (qp.rw) {
         const char* HX = "0123456789abcdef";  // URIUtil's %XX, lower-cased with the name
         const uint32_t mark = A.used;
         for (int q = s; q < ne; ++q) {
@@ -2048,6 +2127,7 @@ __host__ __device__ LP_INLINE uint32_t query_piece(const Program& P, const Query
             else A.put((c - 'A') < 26u ? (c | 32) : c);
         }
         nref = mkref(mark, A.used - mark, true);
+        A.used = (A.used + 3) & ~3u;  // the value's words start aligned
     } else {
         nref = mkref(s, ne - s, false);
     }
@@ -2058,7 +2138,7 @@ __host__ __device__ LP_INLINE uint32_t query_piece(const Program& P, const Query
         if (Q.name_len[k] != nlen) continue;
         bool same = true;
         for (uint32_t q = 0; q < nlen && same; ++q) {
-            const uint32_t c = rw ? (uint32_t)region[ref_off(nref) + q] : L[s + (int)q];
+            const uint32_t c = qp.rw ? (uint32_t)region[ref_off(nref) + q] : L[s + (int)q];
             same = c == P.lit_byte((int)(Q.name_off[k] + q));
         }
         want = same;
@@ -2070,11 +2150,27 @@ __host__ __device__ LP_INLINE uint32_t query_piece(const Program& P, const Query
     }
     uint64_t vref;
     if (eq < 0) vref = mkref(0, 0, false);  // no '=' -> ""
-    else if (!pv) vref = mkref(eq + 1, e - eq - 1, false);
+    else if (!qp.pv) vref = mkref(eq + 1, e - eq - 1, false);
     else vref = url_decode_value(L, eq + 1, e, A);
     slot[0] = nref;
     slot[1] = vref;
     return A.used - a1;
+}
+
+// One query piece, its bytes spilled on its own (the test-only CPU
+// emulation; the kernel allocates the spills of a whole round of pieces at
+// once).  R: the owning line's arena region.  R.ovf when a spill did not fit.
+template <typename LN>
+__host__ __device__ LP_INLINE uint32_t query_piece(const Program& P, const QueryStage& Q, const LN& L, Arena& R,
+                                                   LP_G uint64_t* slot) {
+    const QPrep qp = query_prep(L, slot);
+    Arena A;
+    if (!spill(R, qp.need, A)) {
+        slot[0] = REF_SKIP;
+        slot[1] = 0;
+        return 0;
+    }
+    return query_finish(P, Q, L, A, R.p, slot, qp);
 }
 
 // HttpUriDissector fast path on the line bytes [a,b).  Returns status.
@@ -2114,7 +2210,7 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
             } else if (fa < 0 && qsi >= 0) {
                 T.on = T.set = true;
                 T.maxp = usep + 1;
-                T.tab = (A.used + 7) & ~7u;
+                T.tab = (A.used + 15) & ~15u;
                 T.reg = T.tab + 16 * T.maxp;
                 T.s = q + 1;
             }
@@ -2168,7 +2264,7 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
                 // the rawQuery starts: table, pending list, piece regions
                 T.on = T.set = true;
                 T.maxp = usep + 1;
-                T.tab = (A.used + 7) & ~7u;
+                T.tab = (A.used + 15) & ~15u;
                 T.reg = T.tab + 16 * T.maxp;
                 T.s = q + 1;
             }

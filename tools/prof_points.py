@@ -58,4 +58,9 @@ for w in range(W):
 for (a, b), (s_, c) in sorted(acc.items(), key=lambda kv: order.index(kv[0][0]) * 100 + order.index(kv[0][1])):
     print("  %-18s -> %-18s %9.0f cycles/wave  (%d waves)" % (names[a], names[b], s_ / c, c))
     tot += s_ / max(1, W)
+acc_names = {57: "qp owner search", 58: "qp slot read + '=' find", 59: "qp name scan", 60: "qp spill",
+             61: "qp want", 62: "qp value decode", 63: "qp slot write + tail"}
+for k, nm in acc_names.items():
+    v = T[:, k]
+    print("  [sum] %-28s %9.0f cycles/wave" % (nm, v[T[:, 0] != 0].mean()))
 print("  total %.0f cycles per wave (start -> last point)" % np.mean([r[r != 0].max() - r[0] for r in T if r[0]]))
