@@ -1592,6 +1592,138 @@ __host__ __device__ LP_INLINE bool uri_source(const Program& P, const LineOut& o
     return b > a;
 }
 
+// ---- Set-Cookie headers (ResponseSetCookieListDissector.java:79-110 with
+// JDK 8 java.net.HttpCookie.parse, ResponseSetCookieDissector.java:78-151).
+// The replay splits the list and names / dissects the cookies; the device
+// proves the value lies in the restated subset where none of the reference's
+// exceptions can occur (the oracle's sc_subset / sc_name / sc_expire):
+// printable ASCII without '"', '\\' and '$', no "max-age" / "version" /
+// "set-cookie" (any case: HttpCookie.parse then takes its Netscape branch, one
+// cookie per string); every cookie string (the ", " parts, a part whose
+// "expires=" sits within its last 15 bytes joined with the next one) has a
+// first ';'-token with a '=' before which the trimmed name is a non-empty
+// token that no JDK reserves; with `exp`, every "expires" attribute
+// (case-sensitive key) is "EEE, dd-MMM-yyyy HH:mm:ss GMT" with in-range
+// fields and the right day name (parseExpire's only reachable pattern).
+template <typename LN>
+__host__ __device__ LP_INLINE bool ci_lit_at(const LN& L, int q, int b, const char* lit) {  // lit lower-case
+    for (int k = 0; lit[k]; ++k) {
+        if (q + k >= b) return false;
+        uint32_t c = L[q + k];
+        if (c - 'A' < 26u) c |= 32u;
+        if (c != (uint8_t)lit[k]) return false;
+    }
+    return true;
+}
+template <typename LN>
+__host__ __device__ LP_INLINE bool sc_expire_ok(const LN& L, int a, int b) {
+    if (b - a != 29) return false;
+    const char* shape = "XXX, 00-XXX-0000 00:00:00 GMT";  // X: day / month name bytes (checked below)
+    for (int i = 0; i < 29; ++i) {
+        const uint32_t c = L[a + i], t = (uint8_t)shape[i];
+        if (t == 'X') continue;
+        if (t == '0') { if (!is_digit(c)) return false; }
+        else if (c != t) return false;
+    }
+    const uint32_t dn = L[a] | (L[a + 1] << 8) | (L[a + 2] << 16), mn = L[a + 8] | (L[a + 9] << 8) | (L[a + 10] << 16);
+    const char* days = "MonTueWedThuFriSatSun";
+    const char* mons = "JanFebMarAprMayJunJulAugSepOctNovDec";
+    int dow = -1, mon = -1;
+    for (int k = 0; k < 7; ++k)
+        if (dn == ((uint32_t)(uint8_t)days[3 * k] | ((uint32_t)(uint8_t)days[3 * k + 1] << 8) |
+                   ((uint32_t)(uint8_t)days[3 * k + 2] << 16))) dow = k;
+    for (int k = 0; k < 12; ++k)
+        if (mn == ((uint32_t)(uint8_t)mons[3 * k] | ((uint32_t)(uint8_t)mons[3 * k + 1] << 8) |
+                   ((uint32_t)(uint8_t)mons[3 * k + 2] << 16))) mon = k + 1;
+    if (dow < 0 || mon < 0) return false;
+    auto d2 = [&](int i) { return (int)(L[a + i] - '0') * 10 + (int)(L[a + i + 1] - '0'); };
+    const int d = d2(5), y = d2(12) * 100 + d2(14), h = d2(17), mi = d2(20), se = d2(23);
+    if (y < 1 || d < 1 || d > month_len(y, mon) || h > 23 || mi > 59 || se > 59) return false;
+    return iso_dow(days_from_civil(y, mon, d)) == dow + 1;
+}
+// The cookie string [s, e): HttpCookie.parseInternal's name is valid; with
+// exp, its "expires" attributes parse.
+template <typename LN>
+__host__ __device__ LP_INLINE bool sc_cookie_ok(const LN& L, int s, int e, bool exp) {
+    int q = s;
+    while (q < e && L[q] == ';') ++q;
+    if (q == e) return false;  // "Empty cookie header string"
+    int te = q;
+    while (te < e && L[te] != ';') ++te;
+    int eq = q;
+    while (eq < te && L[eq] != '=') ++eq;
+    if (eq == te) return false;  // "Invalid cookie name-value pair"
+    int na = q, nb = eq;
+    while (na < nb && L[na] <= ' ') ++na;
+    while (nb > na && L[nb - 1] <= ' ') --nb;
+    if (na == nb) return false;
+    for (int k = na; k < nb; ++k)
+        if (L[k] == ' ' || L[k] == ',') return false;  // isToken (the subset has no controls, ';' or '$')
+    const int nl = nb - na;
+    auto is = [&](const char* r, int n) { return nl == n && ci_lit_at(L, na, nb, r); };
+    if (is("comment", 7) || is("commenturl", 10) || is("discard", 7) || is("domain", 6) || is("expires", 7) ||
+        is("path", 4) || is("port", 4) || is("secure", 6))
+        return false;  // names older JDKs reserve
+    if (!exp) return true;
+    // ResponseSetCookieDissector: split(";"), trim, split("=", 2); key "expires" (i > 0)
+    for (int ps = s, i = 0; ps <= e; ++i) {
+        int pe = ps;
+        while (pe < e && L[pe] != ';') ++pe;
+        if (i > 0) {
+            int ka = ps, kb = pe;
+            while (ka < kb && L[ka] <= ' ') ++ka;
+            int x = ka;
+            while (x < kb && L[x] != '=') ++x;
+            int ke = x;
+            while (ke > ka && L[ke - 1] <= ' ') --ke;
+            if (ke - ka == 7 && L[ka] == 'e' && L[ka + 1] == 'x' && L[ka + 2] == 'p' && L[ka + 3] == 'i' &&
+                L[ka + 4] == 'r' && L[ka + 5] == 'e' && L[ka + 6] == 's') {
+                if (x == kb) return false;  // no '=': parseExpire("") throws
+                int va = x + 1, vb = kb;
+                while (va < vb && L[va] <= ' ') ++va;
+                while (vb > va && L[vb - 1] <= ' ') --vb;
+                if (!sc_expire_ok(L, va, vb)) return false;
+            }
+        }
+        ps = pe + 1;
+    }
+    return true;
+}
+template <typename LN>
+__host__ __device__ LP_INLINE bool setcookie_ok(const LN& L, int a, int b, bool exp) {
+    if (b <= a) return true;  // empty: nothing is dissected
+    for (int q = a; q < b; ++q) {
+        const uint32_t c = L[q];
+        if (c < 0x20 || c > 0x7E || c == '"' || c == '\\' || c == '$') return false;
+        const uint32_t lc = c | 32u;
+        if ((lc == 'm' && ci_lit_at(L, q, b, "max-age")) || (lc == 'v' && ci_lit_at(L, q, b, "version")) ||
+            (lc == 's' && ci_lit_at(L, q, b, "set-cookie")))
+            return false;
+    }
+    // split(", "): trailing empty parts are dropped
+    int t = b;
+    while (t - a >= 2 && L[t - 2] == ',' && L[t - 1] == ' ') t -= 2;
+    if (t == a) return true;
+    int prev = -1;
+    for (int s = a; s <= t;) {
+        int e = s;
+        while (e < t && !(L[e] == ',' && e + 1 < t && L[e + 1] == ' ')) ++e;
+        // a part whose "expires=" starts within its last 15 bytes waits for the next
+        int ei = -1;
+        for (int q = s; q + 8 <= e && ei < 0; ++q)
+            if ((L[q] | 32u) == 'e' && ci_lit_at(L, q, e, "expires=")) ei = q - s;
+        if (ei >= 0 && (e - s) - 15 < ei) {
+            prev = s;
+        } else {
+            if (!sc_cookie_ok(L, prev >= 0 ? prev : s, e, exp)) return false;
+            prev = -1;
+        }
+        if (e >= t) break;
+        s = e + 2;
+    }
+    return true;
+}
+
 // Phase 1: guard, match, tokens, time, first line; arena need for phase 2.
 // clean: the caller already proved every byte of the line passes the
 // fast-path guard (the kernel checks the whole staged window at once).
@@ -1673,6 +1805,16 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
         for (int q = find_fwd(L, a, b, [](uint32_t w) { return swar::eq(w, '%'); }); q < b;
              q = find_fwd(L, q + 1, b, [](uint32_t w) { return swar::eq(w, '%'); }))
             if (q + 2 >= b || !is_hex(L[q + 1]) || !is_hex(L[q + 2])) { o.status = ST_FALLBACK; return; }
+    }
+    // Set-Cookie lists the replay splits (the subset where HttpCookie.parse cannot throw)
+    for (uint32_t gm = (uint32_t)P.guard_setc[fmt]; gm; gm &= gm - 1) {
+        const int k = __builtin_ctz(gm);
+        if (o.tok_flags & (1u << k)) continue;  // "-": null, nothing is dissected
+        const uint32_t sp = o.caps.get(k);
+        if (!setcookie_ok(L, (int)(sp & 0xFFFF), (int)(sp >> 16), (P.guard_setc_exp[fmt] >> k) & 1)) {
+            o.status = ST_FALLBACK;
+            return;
+        }
     }
     LP_PROF(5);
     // TimeStampDissector

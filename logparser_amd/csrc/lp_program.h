@@ -185,6 +185,14 @@ struct Program {
     // cookies): bit k -> phase 1 sends the line to FALLBACK unless every '%'
     // is followed by two hex digits and the value is ASCII
     int32_t guard_pct[MAX_FMT];
+    // token slots of format f holding a Set-Cookie header list the replay
+    // splits into cookies (ResponseSetCookieListDissector): bit k -> phase 1
+    // sends the line to FALLBACK unless the value is in the restated subset
+    // where java.net.HttpCookie.parse cannot throw (setcookie_ok);
+    // guard_setc_exp: the same slots whose cookies ResponseSetCookieDissector
+    // dissects (every "expires" must then parse)
+    int32_t guard_setc[MAX_FMT];
+    int32_t guard_setc_exp[MAX_FMT];
     int32_t pad_[2];
     Elem elems[MAX_ELEMS];
     TimeStage time[MAX_TIME];

@@ -1269,6 +1269,17 @@ void Plan::compile_program() {
                 case D_LOCALIZED:
                     if (ok != O_TOKEN) { device_ok_ = false; why_ = "localized time from a derived value"; return; }
                     break;
+                case D_SETCOOKIES: {
+                    // ResponseSetCookieListDissector / ResponseSetCookieDissector:
+                    // split, joined, named and dissected in the replay; the device
+                    // proves HttpCookie.parse and parseExpire cannot throw (setcookie_ok)
+                    if (ok != O_TOKEN) { device_ok_ = false; why_ = "Set-Cookie list from a derived value"; return; }
+                    P.guard_setc[cur_fmt] |= 1 << oi;
+                    const std::string pre = "HTTP.SETCOOKIE:" + complete + ".";
+                    for (const auto& kv : compiled_)
+                        if (kv.first.compare(0, pre.size(), pre) == 0) P.guard_setc_exp[cur_fmt] |= 1 << oi;
+                    break;
+                }
                 case D_COOKIES:
                     // RequestCookieListDissector: split and decoded in the replay;
                     // the device proves the decode cannot fail (guard_pct)
@@ -1459,7 +1470,8 @@ const char* MONTH_FULL[] = {"January", "February", "March", "April", "May", "Jun
 
 static thread_local int t_origin_kind = 0, t_origin_idx = 0, t_fmt = 0;  // t_fmt: the line's LogFormat
 
-void Plan::emit(Ctx& c, const std::string& base, const std::string& type, const std::string& name, const MVal& v) const {
+void Plan::emit(Ctx& c, const std::string& base, const std::string& type, const std::string& name, const MVal& v,
+                const MVal* dv) const {
     std::string complete, wild;
     if (base.empty()) {
         complete = name;
@@ -1476,7 +1488,7 @@ void Plan::emit(Ctx& c, const std::string& base, const std::string& type, const 
             for (const auto& in : it->second) {
                 t_origin_kind = ok;
                 t_origin_idx = oi;
-                run_phase(c, in, complete, v);
+                run_phase(c, in, complete, dv ? *dv : v);
             }
     }
     const bool exact = needed_.count(needed) > 0, wildcard = needed_.count(wild) > 0;
@@ -1752,6 +1764,106 @@ void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const 
             }
             c.pool.emplace_back(std::move(val));
             emit(c, name, "HTTP.COOKIE", nm, mstr((const uint8_t*)c.pool.back().data(), (uint32_t)c.pool.back().size()));
+        }
+        return;
+    }
+    case D_SETCOOKIES: {
+        // ResponseSetCookieListDissector.dissect (dissectors/ResponseSetCookieListDissector.java:79-110):
+        // split(", ") (trailing empty parts dropped), a part whose lower-cased
+        // "expires=" starts within its last 15 chars is joined with the next
+        // one, HttpCookie.parse names each cookie string (the device proved the
+        // Netscape branch: one cookie, the first ';'-token's name before '=',
+        // trimmed), lower-cased; the value is the cookie string itself
+        if (v.null || v.len == 0) return;
+        const bool all = has("*");
+        uint32_t t = v.len;
+        while (t >= 2 && v.p[t - 2] == ',' && v.p[t - 1] == ' ') t -= 2;
+        if (t == 0) return;
+        int64_t prev = -1;
+        // (name, cookie string) in order; a name's further dissection reads
+        // the Parsable's cache, which holds the LAST value added under that
+        // name (core/Parsable.java:172-183, Parser.java:735-753)
+        std::vector<std::pair<std::string, MVal>> got;
+        for (uint32_t s = 0; s <= t;) {
+            uint32_t e = s;
+            while (e < t && !(v.p[e] == ',' && e + 1 < t && v.p[e + 1] == ' ')) ++e;
+            int64_t ei = -1;
+            for (uint32_t q = s; q + 8 <= e && ei < 0; ++q) {
+                static const char ex[] = "expires=";
+                bool m = true;
+                for (int k = 0; k < 8 && m; ++k) m = (v.p[q + k] | (v.p[q + k] >= 'A' && v.p[q + k] <= 'Z' ? 32 : 0)) == ex[k];
+                if (m) ei = q - s;
+            }
+            if (ei >= 0 && (int64_t)(e - s) - 15 < ei) {
+                prev = s;
+            } else {
+                const uint32_t cs = prev >= 0 ? (uint32_t)prev : s;
+                prev = -1;
+                uint32_t q = cs;
+                while (q < e && v.p[q] == ';') ++q;
+                uint32_t eq = q;
+                while (eq < e && v.p[eq] != '=' && v.p[eq] != ';') ++eq;
+                uint32_t na = q, nb = eq;
+                while (na < nb && v.p[na] <= ' ') ++na;
+                while (nb > na && v.p[nb - 1] <= ' ') --nb;
+                std::string nm((const char*)v.p + na, nb - na);
+                for (auto& ch : nm) if (ch >= 'A' && ch <= 'Z') ch = char(ch + 32);
+                if (all || has(nm.c_str())) got.emplace_back(nm, mstr(v.p + cs, e - cs));
+            }
+            if (e >= t) break;
+            s = e + 2;
+        }
+        for (size_t k = 0; k < got.size(); ++k) {
+            const MVal* last = &got[k].second;
+            for (size_t j = k + 1; j < got.size(); ++j)
+                if (got[j].first == got[k].first) last = &got[j].second;
+            set_origin(O_NONE, 0);
+            emit(c, name, "HTTP.SETCOOKIE", got[k].first, got[k].second, last);
+        }
+        return;
+    }
+    case D_SETCOOKIE: {
+        // ResponseSetCookieDissector.dissect (dissectors/ResponseSetCookieDissector.java:78-135):
+        // split(";"), each part trimmed and split("=", 2) with key and value
+        // trimmed; part 0 is the "value", later parts "expires" (epoch seconds
+        // as STRING, milliseconds as TIME.EPOCH; the device proved the date
+        // matches "EEE, dd-MMM-yyyy HH:mm:ss GMT"), "domain", "comment", "path"
+        if (v.null || v.len == 0) return;
+        auto trim = [&](uint32_t& a, uint32_t& b) {
+            while (a < b && v.p[a] <= ' ') ++a;
+            while (b > a && v.p[b - 1] <= ' ') --b;
+        };
+        for (uint32_t ps = 0, part = 0; ps <= v.len; ++part) {
+            uint32_t pe = ps;
+            while (pe < v.len && v.p[pe] != ';') ++pe;
+            uint32_t a = ps, b = pe;
+            trim(a, b);
+            uint32_t x = a;
+            while (x < b && v.p[x] != '=') ++x;
+            uint32_t ka = a, kb = x, va = x < b ? x + 1 : b, vb = b;
+            trim(ka, kb);
+            trim(va, vb);
+            const std::string key((const char*)v.p + ka, kb - ka);
+            set_origin(O_NONE, 0);
+            if (pe == v.len && a == b && part > 0) break;  // a trailing empty part (split drops it)
+            if (part == 0) {
+                emit(c, name, "STRING", "value", mstr(v.p + va, vb - va));
+            } else if (key == "expires") {
+                const uint8_t* d = v.p + va;
+                static const char mons[] = "JanFebMarAprMayJunJulAugSepOctNovDec";
+                int mon = 1;
+                for (int k = 0; k < 12; ++k)
+                    if (d[8] == mons[3 * k] && d[9] == mons[3 * k + 1] && d[10] == mons[3 * k + 2]) mon = k + 1;
+                auto d2 = [&](int i) { return (d[i] - '0') * 10 + (d[i + 1] - '0'); };
+                const int64_t days = days_from_civil(d2(12) * 100 + d2(14), mon, d2(5));
+                const int64_t ms = (days * 86400 + d2(17) * 3600 + d2(20) * 60 + d2(23)) * 1000;
+                emit(c, name, "STRING", "expires", mlong(ms / 1000));
+                set_origin(O_NONE, 0);
+                emit(c, name, "TIME.EPOCH", "expires", mlong(ms));
+            } else if (key == "domain" || key == "comment" || key == "path") {
+                emit(c, name, "STRING", key, mstr(v.p + va, vb - va));
+            }
+            ps = pe + 1;
         }
         return;
     }

@@ -147,7 +147,9 @@ private:
     // replay
     struct Ctx;
     void replay(Ctx& c) const;
-    void emit(Ctx& c, const std::string& base, const std::string& type, const std::string& name, const MVal& v) const;
+    // dv: the value further dissectors read (default v)
+    void emit(Ctx& c, const std::string& base, const std::string& type, const std::string& name, const MVal& v,
+              const MVal* dv = nullptr) const;
     void run_phase(Ctx& c, const Instance& in, const std::string& name, const MVal& v) const;
 
     std::vector<std::unique_ptr<Format>> formats_;

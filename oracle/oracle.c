@@ -1083,8 +1083,7 @@ static void inst_prepare(orc_parser *p, instance *in, const char *subroot, const
         break;
     }
     case D_LOCALIZED: break;
-    case D_SETCOOKIES:
-    case D_SETCOOKIE: case D_UNIQUEID:
+    case D_UNIQUEID:
         if (!p->unsupported) {
             p->unsupported = 1;
             snprintf(p->unsupported_why, sizeof p->unsupported_why, "unsupported dissector for input type %s", in->d->in_type);
@@ -2528,6 +2527,139 @@ static void d_cookies(parsable *ps, instance *in, const char *inputname) {
     }
 }
 
+/* ---- Set-Cookie (ResponseSetCookieListDissector.java:79-110 with JDK 8
+ * java.net.HttpCookie.parse, ResponseSetCookieDissector.java:78-151).
+ * Restated on the subset where HttpCookie.parse takes its Netscape
+ * (version 0) branch: printable ASCII without '"', '\\' and '$', and none of
+ * "max-age", "version", "set-cookie" (any case) -- guessCookieVersion then
+ * returns 0 and parseInternal reads the whole string as one cookie.  Inputs
+ * outside it, and inputs on which the reference throws out of the parser
+ * (IllegalArgumentException from HttpCookie, DateTimeParseException from
+ * parseExpire), are UNSUPPORTED. */
+static int sc_subset(parsable *ps, js s) {
+    for (int i = 0; i < s.n; i++) {
+        const int c = s.c[i];
+        if (c < 0x20 || c > 0x7E || c == '"' || c == '\\' || c == '$') return 0;
+    }
+    js low = js_lower(ps->a, s);
+    return js_index_of(low, js_lit(ps->a, "max-age"), 0) < 0 && js_index_of(low, js_lit(ps->a, "version"), 0) < 0 &&
+           js_index_of(low, js_lit(ps->a, "set-cookie"), 0) < 0;
+}
+
+/* HttpCookie.parseInternal's name of cookie string v (StringTokenizer(";")
+ * first token, split at its first '=', trimmed; the HttpCookie constructor's
+ * isToken / '$' checks): 1 and *name, or 0 when the reference throws.  Names
+ * that older JDKs reserve (isReserved) are refused too. */
+static int sc_name(parsable *ps, js v, js *name) {
+    int q = 0;
+    while (q < v.n && v.c[q] == ';') q++;
+    if (q == v.n) return 0;  /* "Empty cookie header string" */
+    int te = q;
+    while (te < v.n && v.c[te] != ';') te++;
+    int eq = -1;
+    for (int i = q; i < te; i++) if (v.c[i] == '=') { eq = i; break; }
+    if (eq < 0) return 0;  /* "Invalid cookie name-value pair" */
+    js nm = js_trim(v, q, eq);
+    if (nm.n == 0 || nm.c[0] == '$') return 0;
+    for (int i = 0; i < nm.n; i++) {
+        const int c = nm.c[i];
+        if (c < 0x20 || c >= 0x7F || c == ',' || c == ';' || c == ' ') return 0;  /* isToken */
+    }
+    static const char *const reserved[] = {"comment", "commenturl", "discard", "domain", "expires", "max-age",
+                                           "path", "port", "secure", "version", NULL};
+    js low = js_lower(ps->a, nm);
+    for (int k = 0; reserved[k]; k++) if (js_eq_lit(low, reserved[k])) return 0;
+    *name = nm;
+    return 1;
+}
+
+static void d_setcookies(parsable *ps, instance *in, const char *inputname) {
+    val *vp = cache_get(ps, "HTTP.SETCOOKIES", inputname);
+    js s = v_getstring(ps->a, *vp);
+    if (s.null || s.n == 0) return;
+    if (!sc_subset(ps, s)) { ps->unsupported = 1; return; }
+    const int want_all = has_req(in, "*");
+    int st[512], en[512];
+    const int np = java_split2(s, 0, s.n, ',', ' ', st, en, 512);  /* fieldValue.split(", ") */
+    if (np < 0) { ps->unsupported = 1; return; }
+    int prev = -1;
+    for (int k = 0; k < np; k++) {
+        js part = js_sub(s, st[k], en[k]);
+        const int ei = js_index_of(js_lower(ps->a, part), js_lit(ps->a, "expires="), 0);
+        if (ei != -1 && part.n - 15 < ei) { prev = k; continue; }  /* "expires=XXXXXXX".length() */
+        /* previous + ", " + part: the parts are contiguous in s */
+        js value = prev >= 0 ? js_sub(s, st[prev], en[k]) : part;
+        prev = -1;
+        js name;
+        if (!sc_name(ps, value, &name)) { ps->unsupported = 1; return; }
+        js low = js_lower(ps->a, name);
+        char *nm = js_cstr(ps, low);
+        if (want_all || has_req(in, nm)) add_str(ps, inputname, "HTTP.SETCOOKIE", nm, value);
+    }
+}
+
+/* ResponseSetCookieDissector.parseExpire (:138-151): only its first pattern
+ * "EEE',' dd-MMM-yyyy HH:mm:ss zzz" can ever succeed (a DateTimeParseException
+ * is not the IllegalArgumentException the loop catches).  Restated for the
+ * zone "GMT", 4-digit years, in-range fields and a matching day name; anything
+ * else UNSUPPORTED.  1 and *ms on success. */
+static int sc_expire(js v, int64_t *ms) {
+    static const char *const days[] = {"Mon", "Tue", "Wed", "Thu", "Fri", "Sat", "Sun"};
+    static const char *const mons[] = {"Jan", "Feb", "Mar", "Apr", "May", "Jun",
+                                       "Jul", "Aug", "Sep", "Oct", "Nov", "Dec"};
+    if (v.n != 29) return 0;
+    const char *shape = "AAA, 00-AAA-0000 00:00:00 GMT";
+    for (int i = 0; i < 29; i++) {
+        const int c = v.c[i], t = shape[i];
+        if (t == 'A') { if (!((c >= 'A' && c <= 'Z') || (c >= 'a' && c <= 'z'))) return 0; }
+        else if (t == '0') { if (c < '0' || c > '9') return 0; }
+        else if (c != t) return 0;
+    }
+    int dow = -1, mon = -1;
+    for (int k = 0; k < 7; k++) if (v.c[0] == days[k][0] && v.c[1] == days[k][1] && v.c[2] == days[k][2]) dow = k;
+    for (int k = 0; k < 12; k++) if (v.c[8] == mons[k][0] && v.c[9] == mons[k][1] && v.c[10] == mons[k][2]) mon = k + 1;
+    if (dow < 0 || mon < 0) return 0;
+#define D2(i) ((v.c[i] - '0') * 10 + (v.c[i + 1] - '0'))
+    const int d = D2(5), y = D2(12) * 100 + D2(14), h = D2(17), mi = D2(20), se = D2(23);
+#undef D2
+    static const int ml[] = {31, 28, 31, 30, 31, 30, 31, 31, 30, 31, 30, 31};
+    const int leap = (y % 4 == 0 && y % 100 != 0) || y % 400 == 0;
+    const int mlen = ml[mon - 1] + (mon == 2 && leap);
+    if (y < 1 || d < 1 || d > mlen || h > 23 || mi > 59 || se > 59) return 0;
+    const int64_t days_ = days_from_civil(y, mon, d);
+    const int iso = (int)(((days_ % 7) + 7 + 3) % 7);  /* 1970-01-01 was a Thursday (ISO 4 -> index 3) */
+    if (iso != dow) return 0;
+    *ms = (days_ * 86400 + h * 3600 + mi * 60 + se) * 1000;
+    return 1;
+}
+
+static void d_setcookie(parsable *ps, instance *in, const char *inputname) {
+    (void)in;
+    val *vp = cache_get(ps, "HTTP.SETCOOKIE", inputname);
+    js s = v_getstring(ps->a, *vp);
+    if (s.null || s.n == 0) return;
+    js *parts;
+    const int np = js_split_char(ps->a, s, ';', &parts);
+    for (int i = 0; i < np; i++) {
+        js part = js_trim(parts[i], 0, parts[i].n);
+        js *kv;
+        const int nkv = js_split_char_limit(ps->a, part, '=', 2, &kv);
+        js key = js_trim(kv[0], 0, kv[0].n);
+        js value = nkv == 2 ? js_trim(kv[1], 0, kv[1].n) : js_lit(ps->a, "");
+        if (i == 0) {
+            add_str(ps, inputname, "STRING", "value", value);
+        } else if (js_eq_lit(key, "expires")) {
+            int64_t ms;
+            if (!sc_expire(value, &ms)) { ps->unsupported = 1; return; }
+            add_long(ps, inputname, "STRING", "expires", ms / 1000);
+            add_long(ps, inputname, "TIME.EPOCH", "expires", ms);
+        } else if (js_eq_lit(key, "domain") || js_eq_lit(key, "comment") || js_eq_lit(key, "path")) {
+            char *nm = js_cstr(ps, key);
+            add_str(ps, inputname, "STRING", nm, value);
+        }
+    }
+}
+
 /* UpstreamListDissector.dissect (nginxmodules/UpstreamListDissector.java:79-125):
  * split(", ") into servers, each split(": ") into original / redirected,
  * both trimmed; N.value and N.redirected per server. */
@@ -2569,6 +2701,8 @@ static void run_instance(parsable *ps, instance *in, const char *name) {
     case D_MS2US: d_ms2us(ps, in, name); break;
     case D_UPSTREAM: d_upstream(ps, in, name); break;
     case D_COOKIES: d_cookies(ps, in, name); break;
+    case D_SETCOOKIES: d_setcookies(ps, in, name); break;
+    case D_SETCOOKIE: d_setcookie(ps, in, name); break;
     default: ps->unsupported = 1; break;
     }
 }

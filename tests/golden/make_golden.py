@@ -63,8 +63,10 @@ APACHE_TEST_FIELDS = [
     "HTTP.COOKIES:request.cookies", "HTTP.SETCOOKIES:response.cookies",
     "MICROSECONDS:response.server.processing.time", "HTTP.HEADER:response.header.etag",
 ]
-APACHE_SKIPPED = ["HTTP.COOKIE:request.cookies.jquery-ui-theme", "HTTP.SETCOOKIE:response.cookies.apache",
-                  "STRING:response.cookies.apache.domain", "SCREENWIDTH:request.firstline.uri.query.res.width",
+APACHE_SKIPPED = ["HTTP.COOKIE:request.cookies.jquery-ui-theme (the (cookies) case below)",
+                  "HTTP.SETCOOKIE:response.cookies.apache (the (cookies) case below)",
+                  "STRING:response.cookies.apache.domain (the (cookies) case below)",
+                  "SCREENWIDTH:request.firstline.uri.query.res.width",
                   "SCREENHEIGHT:request.firstline.uri.query.res.height"]
 
 case("hpt/ApacheHttpdLogParserTest.java:104-163", FULLCOMBINED,
@@ -112,9 +114,14 @@ case("hpt/ApacheHttpdLogParserTest.java:104-163 (cookies)", FULLCOMBINED,
      "\"Mozilla/5.0 (X11; Linux i686 on x86_64; rv:11.0) Gecko/20100101 Firefox/11.0\" "
      "\"jquery-ui-theme=Eggplant\" \"Apache=127.0.0.1.1344635380111339; path=/; domain=.basjes.nl\" \"-\" "
      "\"\\\"3780ff-4bd-4c1ce3df91380\\\"\"",
-     ["HTTP.COOKIES:request.cookies", "HTTP.COOKIE:request.cookies.jquery-ui-theme"],
+     ["HTTP.COOKIES:request.cookies", "HTTP.COOKIE:request.cookies.jquery-ui-theme",
+      "HTTP.SETCOOKIES:response.cookies", "HTTP.SETCOOKIE:response.cookies.apache",
+      "STRING:response.cookies.apache.domain"],
      expect={"HTTP.COOKIES:request.cookies": "jquery-ui-theme=Eggplant",
-             "HTTP.COOKIE:request.cookies.jquery-ui-theme": "Eggplant"})
+             "HTTP.COOKIE:request.cookies.jquery-ui-theme": "Eggplant",
+             "HTTP.SETCOOKIES:response.cookies": "Apache=127.0.0.1.1344635380111339; path=/; domain=.basjes.nl",
+             "HTTP.SETCOOKIE:response.cookies.apache": "Apache=127.0.0.1.1344635380111339; path=/; domain=.basjes.nl",
+             "STRING:response.cookies.apache.domain": ".basjes.nl"})
 
 # hpt/CookiesTest.java:110-127,157-218 (cookiesTest): the request cookies of COOKIES_LINE
 COOKIES_FMT = ("%h %a %A %l %u %t \"%r\" %>s %b %p \"%q\" \"%{Referer}i\" %D \"%{User-agent}i\" "
@@ -131,7 +138,70 @@ case("hpt/CookiesTest.java:110-127,157-218", COOKIES_FMT,
      expect={"HTTP.COOKIE:request.cookies.jquery-ui-theme": "Eggplant",
              "HTTP.COOKIE:request.cookies.apache": "127.0.0.1.1351111543699529",
              "STRING:request.status.last": "200", "HTTP.URI:request.firstline.uri": "/index.php"},
-     skipped=["HTTP.SETCOOKIES / HTTP.SETCOOKIE fields (ResponseSetCookieDissector: not restated)"])
+     skipped=["HTTP.SETCOOKIES / HTTP.SETCOOKIE fields (the next case)"])
+
+# hpt/CookiesTest.java:71-80,219-232: the Set-Cookie list of COOKIES_LINE
+# (ResponseSetCookieListDissector + ResponseSetCookieDissector).  The test
+# accepts the expires seconds within 2 (a Double compare); the value is the
+# Long 1577836810 (its getString is "1577836810").
+case("hpt/CookiesTest.java:71-80,219-232", COOKIES_FMT,
+     "127.0.0.1 127.0.0.1 127.0.0.1 - - [31/Dec/2012:23:00:44 -0700] \"GET /index.php HTTP/1.1\" "
+     "200 - 80 \"\" \"-\" 80991 \"Mozilla/5.0 (X11; Linux i686 on x86_64; rv:11.0) Gecko/20100101 Firefox/11.0\" "
+     "\"jquery-ui-theme=Eggplant; Apache=127.0.0.1.1351111543699529\" "
+     "\"NBA-0=, NBA-1=1234, NBA-2=1234; expires=Wed, 01-Jan-2020 00:00:10 GMT, "
+     "NBA-3=1234; expires=Wed, 01-Jan-2020 00:00:10 GMT; path=/, "
+     "NBA-4=1234; expires=Wed, 01-Jan-2020 00:00:10 GMT; path=/; domain=.basj.es\" \"-\" \"-\"",
+     ["HTTP.SETCOOKIES:response.cookies", "HTTP.SETCOOKIE:response.cookies.nba-4", "STRING:response.cookies.nba-4.value",
+      "STRING:response.cookies.nba-4.expires", "STRING:response.cookies.nba-4.path",
+      "STRING:response.cookies.nba-4.domain"],
+     expect={"HTTP.SETCOOKIES:response.cookies":
+             "NBA-0=, NBA-1=1234, NBA-2=1234; expires=Wed, 01-Jan-2020 00:00:10 GMT, "
+             "NBA-3=1234; expires=Wed, 01-Jan-2020 00:00:10 GMT; path=/, "
+             "NBA-4=1234; expires=Wed, 01-Jan-2020 00:00:10 GMT; path=/; domain=.basj.es",
+             "HTTP.SETCOOKIE:response.cookies.nba-4": "NBA-4=1234; expires=Wed, 01-Jan-2020 00:00:10 GMT; path=/; domain=.basj.es",
+             "STRING:response.cookies.nba-4.value": "1234",
+             "STRING:response.cookies.nba-4.expires": {"l": 1577836810},
+             "STRING:response.cookies.nba-4.path": "/",
+             "STRING:response.cookies.nba-4.domain": ".basj.es"})
+
+# hpt/dissectors/TestCookieDissector.java:43-135 (testResponseSetCookies), as
+# the %{Set-Cookie}o token of a one-token LogFormat ("cookies" -> "response.cookies")
+_SC_IN = ("NBA-0=, NBA-1=1234, NBA-2=1234; expires=Wed, 01-Jan-2020 00:00:10 GMT, "
+          "NBA-3=1234; expires=Wed, 01-Jan-2020 00:00:10 GMT; path=/xx, "
+          "NBA-4=1234; expires=Wed, 01-Jan-2020 00:00:10 GMT; path=/xx; domain=.basj.es, "
+          "NBA-5=1234; path=/xx; domain=.basj.es, "
+          "NBA-6=1234; expires=Wed, 01-Jan-2020 00:00:10 GMT; domain=.basj.es, "
+          "NBA-7=1234; expires=Wed, 01-Jan-2020 00:00:10 GMT; domain=.basj.es; comment=bla bla bla")
+_SC = {0: ("NBA-0=", "", None, None, None, None), 1: ("NBA-1=1234", "1234", None, None, None, None),
+       2: ("NBA-2=1234; expires=Wed, 01-Jan-2020 00:00:10 GMT", "1234", True, None, None, None),
+       3: ("NBA-3=1234; expires=Wed, 01-Jan-2020 00:00:10 GMT; path=/xx", "1234", True, "/xx", None, None),
+       4: ("NBA-4=1234; expires=Wed, 01-Jan-2020 00:00:10 GMT; path=/xx; domain=.basj.es", "1234", True, "/xx",
+           ".basj.es", None),
+       5: ("NBA-5=1234; path=/xx; domain=.basj.es", "1234", None, "/xx", ".basj.es", None),
+       6: ("NBA-6=1234; expires=Wed, 01-Jan-2020 00:00:10 GMT; domain=.basj.es", "1234", True, None, ".basj.es", None),
+       7: ("NBA-7=1234; expires=Wed, 01-Jan-2020 00:00:10 GMT; domain=.basj.es; comment=bla bla bla", "1234", True,
+           None, ".basj.es", "bla bla bla")}
+_sc_fields, _sc_expect, _sc_absent = ["HTTP.SETCOOKIES:response.cookies"], {"HTTP.SETCOOKIES:response.cookies": _SC_IN}, []
+for _k, (_c, _v, _ex, _p, _d, _cm) in _SC.items():
+    _b = "response.cookies.nba-%d" % _k
+    _sc_fields += ["HTTP.SETCOOKIE:" + _b, "STRING:%s.value" % _b, "STRING:%s.expires" % _b,
+                   "TIME.EPOCH:%s.expires" % _b, "STRING:%s.path" % _b, "STRING:%s.domain" % _b,
+                   "STRING:%s.comment" % _b]
+    _sc_expect["HTTP.SETCOOKIE:" + _b] = _c
+    _sc_expect["STRING:%s.value" % _b] = _v
+    if _ex:
+        _sc_expect["STRING:%s.expires" % _b] = {"l": 1577836810}
+        _sc_expect["TIME.EPOCH:%s.expires" % _b] = {"l": 1577836810000}
+    else:
+        _sc_absent += ["STRING:%s.expires" % _b, "TIME.EPOCH:%s.expires" % _b]
+    for _t, _x in (("path", _p), ("domain", _d), ("comment", _cm)):
+        if _x is None:
+            if _k != 7 or _t == "path":
+                _sc_absent.append("STRING:%s.%s" % (_b, _t))
+        else:
+            _sc_expect["STRING:%s.%s" % (_b, _t)] = _x
+case("hpt/dissectors/TestCookieDissector.java:43-135", "%{Set-Cookie}o", _SC_IN, _sc_fields, expect=_sc_expect,
+     absent=_sc_absent)
 
 # hpt/dissectors/TestCookieDissector.java:26-40 (testRequestCookies), as the
 # %{Cookie}i token of a one-token LogFormat

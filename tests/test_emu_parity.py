@@ -583,3 +583,102 @@ def test_iso8601_timestamps_emulated(oracle, emu):
     assert e.status == 0, e.err
     s = compare(o, e, iso_lines(4000, 21), allow_fallback=False)
     assert s["ok"] > 2500 and s["bad"] > 300, s
+
+
+SETCOOKIE_FMT = '%h %l %u %t "%r" %>s %b "%{Set-Cookie}o"'
+_DAYS = ["Mon", "Tue", "Wed", "Thu", "Fri", "Sat", "Sun"]
+_MONS = ["Jan", "Feb", "Mar", "Apr", "May", "Jun", "Jul", "Aug", "Sep", "Oct", "Nov", "Dec"]
+
+
+def _expires(rng):
+    """an "expires" date: mostly "EEE, dd-MMM-yyyy HH:mm:ss GMT" with the right
+    day name; some with a wrong day name, another zone or another layout
+    (the reference throws on those: FALLBACK)"""
+    import datetime
+    d = datetime.datetime(1990, 1, 1) + datetime.timedelta(seconds=rng.randrange(0, 60 * 365 * 86400))
+    day = _DAYS[d.weekday()]
+    r = rng.random()
+    if r < 0.05:
+        day = _DAYS[(d.weekday() + 1) % 7]
+    zone = "GMT" if rng.random() > 0.05 else rng.choice(["UTC", "PST", "CET"])
+    if rng.random() < 0.04:
+        return "%s, %02d %s %04d %02d:%02d:%02d %s" % (day, d.day, _MONS[d.month - 1], d.year, d.hour, d.minute,
+                                                       d.second, zone)
+    return "%s, %02d-%s-%04d %02d:%02d:%02d %s" % (day, d.day, _MONS[d.month - 1], d.year, d.hour, d.minute,
+                                                   d.second, zone)
+
+
+def setcookie_lines(n, seed):
+    """'combined'-like lines ending in a Set-Cookie header list: several
+    cookies joined by ", " with expires / path / domain / comment / Secure /
+    HttpOnly attributes, upper-case and blank-padded names, "-" and empty
+    headers, and inputs outside the restated subset or on which the reference
+    throws (Max-Age, quotes, '$' names, reserved names, names without '=',
+    bad dates: FALLBACK)"""
+    rng = random.Random(seed)
+    base = lpa.synth_combined(seed, 0, n).split(b"\n")[:-1]
+    out = []
+    for l in base:
+        head = l.rsplit(b' "', 2)[0]
+        r = rng.random()
+        if r < 0.15:
+            hdr = "-"
+        elif r < 0.18:
+            hdr = ""
+        else:
+            cookies = []
+            for _ in range(rng.randrange(1, 5)):
+                name = rng.choice(["SESSION", "sid", "NBA-1", "_ga", " pad ", "x.y", "Theme", "sid"])
+                if rng.random() < 0.08:
+                    name = rng.choice(["a b", "$v", "Path", "", "x,z"])
+                val = rng.choice(["1234", "", "abc=def", "a:b", "bla bla", "%41", "x,y", "1234"])
+                if rng.random() < 0.03:
+                    val = 'q"q'
+
+                c = name + "=" + val if rng.random() > 0.03 else name
+                for _ in range(rng.randrange(0, 4)):
+                    a = rng.random()
+                    if a < 0.35:
+                        c += "; expires=" + _expires(rng)
+                    elif a < 0.5:
+                        c += "; path=/" + rng.choice(["", "xx", "a/b"])
+                    elif a < 0.62:
+                        c += "; domain=." + rng.choice(["basj.es", "example.com"])
+                    elif a < 0.7:
+                        c += "; comment=bla bla"
+                    elif a < 0.78:
+                        c += "; " + rng.choice(["Secure", "HttpOnly", "secure"])
+                    elif a < 0.85:
+                        c += "; Expires=" + _expires(rng)
+                    elif a < 0.865:
+                        c += "; Max-Age=" + rng.choice(["10", "x"])
+                    elif a < 0.9:
+                        c += ";;  path = /sp "
+                    else:
+                        c += "; Domain=.Basj.ES"
+                cookies.append(c)
+            hdr = ", ".join(cookies) + (", " if rng.random() < 0.05 else "")
+        out.append(head + b' "' + hdr.encode() + b'"')
+    return out
+
+
+SETCOOKIE_FIELDS = [
+    ["HTTP.SETCOOKIES:response.cookies", "HTTP.SETCOOKIE:response.cookies.*"],
+    ["HTTP.SETCOOKIE:response.cookies.sid", "STRING:response.cookies.sid.value", "STRING:response.cookies.sid.expires",
+     "TIME.EPOCH:response.cookies.sid.expires", "STRING:response.cookies.sid.path",
+     "STRING:response.cookies.sid.domain", "STRING:response.cookies.sid.comment",
+     "STRING:response.cookies.session.value", "TIME.EPOCH:response.cookies.nba-1.expires",
+     "STRING:request.status.last"],
+]
+
+
+@pytest.mark.parametrize("which", [0, 1])
+def test_set_cookies_emulated(oracle, emu, which):
+    """ResponseSetCookieListDissector + ResponseSetCookieDissector: ", " split
+    with the expires join, HttpCookie names, "; " attributes, expires dates"""
+    fields = SETCOOKIE_FIELDS[which]
+    o = oracle.Oracle(SETCOOKIE_FMT, fields)
+    e = emu.Emu(SETCOOKIE_FMT, fields)
+    assert e.status == 0, e.err
+    s = compare(o, e, setcookie_lines(3000, 21 + which))
+    assert s["ok"] > 1000 and s["fallback"] < 2000, s

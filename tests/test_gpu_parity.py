@@ -558,3 +558,12 @@ def test_upstream_cache_status_gpu(oracle):
     fields = oracle.possible_paths(CACHE_FMT)
     s, _ = gpu_vs_oracle(oracle, CACHE_FMT, fields, cache_status_lines(20000, 9), allow_fallback=False)
     assert s["ok"] > 14000 and s["bad"] > 2000, s
+
+
+@pytest.mark.parametrize("which", [0, 1])
+def test_set_cookies_gpu(oracle, which):
+    """ResponseSetCookieListDissector + ResponseSetCookieDissector on the
+    device path (guard) and the replay, against the oracle"""
+    from test_emu_parity import SETCOOKIE_FMT, SETCOOKIE_FIELDS, setcookie_lines
+    s, _ = gpu_vs_oracle(oracle, SETCOOKIE_FMT, SETCOOKIE_FIELDS[which], setcookie_lines(20000, 31 + which))
+    assert s["ok"] > 8000, s
