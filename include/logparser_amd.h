@@ -229,6 +229,16 @@ typedef void (*lp_emit_fn)(void *ctx, const char *base, const char *type, const 
                            const uint8_t *p, uint32_t len, int64_t l);
 int lp_result_emit(lp_handle *h, const lp_result *r, int64_t i, lp_emit_fn fn, void *ctx);
 
+/* Parser.getCasts(name) (parser-core/.../core/Parser.java:127-129, filled
+ * at :438-439 from each dissector's prepareForDissect): the casts of a
+ * "TYPE:path" the handle delivers, as LP_CAST_* bits (0 = NO_CASTS), or
+ * LP_E_MISSING when no dissector delivers it.  The caller's setter side
+ * (Parser.store, :760-876) needs them to pick String / Long / Double setters. */
+#define LP_CAST_STRING 1
+#define LP_CAST_LONG 2
+#define LP_CAST_DOUBLE 4
+int lp_casts(lp_handle *h, const char *target);
+
 /* Description of the compiled device program (for logs/tests), NUL-terminated. */
 int64_t lp_describe(lp_handle *h, char *out, size_t cap);
 

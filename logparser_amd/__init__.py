@@ -23,6 +23,10 @@ import os
 
 import numpy as np
 
+from .setters import (CAST_DOUBLE, CAST_LONG, CAST_STRING, NO_CASTS, STRING_ONLY, STRING_OR_DOUBLE,  # noqa: F401
+                      STRING_OR_LONG, STRING_OR_LONG_OR_DOUBLE, FatalErrorDuringCallOfSetterMethod, SetterPolicy,
+                      Target, cleanup_field_value, deliver)
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("LOGPARSER_AMD_LIB") or os.path.join(_HERE, "_lib", "liblogparser_amd.so")
 
@@ -122,6 +126,8 @@ def lib():
     L.lp_result_record_json.argtypes = [ctypes.c_void_p, ctypes.POINTER(LpResult), ctypes.c_int64, ctypes.c_char_p,
                                         ctypes.c_size_t]
     L.lp_result_emit.argtypes = [ctypes.c_void_p, ctypes.POINTER(LpResult), ctypes.c_int64, EMIT_FN, ctypes.c_void_p]
+    L.lp_casts.restype = ctypes.c_int
+    L.lp_casts.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
     L.lp_describe.restype = ctypes.c_int64
     L.lp_describe.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_size_t]
     L.lp_synth_combined.restype = ctypes.c_int64
@@ -294,6 +300,10 @@ class HttpdLoglineParser:
     def __init__(self, logformat, fields=(), device=0, force_direct=False, reserve_lines=0, reserve_arena=0):
         self.logformat = logformat
         self.fields = list(fields)
+        self._targets = {}       # cleaned "TYPE:path" -> [Target] (Parser.targets)
+        self._remaps = {}        # path -> {TYPE} (Parser.typeRemappings)
+        self._remap_casts = {}   # "TYPE:path" -> casts of a remapped target
+        self._engine_fields = None
         self.device = device
         self.force_direct = force_direct
         self.reserve = (reserve_lines, reserve_arena)
@@ -301,11 +311,75 @@ class HttpdLoglineParser:
         self.device_program_ok = None
         self.unsupported_reason = ""
 
-    # Parser.addParseTarget (core/Parser.java:581-635)
-    def add_parse_target(self, *fields):
+    # Parser.addParseTarget (core/Parser.java:517-635)
+    def add_parse_target(self, *fields, setter=None, setter_policy=SetterPolicy.ALWAYS, value_class=str):
+        """Request fields.  With a setter (a method name of the record passed
+        to parse, or a callable taking (value) or (name, value)), parse(line,
+        record) delivers them through it with Parser.store's rules: value_class
+        str / int / float = a String / Long / Double setter, setter_policy a
+        SetterPolicy."""
         self.fields.extend(fields)
+        if setter is not None:
+            for f in fields:
+                self._targets.setdefault(cleanup_field_value(f), []).append(Target(setter, setter_policy, value_class))
         self._close()
         return self
+
+    # Parser.addTypeRemapping(s) / setTypeRemappings (core/Parser.java:636-677)
+    def add_type_remapping(self, input_name, new_type, casts=STRING_ONLY):
+        name, typ = input_name.strip().lower(), new_type.strip().upper()
+        if typ not in self._remaps.setdefault(name, set()):
+            self._remaps[name].add(typ)
+            self._remap_casts[typ + ":" + name] = casts
+        self._close()
+        return self
+
+    def add_type_remappings(self, mappings):
+        for name, types in mappings.items():
+            for t in types:
+                self.add_type_remapping(name, t)
+        return self
+
+    def set_type_remappings(self, mappings):
+        self._remaps, self._remap_casts = {}, {}
+        return self.add_type_remappings(mappings or {})
+
+    # Parser.getCasts (core/Parser.java:127-129)
+    def get_casts(self, name):
+        """CAST_* bits of a requested "TYPE:path" (None if unknown)"""
+        name = cleanup_field_value(name)
+        self._ensure()
+        if name in self._remap_casts:
+            return self._remap_casts[name]
+        c = lib().lp_casts(self._h, name.encode())
+        return None if c < 0 else c
+
+    def _plan_fields(self):
+        """The paths the engine compiles: the requested ones, less those only a
+        type remapping delivers, plus the original paths the remapped names
+        come from."""
+        if not self._remaps:
+            return list(self.fields)
+        remapped = {t + ":" + n for n, ts in self._remaps.items() for t in ts}
+        out = [f for f in self.fields if cleanup_field_value(f) not in remapped]
+        possible = get_possible_paths(self.logformat)
+
+        def known(field):
+            pt, pn = field.split(":", 1)
+            return any(p == field or (p.endswith(".*") and p.split(":", 1)[0] == pt and
+                                      pn.startswith(p.split(":", 1)[1][:-1])) for p in possible)
+        for f in out:
+            c = cleanup_field_value(f)
+            # a path below a remapped name that only the remapped type's
+            # dissectors could deliver (Parser.java:446-455): not on the engine
+            if not known(c) and any(c.split(":", 1)[1].startswith(n + ".") for n in self._remaps):
+                raise FallbackRequired("%s: dissecting a type-remapped value is left to the reference dissector" % f)
+        for n in self._remaps:
+            for pp in possible:
+                pt, pn = pp.split(":", 1)
+                if pn == n or (pn.endswith(".*") and n.startswith(pn[:-1]) and len(n) > len(pn) - 1):
+                    out.append(pt + ":" + n)
+        return out
 
     def get_possible_paths(self, max_depth=15):
         return get_possible_paths(self.logformat, max_depth)
@@ -314,12 +388,14 @@ class HttpdLoglineParser:
         if self._h:
             return
         L = lib()
-        arr = (ctypes.c_char_p * max(1, len(self.fields)))()
-        for i, f in enumerate(self.fields):
+        fields = self._plan_fields()
+        self._engine_fields = fields
+        arr = (ctypes.c_char_p * max(1, len(fields)))()
+        for i, f in enumerate(fields):
             arr[i] = f.encode()
         st = ctypes.c_int(0)
         err = ctypes.create_string_buffer(1024)
-        h = L.lp_compile(self.logformat.encode(), arr, len(self.fields), self.device, ctypes.byref(st), err, 1024)
+        h = L.lp_compile(self.logformat.encode(), arr, len(fields), self.device, ctypes.byref(st), err, 1024)
         msg = err.value.decode(errors="replace")
         if not h:
             if st.value == LP_E_MISSING:
@@ -396,8 +472,11 @@ class HttpdLoglineParser:
         return {"lines": c[0], "ok": c[1], "bad": c[2], "fallback": c[3], "overflow_waves": c[4], "retries": c[5],
                 "ms_total": t[0], "ms_index": t[1], "ms_parse": t[2], "bytes_in": b[0], "bytes_out": b[1]}
 
-    def parse(self, line):
-        """Parser.parse(line) (core/Parser.java:700-709): the record's values,
+    def parse(self, line, record=None):
+        """Parser.parse(line) / parse(record, line) (core/Parser.java:700-756):
+        without setters the record's values as {"TYPE:path": [values]}; with
+        setters (add_parse_target(..., setter=...)) the values are delivered
+        into `record` through them and `record` is returned.
         DissectionFailure for a bad line, FallbackRequired when the device
         cannot prove the line."""
         if isinstance(line, str):
@@ -411,7 +490,21 @@ class HttpdLoglineParser:
             raise DissectionFailure("The input line does not match the specified log format.")
         if r.status[0] == LINE_FALLBACK:
             raise FallbackRequired(self.unsupported_reason or "line outside the device's proven subset")
-        return r.record(0)
+        if not self._targets:
+            return r.record(0)
+        _, res = r.copy_to_host()
+        return self.deliver(r.emissions_from(res, 0), record)
+
+    def deliver(self, emissions, record):
+        """Parser.store of one line's emissions (BatchResult.emissions_from)
+        into `record` through the registered setters"""
+        casts = {}
+
+        def cast_of(name):
+            if name not in casts:
+                casts[name] = self.get_casts(name)
+            return casts[name]
+        return deliver(emissions, record, self._targets, cast_of, self._remaps)
 
     def describe(self):
         self._ensure()

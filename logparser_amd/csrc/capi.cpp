@@ -669,6 +669,12 @@ int lp_last_bytes(lp_handle* h, uint64_t* out, int n) {
     return n < 2 ? n : 2;
 }
 
+int lp_casts(lp_handle* h, const char* target) {
+    if (!h || !target) return LP_E_INVALID;
+    const int c = h->plan.casts(target);
+    return c < 0 ? LP_E_MISSING : c;
+}
+
 int64_t lp_describe(lp_handle* h, char* out, size_t cap) {
     if (!h) return LP_E_INVALID;
     std::string d = h->plan.describe();

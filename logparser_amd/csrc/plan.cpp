@@ -975,6 +975,69 @@ int Plan::build_dissectors(const std::string& logformats, std::string& err) {
     return LP_OK;
 }
 
+// Dissector.prepareForDissect(inputname, outputname) of dissector d for the
+// output `otype:cf` below input `in_name`: the casts Parser records in
+// castsOfTargets (core/Parser.java:438-439)
+int Plan::casts_of(const Dissector& d, const std::string& otype, const std::string& in_name,
+                   const std::string& cf) const {
+    const std::string n = d.cls == D_ROOT ? cf : extract_field_name(in_name, cf);
+    constexpr int SO = CAST_S, SL = CAST_S | CAST_L, SLD = CAST_S | CAST_L | CAST_D, NONE = 0;
+    switch (d.cls) {
+    case D_ROOT: {
+        // HttpdLogFormatDissector.prepareForDissect (:226-235): the union over
+        // the LogFormats of TokenFormatDissector's first output named cf (:163-174)
+        int r = 0;
+        for (const auto& f : formats_) {
+            int c = SO;
+            bool found = false;
+            for (const auto& t : f->tokens) {
+                for (const auto& o : t.outs)
+                    if (o.name == cf) { c = o.casts; found = true; break; }
+                if (found) break;
+            }
+            r |= c;
+        }
+        return r;
+    }
+    case D_TIMESTAMP: case D_TIMESTAMP_ISO: case D_STRFTIME: {  // TimeStampDissector.java:223-352
+        static const char* const so[] = {"monthname", "date", "time", "timezone", "monthname_utc", "date_utc",
+                                         "time_utc"};
+        static const char* const sl[] = {"day", "month", "weekofweekyear", "weekyear", "year", "hour", "minute",
+                                         "second", "millisecond", "microsecond", "nanosecond", "epoch"};
+        for (const char* x : so) if (n == x) return SO;
+        for (const char* x : sl) if (n == x || n == std::string(x) + "_utc") return SL;
+        return NONE;
+    }
+    case D_URI:  // HttpUriDissector.java:76-105
+        if (n == "port") return SL;
+        for (const char* x : {"protocol", "userinfo", "host", "path", "query", "ref"}) if (n == x) return SO;
+        return NONE;
+    case D_SETCOOKIE: return n == "expires" ? SL : SO;  // ResponseSetCookieDissector.java:63-72
+    case D_UNIQUEID:  // ModUniqueIdDissector.java:76-100
+        for (const char* x : {"epoch", "ip", "processid", "counter", "threadindex"}) if (n == x) return SL;
+        return NONE;
+    case D_CLF2NUM: case D_NUM2CLF: case D_SECMILLIS: case D_MS2US:  // TypeConvertBaseDissector.java:36-45
+        return n.empty() ? SL : NONE;
+    case D_BINIP: return n.empty() ? SL : NONE;  // NginxHttpdLogFormatDissector.java:151-160
+    case D_UPSTREAM: {  // UpstreamModule.java:178-196 (same casts for .value and .redirected)
+        const bool item = n.size() > 6 && (n.compare(n.size() - 6, 6, ".value") == 0 ||
+                                           (n.size() > 11 && n.compare(n.size() - 11, 11, ".redirected") == 0));
+        if (!item) return NONE;
+        if (d.in_type == "UPSTREAM_BYTES_LIST") return SL;
+        if (d.in_type == "UPSTREAM_SECOND_MILLIS_LIST") return SLD;
+        return SO;
+    }
+    default:  // first line, protocol, query string, cookies, Set-Cookie lists, localized time: STRING_ONLY
+        return SO;
+    }
+    (void)otype;
+}
+
+int Plan::casts(const std::string& target) const {
+    auto it = casts_.find(target);
+    return it == casts_.end() ? -1 : it->second;
+}
+
 void Plan::find_useful(const std::set<std::string>& possible, const std::string& type, const std::string& name,
                        bool is_root) {
     std::string srid = type + ":" + name;
@@ -1008,6 +1071,7 @@ void Plan::find_useful(const std::set<std::string>& possible, const std::string&
                     in = &it->second.back();
                 }
                 in->requested.insert(extract_field_name(name, cf));
+                casts_[otype + ":" + cf] = casts_of(d, otype, name, cf);
                 if (d.cls == D_ROOT)
                     for (auto& f : formats_) f->requested.insert(cf);  // TokenFormatDissector.prepareForDissect
                 find_useful(possible, otype, cf, false);

@@ -125,6 +125,9 @@ public:
                               std::string& err);
 
     const Program& program() const { return prog_; }
+    // Parser.getCasts(name) (core/Parser.java:127-129): CAST_* bits of a
+    // "TYPE:path" the dissectors deliver for the requested paths, -1 unknown
+    int casts(const std::string& target) const;
     bool device_ok() const { return device_ok_; }
     const std::string& unsupported_reason() const { return why_; }
     std::string describe() const;
@@ -143,6 +146,7 @@ private:
     void find_useful(const std::set<std::string>& possible, const std::string& type, const std::string& name,
                      bool is_root);
     void compile_program();
+    int casts_of(const Dissector& d, const std::string& otype, const std::string& in_name, const std::string& cf) const;
 
     // replay
     struct Ctx;
@@ -156,6 +160,7 @@ private:
     std::vector<std::unique_ptr<Dissector>> dis_;
     std::string root_type_ = "HTTPLOGLINE";
     std::set<std::string> needed_, useful_, located_;
+    std::map<std::string, int> casts_;  // castsOfTargets
     std::map<std::string, std::vector<Instance>> compiled_;
     Program prog_{};
     bool device_ok_ = true;

@@ -35,6 +35,9 @@ void* emu_new(const char* fmt, const char* const* fields, int n, int* status, ch
 
 void emu_free(void* h) { delete (Emu*)h; }
 
+// Parser.getCasts of a "TYPE:path" (the planner's castsOfTargets), -1 unknown
+int emu_casts(void* h, const char* target) { return ((Emu*)h)->plan.casts(target); }
+
 int emu_describe(void* h, char* out, int cap) {
     std::string d = ((Emu*)h)->plan.describe();
     snprintf(out, cap, "%s", d.c_str());

@@ -45,6 +45,8 @@ def lib():
                                    ctypes.c_int]
         L.emu_describe.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]
         L.emu_set_masks.argtypes = [ctypes.c_int]
+        L.emu_casts.restype = ctypes.c_int
+        L.emu_casts.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
         L.emu_possible_paths.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
         L.emu_token_table.restype = ctypes.c_int
         L.emu_token_table.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
@@ -95,6 +97,10 @@ class Emu:
             out.append((st, self.buf.value.decode("utf-8") if st in (0, 3) else None))
             start = end + 1
         return out
+
+    def casts(self, target):
+        c = lib().emu_casts(self.h, target.encode())
+        return None if c < 0 else c
 
     def describe(self):
         b = ctypes.create_string_buffer(1 << 16)

@@ -567,3 +567,39 @@ def test_set_cookies_gpu(oracle, which):
     from test_emu_parity import SETCOOKIE_FMT, SETCOOKIE_FIELDS, setcookie_lines
     s, _ = gpu_vs_oracle(oracle, SETCOOKIE_FMT, SETCOOKIE_FIELDS[which], setcookie_lines(20000, 31 + which))
     assert s["ok"] > 8000, s
+
+
+def test_setters_and_remapping_gpu():
+    """parse(line, record) through setters (Parser.store rules, SetterPolicy,
+    Long setters on STRING_OR_LONG paths, lp_casts) and a type remapping, on
+    the engine"""
+    import datetime
+    from test_setters import Rec
+    line = ('1.2.3.4 - - [10/Oct/2020:13:55:36 -0700] "GET /a?g=http%3A%2F%2Fx.y%2Fz&Q=1 HTTP/1.1" 200 - '
+            '"http://ref.example:8080/x" "UA"')
+    p = lpa.HttpdLoglineParser("combined")
+    p.add_parse_target("TIME.EPOCH:request.receive.time.epoch", setter="set_long", value_class=int)
+    p.add_parse_target("BYTESCLF:response.body.bytes", setter="set_long", value_class=int,
+                       setter_policy=lpa.SetterPolicy.NOT_NULL)
+    p.add_parse_target("STRING:request.firstline.uri.query.*", setter="set_string")
+    p.add_parse_target("HTTP.PORT:request.referer.port", "TIME.MONTHNAME:request.receive.time.monthname",
+                       setter="set_string")
+    p.add_parse_target("HTTP.PORT:request.referer.port", setter="set_long", value_class=int)
+    p.add_type_remapping("request.firstline.uri.query.g", "HTTP.URI")
+    p.add_parse_target("HTTP.URI:request.firstline.uri.query.g", setter="set_string")
+    assert p.get_casts("TIME.EPOCH:request.receive.time.epoch") == lpa.STRING_OR_LONG
+    assert p.get_casts("STRING:request.firstline.uri.query.*") == lpa.STRING_ONLY
+    assert p.get_casts("HTTP.URI:request.firstline.uri.query.g") == lpa.STRING_ONLY
+    r = p.parse(line, Rec())
+    epoch = int(datetime.datetime(2020, 10, 10, 13, 55, 36,
+                                  tzinfo=datetime.timezone(datetime.timedelta(hours=-7))).timestamp()) * 1000
+    assert r.l == {"TIME.EPOCH:request.receive.time.epoch": epoch, "HTTP.PORT:request.referer.port": 8080}
+    assert r.s == {"STRING:request.firstline.uri.query.g": "http://x.y/z", "STRING:request.firstline.uri.query.q": "1",
+                   "HTTP.URI:request.firstline.uri.query.g": "http://x.y/z",
+                   "HTTP.PORT:request.referer.port": "8080",
+                   "TIME.MONTHNAME:request.receive.time.monthname": "October"}
+    # a Double setter on a STRING_OR_LONG path is never called: FatalErrorDuringCallOfSetterMethod
+    q = lpa.HttpdLoglineParser("combined")
+    q.add_parse_target("BYTES:response.body.bytes", setter="set_double", value_class=float)
+    with pytest.raises(lpa.FatalErrorDuringCallOfSetterMethod):
+        q.parse(line.replace(" 200 - ", " 200 512 "), Rec())
