@@ -239,6 +239,36 @@ int lp_result_emit(lp_handle *h, const lp_result *r, int64_t i, lp_emit_fn fn, v
 #define LP_CAST_DOUBLE 4
 int lp_casts(lp_handle *h, const char *target);
 
+/* Typed columns of a batch, the output side of a parse: what a caller with
+ * one setter per column type builds per line -- the Hadoop ParsedRecord
+ * (httpdlog-inputformat/.../ParsedRecord.java:154-214: set(name, String /
+ * Long / Double), nulls ignored, the last value wins) read back column by
+ * column as the Hive SerDe does (httpdlog-serde/.../ApacheHttpdlogDeserializer.java:
+ * 224-240 STRING / BIGINT / DOUBLE columns, :295-323 one row per line).
+ * From a host copy (lp_result_copy with the input), rows [first, first+count):
+ *   kind LP_CAST_STRING: i64 = byte offsets [count + 1] into chars (Arrow
+ *        layout: row k = chars[i64[k], i64[k + 1])), chars_cap bytes at chars;
+ *   kind LP_CAST_LONG:   i64 = values [count];  LP_CAST_DOUBLE: f64 = values;
+ *   valid[k] = 1 when row k has a value (lines not OK have none).
+ * path: a requested "TYPE:path" (a wildcard request's member by its full
+ * path).  Returns LP_OK; LP_E_NOMEM when a STRING column's chars_cap is too
+ * small (chars_len = bytes needed: call again); LP_E_MISSING for a path the
+ * handle does not deliver; LP_E_INVALID when the path's casts (lp_casts) do
+ * not include the column's type (the reference's store would call no setter).
+ * threads: host threads to replay with. */
+typedef struct lp_table_col {
+    const char *path;
+    int32_t kind;
+    uint8_t *valid;
+    int64_t *i64;
+    double *f64;
+    char *chars;
+    uint64_t chars_cap;
+    uint64_t chars_len;
+} lp_table_col;
+int lp_result_table(lp_handle *h, const lp_result *r, int64_t first, int64_t count, lp_table_col *cols, int n_cols,
+                    int threads);
+
 /* Description of the compiled device program (for logs/tests), NUL-terminated. */
 int64_t lp_describe(lp_handle *h, char *out, size_t cap);
 

@@ -48,6 +48,12 @@ EMIT_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_char_p, ctypes.c_char
 VALUE_STRING, VALUE_NULL, VALUE_LONG = 0, 1, 2
 
 
+class LpTableCol(ctypes.Structure):
+    _fields_ = [("path", ctypes.c_char_p), ("kind", ctypes.c_int32), ("valid", ctypes.c_void_p),
+                ("i64", ctypes.c_void_p), ("f64", ctypes.c_void_p), ("chars", ctypes.c_void_p),
+                ("chars_cap", ctypes.c_uint64), ("chars_len", ctypes.c_uint64)]
+
+
 class LpResult(ctypes.Structure):
     """lp_result (include/logparser_amd.h): the SoA results of one batch"""
     _fields_ = [("n_lines", ctypes.c_int64), ("input_bytes", ctypes.c_uint64), ("input", ctypes.c_void_p),
@@ -126,6 +132,9 @@ def lib():
     L.lp_result_record_json.argtypes = [ctypes.c_void_p, ctypes.POINTER(LpResult), ctypes.c_int64, ctypes.c_char_p,
                                         ctypes.c_size_t]
     L.lp_result_emit.argtypes = [ctypes.c_void_p, ctypes.POINTER(LpResult), ctypes.c_int64, EMIT_FN, ctypes.c_void_p]
+    L.lp_result_table.restype = ctypes.c_int
+    L.lp_result_table.argtypes = [ctypes.c_void_p, ctypes.POINTER(LpResult), ctypes.c_int64, ctypes.c_int64,
+                                  ctypes.POINTER(LpTableCol), ctypes.c_int, ctypes.c_int]
     L.lp_casts.restype = ctypes.c_int
     L.lp_casts.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
     L.lp_describe.restype = ctypes.c_int64
@@ -275,6 +284,47 @@ class BatchResult:
         rc = lib().lp_result_emit(self._p._h, ctypes.byref(res), i, fn, None)
         if rc < 0:
             raise ValueError("lp_result_emit(%d) failed: %d" % (i, rc))
+        return out
+
+    def table_from(self, res, columns, first=0, count=None, threads=16):
+        """lp_result_table: typed columns of rows [first, first+count) from a
+        host copy.  columns: [(path, str | int | float)].  Returns {path:
+        (values, valid)}: values a list of str / None for STRING columns, a
+        numpy int64 / float64 array for BIGINT / DOUBLE ones."""
+        count = self.n_lines - first if count is None else count
+        kinds = {str: CAST_STRING, int: CAST_LONG, float: CAST_DOUBLE}
+        cols = (LpTableCol * len(columns))()
+        keep = []
+        for k, (path, typ) in enumerate(columns):
+            c = cols[k]
+            c.path = path.encode()
+            c.kind = kinds[typ]
+            valid = np.zeros(max(1, count), dtype=np.uint8)
+            i64 = np.zeros(count + 1, dtype=np.int64)
+            f64 = np.zeros(max(1, count), dtype=np.float64)
+            c.valid, c.i64, c.f64 = valid.ctypes.data, i64.ctypes.data, f64.ctypes.data
+            keep.append((valid, i64, f64))
+        L = lib()
+        rc = L.lp_result_table(self._p._h, ctypes.byref(res), first, count, cols, len(columns), threads)
+        if rc == LP_E_NOMEM:
+            for k in range(len(columns)):
+                if cols[k].kind == CAST_STRING:
+                    buf = np.zeros(max(1, cols[k].chars_len), dtype=np.uint8)
+                    keep[k] = keep[k] + (buf,)
+                    cols[k].chars, cols[k].chars_cap = buf.ctypes.data, buf.nbytes
+            rc = L.lp_result_table(self._p._h, ctypes.byref(res), first, count, cols, len(columns), threads)
+        if rc != LP_OK:
+            raise ValueError("lp_result_table failed: %d" % rc)
+        out = {}
+        for k, (path, typ) in enumerate(columns):
+            valid, i64, f64 = keep[k][:3]
+            ok = valid[:count].astype(bool)
+            if typ is str:
+                chars = keep[k][3].tobytes() if len(keep[k]) > 3 else b""
+                vals = [chars[i64[j]:i64[j + 1]].decode("utf-8") if ok[j] else None for j in range(count)]
+                out[path] = (vals, ok)
+            else:
+                out[path] = ((i64[:count] if typ is int else f64[:count]).copy(), ok)
         return out
 
     def record_json_from(self, res, i):

@@ -4,6 +4,10 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <cmath>
+#include <regex>
+#include <thread>
+#include <unordered_map>
 #include <memory>
 #include <string>
 #include <vector>
@@ -722,6 +726,153 @@ int64_t lp_result_record_json(lp_handle* h, const lp_result* r, int64_t i, char*
     if (!out || js.size() + 1 > cap) return -100 - (int64_t)(js.size() + 1);
     memcpy(out, js.c_str(), js.size() + 1);
     return (int64_t)js.size();
+}
+
+// ---- typed columns of a batch (the output side: ParsedRecord / the Hive SerDe)
+namespace {
+// Long.parseLong: optional sign, decimal digits only, in range
+bool java_parse_long(const uint8_t* p, uint32_t n, int64_t& out) {
+    uint32_t k = 0;
+    bool neg = false;
+    if (n && (p[0] == '-' || p[0] == '+')) { neg = p[0] == '-'; k = 1; }
+    if (k == n) return false;
+    unsigned __int128 v = 0;
+    for (; k < n; ++k) {
+        if (p[k] < '0' || p[k] > '9') return false;
+        v = v * 10 + (p[k] - '0');
+        if (v > ((unsigned __int128)1 << 63)) return false;
+    }
+    if (!neg && v == ((unsigned __int128)1 << 63)) return false;
+    out = neg ? (int64_t)(0 - (uint64_t)v) : (int64_t)v;
+    return true;
+}
+// Double.parseDouble (FloatingDecimal.readJavaFormatString): chars <= ' '
+// trimmed; [+-] then NaN | Infinity | decimal digits with an optional '.',
+// exponent and f/F/d/D suffix | a hex float with a binary exponent
+bool java_parse_double(const uint8_t* p, uint32_t n, double& out) {
+    uint32_t a = 0, b = n;
+    while (a < b && p[a] <= ' ') ++a;
+    while (b > a && p[b - 1] <= ' ') --b;
+    std::string t((const char*)p + a, b - a);
+    static const std::regex dec("[+-]?(NaN|Infinity|(([0-9]+\\.?[0-9]*|\\.[0-9]+)([eE][+-]?[0-9]+)?)[fFdD]?)");
+    static const std::regex hex("[+-]?0[xX]([0-9a-fA-F]+\\.?[0-9a-fA-F]*|\\.[0-9a-fA-F]+)[pP][+-]?[0-9]+[fFdD]?");
+    const bool d = std::regex_match(t, dec), x = !d && std::regex_match(t, hex);
+    if (!d && !x) return false;
+    const bool neg = !t.empty() && t[0] == '-';
+    if (t.find("NaN") != std::string::npos) { out = std::nan(""); return true; }
+    if (t.find("Infinity") != std::string::npos) { out = neg ? -HUGE_VAL : HUGE_VAL; return true; }
+    if (!t.empty() && strchr("fFdD", t.back())) t.pop_back();
+    out = strtod(t.c_str(), nullptr);
+    return true;
+}
+struct TableCtx {
+    const std::unordered_map<std::string, std::vector<int>>* by_path;
+    lp_table_col* cols;
+    int64_t row;           // row in the output
+    std::vector<std::string>* sbuf;  // per column: this chunk's STRING bytes
+    std::vector<std::vector<std::pair<uint32_t, uint32_t>>>* sref;  // per column: (offset, len) per chunk row
+    int64_t row0;          // first output row of the chunk
+};
+void table_value(void* vctx, const std::string& target, const lp::MVal& v) {
+    TableCtx& t = *(TableCtx*)vctx;
+    auto it = t.by_path->find(target);
+    if (it == t.by_path->end()) return;
+    for (int c : it->second) {
+        lp_table_col& C = t.cols[c];
+        // ParsedRecord.set(name, value) (ParsedRecord.java:154-170): a null is
+        // ignored, the last value wins (Value.getString / getLong / getDouble)
+        if (v.null) continue;
+        if (C.kind == LP_CAST_STRING) {
+            std::string& buf = (*t.sbuf)[c];
+            const uint32_t off = (uint32_t)buf.size();
+            if (v.is_long) buf += std::to_string(v.l);
+            else buf.append((const char*)v.p, v.len);
+            (*t.sref)[c][t.row - t.row0] = {off, (uint32_t)buf.size() - off};
+            C.valid[t.row] = 1;
+        } else if (C.kind == LP_CAST_LONG) {
+            int64_t x;
+            if (v.is_long) x = v.l;
+            else if (!java_parse_long(v.p, v.len, x)) continue;
+            C.i64[t.row] = x;
+            C.valid[t.row] = 1;
+        } else {
+            double x;
+            if (v.is_long) x = (double)v.l;
+            else if (!java_parse_double(v.p, v.len, x)) continue;
+            C.f64[t.row] = x;
+            C.valid[t.row] = 1;
+        }
+    }
+}
+}  // namespace
+
+int lp_result_table(lp_handle* h, const lp_result* r, int64_t first, int64_t count, lp_table_col* cols, int n_cols,
+                    int threads) {
+    if (!h || !r || !cols || n_cols <= 0 || !r->on_host || !r->input) return LP_E_INVALID;
+    if (first < 0 || count < 0 || first + count > r->n_lines) return LP_E_INVALID;
+    std::unordered_map<std::string, std::vector<int>> by_path;
+    for (int c = 0; c < n_cols; ++c) {
+        const lp_table_col& C = cols[c];
+        if (!C.path || !C.valid || (C.kind == LP_CAST_STRING ? !C.i64 : C.kind == LP_CAST_LONG ? !C.i64 : !C.f64))
+            return LP_E_INVALID;
+        if (C.kind != LP_CAST_STRING && C.kind != LP_CAST_LONG && C.kind != LP_CAST_DOUBLE) return LP_E_INVALID;
+        // the casts of the requested path (or of its wildcard request) must
+        // allow the column type: else the reference's store finds no setter
+        std::string p = C.path;
+        int casts = h->plan.casts(p);
+        if (casts < 0) {
+            const size_t dot = p.rfind('.');
+            if (dot != std::string::npos) casts = h->plan.casts(p.substr(0, dot) + ".*");
+        }
+        if (casts < 0) return LP_E_MISSING;
+        if (!(casts & C.kind)) return LP_E_INVALID;
+        by_path[p].push_back(c);
+    }
+    lp::ResultView V;
+    make_view(h, *r, V);
+    const int T = std::max(1, std::min(threads > 0 ? threads : 1, 64));
+    const int64_t per = (count + T - 1) / T;
+    std::vector<std::vector<std::string>> sbuf(T, std::vector<std::string>(n_cols));
+    std::vector<std::vector<std::vector<std::pair<uint32_t, uint32_t>>>> sref(T);
+    auto work = [&](int t) {
+        const int64_t a = std::min(count, t * per), b = std::min(count, a + per);
+        sref[t].assign(n_cols, std::vector<std::pair<uint32_t, uint32_t>>((size_t)(b - a), {0u, 0u}));
+        TableCtx ctx{&by_path, cols, 0, &sbuf[t], &sref[t], a};
+        for (int64_t k = a; k < b; ++k) {
+            for (int c = 0; c < n_cols; ++c) cols[c].valid[k] = 0;
+            const int64_t i = first + k;
+            if (!V.status || V.status[i] != LP_LINE_OK) continue;
+            ctx.row = k;
+            h->plan.rec_row(V, i, table_value, &ctx);
+        }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < T; ++t) pool.emplace_back(work, t);
+    work(0);
+    for (auto& th : pool) th.join();
+    // STRING columns (Arrow layout): row k = chars[offsets[k], offsets[k + 1]),
+    // the row's last value; a row without one is empty (valid 0)
+    int rc = LP_OK;
+    for (int c = 0; c < n_cols; ++c) {
+        lp_table_col& C = cols[c];
+        if (C.kind != LP_CAST_STRING) continue;
+        uint64_t need = 0;
+        for (int64_t k = 0; k < count; ++k)
+            if (C.valid[k]) need += sref[(size_t)(k / per)][c][(size_t)(k % per)].second;
+        C.chars_len = need;
+        if (need > C.chars_cap || (need && !C.chars)) { rc = LP_E_NOMEM; continue; }
+        uint64_t pos = 0;
+        for (int64_t k = 0; k < count; ++k) {
+            C.i64[k] = (int64_t)pos;
+            if (!C.valid[k]) continue;
+            const int t = (int)(k / per);
+            const auto& pr = sref[(size_t)t][c][(size_t)(k % per)];
+            memcpy(C.chars + pos, sbuf[(size_t)t][c].data() + pr.first, pr.second);
+            pos += pr.second;
+        }
+        C.i64[count] = (int64_t)pos;
+    }
+    return rc;
 }
 
 int lp_result_emit(lp_handle* h, const lp_result* r, int64_t i, lp_emit_fn fn, void* ctx) {

@@ -2071,6 +2071,13 @@ int Plan::emit_row(const ResultView& R, int64_t i, EmitFn fn, void* ctx) const {
     return (int)c.em.size();
 }
 
+int Plan::rec_row(const ResultView& R, int64_t i, RecFn fn, void* ctx) const {
+    Ctx c{R, i, R.input + R.line_off[i], R.region(i), {}, {}, {}};
+    replay(c);
+    for (const auto& e : c.rec) fn(ctx, e.first, e.second);
+    return (int)c.rec.size();
+}
+
 std::string Plan::record_json(const ResultView& R, int64_t i) const {
     Ctx c{R, i, R.input + R.line_off[i], R.region(i), {}, {}, {}};
     replay(c);

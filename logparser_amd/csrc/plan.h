@@ -140,6 +140,11 @@ public:
     using EmitFn = void (*)(void* ctx, const char* base, const char* type, const char* name, int kind,
                             const uint8_t* p, uint32_t len, int64_t l);
     int emit_row(const ResultView& R, int64_t i, EmitFn fn, void* ctx) const;
+    // the values Parser.store would hand the record's setters for line i:
+    // (requested "TYPE:path", value) in delivery order (wildcard requests
+    // by the value's full path)
+    using RecFn = void (*)(void* ctx, const std::string& target, const MVal& v);
+    int rec_row(const ResultView& R, int64_t i, RecFn fn, void* ctx) const;
 
 private:
     int build_dissectors(const std::string& logformats, std::string& err);

@@ -603,3 +603,43 @@ def test_setters_and_remapping_gpu():
     q.add_parse_target("BYTES:response.body.bytes", setter="set_double", value_class=float)
     with pytest.raises(lpa.FatalErrorDuringCallOfSetterMethod):
         q.parse(line.replace(" 200 - ", " 200 512 "), Rec())
+
+
+def test_result_table_gpu(demolog_lines):
+    """lp_result_table (ParsedRecord / Hive SerDe columns) equals the records:
+    per row the last non-null value of the path, converted as Value.getLong /
+    getDouble; lines not OK have no values; a column type outside the path's
+    casts is refused"""
+    from logparser_amd.setters import Value
+    fields = lpa.get_possible_paths("combined")
+    data = b"".join(l + b"\n" for l in demolog_lines) + lpa.synth_combined(7, 0, 20000) + b"garbage line\n"
+    p = lpa.HttpdLoglineParser("combined", fields)
+    r = p.parse_batch(data)
+    _, res = r.copy_to_host()
+    cols = [("TIME.EPOCH:request.receive.time.epoch", int), ("BYTESCLF:response.body.bytes", int),
+            ("HTTP.PATH:request.firstline.uri.path", str),
+            ("STRING:request.firstline.uri.query.username", str), ("HTTP.HOST:request.referer.host", str),
+            ("TIME.MONTHNAME:request.receive.time.monthname", str), ("HTTP.PORT:request.referer.port", int),
+            ("STRING:request.status.last", str)]
+    t = r.table_from(res, cols, threads=8)
+    n_ok = 0
+    for i in range(r.n_lines):
+        rec = r.record(i) if r.status[i] == lpa.LINE_OK else {}
+        n_ok += r.status[i] == lpa.LINE_OK
+        for path, typ in cols:
+            vals, ok = t[path]
+            want = None
+            for v in rec.get(path, []):
+                v = v["l"] if isinstance(v, dict) else v
+                if v is None:
+                    continue
+                x = Value(v)
+                c = x.get_string() if typ is str else x.get_long() if typ is int else x.get_double()
+                if c is not None:
+                    want = c
+            got = (vals[i] if ok[i] else None) if typ is str else (vals[i].item() if ok[i] else None)
+            assert got == want, (i, path, got, want)
+    assert n_ok > 20000
+    # BYTESCLF is STRING_OR_LONG: a DOUBLE column finds no setter
+    with pytest.raises(ValueError):
+        r.table_from(res, [("BYTES:response.body.bytes", float)])
