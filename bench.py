@@ -261,7 +261,7 @@ def host_delivery(lpa, torch, parser, n_lines, workload, sample=100000):
     # side) of 8 requested paths, 16 host threads
     cols = [(f, str) for f in parser.fields if not f.endswith("*")][:8]
     t2 = time.perf_counter()
-    r.table_from(res2, cols, threads=16)
+    r.table_from(res2, cols, threads=16, decode=False)
     dt3 = time.perf_counter() - t2
     return {"soa_copy_lines_per_s": round(n_lines / dt, 1), "soa_copy_gbs": round(need / dt / 1e9, 3),
             "soa_bytes": int(need), "records_json_per_s_1thread": round(len(ok) / dt2, 1),

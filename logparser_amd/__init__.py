@@ -286,11 +286,12 @@ class BatchResult:
             raise ValueError("lp_result_emit(%d) failed: %d" % (i, rc))
         return out
 
-    def table_from(self, res, columns, first=0, count=None, threads=16):
+    def table_from(self, res, columns, first=0, count=None, threads=16, decode=True):
         """lp_result_table: typed columns of rows [first, first+count) from a
         host copy.  columns: [(path, str | int | float)].  Returns {path:
-        (values, valid)}: values a list of str / None for STRING columns, a
-        numpy int64 / float64 array for BIGINT / DOUBLE ones."""
+        (values, valid)}: values a list of str / None for STRING columns
+        (decode=False: the Arrow pair (offsets, chars bytes) as numpy arrays),
+        a numpy int64 / float64 array for BIGINT / DOUBLE ones."""
         count = self.n_lines - first if count is None else count
         kinds = {str: CAST_STRING, int: CAST_LONG, float: CAST_DOUBLE}
         cols = (LpTableCol * len(columns))()
@@ -319,7 +320,9 @@ class BatchResult:
         for k, (path, typ) in enumerate(columns):
             valid, i64, f64 = keep[k][:3]
             ok = valid[:count].astype(bool)
-            if typ is str:
+            if typ is str and not decode:
+                out[path] = ((i64, keep[k][3] if len(keep[k]) > 3 else np.zeros(0, np.uint8)), ok)
+            elif typ is str:
                 chars = keep[k][3].tobytes() if len(keep[k]) > 3 else b""
                 vals = [chars[i64[j]:i64[j + 1]].decode("utf-8") if ok[j] else None for j in range(count)]
                 out[path] = (vals, ok)

@@ -15,6 +15,13 @@
 //                                         core/Parser.java:237-490, 904-1012
 //   Parsable.addDissection                core/Parsable.java:142-193 (replay)
 #include "plan.h"
+
+#include <atomic>
+#include <unordered_map>
+
+namespace {
+std::atomic<uint64_t> g_plan_gen{1};  // Plan build ids (the replay memo's key)
+}  // namespace
 #include "lp_device.h"
 
 #include <algorithm>
@@ -1081,6 +1088,7 @@ void Plan::find_useful(const std::set<std::string>& possible, const std::string&
 }
 
 int Plan::build(const std::string& logformats, const std::vector<std::string>& fields, std::string& err) {
+    gen_ = g_plan_gen.fetch_add(1);
     int r = build_dissectors(logformats, err);
     if (r != LP_OK) return r;
     for (const auto& f : fields) needed_.insert(cleanup_field(f));
@@ -1534,31 +1542,66 @@ const char* MONTH_FULL[] = {"January", "February", "March", "April", "May", "Jun
 
 static thread_local int t_origin_kind = 0, t_origin_idx = 0, t_fmt = 0;  // t_fmt: the line's LogFormat
 
+// Parsable.addDissection's decisions for one (type, base, name), memoized per
+// thread and plan: the set / map lookups on strings dominated the replay
+namespace {
+struct EmitDec {
+    std::string complete, needed;
+    const std::vector<Instance>* ins = nullptr;  // further dissectors (useful intermediate)
+    bool exact = false, wild = false;
+};
+struct EmitMemo {
+    uint64_t gen = 0;
+    std::unordered_map<std::string, EmitDec> m;
+    std::string key;
+};
+thread_local EmitMemo t_memo;
+}  // namespace
+
 void Plan::emit(Ctx& c, const std::string& base, const std::string& type, const std::string& name, const MVal& v,
                 const MVal* dv) const {
-    std::string complete, wild;
-    if (base.empty()) {
-        complete = name;
-        wild = type + ":*";
-    } else {
-        complete = name.empty() ? base : base + "." + name;
-        wild = type + ":" + base + ".*";
+    EmitMemo& M = t_memo;
+    if (M.gen != gen_) {
+        M.m.clear();
+        M.gen = gen_;
     }
-    std::string needed = type + ":" + complete;
-    int ok = t_origin_kind, oi = t_origin_idx;
-    if (useful_.count(complete)) {
-        auto it = compiled_.find(needed);
-        if (it != compiled_.end())
-            for (const auto& in : it->second) {
-                t_origin_kind = ok;
-                t_origin_idx = oi;
-                run_phase(c, in, complete, dv ? *dv : v);
-            }
+    M.key.assign(type);
+    M.key += '\x1f';
+    M.key += base;
+    M.key += '\x1f';
+    M.key += name;
+    auto it = M.m.find(M.key);
+    if (it == M.m.end()) {
+        EmitDec d;
+        std::string wild;
+        if (base.empty()) {
+            d.complete = name;
+            wild = type + ":*";
+        } else {
+            d.complete = name.empty() ? base : base + "." + name;
+            wild = type + ":" + base + ".*";
+        }
+        d.needed = type + ":" + d.complete;
+        if (useful_.count(d.complete)) {
+            auto ci = compiled_.find(d.needed);
+            if (ci != compiled_.end()) d.ins = &ci->second;
+        }
+        d.exact = needed_.count(d.needed) > 0;
+        d.wild = needed_.count(wild) > 0;
+        it = M.m.emplace(M.key, std::move(d)).first;
     }
-    const bool exact = needed_.count(needed) > 0, wildcard = needed_.count(wild) > 0;
-    if (exact) c.rec.emplace_back(needed, v);
-    if (wildcard) c.rec.emplace_back(needed, v);
-    if (exact || wildcard) c.em.push_back(Emission{base, type, name, v});
+    const EmitDec& d = it->second;  // node-based map: stays valid while the row inserts more
+    if (d.ins) {
+        const int ok = t_origin_kind, oi = t_origin_idx;
+        for (const auto& in : *d.ins) {
+            t_origin_kind = ok;
+            t_origin_idx = oi;
+            run_phase(c, in, d.complete, dv ? *dv : v);
+        }
+    }
+    if (d.exact) c.rec.emplace_back(d.needed, v);
+    if (d.wild) c.rec.emplace_back(d.needed, v);
+    if (d.exact || d.wild) c.em.push_back(Emission{base, type, name, v});
 }
 
 void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const MVal& v) const {
@@ -1966,16 +2009,21 @@ void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const 
 namespace {
 void json_str(std::string& o, const uint8_t* p, uint32_t n) {
     o += '"';
+    uint32_t run = 0;  // bytes [run, k) need no escape: appended in one go
     for (uint32_t k = 0; k < n; ++k) {
-        uint8_t ch = p[k];
+        const uint8_t ch = p[k];
+        if (ch != '"' && ch != '\\' && ch >= 0x20) continue;
+        o.append((const char*)p + run, k - run);
+        run = k + 1;
         if (ch == '"') o += "\\\"";
         else if (ch == '\\') o += "\\\\";
-        else if (ch < 0x20) {
+        else {
             char b[8];
             snprintf(b, sizeof b, "\\u%04x", ch);
             o += b;
-        } else o += (char)ch;
+        }
     }
+    o.append((const char*)p + run, n - run);
     o += '"';
 }
 void json_s(std::string& o, const std::string& s) { json_str(o, (const uint8_t*)s.data(), (uint32_t)s.size()); }
@@ -2043,6 +2091,11 @@ std::string token_table_json(bool nginx) {
 void Plan::replay(Ctx& c) const {
     const ResultView& R = c.R;
     const int64_t i = c.i;
+    // memoized decisions: bounded (query / cookie names are open-ended);
+    // cleared only between rows (emit keeps references into the map)
+    if (t_memo.m.size() > (1u << 15)) t_memo.m.clear();
+    c.rec.reserve(256);
+    c.em.reserve(256);
     // the LogFormat the line was routed to (HttpdLogFormatDissector's active format)
     const int fi = prog_.n_fmt > 1 ? R.fmt_id[i] : 0;
     t_fmt = fi;

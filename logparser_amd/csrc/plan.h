@@ -166,6 +166,7 @@ private:
     std::string root_type_ = "HTTPLOGLINE";
     std::set<std::string> needed_, useful_, located_;
     std::map<std::string, int> casts_;  // castsOfTargets
+    uint64_t gen_ = 0;                  // this build's id (the replay's per-thread memo)
     std::map<std::string, std::vector<Instance>> compiled_;
     Program prog_{};
     bool device_ok_ = true;
