@@ -252,6 +252,10 @@ constexpr int PW = 64;
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+#ifndef LP_STAGE_PRIO
+#define LP_STAGE_PRIO 0
+#endif
+
 struct WaveStack {  // per-lane DFS stack, lane-interleaved (conflict-free)
     uint32_t* base;
     __device__ uint32_t& operator[](int k) const { return base[k * PW]; }
@@ -318,6 +322,11 @@ __device__ __forceinline__ bool stage_window(const uint8_t* __restrict__ buf, ui
     const uint64_t full_end = nbytes & ~15ull;  // 16-byte pieces wholly inside the buffer
     for (int k0 = lane; k0 < nv4; k0 += SB * PW) {
         u32x4 v[SB];
+#if LP_STAGE_PRIO
+        // the window's loads leave before the other waves' ALU work (they
+        // are this wave's critical path; the CU has other waves to issue)
+        __builtin_amdgcn_s_setprio(3);
+#endif
 #pragma unroll
         for (int j = 0; j < SB; ++j) {
             const int k = k0 + j * PW;
@@ -325,6 +334,9 @@ __device__ __forceinline__ bool stage_window(const uint8_t* __restrict__ buf, ui
             v[j] = u32x4{0, 0, 0, 0};
             if (k < nv && p + 16 <= full_end) v[j] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(buf + p));
         }
+#if LP_STAGE_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
 #pragma unroll
         for (int j = 0; j < SB; ++j) {
             const int k = k0 + j * PW;
