@@ -18,7 +18,7 @@ def test_parity_under_asan_ubsan():
             ["gcc", "-print-file-name=libasan.so"], capture_output=True, text=True).stdout.strip()):
         pytest.skip("no libasan")
     r = subprocess.run([os.path.join(ROOT, "tools", "asan_check.sh"),
-                        "golden or synthetic_config2 or utf8 or upstream or setup or resilient"],
+                        "golden or synthetic_config2 or utf8 or upstream or setup or resilient or cookies"],
                        capture_output=True, text=True, timeout=850)
     tail = (r.stdout + r.stderr)[-3000:]
     assert r.returncode == 0, tail

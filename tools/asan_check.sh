@@ -8,7 +8,7 @@
 set -euo pipefail
 R=$(cd "$(dirname "$0")/.." && pwd)
 make -s -C "$R/oracle" asan
-SEL=${1:-"golden or synthetic_config2 or mutated or nginx_config4 or utf8 or upstream or strftime or authority or ip_token or setup or oracle_vs or resilient"}
+SEL=${1:-"golden or synthetic_config2 or mutated or nginx_config4 or utf8 or upstream or strftime or authority or ip_token or setup or oracle_vs or resilient or cookies"}
 export LD_PRELOAD=$(gcc -print-file-name=libasan.so):$(gcc -print-file-name=libubsan.so)
 export ASAN_OPTIONS=detect_leaks=0:abort_on_error=1:halt_on_error=1${ASAN_LOG:+:log_path=$ASAN_LOG}
 export UBSAN_OPTIONS=halt_on_error=1:print_stacktrace=1${ASAN_LOG:+:log_path=$ASAN_LOG}
