@@ -195,19 +195,14 @@ def pcie_inclusive(torch, parser, buf, batches, max_bytes):
             "lines": lines2}
 
 
-def cpu_baseline(lpa, workload, fields, sample_lines, threads, repeats=3):
-    """The oracle (C restatement of the reference semantics) on the GPU box's
-    host cores, on the first sample_lines lines of the same workload: the
-    median of `repeats` timed runs (spread reported)."""
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_lib
-    oracle_lib.lib()
+def cpu_run(oracle_lib, lpa, workload, fields, sample_lines, threads, repeats, seconds):
+    """Median of `repeats` timed oracle runs on `threads` threads over the
+    first lines of the workload (about `seconds` of work per run)."""
     fmt = lpa.SYNTH_FORMATS[workload]
     probe = lpa.synth(workload, SEEDS[workload], 0, 2000)
     secs, _ = oracle_lib.bench(fmt, fields, probe, 1)
     rate1 = 2000 / max(secs, 1e-6)
-    # aim at ~5 s of work per run on `threads` threads (~15 s in all)
-    n = int(min(sample_lines, max(20000, rate1 * threads * 5)))
+    n = int(min(sample_lines, max(20000, rate1 * threads * seconds)))
     data = lpa.synth(workload, SEEDS[workload], 0, n)
     runs = []
     for _ in range(repeats):
@@ -215,20 +210,40 @@ def cpu_baseline(lpa, workload, fields, sample_lines, threads, repeats=3):
         runs.append(secs)
     runs.sort()
     secs = runs[len(runs) // 2]
+    return {"value": round(len(data) / secs / 1e9, 6), "lines_per_s": round(counts[0] / secs, 1), "cores": threads,
+            "lines": counts[0], "bytes": len(data), "counts": counts, "seconds": round(secs, 2),
+            "spread_gbs": [round(len(data) / t / 1e9, 6) for t in reversed(runs)]}
+
+
+def cpu_baseline(lpa, workload, fields, sample_lines, threads, share_threads=16, repeats=3):
+    """The oracle (C restatement of the reference semantics) on the GPU box's
+    host cores, on the first lines of the same workload: `threads` threads
+    (default every CPU the box reports) -- the median of `repeats` timed runs
+    -- and, beside it, the per-GPU CPU share (16 threads of the box)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+    oracle_lib.lib()
+    threads = threads or os.cpu_count() or 1
+    full = cpu_run(oracle_lib, lpa, workload, fields, sample_lines, threads, repeats, 3)
+    share = cpu_run(oracle_lib, lpa, workload, fields, sample_lines, min(share_threads, threads), 1, 4)
+    c = full["counts"]
     return {
-        "value": round(len(data) / secs / 1e9, 6),
+        "value": full["value"],
         "unit": "GB/s",
-        "lines_per_s": round(counts[0] / secs, 1),
+        "lines_per_s": full["lines_per_s"],
         "cores": threads,
         "host_cpus": os.cpu_count(),
         "kind": "port",
         "sample": "first %d lines (%.1f MB) of the config-%d workload, all %d paths, oracle/ C restatement, "
-                  "%d threads (the GPU box's CPU share; os.cpu_count() = %s), one parser per thread, median of %d "
+                  "%d threads = every CPU the box reports (os.cpu_count()), one parser per thread, median of %d "
                   "runs; ok=%d bad=%d unsupported=%d" % (
-                      counts[0], len(data) / 1e6, workload, len(fields), threads, os.cpu_count(), repeats,
-                      counts[1], counts[2], counts[3]),
-        "seconds": round(secs, 2),
-        "spread_gbs": [round(len(data) / t / 1e9, 6) for t in reversed(runs)],
+                      full["lines"], full["bytes"] / 1e6, workload, len(fields), threads, repeats, c[1], c[2], c[3]),
+        "seconds": full["seconds"],
+        "spread_gbs": full["spread_gbs"],
+        "per_gpu_share": {"value": share["value"], "unit": "GB/s", "lines_per_s": share["lines_per_s"],
+                          "cores": share["cores"], "seconds": share["seconds"],
+                          "sample": "first %d lines, %d threads (one GPU's CPU share of the box), one run"
+                                    % (share["lines"], share["cores"])},
     }
 
 
@@ -291,8 +306,8 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--lines", type=int, default=100_000_000, help="lines per GPU")
-    ap.add_argument("--cpu-sample-lines", type=int, default=2_000_000)
-    ap.add_argument("--cpu-threads", type=int, default=16, help="the GPU box's CPU share per GPU")
+    ap.add_argument("--cpu-sample-lines", type=int, default=4_000_000)
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = os.cpu_count())")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-delivery", action="store_true", help="skip the host delivery measurement (huge batches)")
     ap.add_argument("--workload", type=int, default=2, choices=(2, 3, 4, 5), help="BASELINE.json config")
@@ -457,8 +472,10 @@ def main():
     if rank == 0 and wl != 5 and not args.no_delivery:
         result["delivery"] = host_delivery(lpa, torch, parser, stats["lines"], wl)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        log("cpu baseline (oracle, %d threads) ..." % args.cpu_threads)
+        log("cpu baseline (oracle, %d threads) ..." % (args.cpu_threads or os.cpu_count()))
         result["cpu_baseline"] = cpu_baseline(lpa, wl, fields, args.cpu_sample_lines, args.cpu_threads)
+        # vs_baseline stays null: BASELINE.md publishes no number for this metric
+        result["vs_cpu_baseline"] = round(result["value"] / result["cpu_baseline"]["value"], 1)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -88,24 +88,39 @@ int64_t lp_possible_paths(const char *logformats, int max_depth, char *out, size
 /* Options (lp_set_option). */
 #define LP_OPT_FORCE_DIRECT 1  /* 1: every wave reads its lines from HBM (no LDS window);
                                   diagnostics and tests of the direct path only */
+#define LP_OPT_MAX_RETRIES 2   /* re-runs of a batch whose line / arena estimates were short
+                                  (default 3, 0..16); an arena still short after them degrades:
+                                  the lines that did not fit are FALLBACK, lp_counters out[6] */
+#define LP_OPT_ARENA_BYTES 3   /* tests: exact arena capacity of each batch's first run (0 = estimate) */
 int lp_set_option(lp_handle *h, int option, int64_t value);
 
-/* Capacity for the coming batches: columns for max_lines lines and
- * arena_bytes of side arena (0 = estimated).  With it (or after a first
- * batch, whose line count sizes the buffers) lp_parse_batch enqueues the whole
- * batch without waiting for the device; a batch that outgrows the buffers is
- * re-run with exact sizes inside lp_sync. */
+/* Capacity for the coming batches: columns for max_lines lines and at least
+ * arena_bytes of side arena (0 = estimated; the estimate wins when larger).
+ * With it (or after a first batch, whose line count sizes the buffers)
+ * lp_parse_batch enqueues the whole batch without waiting for the device; a
+ * batch that outgrows the buffers is re-run with exact sizes inside lp_sync
+ * (at most LP_OPT_MAX_RETRIES times; an arena still short then sends the
+ * lines that did not fit to FALLBACK instead of failing the batch). */
 int lp_reserve(lp_handle *h, int64_t max_lines, uint64_t arena_bytes);
 
-/* Parse every '\n'-terminated line of buf[0, nbytes) (a final line without
- * '\n' counts; Hadoop LineRecordReader semantics on '\n').  stream: a
- * hipStream_t (NULL = default stream).  Enqueues all work on the stream and
- * returns without synchronizing (except a handle's first batch without a
- * reservation, which waits for its line count); call lp_sync before reading
- * results.  A batch still pending on the handle is finished first: to overlap
- * batches, use one handle per stream.  On error the handle holds no batch
- * (the accessors return LP_E_STATE) until a batch succeeds. */
+/* Parse every line of buf[0, nbytes), Hadoop LineRecordReader semantics
+ * (ApacheHttpdLogfileRecordReader.java:57, 115): a line ends at '\n', at a
+ * lone '\r' or at "\r\n", the terminator is not part of it, and a final
+ * line without one counts.  stream: a hipStream_t (NULL = default stream).
+ * Enqueues all work on the stream and returns without synchronizing (except a
+ * handle's first batch without a reservation, which waits for its line
+ * count); call lp_sync before reading results.  A batch still pending on the
+ * handle is finished first: to overlap batches, use one handle per stream.
+ * On error the handle holds no batch (the accessors return LP_E_STATE) until
+ * a batch succeeds.
+ * first_line_no (lp_parse_batch_at): the global number of the batch's first
+ * line (a split reader's position in the stream); it comes
+ * back in lp_result.first_line.  lp_parse_batch continues the handle's
+ * numbering (0 for its first batch, then the previous batch's first line +
+ * its line count). */
 int lp_parse_batch(lp_handle *h, const uint8_t *buf, uint64_t nbytes, int buf_flags, void *stream);
+int lp_parse_batch_at(lp_handle *h, const uint8_t *buf, uint64_t nbytes, int64_t first_line_no, int buf_flags,
+                      void *stream);
 int lp_sync(lp_handle *h);
 
 /* Results of the last batch (after lp_sync). */
@@ -122,7 +137,9 @@ int64_t lp_line_record_json(lp_handle *h, int64_t i, char *out, size_t cap);
 /* out[0..3] = lines, ok, bad, fallback of the last batch (device counters);
  * diagnostics: out[4] = waves parsed by the overflow kernel (their lines'
  * window exceeded the main kernel's LDS window), out[5] = re-runs of the
- * batch (capacity / arena estimates exceeded).  Returns the words written. */
+ * batch (capacity / arena estimates exceeded), out[6] = arena overflows the
+ * final run left (lines sent to FALLBACK for want of arena; 0 normally).
+ * Returns the words written. */
 int lp_counters(lp_handle *h, uint64_t *out, int n);
 
 /* Device-side timing of the last batch, in milliseconds, measured with HIP
@@ -190,6 +207,7 @@ typedef struct lp_column {
 } lp_column;
 typedef struct lp_result {
     int64_t n_lines;
+    int64_t first_line;        /* global number of line 0 of the batch (lp_parse_batch_at) */
     uint64_t input_bytes;
     const uint8_t *input;      /* line i = input[line_off[i], line_off[i+1] - 1), less the '\r' of a
                                   "\r\n" terminator; NULL if not copied */

@@ -33,7 +33,7 @@ LIB_PATH = os.environ.get("LOGPARSER_AMD_LIB") or os.path.join(_HERE, "_lib", "l
 LP_OK, LP_E_INVALID, LP_E_MISSING, LP_E_UNSUPPORTED, LP_E_DEVICE, LP_E_NOMEM, LP_E_STATE = 0, -1, -2, -3, -4, -5, -6
 LINE_OK, LINE_BAD, LINE_FALLBACK = 0, 1, 2
 BUF_HOST, BUF_DEVICE = 0, 1
-OPT_FORCE_DIRECT = 1
+OPT_FORCE_DIRECT, OPT_MAX_RETRIES, OPT_ARENA_BYTES = 1, 2, 3
 ARENA_SHARDS = 64
 
 
@@ -56,7 +56,8 @@ class LpTableCol(ctypes.Structure):
 
 class LpResult(ctypes.Structure):
     """lp_result (include/logparser_amd.h): the SoA results of one batch"""
-    _fields_ = [("n_lines", ctypes.c_int64), ("input_bytes", ctypes.c_uint64), ("input", ctypes.c_void_p),
+    _fields_ = [("n_lines", ctypes.c_int64), ("first_line", ctypes.c_int64), ("input_bytes", ctypes.c_uint64),
+                ("input", ctypes.c_void_p),
                 ("line_off", ctypes.c_void_p), ("columns", ctypes.c_void_p), ("columns_bytes", ctypes.c_uint64),
                 ("arena", ctypes.c_void_p), ("arena_bytes", ctypes.c_uint64), ("shard_cap", ctypes.c_uint64),
                 ("shard_off", ctypes.c_uint64 * ARENA_SHARDS), ("n_columns", ctypes.c_int32),
@@ -110,6 +111,9 @@ def lib():
     L.lp_possible_paths.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]
     L.lp_parse_batch.restype = ctypes.c_int
     L.lp_parse_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
+    L.lp_parse_batch_at.restype = ctypes.c_int
+    L.lp_parse_batch_at.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int64, ctypes.c_int,
+                                    ctypes.c_void_p]
     L.lp_sync.argtypes = [ctypes.c_void_p]
     L.lp_num_lines.restype = ctypes.c_int64
     L.lp_num_lines.argtypes = [ctypes.c_void_p]
@@ -209,9 +213,9 @@ class BatchResult:
             if rc != LP_OK:
                 raise EngineUnavailable("lp_line_status failed: %d" % rc)
         self.status = st[: self.n_lines]
-        c = (ctypes.c_uint64 * 4)()
-        L.lp_counters(parser._h, c, 4)
-        self.counters = {"lines": c[0], "ok": c[1], "bad": c[2], "fallback": c[3]}
+        c = (ctypes.c_uint64 * 7)()
+        L.lp_counters(parser._h, c, 7)
+        self.counters = {"lines": c[0], "ok": c[1], "bad": c[2], "fallback": c[3], "retries": c[5], "arena_ovf": c[6]}
         t = (ctypes.c_float * 3)()
         L.lp_last_timing(parser._h, t, 3)
         self.timing_ms = {"total": t[0], "index": t[1], "parse": t[2]}
@@ -350,7 +354,8 @@ class HttpdLoglineParser:
     """GPU-backed equivalent of new HttpdLoglineParser<>(RECORD.class, logformat)
     with addParseTarget(...) for each requested "TYPE:path"."""
 
-    def __init__(self, logformat, fields=(), device=0, force_direct=False, reserve_lines=0, reserve_arena=0):
+    def __init__(self, logformat, fields=(), device=0, force_direct=False, reserve_lines=0, reserve_arena=0,
+                 options=None):
         self.logformat = logformat
         self.fields = list(fields)
         self._targets = {}       # cleaned "TYPE:path" -> [Target] (Parser.targets)
@@ -360,6 +365,7 @@ class HttpdLoglineParser:
         self.device = device
         self.force_direct = force_direct
         self.reserve = (reserve_lines, reserve_arena)
+        self.options = dict(options or {})  # lp_set_option(OPT_*, value) after lp_compile
         self._h = None
         self.device_program_ok = None
         self.unsupported_reason = ""
@@ -461,6 +467,9 @@ class HttpdLoglineParser:
             L.lp_set_option(h, OPT_FORCE_DIRECT, 1)
         if self.reserve[0] or self.reserve[1]:
             L.lp_reserve(h, self.reserve[0], self.reserve[1])
+        for opt, val in self.options.items():
+            if L.lp_set_option(h, opt, val) != LP_OK:
+                raise ValueError("lp_set_option(%r, %r) rejected" % (opt, val))
         self.device_program_ok = st.value == LP_OK
         self.unsupported_reason = msg if st.value == LP_E_UNSUPPORTED else ""
 
@@ -516,13 +525,14 @@ class HttpdLoglineParser:
         rc = L.lp_sync(self._h)
         if rc != LP_OK:
             raise EngineUnavailable("lp_sync failed: %d" % rc)
-        c = (ctypes.c_uint64 * 6)()
-        L.lp_counters(self._h, c, 6)
+        c = (ctypes.c_uint64 * 7)()
+        L.lp_counters(self._h, c, 7)
         t = (ctypes.c_float * 3)()
         L.lp_last_timing(self._h, t, 3)
         b = (ctypes.c_uint64 * 2)()
         L.lp_last_bytes(self._h, b, 2)
         return {"lines": c[0], "ok": c[1], "bad": c[2], "fallback": c[3], "overflow_waves": c[4], "retries": c[5],
+                "arena_ovf": c[6],
                 "ms_total": t[0], "ms_index": t[1], "ms_parse": t[2], "bytes_in": b[0], "bytes_out": b[1]}
 
     def parse(self, line, record=None):

@@ -78,6 +78,11 @@ struct lp_handle {
     double mean_line = 0;          // input bytes per line of the last batch
     double arena_per_line = 0;     // arena bytes (largest shard x shards) per line of the last batch
     bool force_direct = false;
+    int max_retries = 3;           // re-runs of a batch whose estimates were short (LP_OPT_MAX_RETRIES)
+    uint64_t arena_first = 0;      // LP_OPT_ARENA_BYTES: exact arena of a batch's first run (tests)
+    uint64_t arena_ovf = 0;        // arena overflow events of the last batch's final run (its lines FALLBACK)
+    int64_t first_line = 0;        // global number of the last batch's first line
+    int64_t next_line = 0;         // ... of the next batch's (lp_parse_batch continues the numbering)
     hipEvent_t ev[4]{};
     bool have_events = false;
     uint64_t counters[4]{};
@@ -263,12 +268,11 @@ int enqueue(lp_handle* h, bool sync_count) {
     if (lp::launch_offsets(d_nlmask, nbytes, d_chunk, h->line_off.as<uint64_t>(), cap, s) != 0) return LP_E_DEVICE;
     hipEventRecord(h->ev[1], s);
     if (!alloc_columns(h, cap)) return LP_E_NOMEM;
-    // arena: ARENA_SHARDS shards of shard_cap bytes
-    uint64_t acap = h->reserve_arena;
-    if (!acap) {
-        const double per = h->arena_per_line > 0 ? h->arena_per_line * 1.25 : 64.0;
-        acap = (uint64_t)(per * (double)cap) + (1u << 20);
-    }
+    // arena: ARENA_SHARDS shards of shard_cap bytes; the reservation is a
+    // minimum (a re-run after an overflow needs the grown estimate)
+    const double per = h->arena_per_line > 0 ? h->arena_per_line * 1.25 : 64.0;
+    uint64_t acap = std::max<uint64_t>(h->reserve_arena, (uint64_t)(per * (double)cap) + (1u << 20));
+    if (h->arena_first && h->retries == 0) acap = h->arena_first;
     if (!h->plan.device_ok() || P.n_uri == 0) acap = 4096 * LP_ARENA_SHARDS;
     h->shard_cap = (acap / LP_ARENA_SHARDS + 255) & ~255ull;
     if (!h->arena.ensure(h->shard_cap * LP_ARENA_SHARDS)) return LP_E_NOMEM;
@@ -328,7 +332,7 @@ int finish(lp_handle* h) {
             top_max = std::max<uint64_t>(top_max, h->shard_top[s]);
         }
         const int64_t n = (int64_t)m.n_lines;
-        if (h->plan.device_ok() && (m.cap_ovf || m.arena_ovf) && h->retries < 3) {
+        if (h->plan.device_ok() && (m.cap_ovf || m.arena_ovf) && h->retries < h->max_retries) {
             // exact sizes: the line count, every shard as large as the largest
             // request (shard tops count what was asked for, also past the end)
             ++h->retries;
@@ -341,7 +345,12 @@ int finish(lp_handle* h) {
             if (st != LP_OK) return st;
             continue;
         }
-        if (m.cap_ovf || m.arena_ovf) return LP_E_NOMEM;
+        // more lines than columns: nothing was parsed.  An arena that is still
+        // short after the re-runs degrades instead: the lines whose region or
+        // pieces did not fit are FALLBACK (the kernels marked them), the rest
+        // of the batch is delivered
+        if (m.cap_ovf) return LP_E_NOMEM;
+        h->arena_ovf = m.arena_ovf;
         h->n_lines = n;
         if (h->plan.device_ok()) {
             for (int k = 0; k < 4; ++k) h->counters[k] = m.counters[k];
@@ -415,6 +424,7 @@ int64_t copy_result(lp_handle* h, uint8_t* dst, uint64_t cap, bool with_input, l
     lp_result& R = *r;
     R = lp_result{};
     R.n_lines = n;
+    R.first_line = h->first_line;
     R.input_bytes = h->nbytes;
     R.input = with_input ? dst + o_input : nullptr;
     R.line_off = reinterpret_cast<const uint64_t*>(dst + o_lines);
@@ -483,7 +493,7 @@ void lp_free(lp_handle* h) {
     hipSetDevice(h->device);
     if (h->pending) hipStreamSynchronize(h->stream);
     for (auto* b : {&h->input, &h->chunk, &h->line_off, &h->cols, &h->arena, &h->meta, &h->waves, &h->args, &h->route,
-                    &h->ovf})
+                    &h->ovf, &h->hist})
         b->release();
     if (h->have_events)
         for (auto& ev : h->ev) hipEventDestroy(ev);
@@ -505,6 +515,14 @@ int lp_set_option(lp_handle* h, int option, int64_t value) {
     if (!h) return LP_E_INVALID;
     switch (option) {
     case LP_OPT_FORCE_DIRECT: h->force_direct = value != 0; return LP_OK;
+    case LP_OPT_MAX_RETRIES:
+        if (value < 0 || value > 16) return LP_E_INVALID;
+        h->max_retries = (int)value;
+        return LP_OK;
+    case LP_OPT_ARENA_BYTES:
+        if (value < 0) return LP_E_INVALID;
+        h->arena_first = (uint64_t)value;
+        return LP_OK;
     default: return LP_E_INVALID;
     }
 }
@@ -518,7 +536,14 @@ int lp_reserve(lp_handle* h, int64_t max_lines, uint64_t arena_bytes) {
 }
 
 int lp_parse_batch(lp_handle* h, const uint8_t* buf, uint64_t nbytes, int buf_flags, void* stream) {
-    if (!h || (!buf && nbytes)) return LP_E_INVALID;
+    if (!h) return LP_E_INVALID;
+    if (h->pending) lp_sync(h);  // the previous batch's line count continues the numbering
+    return lp_parse_batch_at(h, buf, nbytes, h->next_line, buf_flags, stream);
+}
+
+int lp_parse_batch_at(lp_handle* h, const uint8_t* buf, uint64_t nbytes, int64_t first_line_no, int buf_flags,
+                      void* stream) {
+    if (!h || (!buf && nbytes) || first_line_no < 0) return LP_E_INVALID;
     if (hipSetDevice(h->device) != hipSuccess) return LP_E_DEVICE;
     if (h->pending) lp_sync(h);
     // the handle holds no valid batch until this one has been enqueued
@@ -526,6 +551,8 @@ int lp_parse_batch(lp_handle* h, const uint8_t* buf, uint64_t nbytes, int buf_fl
     h->host_valid = false;
     h->n_lines = 0;
     h->retries = 0;
+    h->arena_ovf = 0;
+    h->first_line = h->next_line = first_line_no;
     hipStream_t s = (hipStream_t)stream;
     h->stream = s;
     h->nbytes = nbytes;
@@ -571,6 +598,8 @@ int lp_sync(lp_handle* h) {
     if (st != LP_OK) {
         h->valid = false;
         h->n_lines = 0;
+    } else {
+        h->next_line = h->first_line + h->n_lines;
     }
     return st;
 }
@@ -623,10 +652,10 @@ int lp_counters(lp_handle* h, uint64_t* out, int n) {
     if (!h || !out) return LP_E_INVALID;
     const int st = ensure_synced(h);
     if (st != LP_OK) return st;
-    const uint64_t v[6] = {h->counters[0], h->counters[1], h->counters[2], h->counters[3], h->ovf_waves,
-                           (uint64_t)h->retries};
-    for (int k = 0; k < n && k < 6; ++k) out[k] = v[k];
-    return n < 6 ? n : 6;
+    const uint64_t v[7] = {h->counters[0], h->counters[1], h->counters[2], h->counters[3], h->ovf_waves,
+                           (uint64_t)h->retries, h->arena_ovf};
+    for (int k = 0; k < n && k < 7; ++k) out[k] = v[k];
+    return n < 7 ? n : 7;
 }
 
 int lp_histograms(lp_handle* h, uint64_t* out, int out_on_device) {
@@ -694,6 +723,7 @@ int lp_result_view(lp_handle* h, lp_result* out) {
     lp_result& R = *out;
     R = lp_result{};
     R.n_lines = h->n_lines;
+    R.first_line = h->first_line;
     R.input_bytes = h->nbytes;
     R.input = h->d_buf;
     R.line_off = h->line_off.as<uint64_t>();
@@ -770,7 +800,7 @@ struct TableCtx {
     lp_table_col* cols;
     int64_t row;           // row in the output
     std::vector<std::string>* sbuf;  // per column: this chunk's STRING bytes
-    std::vector<std::vector<std::pair<uint32_t, uint32_t>>>* sref;  // per column: (offset, len) per chunk row
+    std::vector<std::vector<std::pair<uint64_t, uint32_t>>>* sref;  // per column: (offset, len) per chunk row
     int64_t row0;          // first output row of the chunk
 };
 void table_value(void* vctx, const std::string& target, const lp::MVal& v) {
@@ -784,10 +814,10 @@ void table_value(void* vctx, const std::string& target, const lp::MVal& v) {
         if (v.null) continue;
         if (C.kind == LP_CAST_STRING) {
             std::string& buf = (*t.sbuf)[c];
-            const uint32_t off = (uint32_t)buf.size();
+            const uint64_t off = buf.size();  // a chunk's bytes of one column may pass 4 GiB
             if (v.is_long) buf += std::to_string(v.l);
             else buf.append((const char*)v.p, v.len);
-            (*t.sref)[c][t.row - t.row0] = {off, (uint32_t)buf.size() - off};
+            (*t.sref)[c][t.row - t.row0] = {off, (uint32_t)(buf.size() - off)};
             C.valid[t.row] = 1;
         } else if (C.kind == LP_CAST_LONG) {
             int64_t x;
@@ -833,10 +863,10 @@ int lp_result_table(lp_handle* h, const lp_result* r, int64_t first, int64_t cou
     const int T = std::max(1, std::min(threads > 0 ? threads : 1, 64));
     const int64_t per = (count + T - 1) / T;
     std::vector<std::vector<std::string>> sbuf(T, std::vector<std::string>(n_cols));
-    std::vector<std::vector<std::vector<std::pair<uint32_t, uint32_t>>>> sref(T);
+    std::vector<std::vector<std::vector<std::pair<uint64_t, uint32_t>>>> sref(T);
     auto work = [&](int t) {
         const int64_t a = std::min(count, t * per), b = std::min(count, a + per);
-        sref[t].assign(n_cols, std::vector<std::pair<uint32_t, uint32_t>>((size_t)(b - a), {0u, 0u}));
+        sref[t].assign(n_cols, std::vector<std::pair<uint64_t, uint32_t>>((size_t)(b - a), {0ull, 0u}));
         TableCtx ctx{&by_path, cols, 0, &sbuf[t], &sref[t], a};
         for (int64_t k = a; k < b; ++k) {
             for (int c = 0; c < n_cols; ++c) cols[c].valid[k] = 0;

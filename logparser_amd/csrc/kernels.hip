@@ -395,11 +395,6 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
     LP_PROF(1);
     if (active) phase1(P, elems, L, o, stk, C, li, clean, P.n_fmt > 1 ? (int)C.fmt_id[li] : 0);
     LP_PROF(9);
-#if LP_EXP == 13 || LP_EXP == 12
-    if (active) write_line(P, o, C, li);  // experiment: stop after phase 1
-    WC.act += (uint32_t)__popcll(__ballot(active));
-    return;
-#endif
     // wave-aggregated arena allocation from the wave's shard (every lane reaches this point)
     const uint32_t need = (active && o.status == ST_OK) ? o.arena_need : 0u;
     const int lane = threadIdx.x;
@@ -445,7 +440,7 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
     // QueryStringFieldDissector pieces of all lines of the wave, spread evenly
     // over the lanes (a line's pieces vary from 0 to dozens; one lane per line
     // would leave most lanes idle while the longest query finishes)
-    if (P.n_query > 0 && LP_EXP != 14) {
+    if (P.n_query > 0) {
         __syncthreads();  // the table slots written in phase 2 are visible to every lane
         const bool has = active && o.status == ST_OK && need != 0;
         const unsigned long long my_ab = has ? my_region : 0ull;
@@ -466,6 +461,7 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
                 const uint32_t ob = __shfl(base, own), olist = __shfl(my_list, own);
                 const unsigned long long oab = __shfl(my_ab, own);
                 const auto OL = owner_line(L, own);
+                bool piece_ovf = false;
                 LP_G uint64_t* slot = reinterpret_cast<LP_G uint64_t*>(C.arena + oab + olist + 16 * (g - ob));
                 QPrep qp;
                 if (g < tot) qp = query_prep(OL, slot);
@@ -487,10 +483,21 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
                     if (qp.need && (at + qp.need > C.shard_cap || at - rel + qp.need > 0x7FFFFFFFull)) {
                         slot[0] = REF_SKIP;
                         slot[1] = 0;
+                        piece_ovf = true;
                         atomicAdd(&C.meta->arena_ovf, 1ull);  // the batch is re-run with a larger arena
                     } else {
                         Arena A{C.arena + oab, (uint32_t)(at - rel), (uint32_t)(at - rel + qp.need)};
                         written += query_finish(P, P.query[qs], OL, A, C.arena + oab, slot, qp);
+                    }
+                }
+                // a piece that did not fit: its line goes to FALLBACK (the
+                // batch is re-run with a larger arena, or, when the re-runs
+                // are spent, delivered with those lines FALLBACK)
+                for (uint64_t m = __ballot(piece_ovf); m; m &= m - 1) {
+                    const int o_lane = __shfl(own, (int)__builtin_ctzll(m));
+                    if (lane == o_lane && o.status == ST_OK) {
+                        o.status = ST_FALLBACK;
+                        C.status[li] = (uint8_t)ST_FALLBACK;
                     }
                 }
             }
@@ -548,9 +555,6 @@ __global__ __launch_bounds__(PW, 2) void k_parse_lines(const uint8_t* __restrict
         const uint64_t a = r ? a1 : a0, b = r ? b1 : b0;
         const bool clean = stage_window(buf, nbytes, a, b, win, msk16);
         __syncthreads();
-#if LP_EXP == 11
-        if (clean) return;  // experiment: stop after staging
-#endif
         const bool mine = W.active && (rounds == 1 || ((int)threadIdx.x >= PW / 2) == (r != 0));
         const int n = mine ? crlf_len(W.n, W.n > 0 ? win[W.e - 1 - a] : 0u) : 0;
         const LineT<lds_bytes, lds_u64> L{(lds_bytes)win, mine ? (uint32_t)(W.s - a) : 0u, n,

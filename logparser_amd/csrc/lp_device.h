@@ -54,10 +54,6 @@ __device__ __forceinline__ void lp_prof_acc(int k, unsigned long long& t0) {
 #endif
 #define LP_PROF_EL_BEGIN()
 #define LP_PROF_EL_END(i)
-// profiling experiments only (tools/build_exp.sh): 0 = the product
-#ifndef LP_EXP
-#define LP_EXP 0
-#endif
 
 // ----------------------------------------------------------- byte classes
 __host__ __device__ LP_INLINE bool is_ws(uint32_t c) { return c == ' ' || (c >= 9 && c <= 13); }      // \s
@@ -1766,9 +1762,6 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
     }
     LP_PROF(4);
     if (st != ST_OK) { o.status = st; return; }
-#if LP_EXP == 12
-    return;  // experiment: stop after the match
-#endif
     // decodeExtractedValue: "-" -> null (Apache: ApacheHttpdLogFormatDissector.java:169-196,
     // NGINX: NginxHttpdLogFormatDissector.java:107-119).  Slots unrolled (the
     // spans stay in registers); only one-byte values are read.
@@ -2365,13 +2358,7 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
         return true;
     });
     LP_PROF(51 + 4 * u);
-#if LP_EXP == 2
-    if (0)
-#endif
     if (resume >= 0) for_uev(L, resume, b, [&](int q, uint32_t c) {
-#if LP_EXP == 1
-        return true;
-#endif
         // non-ASCII: URIUtil.encode keeps the UTF-8 bytes raw and the
         // dissector reads them back as US-ASCII (U+FFFD each); not on the device
         if (c >= 0x80) { st = ST_FALLBACK; return false; }
@@ -2460,7 +2447,7 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
             scheme_ref = (int64_t)mkref(a, p - a, false);
             ++p;
             if (!(p < b && cur.at(p) == '/')) return ST_FALLBACK;                          // opaque URI
-            if (LP_EXP != 3 && p + 1 < b && cur.at(p + 1) == '/') {
+            if (p + 1 < b && cur.at(p + 1) == '/') {
                 // authority [as, ae): up to '/', '#' or the first '?'; only chars
                 // in both L_SERVER and L_REG_NAME of java.net.URI (no '@'
                 // userinfo, no escapes), else FALLBACK

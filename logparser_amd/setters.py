@@ -75,7 +75,14 @@ def java_parse_double(s):
 def java_double_to_string(d):
     """Double.toString: "NaN", "Infinity", plain decimal with at least one
     fraction digit for 1e-3 <= |d| < 1e7, else computerized scientific
-    notation ("1.0E7"); shortest round-trip digits"""
+    notation ("1.0E7"); shortest round-trip digits.
+
+    The digits are those of JDK 19+ (JDK-4511638, shortest round trip).  The
+    reference's pinned JDK 8 (FloatingDecimal.dtoa) prints more digits for
+    some values (e.g. 8.41E21 as "8.409999999999999E21").  Parity unpinned:
+    no reference test covers it, and no dissector on this path delivers a
+    DOUBLE value (only the out-of-scope GeoIP ones do), so getString of a
+    Double is reached only through a caller's own setter types."""
     if math.isnan(d):
         return "NaN"
     if math.isinf(d):

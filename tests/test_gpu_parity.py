@@ -377,6 +377,71 @@ def test_arena_overflow_retry(oracle):
     assert s["ok"] == 20000
 
 
+def _query_lines(n):
+    q = "&".join("k%d=v%%41%d+x" % (j, j) for j in range(12))
+    return [('10.0.0.%d - - [01/Jan/2021:00:00:%02d +0000] "GET /b?%s HTTP/1.1" 200 1 "http://h.nl/r?%s" "u"'
+             % (i % 250, i % 60, q, q)).encode() for i in range(n)]
+
+
+def test_tiny_arena_reruns(oracle):
+    """A first run with a far too small arena (LP_OPT_ARENA_BYTES) is re-run
+    inside lp_sync with the exact size: LP_OK, retries > 0, every line equals
+    the oracle (re-runs must not keep the short reservation)."""
+    fields = paths(oracle)
+    lines = _query_lines(20000)
+    p = lpa.HttpdLoglineParser("combined", fields, reserve_arena=4096, options={lpa.OPT_ARENA_BYTES: 64 * 1024})
+    r = p.parse_batch(b"".join(l + b"\n" for l in lines))
+    assert r.counters["retries"] > 0 and r.counters["arena_ovf"] == 0, r.counters
+    assert r.counters["ok"] == len(lines)
+    o = oracle.Oracle("combined", fields)
+    for i in range(0, len(lines), 97):
+        s1, js = o.parse_raw(lines[i])
+        assert s1 == oracle.OK and js == r.record_json(i), i
+
+
+def test_arena_overflow_degrades_to_fallback(oracle):
+    """No re-runs allowed and a tiny arena: the batch is still delivered
+    (LP_OK); the lines whose arena region or query pieces did not fit are
+    FALLBACK, every other line equals the oracle."""
+    fields = paths(oracle)
+    lines = _query_lines(20000)
+    p = lpa.HttpdLoglineParser("combined", fields, options={lpa.OPT_MAX_RETRIES: 0, lpa.OPT_ARENA_BYTES: 256 * 1024})
+    r = p.parse_batch(b"".join(l + b"\n" for l in lines))
+    c = r.counters
+    assert c["retries"] == 0 and c["arena_ovf"] > 0, c
+    assert c["fallback"] > 0 and c["ok"] > 0 and c["ok"] + c["fallback"] == len(lines), c
+    assert int((r.status == lpa.LINE_FALLBACK).sum()) == c["fallback"]
+    o = oracle.Oracle("combined", fields)
+    for i in range(len(lines)):
+        if r.status[i] == lpa.LINE_OK and (i % 7 == 0 or r.status[max(0, i - 1)] != lpa.LINE_OK):
+            s1, js = o.parse_raw(lines[i])
+            assert s1 == oracle.OK and js == r.record_json(i), i
+    print("arena degrade: %d of %d lines FALLBACK, %d overflow events" % (c["fallback"], len(lines), c["arena_ovf"]))
+
+
+def test_first_line_numbers(oracle):
+    """lp_parse_batch_at numbers a batch's lines from first_line_no (a split
+    reader's position); lp_parse_batch continues the handle's numbering; the
+    number comes back in lp_result.first_line."""
+    import ctypes
+    L = lpa.lib()
+    data = lpa.synth_combined(5, 0, 1000)
+    t = __import__("torch").frombuffer(bytearray(data), dtype=__import__("torch").uint8).cuda()
+    p = lpa.HttpdLoglineParser("combined", ["IP:connection.client.host"])
+    p._ensure()
+    res = lpa.LpResult()
+    assert L.lp_parse_batch_at(p._h, ctypes.c_void_p(t.data_ptr()), len(data), 123456789, lpa.BUF_DEVICE, None) == 0
+    assert L.lp_sync(p._h) == 0 and L.lp_result_view(p._h, ctypes.byref(res)) == 0
+    assert res.first_line == 123456789 and res.n_lines == 1000
+    assert L.lp_parse_batch(p._h, ctypes.c_void_p(t.data_ptr()), len(data), lpa.BUF_DEVICE, None) == 0
+    assert L.lp_sync(p._h) == 0 and L.lp_result_view(p._h, ctypes.byref(res)) == 0
+    assert res.first_line == 123456789 + 1000
+    buf = bytearray(-L.lp_result_copy(p._h, None, 0, 0, None))
+    host = (ctypes.c_uint8 * len(buf)).from_buffer(buf)
+    assert L.lp_result_copy(p._h, host, len(buf), 0, ctypes.byref(res)) > 0 and res.first_line == 124457789
+    assert L.lp_parse_batch_at(p._h, None, 0, -1, lpa.BUF_DEVICE, None) == lpa.LP_E_INVALID
+
+
 def test_async_batches_and_capacity_retry(oracle):
     """Later batches of a handle are enqueued without a line count (capacity
     from the previous batch); a batch of much shorter lines outgrows the
