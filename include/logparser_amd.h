@@ -138,7 +138,9 @@ int64_t lp_line_record_json(lp_handle *h, int64_t i, char *out, size_t cap);
  * diagnostics: out[4] = waves parsed by the overflow kernel (their lines'
  * window exceeded the main kernel's LDS window), out[5] = re-runs of the
  * batch (capacity / arena estimates exceeded), out[6] = arena overflows the
- * final run left (lines sent to FALLBACK for want of arena; 0 normally).
+ * final run left (lines sent to FALLBACK for want of arena; 0 normally),
+ * out[7] = waves whose URI bytes exceeded the URI kernel's compact buffer
+ * (their URI stages read the input from HBM directly).
  * Returns the words written. */
 int lp_counters(lp_handle *h, uint64_t *out, int n);
 

@@ -213,9 +213,10 @@ class BatchResult:
             if rc != LP_OK:
                 raise EngineUnavailable("lp_line_status failed: %d" % rc)
         self.status = st[: self.n_lines]
-        c = (ctypes.c_uint64 * 7)()
-        L.lp_counters(parser._h, c, 7)
-        self.counters = {"lines": c[0], "ok": c[1], "bad": c[2], "fallback": c[3], "retries": c[5], "arena_ovf": c[6]}
+        c = (ctypes.c_uint64 * 8)()
+        L.lp_counters(parser._h, c, 8)
+        self.counters = {"lines": c[0], "ok": c[1], "bad": c[2], "fallback": c[3]}
+        self.diag = {"overflow_waves": c[4], "retries": c[5], "arena_ovf": c[6], "uri_overflow_waves": c[7]}
         t = (ctypes.c_float * 3)()
         L.lp_last_timing(parser._h, t, 3)
         self.timing_ms = {"total": t[0], "index": t[1], "parse": t[2]}
@@ -525,14 +526,14 @@ class HttpdLoglineParser:
         rc = L.lp_sync(self._h)
         if rc != LP_OK:
             raise EngineUnavailable("lp_sync failed: %d" % rc)
-        c = (ctypes.c_uint64 * 7)()
-        L.lp_counters(self._h, c, 7)
+        c = (ctypes.c_uint64 * 8)()
+        L.lp_counters(self._h, c, 8)
         t = (ctypes.c_float * 3)()
         L.lp_last_timing(self._h, t, 3)
         b = (ctypes.c_uint64 * 2)()
         L.lp_last_bytes(self._h, b, 2)
         return {"lines": c[0], "ok": c[1], "bad": c[2], "fallback": c[3], "overflow_waves": c[4], "retries": c[5],
-                "arena_ovf": c[6],
+                "arena_ovf": c[6], "uri_overflow_waves": c[7],
                 "ms_total": t[0], "ms_index": t[1], "ms_parse": t[2], "bytes_in": b[0], "bytes_out": b[1]}
 
     def parse(self, line, record=None):

@@ -87,6 +87,7 @@ struct lp_handle {
     bool have_events = false;
     uint64_t counters[4]{};
     uint64_t ovf_waves = 0;        // waves of the last batch parsed by k_parse_overflow
+    uint64_t uri_ovf_waves = 0;    // ... whose URI stages ran in k_uri_overflow
     uint64_t shard_top[LP_ARENA_SHARDS]{};
     uint64_t arena_written = 0;
     int retries = 0;
@@ -284,9 +285,10 @@ int enqueue(lp_handle* h, bool sync_count) {
     C.cap_lines = cap;
     const int64_t waves = lp::parse_waves(cap);
     if (!h->waves.ensure(4 * lp::WC_WORDS * (size_t)(waves + 1))) return LP_E_NOMEM;
-    if (!h->ovf.ensure(4 * (size_t)(waves + 1))) return LP_E_NOMEM;
+    if (!h->ovf.ensure(8 * (size_t)(waves + 1))) return LP_E_NOMEM;
     C.wave_counts = h->waves.as<uint32_t>();
     C.ovf_list = h->ovf.as<uint32_t>();
+    C.uri_ovf_list = h->ovf.as<uint32_t>() + (waves + 1);
     if (h->plan.device_ok()) {
         if (P.n_fmt > 1) {  // sticky multi-format routing scratch
             if (!h->route.ensure(8 * (size_t)(lp::fmt_chunks(cap) + 1))) return LP_E_NOMEM;
@@ -299,7 +301,7 @@ int enqueue(lp_handle* h, bool sync_count) {
         if (hipMemcpyAsync(h->args.p, &h->host_args, sizeof(lp::DeviceArgs), hipMemcpyHostToDevice, s) != hipSuccess)
             return LP_E_DEVICE;
         lp::ParseLaunch pl{h->d_buf, nbytes, cap, (uint64_t)(h->mean_line > 0 ? h->mean_line + 0.5 : 0),
-                           P.n_elems, P.max_stack, h->force_direct};
+                           P.n_elems, P.max_stack, h->force_direct, P.n_uri > 0};
         if (!pl.mean_line && cap > 0) pl.mean_line = (nbytes + cap - 1) / (uint64_t)cap;
         hipEventRecord(h->ev[2], s);
         const lp::DeviceArgs* d_args = h->args.as<lp::DeviceArgs>();
@@ -356,6 +358,7 @@ int finish(lp_handle* h) {
             for (int k = 0; k < 4; ++k) h->counters[k] = m.counters[k];
             h->arena_written = m.counters[4];
             h->ovf_waves = m.ovf_waves;
+            h->uri_ovf_waves = m.uri_ovf_waves;
         } else {
             h->counters[0] = (uint64_t)n;
             h->counters[1] = h->counters[2] = 0;
@@ -652,10 +655,10 @@ int lp_counters(lp_handle* h, uint64_t* out, int n) {
     if (!h || !out) return LP_E_INVALID;
     const int st = ensure_synced(h);
     if (st != LP_OK) return st;
-    const uint64_t v[7] = {h->counters[0], h->counters[1], h->counters[2], h->counters[3], h->ovf_waves,
-                           (uint64_t)h->retries, h->arena_ovf};
-    for (int k = 0; k < n && k < 7; ++k) out[k] = v[k];
-    return n < 7 ? n : 7;
+    const uint64_t v[8] = {h->counters[0], h->counters[1], h->counters[2], h->counters[3], h->ovf_waves,
+                           (uint64_t)h->retries, h->arena_ovf, h->uri_ovf_waves};
+    for (int k = 0; k < n && k < 8; ++k) out[k] = v[k];
+    return n < 8 ? n : 8;
 }
 
 int lp_histograms(lp_handle* h, uint64_t* out, int out_on_device) {

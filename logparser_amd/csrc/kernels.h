@@ -37,10 +37,12 @@ struct ParseLaunch {
     uint64_t mean_line;     // expected mean line length (sizes the LDS window)
     int n_elems, stack_depth;
     bool force_direct;      // every wave on the direct (HBM) path: tests / diagnostics only
+    bool uri;               // the program has URI stages (k_uri_lines after the parse kernel)
 };
 // parse every line (staged waves, then the waves whose window did not fit
-// LDS on the direct path), then meta->counters[0..4] += lines, ok, bad,
-// fallback, arena bytes written
+// LDS on the direct path), then the URI stages (k_uri_lines, and its direct
+// path), then meta->counters[0..4] += lines, ok, bad, fallback, arena bytes
+// written (C.ovf_list and C.uri_ovf_list: parse_waves(cap_lines) + 1 entries each)
 int launch_parse(const ParseLaunch& a, const DeviceArgs* d_args, const uint32_t* d_wave_counts, Meta* d_meta,
                  hipStream_t s);
 // sticky routing pass 1: C.fmt_match of every line

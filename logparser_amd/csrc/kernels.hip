@@ -383,21 +383,77 @@ struct WaveCounts {
     }
 };
 
-// Per-line work of one wave: phase 1, arena allocation, phase 2, the wave's
-// query pieces spread over its lanes; adds the lines' counts to WC.
+// Phase 1 of one wave's lines (match, tokens, time, first line) and their
+// rows; adds the lines' counts to WC.  The URI stages run in k_uri_lines.
 template <typename LN>
 __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, const Columns& C, const LN& L,
-                                           bool active, int64_t li, WaveStack stk, bool clean, int64_t wave,
-                                           WaveCounts& WC) {
+                                           bool active, int64_t li, WaveStack stk, bool clean, WaveCounts& WC) {
     LineOut o;
     o.status = ST_OK;
-    o.arena_need = 0;
     LP_PROF(1);
     if (active) phase1(P, elems, L, o, stk, C, li, clean, P.n_fmt > 1 ? (int)C.fmt_id[li] : 0);
     LP_PROF(9);
-    // wave-aggregated arena allocation from the wave's shard (every lane reaches this point)
-    const uint32_t need = (active && o.status == ST_OK) ? o.arena_need : 0u;
+    if (active) write_line(P, o, C, li);
+    if (active && P.n_uri == 0) C.arena_base[li] = 0;  // no URI kernel: an empty region for every line
+    WC.act += (uint32_t)__popcll(__ballot(active));
+    WC.ok += (uint32_t)__popcll(__ballot(active && o.status == ST_OK));
+    WC.bad += (uint32_t)__popcll(__ballot(active && o.status == ST_BAD));
+}
+
+// ------------------------------------------------------------------ URIs
+// The URI and query-string stages of a wave's 64 lines (HttpUriDissector,
+// QueryStringFieldDissector), after k_parse_lines wrote the lines' status and
+// spans.  Each lane's URI sources (request URI, referer, ...) are gathered
+// from the input into a compact LDS buffer (only the URI bytes: a few KiB per
+// wave, so many waves share a CU and hide the arena atomics and the query
+// passes' latencies), with their one-plane UEV mask; then phase 2 per lane,
+// a wave-aggregated arena allocation, and the query pieces spread over the
+// lanes.  A wave whose URI bytes do not fit runs on the direct (HBM) path.
+constexpr uint32_t URI_CAP = 8192;  // compact URI bytes per wave
+
+// Per lane: the line's URI sources.  sp[u] = a | b << 16 (line-relative, 0 =
+// none), cs[u] = the compact buffer offset of line byte a.
+struct UriLane {
+    bool ok;
+    int fmt;
+    uint64_t ls;  // line start in the input
+    RegArr<MAX_URI> sp, cs, usep;
+};
+
+__device__ __forceinline__ UriLane uri_lane(const Program& P, const Columns& C, int64_t li, bool active) {
+    UriLane U;
+    U.ok = active && C.status[li] == ST_OK;
+    U.fmt = U.ok && P.n_fmt > 1 ? (int)C.fmt_id[li] : 0;
+    U.ls = active ? C.line_off[li] : 0;
+    U.sp.fill(0);
+    U.cs.fill(0);
+    U.usep.fill(0);
+    if (U.ok)
+        for (int u = 0; u < P.n_uri; ++u) {
+            int a, b;
+            if (P.uri[u].fmt == U.fmt && uri_source_cols(P, C, li, u, a, b)) U.sp.set(u, mkspan(a, b));
+        }
+    return U;
+}
+
+// Phase 2, the arena allocation and the query pieces of one wave; lu(u) is
+// the lane's line view of URI stage u (valid for every lane, empty stages
+// included: the query pass reads other lanes' views).
+template <typename LU>
+__device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, UriLane& U, LU&& lu, bool active,
+                                         int64_t li, int64_t wave, WaveCounts& WC) {
     const int lane = threadIdx.x;
+    uint32_t need = 0;
+    if (U.ok)
+        for (int u = 0; u < P.n_uri; ++u) {
+            const uint32_t s = U.sp.get(u);
+            if (!s) continue;
+            uint32_t ev;
+            need += uri_need(P, u, lu(u), (int)(s & 0xFFFF), (int)(s >> 16), ev);
+            U.usep.set(u, ev);
+        }
+    need = (need + 15) & ~15u;
+    // wave-aggregated arena allocation from the wave's shard
     uint32_t x = need;
     for (int d = 1; d < 64; d <<= 1) {
         uint32_t y = __shfl_up(x, d);
@@ -413,12 +469,16 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
     const bool fits = wbase + total <= C.shard_cap;
     uint32_t written = 0;
     unsigned long long my_region = 0;
-    if (active) {
-        if (o.status == ST_OK && !fits && need) {
+    UriOut o;
+    o.qlist.fill(0);
+    o.qpend.fill(0);
+    o.status = U.ok ? ST_OK : ST_BAD;
+    if (U.ok) {
+        if (!fits && need) {
             // the shard is full: the batch is re-run with a larger arena
             o.status = ST_FALLBACK;
             atomicAdd(&C.meta->arena_ovf, 1ull);
-        } else if (o.status == ST_OK) {
+        } else {
             const unsigned long long mine = (unsigned long long)shard * C.shard_cap + wbase + x - need;
             my_region = mine;
             C.arena_base[li] = mine;  // also for an empty region: spills are region-relative
@@ -426,15 +486,13 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
             A.top = &C.meta->shard_top[16 * shard];  // spills come from the same shard
             A.base = wbase + x - need;
             A.limit = C.shard_cap;
-            phase2(P, L, o, A, C, li);
+            phase2(P, U.fmt, lu, U.sp, U.usep, o, A, C, li);
             if (A.ovf) {
                 o.status = ST_FALLBACK;
                 atomicAdd(&C.meta->arena_ovf, 1ull);
             }
             written = A.used - A.slack + A.extra;
         }
-        LP_PROF(20);
-        write_line(P, o, C, li);
     }
     LP_PROF(21);
     // QueryStringFieldDissector pieces of all lines of the wave, spread evenly
@@ -442,7 +500,7 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
     // would leave most lanes idle while the longest query finishes)
     if (P.n_query > 0) {
         __syncthreads();  // the table slots written in phase 2 are visible to every lane
-        const bool has = active && o.status == ST_OK && need != 0;
+        const bool has = U.ok && o.status == ST_OK && need != 0;
         const unsigned long long my_ab = has ? my_region : 0ull;
         for (int qs = 0; qs < P.n_query; ++qs) {
             const uint32_t np = has ? o.qpend.get(qs) : 0u;
@@ -453,6 +511,7 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
                 if (lane >= d) incl += y;
             }
             const uint32_t base = incl - np, tot = __shfl(incl, 63);
+            const auto L = lu(P.query[qs].uri);
             for (uint32_t g0 = 0; g0 < tot; g0 += PW) {
                 const uint32_t g = g0 + (uint32_t)lane;
                 int own = 0;  // last lane whose first pending piece index is <= g
@@ -493,22 +552,131 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
                 // a piece that did not fit: its line goes to FALLBACK (the
                 // batch is re-run with a larger arena, or, when the re-runs
                 // are spent, delivered with those lines FALLBACK)
-                for (uint64_t m = __ballot(piece_ovf); m; m &= m - 1) {
-                    const int o_lane = __shfl(own, (int)__builtin_ctzll(m));
-                    if (lane == o_lane && o.status == ST_OK) {
-                        o.status = ST_FALLBACK;
-                        C.status[li] = (uint8_t)ST_FALLBACK;
-                    }
-                }
+                for (uint64_t m = __ballot(piece_ovf); m; m &= m - 1)
+                    if (lane == __shfl(own, (int)__builtin_ctzll(m)) && o.status == ST_OK) o.status = ST_FALLBACK;
             }
         }
     }
     LP_PROF(22);
+    if (U.ok && o.status != ST_OK) C.status[li] = (uint8_t)o.status;
     for (int d = 32; d > 0; d >>= 1) written += __shfl_xor(written, d);
+    const int st = !active ? -1 : U.ok ? o.status : (int)C.status[li];
     WC.act += (uint32_t)__popcll(__ballot(active));
-    WC.ok += (uint32_t)__popcll(__ballot(active && o.status == ST_OK));
-    WC.bad += (uint32_t)__popcll(__ballot(active && o.status == ST_BAD));
+    WC.ok += (uint32_t)__popcll(__ballot(st == ST_OK));
+    WC.bad += (uint32_t)__popcll(__ballot(st == ST_BAD));
     WC.written += written;
+}
+
+// Copy one URI source [ls + a, ls + b) of the input into the compact buffer
+// at dst (4-byte aligned; the source's words whole, so the span starts at
+// dst + ((ls + a) & 3)), then one zero word.  Returns the bytes used.
+__device__ __forceinline__ uint32_t uri_copy(const uint8_t* __restrict__ buf, uint64_t nbytes, uint64_t s0, uint64_t s1,
+                                             uint32_t* dst) {
+    const uint32_t nw = (uint32_t)((s1 - s0) >> 2);
+    const uint64_t full = nbytes & ~3ull;  // whole words inside the buffer
+    constexpr int B = 8;
+    for (uint32_t w0 = 0; w0 < nw; w0 += B) {
+        uint32_t v[B];
+#pragma unroll
+        for (int k = 0; k < B; ++k) {
+            const uint64_t q = s0 + 4ull * (w0 + k);
+            v[k] = 0;
+            if (w0 + k < nw && q + 4 <= full) v[k] = *reinterpret_cast<const uint32_t*>(buf + q);
+            else if (w0 + k < nw)
+                for (int c = 0; c < 4; ++c) v[k] |= q + c < nbytes ? (uint32_t)buf[q + c] << (8 * c) : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < B; ++k)
+            if (w0 + k < nw) dst[w0 + k] = v[k];
+    }
+    dst[nw] = 0;
+    return 4 * nw + 4;
+}
+
+__global__ __launch_bounds__(PW) void k_uri_lines(const uint8_t* __restrict__ buf, uint64_t nbytes,
+                                                  const DeviceArgs* __restrict__ args) {
+    const Program& P = args->prog;
+    const Columns& C = args->cols;
+    const int64_t n_lines = (int64_t)C.meta->n_lines;
+    const int64_t wave = blockIdx.x;
+    if (wave * PW >= n_lines || C.meta->cap_ovf) return;
+    __shared__ __attribute__((aligned(16))) uint32_t cbuf[URI_CAP / 4 + 16];
+    __shared__ uint64_t plane[URI_CAP / 64 + 1];
+    const int lane = threadIdx.x;
+    const int64_t li = wave * PW + lane;
+    const bool active = li < n_lines;
+    UriLane U = uri_lane(P, C, li, active);
+    // compact layout: the lanes' sources one after the other
+    uint32_t size = 0;
+    for (int u = 0; u < P.n_uri; ++u) {
+        const uint32_t s = U.sp.get(u);
+        if (!s) continue;
+        const uint64_t s0 = (U.ls + (s & 0xFFFF)) & ~3ull, s1 = (U.ls + (s >> 16) + 3) & ~3ull;
+        size += (uint32_t)(s1 - s0) + 4;
+    }
+    uint32_t x = size;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+    }
+    const uint32_t total = __shfl(x, 63);
+    if (total > URI_CAP) {  // the direct (HBM) path
+        if (lane == 0) C.uri_ovf_list[atomicAdd(&C.meta->uri_ovf_waves, 1ull)] = (uint32_t)wave;
+        return;
+    }
+    uint32_t off = x - size;
+    for (int u = 0; u < P.n_uri; ++u) {
+        const uint32_t s = U.sp.get(u);
+        if (!s) continue;
+        const uint64_t a = U.ls + (s & 0xFFFF), s0 = a & ~3ull, s1 = (U.ls + (s >> 16) + 3) & ~3ull;
+        U.cs.set(u, off + (uint32_t)(a - s0));
+        off += uri_copy(buf, nbytes, s0, s1, cbuf + off / 4);
+    }
+    // zero the tail of the last 64-byte block (mask words never see stale bytes)
+    const uint32_t tend = (total + 63) & ~63u;
+    for (uint32_t k = total / 4 + lane; k < tend / 4; k += PW) cbuf[k] = 0;
+    __syncthreads();
+    // the UEV plane of the compact buffer, 16 bytes per lane and step
+    uint16_t* pl16 = reinterpret_cast<uint16_t*>(plane);
+    for (uint32_t k = lane; k < tend / 16; k += PW) {
+        const u32x4 v = *reinterpret_cast<const u32x4*>(cbuf + 4 * k);
+        uint32_t m0, m1;
+        bcls::classify16(v[0], v[1], v[2], v[3], m0, m1);
+        pl16[k] = (uint16_t)(m0 | m1);
+    }
+    __syncthreads();
+    typedef LineT<lds_bytes, lds_u64, 1> CL;
+    auto lu = [&](int u) {
+        const uint32_t s = U.sp.get(u);
+        // line byte q lives at cbuf + cs + (q - a): origin cs - a (mod 2^32)
+        return CL{(lds_bytes)cbuf, U.cs.get(u) - (s & 0xFFFFu), (int)(s >> 16), (lds_u64)plane};
+    };
+    WaveCounts WC;
+    uri_wave(P, C, U, lu, active, li, wave, WC);
+    WC.store(C, wave);
+}
+
+// The waves k_uri_lines queued (their URI bytes exceed the compact buffer),
+// on a persistent grid: the lines' bytes are read from HBM directly.
+__global__ __launch_bounds__(PW) void k_uri_overflow(const uint8_t* __restrict__ buf, uint64_t nbytes,
+                                                     const DeviceArgs* __restrict__ args) {
+    const Program& P = args->prog;
+    const Columns& C = args->cols;
+    const int64_t n_lines = (int64_t)C.meta->n_lines;
+    const uint64_t nq = C.meta->uri_ovf_waves;
+    for (uint64_t q = blockIdx.x; q < nq; q += gridDim.x) {
+        const int64_t wave = C.uri_ovf_list[q];
+        const WaveLines W = wave_lines(C, wave, n_lines, nbytes);
+        UriLane U = uri_lane(P, C, W.li, W.active);
+        const LP_G uint8_t* ls = (const LP_G uint8_t*)(buf) + W.s;
+        const uint32_t mis = (uint32_t)((uintptr_t)ls & 3);
+        const LineT<const LP_G uint8_t*> L{ls - mis, mis, crlf_len_hbm(buf, W)};
+        auto lu = [&](int) { return L; };
+        WaveCounts WC;
+        uri_wave(P, C, U, lu, W.active, W.li, wave, WC);
+        __syncthreads();
+        WC.store(C, wave);
+    }
 }
 
 // LDS: [elements (n_elems x 16 B)][DFS stack][byte window (win_cap, a multiple of 64)][mask planes (win_cap / 4)]
@@ -559,7 +727,7 @@ __global__ __launch_bounds__(PW, 2) void k_parse_lines(const uint8_t* __restrict
         const int n = mine ? crlf_len(W.n, W.n > 0 ? win[W.e - 1 - a] : 0u) : 0;
         const LineT<lds_bytes, lds_u64> L{(lds_bytes)win, mine ? (uint32_t)(W.s - a) : 0u, n,
                                           (lds_u64)reinterpret_cast<uint64_t*>(msk16)};
-        parse_wave(P, s_elems, C, L, mine, W.li, stk, clean, wave, WC);
+        parse_wave(P, s_elems, C, L, mine, W.li, stk, clean, WC);
         if (r + 1 < rounds) __syncthreads();  // this round's LDS reads are done before the next staging
     }
     WC.store(C, wave);
@@ -587,7 +755,7 @@ __global__ __launch_bounds__(PW) void k_parse_overflow(const uint8_t* __restrict
         const LP_G uint8_t* ls = (const LP_G uint8_t*)(buf) + W.s;
         const uint32_t mis = (uint32_t)((uintptr_t)ls & 3);
         const LineT<const LP_G uint8_t*> L{ls - mis, mis, crlf_len_hbm(buf, W)};
-        parse_wave(P, s_elems, C, L, W.active, W.li, stk, false, wave, WC);
+        parse_wave(P, s_elems, C, L, W.active, W.li, stk, false, WC);
         __syncthreads();
         WC.store(C, wave);
     }
@@ -893,6 +1061,10 @@ int launch_parse(const ParseLaunch& a, const DeviceArgs* d_args, const uint32_t*
     const size_t lds_ovf = 16 * (size_t)a.n_elems + 4 * (size_t)w.stk_words;
     hipLaunchKernelGGL(k_parse_overflow, dim3((unsigned)grid), dim3(PW), lds_ovf, s, a.buf, a.nbytes, d_args,
                        w.stk_words);
+    if (a.uri) {
+        hipLaunchKernelGGL(k_uri_lines, dim3((unsigned)waves), dim3(PW), 0, s, a.buf, a.nbytes, d_args);
+        hipLaunchKernelGGL(k_uri_overflow, dim3((unsigned)grid), dim3(PW), 0, s, a.buf, a.nbytes, d_args);
+    }
     int64_t rb = (waves + 255) / 256;
     if (rb > 1024) rb = 1024;
     hipLaunchKernelGGL(k_reduce_counts, dim3((unsigned)rb), dim3(256), 0, s, d_wave_counts, d_meta);

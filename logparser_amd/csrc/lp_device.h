@@ -121,12 +121,15 @@ __device__ LP_INLINE uint64_t mask_load(lds_u64 p) { return *p; }
 #endif
 struct NoMasks {};
 
-template <typename Ptr, typename MPtr = NoMasks>
+// NPL = 2: the two planes of the parse kernel's window (QUOTE, WS, UEV);
+// NPL = 1: one UEV plane only (the URI kernel's compact buffer: only the URI
+// scanners run on it, and they only ask for MC_UEV)
+template <typename Ptr, typename MPtr = NoMasks, int NPL = 2>
 struct LineT {
     Ptr b;
     uint32_t o;
     int n;
-    MPtr m = MPtr{};       // planes of the 64-byte block w of b: m[2 w], m[2 w + 1]
+    MPtr m = MPtr{};       // planes of the 64-byte block w of b: m[NPL w .. NPL w + NPL)
     static constexpr bool has_masks = !std::is_same<MPtr, NoMasks>::value;
     __host__ __device__ LP_INLINE uint32_t operator[](int i) const { return b[o + i]; }
     // aligned 32-bit word w of the base (little-endian: byte k at bits 8k..8k+7)
@@ -137,12 +140,17 @@ struct LineT {
         return 4 * w < o + (uint32_t)n ? load_word(b + 4 * w) : 0u;
     }
     __host__ __device__ LP_INLINE uint64_t mask(int c, uint32_t w) const {
-        const uint64_t p0 = mask_load(m + 2 * w), p1 = mask_load(m + 2 * w + 1);
-        return c == MC_QUOTE ? (p0 & ~p1) : c == MC_WS ? (p1 & ~p0) : (p0 | p1);
+        if constexpr (NPL == 1) {
+            return mask_load(m + w);  // c == MC_UEV (the only class of a one-plane line)
+        } else {
+            const uint64_t p0 = mask_load(m + 2 * w), p1 = mask_load(m + 2 * w + 1);
+            return c == MC_QUOTE ? (p0 & ~p1) : c == MC_WS ? (p1 & ~p0) : (p0 | p1);
+        }
     }
 };
 using Line = LineT<const uint8_t*>;
 using MLine = LineT<const uint8_t*, const uint64_t*>;
+using ULine = LineT<const uint8_t*, const uint64_t*, 1>;
 
 // ---- SWAR byte classes on a 32-bit word: bit 8k+7 set when byte k is in
 // the class (exact, no false positives from carries).
@@ -258,6 +266,18 @@ inline void build_masks(const uint8_t* buf, uint32_t n, uint64_t* masks) {
         const int sh = 16 * (k & 3);
         masks[2 * (k >> 2)] |= (uint64_t)a << sh;
         masks[2 * (k >> 2) + 1] |= (uint64_t)b << sh;
+    }
+}
+
+// The UEV plane alone (the URI kernel's compact buffer): 1 x n / 64 words.
+inline void build_uev_plane(const uint8_t* buf, uint32_t n, uint64_t* plane) {
+    for (uint32_t i = 0; i < n / 64; ++i) plane[i] = 0;
+    for (uint32_t k = 0; 16 * k < n; ++k) {
+        uint32_t w[4];
+        for (int j = 0; j < 4; ++j) __builtin_memcpy(&w[j], buf + 16 * k + 4 * j, 4);
+        uint32_t a, b;
+        bcls::classify16(w[0], w[1], w[2], w[3], a, b);
+        plane[k >> 2] |= (uint64_t)(a | b) << (16 * (k & 3));
     }
 }
 
@@ -1542,9 +1562,13 @@ struct LineOut {
     RegArr<MAX_TOK> caps;
     uint32_t tok_flags;
     RegArr<MAX_FL> fl_kind, fl_method, fl_uri, fl_proto;
-    RegArr<MAX_URI> usep;  // '&' + '?' count of each URI source (query table bound)
-    RegArr<MAX_QUERY> qlist, qpend;  // per query stage: the piece table (arena region offset), its length
-    uint32_t arena_need;
+};
+
+// A line's URI stages (the URI kernel): per query stage the piece table
+// (arena region offset) and its pending pieces.
+struct UriOut {
+    int status = ST_OK;
+    RegArr<MAX_QUERY> qlist, qpend;
 };
 
 // Last ' ' in [lo, hi], else -1 (lines with masks: the WS class, skipping TABs).
@@ -1586,6 +1610,33 @@ __host__ __device__ LP_INLINE bool uri_source(const Program& P, const LineOut& o
     a = sp & 0xFFFF;
     b = sp >> 16;
     return b > a;
+}
+
+// The same from the columns phase 1 wrote (the URI kernel runs after it).
+template <typename Cols>
+__host__ __device__ LP_INLINE bool uri_source_cols(const Program& P, const Cols& C, int64_t li, int u, int& a, int& b) {
+    const UriStage& U = P.uri[u];
+    uint32_t sp;
+    if (U.src_tok >= 0) {
+        if (C.tok_flags[li] & (1u << U.src_tok)) return false;  // "-" -> null
+        sp = C.tok_span[U.src_tok][li];
+    } else {
+        if (C.fl_kind[U.src_fl][li] == FL_NONE) return false;
+        sp = C.fl_uri[U.src_fl][li];
+    }
+    a = sp & 0xFFFF;
+    b = sp >> 16;
+    return b > a;
+}
+
+// Arena need of URI stage u on [a, b) (its query table): URIUtil-escaped
+// bytes and '&' / '?' separators are both URI event bytes, so their count
+// bounds the pieces; a URI without event bytes writes nothing to the arena.
+// Rewritten / decoded parts and query values are spilled when they occur.
+template <typename LN>
+__host__ __device__ LP_INLINE uint32_t uri_need(const Program& P, int u, const LN& L, int a, int b, uint32_t& usep) {
+    usep = count_uev(L, a, b);
+    return usep != 0 && P.uri[u].query_stage >= 0 ? 16 + 16 * (usep + 1) : 0u;  // alignment, one slot per piece
 }
 
 // ---- Set-Cookie headers (ResponseSetCookieListDissector.java:79-110 with
@@ -1720,7 +1771,7 @@ __host__ __device__ LP_INLINE bool setcookie_ok(const LN& L, int a, int b, bool 
     return true;
 }
 
-// Phase 1: guard, match, tokens, time, first line; arena need for phase 2.
+// Phase 1: guard, match, tokens, time, first line (the parse kernel).
 // clean: the caller already proved every byte of the line passes the
 // fast-path guard (the kernel checks the whole staged window at once).
 template <typename LN, typename EL, typename Stk, typename Cols>
@@ -1729,15 +1780,11 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
     o.status = ST_OK;
     o.fmt = fmt;
     o.tok_flags = 0;
-    o.arena_need = 0;
     o.caps.fill(0);
     o.fl_kind.fill(FL_NONE);
     o.fl_method.fill(0);
     o.fl_uri.fill(0);
     o.fl_proto.fill(0);
-    o.usep.fill(0);
-    o.qlist.fill(0);
-    o.qpend.fill(0);
     if (L.n > MAX_LINE || fmt >= P.n_fmt) { o.status = ST_FALLBACK; return; }  // too long / routing undecided
     // fast-path guard: TAB, printable ASCII and valid UTF-8 without the
     // chars java.util.regex '.' does not match (line_text_ok)
@@ -1876,26 +1923,6 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
         }
     }
     LP_PROF(7);
-    // arena need of the URI / query stages: their query tables
-    uint32_t need = 0;
-    for (int u = 0; u < P.n_uri; ++u) {
-        int a, b;
-        if (P.uri[u].fmt != fmt || !uri_source(P, o, u, a, b)) continue;
-        // URIUtil-escaped bytes and '&'/'?' separators are both URI event
-        // bytes: their count bounds both.  A URI without event bytes writes
-        // nothing to the arena (no query table, no decoded or rewritten part).
-        // (separators are URI event bytes: their count bounds the pieces).  A
-        // URI without event bytes writes nothing to the arena; rewritten or
-        // decoded parts and query values are spilled when they occur.
-        const uint32_t ev = count_uev(L, a, b);
-        const uint32_t sep = ev;
-        o.usep.set(u, sep);
-        if (ev == 0) continue;
-        const UriStage& U = P.uri[u];
-        if (U.query_stage >= 0) need += 16 + 16 * (sep + 1);  // alignment, one slot per piece
-    }
-    o.arena_need = (need + 15) & ~15u;
-    LP_PROF(8);
 }
 
 // ------------------------------------------------------------ URI stage
@@ -2311,7 +2338,7 @@ __host__ __device__ LP_INLINE uint32_t query_piece(const Program& P, const Query
 // HttpUriDissector fast path on the line bytes [a,b).  Returns status.
 template <typename LN, typename Cols>
 __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L, int a, int b, uint32_t usep, Arena& A,
-                                            Cols& C, int64_t li, LineOut& o) {
+                                            Cols& C, int64_t li, UriOut& o) {
     const UriStage& U = P.uri[u];
     const int qsi = U.want_query ? U.query_stage : -1;
     QueryTable T;
@@ -2564,28 +2591,34 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
 }
 
 // The pending query pieces of one line, one after the other (the test-only
-// CPU emulation; the kernel spreads them over the wave).
-template <typename LN>
-__host__ __device__ LP_INLINE void query_pieces_serial(const Program& P, const LN& L, const LineOut& o, Arena& A) {
+// CPU emulation; the kernel spreads them over the wave).  LQ(us): the line
+// view of URI stage us.
+template <typename LQ>
+__host__ __device__ LP_INLINE void query_pieces_serial(const Program& P, LQ&& lq, const UriOut& o, Arena& A) {
     for (int qs = 0; qs < P.n_query; ++qs) {
+        const auto L = lq(P.query[qs].uri);
         for (uint32_t k = 0; k < o.qpend.get(qs); ++k)
             A.extra += query_piece(P, P.query[qs], L, A, (LP_G uint64_t*)(A.p + o.qlist.get(qs) + 16 * k));
     }
 }
 
-// Phase 2: URI + query stages into the line's arena region.
-template <typename LN, typename Cols>
-__host__ __device__ LP_INLINE void phase2(const Program& P, const LN& L, LineOut& o, Arena& A, Cols& C, int64_t li) {
+// Phase 2 of one line (the URI kernel): the URI stages of its LogFormat.
+// lu(u): the line view of stage u's source (holding at least [a, b)), with
+// sp[u] = a | b << 16 (0: no source), usep[u] its event count.
+template <typename LU, typename Cols>
+__host__ __device__ LP_INLINE void phase2(const Program& P, int fmt, LU&& lu, const RegArr<MAX_URI>& sp,
+                                          const RegArr<MAX_URI>& usep, UriOut& o, Arena& A, Cols& C, int64_t li) {
     for (int u = 0; u < P.n_uri && o.status == ST_OK; ++u) {
-        if (P.uri[u].fmt != o.fmt) continue;  // another LogFormat's URI: nothing to write
-        int a, b;
-        if (!uri_source(P, o, u, a, b)) {
+        if (P.uri[u].fmt != fmt) continue;  // another LogFormat's URI: nothing to write
+        const uint32_t s = sp.get(u);
+        const int a = (int)(s & 0xFFFF), b = (int)(s >> 16);
+        if (b <= a) {
             C.u_flags[u][li] = 0;
             if (P.uri[u].query_stage >= 0) { C.q_count[P.uri[u].query_stage][li] = 0; C.q_params[P.uri[u].query_stage][li] = 0; }
             continue;
         }
         LP_PROF(10 + 2 * u);
-        int st = uri_stage(P, u, L, a, b, o.usep.get(u), A, C, li, o);
+        const int st = uri_stage(P, u, lu(u), a, b, usep.get(u), A, C, li, o);
         LP_PROF(11 + 2 * u);
         if (st != ST_OK) o.status = st;
     }

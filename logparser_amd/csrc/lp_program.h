@@ -269,7 +269,8 @@ struct Meta {
     unsigned long long ovf_waves;    // waves queued for the direct (HBM) parse kernel
     unsigned long long arena_ovf;    // lines whose arena allocation did not fit its shard (retry)
     unsigned long long fmt_state;    // routed LogFormat after the batch's last line
-    unsigned long long pad[3];
+    unsigned long long uri_ovf_waves;// waves whose URI bytes exceed the URI kernel's compact buffer (direct path)
+    unsigned long long pad[2];
     unsigned long long shard_top[ARENA_SHARDS * 16];  // bump pointer of shard s at [16 s] (own 128-B line)
 };
 
@@ -305,6 +306,7 @@ struct Columns {
     uint64_t shard_cap;                  // arena bytes per shard (ARENA_SHARDS shards)
     LP_G Meta* meta;
     LP_G uint32_t* ovf_list;             // waves for the direct parse kernel
+    LP_G uint32_t* uri_ovf_list;         // waves for the direct URI kernel
     LP_G uint32_t* wave_counts;          // [n_waves][WC_WORDS] lines ok bad fallback written (reduced after the launch)
     int64_t cap_lines;                   // lines the columns hold
 };

@@ -109,6 +109,7 @@ struct ResultView {
         const uint64_t b = arena_base[i];
         if (!shard_cap) return arena + b;
         const uint64_t s = b / shard_cap;
+        if (s >= (uint64_t)ARENA_SHARDS) return nullptr;  // no region (never for an OK line)
         return arena + shard_off[s] + (b - s * shard_cap);
     }
 };

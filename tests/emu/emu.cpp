@@ -45,6 +45,7 @@ int emu_describe(void* h, char* out, int cap) {
 }
 
 static int parse_impl(Emu* e, const char* line, int len, const uint8_t* base, uint32_t base_off, char* out, int cap);
+static int g_masks_fwd(int on);
 
 // returns line status (0 OK, 1 BAD, 2 FALLBACK), fills out with the record JSON when OK
 int emu_parse(void* h, const char* line, int len, char* out, int cap) {
@@ -65,9 +66,7 @@ int emu_parse_in(void* h, const char* buf, int64_t start, int len, char* out, in
     return parse_impl((Emu*)h, buf + start, len, (const uint8_t*)buf, (uint32_t)start, out, cap);
 }
 
-static int g_masks = 1;  // 1: lines carry byte-class masks (the kernel's LDS path), 0: SWAR scanners (HBM path)
-
-void emu_set_masks(int on) { g_masks = on; }
+void emu_set_masks(int on) { g_masks_fwd(on); }
 
 // the planner's token table (plan.cpp) as canonical JSON; returns its length
 int emu_token_table(int nginx, char* out, int cap) {
@@ -90,31 +89,89 @@ struct Store {
     std::vector<std::vector<int32_t>> u_port;
 };
 
+// The URI kernel's view of one URI source [a, b) of the line at base + off:
+// the source's whole 4-byte words copied into a compact buffer (the span
+// starts at the same offset mod 4), a zero word after them, zero-filled to
+// 64 bytes, and the buffer's one-plane UEV mask (g_masks), or the whole line
+// (the URI kernel's direct path, SWAR scanners).
+struct UriView {
+    std::vector<uint64_t> buf, plane;
+    uint32_t o = 0;
+    int n = 0;
+};
+static UriView uri_view(const uint8_t* base, uint32_t off, int a, int b) {
+    UriView V;
+    const uint32_t s0 = (off + (uint32_t)a) & ~3u, s1 = (off + (uint32_t)b + 3) & ~3u;
+    const uint32_t lead = 8;  // the span's words do not start the buffer (as in the kernel)
+    const uint32_t used = lead + (s1 - s0) + 4, tot = (used + 63) & ~63u;
+    V.buf.assign(tot / 8 + 1, 0);
+    memset(V.buf.data(), 0x5A, lead);
+    memcpy((uint8_t*)V.buf.data() + lead, base + s0, s1 - s0);
+    V.plane.assign(tot / 64 + 1, 0);
+    build_uev_plane((const uint8_t*)V.buf.data(), tot, V.plane.data());
+    V.o = lead + ((off + (uint32_t)a) & 3u) - (uint32_t)a;
+    V.n = b;
+    return V;
+}
+
+static int g_masks = 1;  // 1: lines carry byte-class masks (the kernels' LDS paths), 0: SWAR scanners (HBM paths)
+
 template <typename LN>
-static int run_line(const Program& P, const LN& L, LineOut& o, uint32_t* stk, Columns& C, Store& R, char* out,
-                    int cap, uint32_t& fmt_state) {
+static int run_line(const Program& P, const LN& L, const uint8_t* base, uint32_t off, LineOut& o, uint32_t* stk,
+                    Columns& C, Store& R, char* out, int cap, uint32_t& fmt_state) {
     if (P.n_fmt > 1) {  // sticky routing, one line at a time (the kernels do it as a scan)
         const uint32_t m = fmt_match_word(P, P.elems, L, stk, false);
         fmt_state = fmt_apply(fmt_table(m, P.n_fmt), fmt_state);
         R.fmt_id.assign(1, (uint8_t)fmt_state);
     }
     phase1(P, P.elems, L, o, stk, C, 0, false, P.n_fmt > 1 ? (int)fmt_state : 0);
-    if (o.status == ST_OK) {
-        // the region, then room for spills (a shard of its own: bump counter
-        // after the region, as the kernel's shard_top)
-        const uint64_t room = o.arena_need + 16ull * (uint64_t)L.n + 4096;
-        R.arena.assign(room + 64, 0);
-        unsigned long long top = o.arena_need;
-        Arena A{R.arena.data(), 0, o.arena_need};
-        A.top = &top;
-        A.base = 0;
-        A.limit = room;
-        phase2(P, L, o, A, C, 0);
-        if (o.status == ST_OK) query_pieces_serial(P, L, o, A);
-        if (A.used > o.arena_need) { snprintf(out, cap, "ARENA OVERFLOW %u > %u", A.used, o.arena_need); return 3; }
-        if (A.ovf) { snprintf(out, cap, "ARENA SPILL OVERFLOW"); return 3; }
-    }
     write_line(P, o, C, 0);
+    if (o.status != ST_OK || P.n_uri == 0) return 0;
+    // the URI kernel: its sources from the columns phase 1 wrote
+    RegArr<MAX_URI> sp, usep;
+    sp.fill(0);
+    usep.fill(0);
+    std::vector<UriView> views(MAX_URI);
+    uint32_t need = 0;
+    for (int u = 0; u < P.n_uri; ++u) {
+        int a, b;
+        if (P.uri[u].fmt != o.fmt || !uri_source_cols(P, C, 0, u, a, b)) continue;
+        sp.set(u, mkspan(a, b));
+        views[u] = uri_view(base, off, a, b);
+        uint32_t ev;
+        if (g_masks) need += uri_need(P, u, ULine{(const uint8_t*)views[u].buf.data(), views[u].o, views[u].n,
+                                                   views[u].plane.data()}, a, b, ev);
+        else need += uri_need(P, u, L, a, b, ev);
+        usep.set(u, ev);
+    }
+    need = (need + 15) & ~15u;
+    // the region, then room for spills (a shard of its own: bump counter
+    // after the region, as the kernel's shard_top)
+    const uint64_t room = need + 16ull * (uint64_t)L.n + 4096;
+    R.arena.assign(room + 64, 0);
+    unsigned long long top = need;
+    Arena A{R.arena.data(), 0, need};
+    A.top = &top;
+    A.base = 0;
+    A.limit = room;
+    UriOut uo;
+    uo.qlist.fill(0);
+    uo.qpend.fill(0);
+    if (g_masks) {
+        auto lu = [&](int u) {
+            return ULine{(const uint8_t*)views[u].buf.data(), views[u].o, views[u].n, views[u].plane.data()};
+        };
+        phase2(P, o.fmt, lu, sp, usep, uo, A, C, 0);
+        if (uo.status == ST_OK) query_pieces_serial(P, lu, uo, A);
+    } else {
+        auto lu = [&](int) { return L; };
+        phase2(P, o.fmt, lu, sp, usep, uo, A, C, 0);
+        if (uo.status == ST_OK) query_pieces_serial(P, lu, uo, A);
+    }
+    if (A.used > need) { snprintf(out, cap, "ARENA OVERFLOW %u > %u", A.used, need); return 3; }
+    if (A.ovf) { snprintf(out, cap, "ARENA SPILL OVERFLOW"); return 3; }
+    o.status = uo.status;
+    C.status[0] = (uint8_t)o.status;
     return 0;
 }
 
@@ -169,10 +226,10 @@ static int parse_impl(Emu* e, const char* line, int len, const uint8_t* base, ui
         std::vector<uint64_t> masks(MC_N * (wn / 64));
         build_masks((const uint8_t*)wbuf.data(), wn, masks.data());
         MLine L{(const uint8_t*)wbuf.data(), base_off - lo, len, masks.data()};
-        st = run_line(P, L, o, stk, C, R, out, cap, e->fmt_state);
+        st = run_line(P, L, base, base_off, o, stk, C, R, out, cap, e->fmt_state);
     } else {
         Line L{base, base_off, len};
-        st = run_line(P, L, o, stk, C, R, out, cap, e->fmt_state);
+        st = run_line(P, L, base, base_off, o, stk, C, R, out, cap, e->fmt_state);
     }
     if (st) return st;
     if (o.status != ST_OK) return o.status;
@@ -199,6 +256,8 @@ static int parse_impl(Emu* e, const char* line, int len, const uint8_t* base, ui
     memcpy(out, js.c_str(), js.size() + 1);
     return 0;
 }
+
+static int g_masks_fwd(int on) { return g_masks = on; }
 
 int emu_possible_paths(const char* fmt, int depth, char* out, int cap) {
     std::vector<std::string> paths;
