@@ -409,7 +409,7 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
 // passes' latencies), with their one-plane UEV mask; then phase 2 per lane,
 // a wave-aggregated arena allocation, and the query pieces spread over the
 // lanes.  A wave whose URI bytes do not fit runs on the direct (HBM) path.
-constexpr uint32_t URI_CAP = 8192;  // compact URI bytes per wave
+constexpr uint32_t URI_CAP = 12288;  // compact URI bytes per wave
 
 // Per lane: the line's URI sources.  sp[u] = a | b << 16 (line-relative, 0 =
 // none), cs[u] = the compact buffer offset of line byte a.
@@ -467,6 +467,7 @@ __device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, Uri
     if (lane == 63 && total) wbase = atomicAdd(&C.meta->shard_top[16 * shard], (unsigned long long)total + 12ull);
     wbase = (__shfl(wbase, 63) + 15) & ~15ull;
     const bool fits = wbase + total <= C.shard_cap;
+    LP_PROF(26);
     uint32_t written = 0;
     unsigned long long my_region = 0;
     UriOut o;
@@ -497,11 +498,15 @@ __device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, Uri
     LP_PROF(21);
     // QueryStringFieldDissector pieces of all lines of the wave, spread evenly
     // over the lanes (a line's pieces vary from 0 to dozens; one lane per line
-    // would leave most lanes idle while the longest query finishes)
+    // would leave most lanes idle while the longest query finishes), QR
+    // rounds of 64 pieces at a time: their table slots loaded together, then
+    // query_prep, ONE spill allocation for the batch, query_finish.
     if (P.n_query > 0) {
+        constexpr int QR = 4;
         __syncthreads();  // the table slots written in phase 2 are visible to every lane
         const bool has = U.ok && o.status == ST_OK && need != 0;
         const unsigned long long my_ab = has ? my_region : 0ull;
+        uint64_t piece_ovf = 0;  // lanes whose line lost a piece for want of arena
         for (int qs = 0; qs < P.n_query; ++qs) {
             const uint32_t np = has ? o.qpend.get(qs) : 0u;
             const uint32_t my_list = o.qlist.get(qs);
@@ -512,50 +517,71 @@ __device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, Uri
             }
             const uint32_t base = incl - np, tot = __shfl(incl, 63);
             const auto L = lu(P.query[qs].uri);
-            for (uint32_t g0 = 0; g0 < tot; g0 += PW) {
-                const uint32_t g = g0 + (uint32_t)lane;
-                int own = 0;  // last lane whose first pending piece index is <= g
-                for (int st = 32; st; st >>= 1)
-                    if (__shfl(base, own + st) <= g) own += st;
-                const uint32_t ob = __shfl(base, own), olist = __shfl(my_list, own);
-                const unsigned long long oab = __shfl(my_ab, own);
-                const auto OL = owner_line(L, own);
-                bool piece_ovf = false;
-                LP_G uint64_t* slot = reinterpret_cast<LP_G uint64_t*>(C.arena + oab + olist + 16 * (g - ob));
-                QPrep qp;
-                if (g < tot) qp = query_prep(OL, slot);
-                // the round's spilled bytes in one allocation from the wave's
+            for (uint32_t g0 = 0; g0 < tot; g0 += QR * PW) {
+                int own[QR];
+                uint64_t t0[QR];
+#pragma unroll
+                for (int k = 0; k < QR; ++k) {
+                    const uint32_t g = g0 + (uint32_t)(k * PW + lane);
+                    int ow = 0;  // last lane whose first pending piece index is <= g
+                    for (int st = 32; st; st >>= 1)
+                        if (__shfl(base, ow + st) <= g) ow += st;
+                    own[k] = ow;
+                    const uint32_t ob = __shfl(base, ow), olist = __shfl(my_list, ow);
+                    const unsigned long long oab = __shfl(my_ab, ow);
+                    t0[k] = 0;
+                    if (g < tot) t0[k] = *reinterpret_cast<const LP_G uint64_t*>(C.arena + oab + olist + 16 * (g - ob));
+                }
+                QPrep qp[QR];
+                uint32_t mine = 0;
+#pragma unroll
+                for (int k = 0; k < QR; ++k) {
+                    const uint32_t g = g0 + (uint32_t)(k * PW + lane);
+                    const auto OL = owner_line(L, own[k]);  // every lane takes part in the shuffles
+                    if (g < tot) qp[k] = query_prep(OL, t0[k]);
+                    mine += qp[k].need;
+                }
+                // the batch's spilled bytes in one allocation from the wave's
                 // shard (every owner is a line of this wave)
-                uint32_t x = qp.need;
+                uint32_t x = mine;
                 for (int d = 1; d < 64; d <<= 1) {
                     const uint32_t y = __shfl_up(x, d);
                     if (lane >= d) x += y;
                 }
                 const uint32_t rtot = __shfl(x, 63);
                 unsigned long long rbase = 0;
-                if (lane == 63 && rtot)
-                    rbase = atomicAdd(&C.meta->shard_top[16 * shard], (unsigned long long)rtot);
-                rbase = __shfl(rbase, 63);
-                if (g < tot) {
-                    const unsigned long long rel = oab - (unsigned long long)shard * C.shard_cap;  // region in the shard
-                    const unsigned long long at = rbase + x - qp.need;                          // piece in the shard
-                    if (qp.need && (at + qp.need > C.shard_cap || at - rel + qp.need > 0x7FFFFFFFull)) {
-                        slot[0] = REF_SKIP;
-                        slot[1] = 0;
-                        piece_ovf = true;
-                        atomicAdd(&C.meta->arena_ovf, 1ull);  // the batch is re-run with a larger arena
-                    } else {
-                        Arena A{C.arena + oab, (uint32_t)(at - rel), (uint32_t)(at - rel + qp.need)};
-                        written += query_finish(P, P.query[qs], OL, A, C.arena + oab, slot, qp);
+                if (lane == 63 && rtot) rbase = atomicAdd(&C.meta->shard_top[16 * shard], (unsigned long long)rtot);
+                unsigned long long at = __shfl(rbase, 63) + x - mine;  // this lane's first piece in the shard
+#pragma unroll
+                for (int k = 0; k < QR; ++k) {
+                    const uint32_t g = g0 + (uint32_t)(k * PW + lane);
+                    const int ow = own[k];
+                    const uint32_t ob = __shfl(base, ow), olist = __shfl(my_list, ow);
+                    const unsigned long long oab = __shfl(my_ab, ow);
+                    const auto OL = owner_line(L, ow);
+                    bool povf = false;
+                    if (g < tot) {
+                        LP_G uint64_t* slot = reinterpret_cast<LP_G uint64_t*>(C.arena + oab + olist + 16 * (g - ob));
+                        const unsigned long long rel = oab - (unsigned long long)shard * C.shard_cap;  // region in the shard
+                        if (qp[k].need && (at + qp[k].need > C.shard_cap || at - rel + qp[k].need > 0x7FFFFFFFull)) {
+                            slot[0] = REF_SKIP;
+                            slot[1] = 0;
+                            povf = true;
+                            atomicAdd(&C.meta->arena_ovf, 1ull);  // the batch is re-run with a larger arena
+                        } else {
+                            Arena A{C.arena + oab, (uint32_t)(at - rel), (uint32_t)(at - rel + qp[k].need)};
+                            written += query_finish(P, P.query[qs], OL, A, C.arena + oab, slot, qp[k]);
+                        }
+                        at += qp[k].need;
                     }
+                    // a piece that did not fit: its line goes to FALLBACK (the
+                    // batch is re-run with a larger arena, or, when the re-runs
+                    // are spent, delivered with those lines FALLBACK)
+                    for (uint64_t m = __ballot(povf); m; m &= m - 1) piece_ovf |= 1ull << __shfl(ow, (int)__builtin_ctzll(m));
                 }
-                // a piece that did not fit: its line goes to FALLBACK (the
-                // batch is re-run with a larger arena, or, when the re-runs
-                // are spent, delivered with those lines FALLBACK)
-                for (uint64_t m = __ballot(piece_ovf); m; m &= m - 1)
-                    if (lane == __shfl(own, (int)__builtin_ctzll(m)) && o.status == ST_OK) o.status = ST_FALLBACK;
             }
         }
+        if (((piece_ovf >> lane) & 1) && o.status == ST_OK) o.status = ST_FALLBACK;
     }
     LP_PROF(22);
     if (U.ok && o.status != ST_OK) C.status[li] = (uint8_t)o.status;
@@ -567,30 +593,13 @@ __device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, Uri
     WC.written += written;
 }
 
-// Copy one URI source [ls + a, ls + b) of the input into the compact buffer
-// at dst (4-byte aligned; the source's words whole, so the span starts at
-// dst + ((ls + a) & 3)), then one zero word.  Returns the bytes used.
-__device__ __forceinline__ uint32_t uri_copy(const uint8_t* __restrict__ buf, uint64_t nbytes, uint64_t s0, uint64_t s1,
-                                             uint32_t* dst) {
-    const uint32_t nw = (uint32_t)((s1 - s0) >> 2);
-    const uint64_t full = nbytes & ~3ull;  // whole words inside the buffer
-    constexpr int B = 8;
-    for (uint32_t w0 = 0; w0 < nw; w0 += B) {
-        uint32_t v[B];
-#pragma unroll
-        for (int k = 0; k < B; ++k) {
-            const uint64_t q = s0 + 4ull * (w0 + k);
-            v[k] = 0;
-            if (w0 + k < nw && q + 4 <= full) v[k] = *reinterpret_cast<const uint32_t*>(buf + q);
-            else if (w0 + k < nw)
-                for (int c = 0; c < 4; ++c) v[k] |= q + c < nbytes ? (uint32_t)buf[q + c] << (8 * c) : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < B; ++k)
-            if (w0 + k < nw) dst[w0 + k] = v[k];
-    }
-    dst[nw] = 0;
-    return 4 * nw + 4;
+// The 16 input bytes at p (16-byte aligned): one load inside the buffer,
+// bytes past nbytes read as 0.
+__device__ __forceinline__ u32x4 load16(const uint8_t* __restrict__ buf, uint64_t nbytes, uint64_t p) {
+    if (p + 16 <= nbytes) return *reinterpret_cast<const u32x4*>(buf + p);
+    uint32_t w[4] = {0, 0, 0, 0};
+    for (int c = 0; c < 16; ++c) w[c >> 2] |= p + c < nbytes ? (uint32_t)buf[p + c] << (8 * (c & 3)) : 0u;
+    return u32x4{w[0], w[1], w[2], w[3]};
 }
 
 __global__ __launch_bounds__(PW) void k_uri_lines(const uint8_t* __restrict__ buf, uint64_t nbytes,
@@ -602,49 +611,74 @@ __global__ __launch_bounds__(PW) void k_uri_lines(const uint8_t* __restrict__ bu
     if (wave * PW >= n_lines || C.meta->cap_ovf) return;
     __shared__ __attribute__((aligned(16))) uint32_t cbuf[URI_CAP / 4 + 16];
     __shared__ uint64_t plane[URI_CAP / 64 + 1];
+    __shared__ uint8_t blk_own[URI_CAP / 16];  // the lane (line) of each gathered block
     const int lane = threadIdx.x;
     const int64_t li = wave * PW + lane;
     const bool active = li < n_lines;
+    LP_PROF(23);
     UriLane U = uri_lane(P, C, li, active);
-    // compact layout: the lanes' sources one after the other
-    uint32_t size = 0;
+    // one region per line: the 16-byte input blocks holding all its URI
+    // sources (request URI, referer, ...: close together in a line), in
+    // line order; a block keeps its alignment, so the wave gathers whole
+    // aligned 16-byte blocks, consecutive lanes taking consecutive blocks
+    uint64_t lo = ~0ull, hi = 0;
     for (int u = 0; u < P.n_uri; ++u) {
         const uint32_t s = U.sp.get(u);
         if (!s) continue;
-        const uint64_t s0 = (U.ls + (s & 0xFFFF)) & ~3ull, s1 = (U.ls + (s >> 16) + 3) & ~3ull;
-        size += (uint32_t)(s1 - s0) + 4;
+        lo = min(lo, U.ls + (s & 0xFFFF));
+        hi = max(hi, U.ls + (s >> 16));
     }
-    uint32_t x = size;
+    const uint64_t r0 = hi ? lo & ~15ull : 0;
+    const uint32_t nblk = hi ? (uint32_t)((((hi + 15) & ~15ull) - r0) >> 4) : 0u;
+    uint32_t x = nblk;
     for (int d = 1; d < 64; d <<= 1) {
         const uint32_t y = __shfl_up(x, d);
         if (lane >= d) x += y;
     }
-    const uint32_t total = __shfl(x, 63);
-    if (total > URI_CAP) {  // the direct (HBM) path
+    const uint32_t tot = __shfl(x, 63), cb = x - nblk;  // blocks of the wave, this line's first block
+    if (16 * tot + 16 > URI_CAP) {  // the direct (HBM) path
         if (lane == 0) C.uri_ovf_list[atomicAdd(&C.meta->uri_ovf_waves, 1ull)] = (uint32_t)wave;
         return;
     }
-    uint32_t off = x - size;
     for (int u = 0; u < P.n_uri; ++u) {
         const uint32_t s = U.sp.get(u);
-        if (!s) continue;
-        const uint64_t a = U.ls + (s & 0xFFFF), s0 = a & ~3ull, s1 = (U.ls + (s >> 16) + 3) & ~3ull;
-        U.cs.set(u, off + (uint32_t)(a - s0));
-        off += uri_copy(buf, nbytes, s0, s1, cbuf + off / 4);
+        if (s) U.cs.set(u, 16 * cb + (uint32_t)(U.ls + (s & 0xFFFF) - r0));
     }
-    // zero the tail of the last 64-byte block (mask words never see stale bytes)
-    const uint32_t tend = (total + 63) & ~63u;
-    for (uint32_t k = total / 4 + lane; k < tend / 4; k += PW) cbuf[k] = 0;
+    for (uint32_t k = 0; k < nblk; ++k) blk_own[cb + k] = (uint8_t)lane;
     __syncthreads();
-    // the UEV plane of the compact buffer, 16 bytes per lane and step
+    // gather: block g of the wave is block g - cb[own] of line own's region;
+    // every round's load in flight before the first store
+    constexpr int GR = 12;  // rounds per batch (URI_CAP / 1024)
     uint16_t* pl16 = reinterpret_cast<uint16_t*>(plane);
-    for (uint32_t k = lane; k < tend / 16; k += PW) {
-        const u32x4 v = *reinterpret_cast<const u32x4*>(cbuf + 4 * k);
-        uint32_t m0, m1;
-        bcls::classify16(v[0], v[1], v[2], v[3], m0, m1);
-        pl16[k] = (uint16_t)(m0 | m1);
+    for (uint32_t g0 = 0; g0 < tot; g0 += GR * PW) {
+        u32x4 v[GR];
+#pragma unroll
+        for (int k = 0; k < GR; ++k) {
+            const uint32_t g = g0 + (uint32_t)(k * PW + lane);
+            const int own = g < tot ? (int)blk_own[g] : 0;
+            const uint64_t src = (uint64_t)__shfl((unsigned long long)r0, own) + 16ull * (g - __shfl(cb, own));
+            v[k] = u32x4{0, 0, 0, 0};
+            if (g < tot) v[k] = load16(buf, nbytes, src);
+        }
+#pragma unroll
+        for (int k = 0; k < GR; ++k) {
+            const uint32_t g = g0 + (uint32_t)(k * PW + lane);
+            if (g >= tot) continue;
+            *reinterpret_cast<u32x4*>(cbuf + 4 * g) = v[k];
+            uint32_t m0, m1;
+            bcls::classify16(v[k][0], v[k][1], v[k][2], v[k][3], m0, m1);
+            pl16[g] = (uint16_t)(m0 | m1);
+        }
+    }
+    LP_PROF(24);
+    // one zero block after the last (the scanners' look-ahead word) and the
+    // rest of the last 64-byte mask block
+    for (uint32_t g = tot + lane; g < ((tot + 1 + 3) & ~3u); g += PW) {
+        *reinterpret_cast<u32x4*>(cbuf + 4 * g) = u32x4{0, 0, 0, 0};
+        pl16[g] = 0;
     }
     __syncthreads();
+    LP_PROF(25);
     typedef LineT<lds_bytes, lds_u64, 1> CL;
     auto lu = [&](int u) {
         const uint32_t s = U.sp.get(u);

@@ -2179,16 +2179,13 @@ __host__ __device__ LP_INLINE uint64_t url_decode_value(const LN& L, int vs, int
 
 // ---- QueryStringFieldDissector (QueryStringFieldDissector.java:56-108).
 // The URI stage's event pass splits the rawQuery at '&' / '?' into a table of
-// one (name ref, value ref) slot per non-empty piece, noting for each piece
-// its last '%' / '+' (a value that may need decoding).  A plain piece of a stage that
-// wants every name is final at once (two line refs).  Any other piece is
-// left "pending": slot[0] = start | end << 16 | (eq + 1) << 32 | flags << 48,
-// slot[1] = offset of 3 bytes of the line's arena region per piece byte, and
-// its slot offset is appended to the line's pending list; query_piece
-// completes it.  The kernel runs query_piece on the pending pieces of all 64
-// lines of a wave spread evenly over its lanes.
+// one 16-byte slot per non-empty piece, noting for each piece its last '%' /
+// '+' (a value that may need decoding): slot[0] = start | end << 16 |
+// (lp + 1) << 48.  The kernel completes the pieces of all 64 lines of a wave
+// spread evenly over its lanes: query_prep (the first '=', what the
+// completion spills), one spill allocation for a batch of pieces, then
+// query_finish, which overwrites the slot with the (name, value) refs.
 constexpr uint64_t REF_SKIP = ~0ull;  // slot of a piece whose name was not requested
-constexpr uint32_t QP_RW = 1, QP_PV = 2;
 
 struct QueryTable {
     uint32_t tab = 0, reg = 0, count = 0, maxp = 0;
@@ -2196,11 +2193,9 @@ struct QueryTable {
     int lp = -1;  // last '%' / '+' of the piece (a value that needs resilientUrlDecode)
     bool on = false, set = false;  // enumerating now / table laid out
     // piece [s, e) ends: its slot gets the raw piece (bounds, the last '%' /
-    // '+', the offset of 3 x its length reserved for rewritten bytes);
-    // query_piece completes every slot afterwards, spread over the wave
+    // '+'); one 16-byte store per slot (tables are 16-byte aligned: regions are)
     __host__ __device__ LP_INLINE void emit(LP_G uint8_t* region, int e) {
         if (e > s) {
-            // one 16-byte store per slot (tables are 16-byte aligned: regions are)
             const uint64_t t0 = (uint64_t)(uint32_t)s | ((uint64_t)(uint32_t)e << 16) | ((uint64_t)(uint32_t)(lp + 1) << 48);
 #if defined(__HIP_DEVICE_COMPILE__)
             typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
@@ -2244,20 +2239,20 @@ __host__ __device__ LP_INLINE int piece_eq_rw(const LN& L, int s, int e, bool& r
 }
 
 // A query piece's split (QueryStringFieldDissector.java:75-104): bounds from
-// its table slot, the first '=', and the arena bytes its completion may write
-// (rewritten name: 3 per name byte; decoded value: at most its length).
+// its table slot word t0, the first '=', and the arena bytes its completion
+// may write (rewritten name: 3 per name byte; decoded value: at most its
+// length).
 struct QPrep {
     int s = 0, e = 0, eq = -1;
     bool rw = false, pv = false;
     uint32_t need = 0;
 };
 template <typename LN>
-__host__ __device__ LP_INLINE QPrep query_prep(const LN& L, const LP_G uint64_t* slot) {
+__host__ __device__ LP_INLINE QPrep query_prep(const LN& L, uint64_t t0) {
     QPrep q;
-    const uint64_t a0 = slot[0];
-    q.s = (int)(a0 & 0xFFFFu);
-    q.e = (int)((a0 >> 16) & 0xFFFFu);
-    const int lp = (int)((a0 >> 48) & 0xFFFFu) - 1;  // the piece's last '%' / '+'
+    q.s = (int)(t0 & 0xFFFFu);
+    q.e = (int)((t0 >> 16) & 0xFFFFu);
+    const int lp = (int)((t0 >> 48) & 0xFFFFu) - 1;  // the piece's last '%' / '+'
     q.eq = piece_eq_rw(L, q.s, q.e, q.rw);
     q.pv = q.eq >= 0 && lp > q.eq;  // '%' / '+' in the value
     const int ne = q.eq >= 0 ? q.eq : q.e;
@@ -2325,7 +2320,7 @@ __host__ __device__ LP_INLINE uint32_t query_finish(const Program& P, const Quer
 template <typename LN>
 __host__ __device__ LP_INLINE uint32_t query_piece(const Program& P, const QueryStage& Q, const LN& L, Arena& R,
                                                    LP_G uint64_t* slot) {
-    const QPrep qp = query_prep(L, slot);
+    const QPrep qp = query_prep(L, slot[0]);
     Arena A;
     if (!spill(R, qp.need, A)) {
         slot[0] = REF_SKIP;

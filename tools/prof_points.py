@@ -29,8 +29,9 @@ st = p.run(t.data_ptr(), len(data))
 L.lp_profile_read(buf.ctypes.data, W * K)
 T = buf.reshape(W, K).astype(np.int64)
 names = {0: "start", 1: "staged", 2: "phase1 entry", 3: "guard", 4: "match", 5: "tok flags", 6: "time",
-         7: "first line", 8: "arena need", 9: "phase1 exit", 10: "uri0 in", 11: "uri0 out", 12: "uri1 in",
-         13: "uri1 out", 20: "phase2 exit", 21: "rows written", 22: "query pieces"}
+         7: "first line", 9: "phase1 exit", 10: "uri0 in", 11: "uri0 out", 12: "uri1 in",
+         13: "uri1 out", 21: "phase2 exit", 22: "query pieces", 23: "uri kernel start", 24: "uri copied",
+         25: "uri plane", 26: "uri arena"}
 for u in range(2):
     for j, nm in enumerate(["pass1", "authority", "path", "query", "frag"]):
         names[30 + 8 * u + j] = "u%d %s done" % (u, nm)
@@ -38,29 +39,25 @@ for u in range(2):
     names[50 + 4 * u] = "u%d walk start" % u
     names[51 + 4 * u] = "u%d fast walk" % u
     names[52 + 4 * u] = "u%d gen walk" % u
-order = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 50, 51, 52, 30, 31, 32, 33, 34, 11, 12, 54, 55, 56, 38, 39, 40, 41, 42, 13,
-         20, 21, 22]
+# the parse kernel, then the URI kernel (k_uri_lines): separate orders
+orders = [[0, 1, 2, 3, 4, 5, 6, 7, 9],
+          [23, 24, 25, 26, 10, 50, 51, 52, 30, 31, 32, 33, 34, 11, 12, 54, 55, 56, 38, 39, 40, 41, 42, 13, 21, 22]]
 print("parse ms %.3f  waves profiled %d" % (st["ms_parse"], int((T[:, 0] != 0).sum())))
-tot = 0.0
-acc = {}
-for w in range(W):
-    row = T[w]
-    prev = None
-    for k in order:
-        if row[k] == 0:
-            continue
-        if prev is not None:
-            key = (prev, k)
-            d = acc.setdefault(key, [0.0, 0])
-            d[0] += row[k] - row[prev]
-            d[1] += 1
-        prev = k
-for (a, b), (s_, c) in sorted(acc.items(), key=lambda kv: order.index(kv[0][0]) * 100 + order.index(kv[0][1])):
-    print("  %-18s -> %-18s %9.0f cycles/wave  (%d waves)" % (names[a], names[b], s_ / c, c))
-    tot += s_ / max(1, W)
-acc_names = {57: "qp owner search", 58: "qp slot read + '=' find", 59: "qp name scan", 60: "qp spill",
-             61: "qp want", 62: "qp value decode", 63: "qp slot write + tail"}
-for k, nm in acc_names.items():
-    v = T[:, k]
-    print("  [sum] %-28s %9.0f cycles/wave" % (nm, v[T[:, 0] != 0].mean()))
-print("  total %.0f cycles per wave (start -> last point)" % np.mean([r[r != 0].max() - r[0] for r in T if r[0]]))
+for order in orders:
+    acc = {}
+    for w in range(W):
+        row = T[w]
+        prev = None
+        for k in order:
+            if row[k] == 0:
+                continue
+            if prev is not None:
+                d = acc.setdefault((prev, k), [0.0, 0])
+                d[0] += row[k] - row[prev]
+                d[1] += 1
+            prev = k
+    for (a, b), (s_, c) in sorted(acc.items(), key=lambda kv: order.index(kv[0][0]) * 100 + order.index(kv[0][1])):
+        print("  %-18s -> %-18s %9.0f cycles/wave  (%d waves)" % (names[a], names[b], s_ / c, c))
+    rows = [r for r in T if r[order[0]] and r[order[-1]]]
+    if rows:
+        print("  kernel total %.0f cycles per wave" % np.mean([r[order[-1]] - r[order[0]] for r in rows]))
