@@ -565,18 +565,7 @@ struct RegArr {
     // set with a wave-uniform index: one indexed register write on the device
     // (the select chain of set() rewrites every element)
     __host__ __device__ LP_INLINE void set_u(int k, uint32_t x) {
-#if defined(__HIP_DEVICE_COMPILE__)
         if ((unsigned)k < (unsigned)N) v[k] = x;
-        return;
-#endif
-        switch (k) {
-#define LP_RA_CASE(J) case J: if constexpr (J < N) v[J] = x; break;
-            LP_RA_CASE(0) LP_RA_CASE(1) LP_RA_CASE(2) LP_RA_CASE(3) LP_RA_CASE(4) LP_RA_CASE(5) LP_RA_CASE(6)
-            LP_RA_CASE(7) LP_RA_CASE(8) LP_RA_CASE(9) LP_RA_CASE(10) LP_RA_CASE(11) LP_RA_CASE(12) LP_RA_CASE(13)
-            LP_RA_CASE(14) LP_RA_CASE(15)
-#undef LP_RA_CASE
-        default: break;
-        }
     }
     __host__ __device__ LP_INLINE void set(int k, uint32_t x) { set_(k, x, std::make_index_sequence<N>{}); }
     __host__ __device__ LP_INLINE void fill(uint32_t x) { set_all(x, std::make_index_sequence<N>{}); }
@@ -1469,89 +1458,304 @@ __host__ __device__ LP_INLINE bool parse_iso_time(const LN& L, int a, int64_t& e
     return true;
 }
 
-// StrfTimeStampDissector with a fixed-width converted formatter
-// (StrfTimeToDateTimeFormatter: appendValue(DAY_OF_MONTH, 2), appendText(
-// MONTH_OF_YEAR, SHORT) in the default locale en_US, appendValue(YEAR, 4),
-// CLOCK_HOUR_OF_DAY (%H) / HOUR_OF_DAY (%T), MINUTE, SECOND, MILLI_ /
-// MICRO_OF_SECOND, appendOffset("+HHMM", "+0000"); parseCaseInsensitive,
-// SMART resolver, zone UTC without %z) on the value [a, b).
-// Returns ST_OK, ST_BAD (DateTimeParseException) or ST_FALLBACK (year 0).
+// WeekFields (java.time.temporal.WeekFields.ComputedDayOfField) of the date
+// with day number `days` in year y: first day of week sow (1 Monday .. 7
+// Sunday), minimal days mind in week 1.
+__host__ __device__ LP_INLINE int wf_start_offset(int day, int ldow, int mind) {
+    const int week_start = ((day - ldow) % 7 + 7) % 7;
+    return week_start + 1 > mind ? 7 - week_start : -week_start;
+}
+__host__ __device__ LP_INLINE int wf_week(int offset, int day) { return (7 + offset + (day - 1)) / 7; }
+__host__ __device__ LP_INLINE int wf_week_of_year(int32_t y, int32_t days, int sow, int mind) {
+    const int doy = (int)(days - days_from_civil(y, 1, 1)) + 1;
+    const int ldow = ((iso_dow(days) - sow) % 7 + 7) % 7 + 1;
+    return wf_week(wf_start_offset(doy, ldow, mind), doy);
+}
+__host__ __device__ LP_INLINE int32_t wf_week_based_year(int32_t y, int32_t days, int sow, int mind) {
+    const int doy = (int)(days - days_from_civil(y, 1, 1)) + 1;
+    const int ldow = ((iso_dow(days) - sow) % 7 + 7) % 7 + 1;
+    const int offset = wf_start_offset(doy, ldow, mind);
+    const int week = wf_week(offset, doy);
+    if (week == 0) return y - 1;
+    if (week >= wf_week(offset, (leap(y) ? 366 : 365) + mind)) return y + 1;
+    return y;
+}
+
+// Text of a strftime text element (default locale en_US, JDK 8 data),
+// lower-case, packed little-endian: months / days of week short and full,
+// "am" / "pm" (AMPM_OF_DAY SHORT is "AM" / "PM"; parsing is case-insensitive).
+__host__ __device__ LP_INLINE int strf_text(int table, int k, uint64_t& lo, uint32_t& hi) {
+    const char* const mon[12] = {"january", "february", "march", "april", "may", "june", "july", "august",
+                                 "september", "october", "november", "december"};
+    const char* const dow[7] = {"monday", "tuesday", "wednesday", "thursday", "friday", "saturday", "sunday"};
+    const char* const ap[2] = {"am", "pm"};
+    const char* t = table == ST_MON_SHORT || table == ST_MON_FULL ? mon[k] : table == ST_DOW_SHORT || table == ST_DOW_FULL ? dow[k] : ap[k];
+    int n = 0;
+    while (t[n]) ++n;
+    if (table == ST_MON_SHORT || table == ST_DOW_SHORT) n = 3;  // "Jan" .. "Dec", "Mon" .. "Sun"
+    lo = 0;
+    hi = 0;
+    for (int q = 0; q < n && q < 8; ++q) lo |= (uint64_t)(uint8_t)t[q] << (8 * q);
+    if (n > 8) hi = (uint8_t)t[8];
+    return n;
+}
+
+// StrfTimeStampDissector (hp/dissectors/StrfTimeStampDissector.java:44-70)
+// on the value [a, b): DateTimeFormatter.parse(text, ZonedDateTime::from)
+// with the elements of T (parseCaseInsensitive, strict), then JDK 8's
+// java.time.format.Parsed.resolve under ResolverStyle.SMART: instant seconds
+// (at the parsed zone, else the formatter's UTC, else the offset) -> date +
+// second-of-day; IsoChronology.resolveDate (YEAR + MONTH + DAY with the
+// month-length clamp, else YEAR + DAY_OF_YEAR); resolveTimeFields
+// (CLOCK_HOUR_OF_DAY 0..24, CLOCK_HOUR_OF_AMPM 0..12 with AMPM_OF_DAY,
+// second-of-day, each with updateCheckConflict); WeekFields.ISO.dayOfWeek()
+// replacing DAY_OF_WEEK; resolveTimeLenient (defaulted minute / second /
+// nano, 24:00 end of day); crossCheck of every field left against the date
+// and time.  A field parsed twice must agree (DateTimeParseContext).
+// Returns ST_OK, ST_BAD (DateTimeParseException) or ST_FALLBACK (outside the
+// restated subset: non-ASCII text, zone names other than UTC / GMT, signs,
+// 19-digit numbers, week-based dates, years outside 1..9999).  The oracle's
+// strf_parse restates the same steps independently.
 template <typename LN>
 __host__ __device__ LP_INLINE int parse_strf_time(const TimeStage& T, const LN& L, int a, int b, int64_t& epoch_ms,
                                                   uint64_t& local, uint64_t& utc, uint32_t& nanos) {
-    if (b - a != (int)T.width) return ST_BAD;  // fixed-width fields: text left over or missing
-    int day = 0, month = 0, year = 0, hod = -1, clockh = -1, mi = 0, ss = 0, off = 0;
-    uint32_t nos = 0;
-    auto low = [](uint32_t c) { return (c - 'A') < 26u ? (c | 32u) : c; };
+    RegArr<SF_NFIELDS> fv;  // field values (SF_INSTANT: low word; high word in inst_hi)
+    fv.fill(0);
+    uint32_t has = 0, inst_hi = 0;
+    bool zone_utc = false;
+    int pos = a;
+    auto low = [](uint32_t c) { return c | 0x20u; };  // safe fold against lower-case ASCII letters
     for (int k = 0; k < T.n_ops; ++k) {
-        const int p = a + T.off[k];
         const uint32_t op = T.op[k];
-        if (op == SF_LIT) {
-            if (low(L[p]) != low(T.ch[k])) return ST_BAD;
+        const int kind = (int)(op & 0xFF), field = (int)((op >> 8) & 0xFF), width = (int)((op >> 16) & 0xFF);
+        const uint32_t arg = op >> 24;
+        uint32_t v = 0;
+        switch (kind) {
+        case SE_LIT: {  // CharLiteralPrinterParser, case-insensitive
+            if (pos >= b) return ST_BAD;
+            const uint32_t c = L[pos];
+            const bool eq = c == arg || ((arg | 0x20u) - 'a' < 26u && low(c) == (arg | 0x20u));
+            if (!eq) return c >= 0x80 ? ST_FALLBACK : ST_BAD;
+            ++pos;
             continue;
         }
-        if (op == SF_MONTXT) {
-            const uint32_t m3 = (low(L[p]) << 16) | (low(L[p + 1]) << 8) | low(L[p + 2]);
-            const uint32_t names[12] = {0x6a616e, 0x666562, 0x6d6172, 0x617072, 0x6d6179, 0x6a756e,
-                                        0x6a756c, 0x617567, 0x736570, 0x6f6374, 0x6e6f76, 0x646563};
-            month = 0;
-            for (int q = 0; q < 12; ++q) month = names[q] == m3 ? q + 1 : month;
-            if (!month) return ST_BAD;
+        case SE_NUM: case SE_RED2: {  // fixed width, NOT_NEGATIVE; reduced: base 2000
+            if (pos + width > b) return ST_BAD;
+            for (int q = 0; q < width; ++q) {
+                const uint32_t d = L[pos + q] - '0';
+                if (d > 9) return ST_BAD;
+                v = v * 10 + d;
+            }
+            pos += width;
+            if (kind == SE_RED2) v += 2000;
+            break;
+        }
+        case SE_NUMV: {  // 1..19 digits (INSTANT_SECONDS, week-of-year)
+            if (pos < b && (L[pos] == '+' || L[pos] == '-')) return ST_FALLBACK;
+            uint64_t w = 0;
+            int q = pos;
+            while (q < b && q - pos < 19 && L[q] - '0' < 10u) { w = w * 10 + (L[q] - '0'); ++q; }
+            if (q == pos) return ST_BAD;
+            if (q - pos >= 19 || w > 0xFFFFFFFFFFull) return ST_FALLBACK;  // beyond the restated range
+            pos = q;
+            if (field == SF_INSTANT) {
+                const uint32_t hi = (uint32_t)(w >> 32);
+                if (((has >> SF_INSTANT) & 1u) && (fv.get(SF_INSTANT) != (uint32_t)w || inst_hi != hi)) return ST_BAD;
+                inst_hi = hi;
+            }
+            v = (uint32_t)w;
+            if (field != SF_INSTANT && w > 0x7FFFFFFFull) return ST_FALLBACK;
+            break;
+        }
+        case SE_PAD2: {  // PadPrinterParserDecorator(2, ' '): spaces, then digits to the end
+            if (pos + 2 > b) return ST_BAD;
+            int q = pos;
+            while (q < pos + 2 && L[q] == ' ') ++q;
+            if (q < pos + 2 && (L[q] == '+' || L[q] == '-')) return ST_FALLBACK;
+            if (q == pos + 2) return ST_BAD;
+            for (int r = q; r < pos + 2; ++r) {
+                const uint32_t d = L[r] - '0';
+                if (d > 9) return ST_BAD;
+                v = v * 10 + d;
+            }
+            pos += 2;
+            break;
+        }
+        case SE_TEXT: {  // TextPrinterParser: the longest entry that matches
+            uint64_t tlo = 0;
+            uint32_t thi = 0;
+            for (int q = 0; q < 9 && pos + q < b; ++q) {
+                const uint32_t c = L[pos + q];
+                // java's case-insensitive charEquals folds a few non-ASCII
+                // letters to ASCII ones (U+017F, U+0131, U+0130, U+212A)
+                if (c >= 0x80) return ST_FALLBACK;
+                if (q < 8) tlo |= (uint64_t)low(c) << (8 * q);
+                else thi = low(c);
+            }
+            const int nt = arg == ST_MON_SHORT || arg == ST_MON_FULL ? 12 : arg == ST_AMPM_UP || arg == ST_AMPM_LOW ? 2 : 7;
+            int best = -1, blen = 0;
+            for (int t = 0; t < nt; ++t) {
+                uint64_t elo;
+                uint32_t ehi;
+                const int n = strf_text(arg, t, elo, ehi);
+                if (pos + n > b || n <= blen) continue;
+                const uint64_t m = n >= 8 ? ~0ull : (1ull << (8 * n)) - 1;
+                if (((tlo ^ elo) & m) == 0 && (n <= 8 || (thi & 0xFFu) == ehi)) { best = t; blen = n; }
+            }
+            if (best < 0) return ST_BAD;
+            pos += blen;
+            v = arg == ST_AMPM_UP || arg == ST_AMPM_LOW ? (uint32_t)best : (uint32_t)best + 1;
+            break;
+        }
+        case SE_OFF: {  // appendOffset("+HHMM", "+0000")
+            if (pos + 5 > b) return ST_BAD;
+            const uint32_t sg = L[pos];
+            int off = 0;
+            if (!(sg == '+' && L[pos + 1] == '0' && L[pos + 2] == '0' && L[pos + 3] == '0' && L[pos + 4] == '0')) {
+                if (sg != '+' && sg != '-') return ST_BAD;
+                for (int q = 1; q <= 4; ++q) if (L[pos + q] - '0' > 9u) return ST_BAD;
+                const int oh = (int)(L[pos + 1] - '0') * 10 + (int)(L[pos + 2] - '0');
+                const int om = (int)(L[pos + 3] - '0') * 10 + (int)(L[pos + 4] - '0');
+                if (oh > 59 || om > 59) return ST_BAD;
+                off = (sg == '-' ? -1 : 1) * (oh * 3600 + om * 60);
+            }
+            pos += 5;
+            v = (uint32_t)off;
+            break;
+        }
+        case SE_ZONE: {  // appendZoneText(SHORT): "UTC" / "GMT" not followed by an offset
+            if (pos + 3 > b) return ST_FALLBACK;
+            const uint32_t c0 = low(L[pos]), c1 = low(L[pos + 1]), c2 = low(L[pos + 2]);
+            const bool ok = (c0 == 'u' && c1 == 't' && c2 == 'c') || (c0 == 'g' && c1 == 'm' && c2 == 't');
+            if (!ok || (pos + 3 < b && (L[pos + 3] == '+' || L[pos + 3] == '-'))) return ST_FALLBACK;
+            pos += 3;
+            zone_utc = true;
             continue;
         }
-        if (op == SF_OFF) {
-            const uint32_t sg = L[p];
-            if (sg == '+' && L[p + 1] == '0' && L[p + 2] == '0' && L[p + 3] == '0' && L[p + 4] == '0') { off = 0; continue; }
-            if (sg != '+' && sg != '-') return ST_BAD;
-            for (int q = 1; q <= 4; ++q) if (!is_digit(L[p + q])) return ST_BAD;
-            const int oh = (int)(L[p + 1] - '0') * 10 + (int)(L[p + 2] - '0'), om = (int)(L[p + 3] - '0') * 10 + (int)(L[p + 4] - '0');
-            if (oh > 59 || om > 59) return ST_BAD;
-            off = (sg == '-' ? -1 : 1) * (oh * 3600 + om * 60);
-            continue;
+        default: return ST_FALLBACK;
         }
-        const int w = op == SF_YEAR ? 4 : op == SF_MSEC ? 3 : op == SF_USEC ? 6 : 2;
-        int v = 0;
-        for (int q = 0; q < w; ++q) {
-            const uint32_t c = L[p + q];
-            if (!is_digit(c)) return ST_BAD;
-            v = v * 10 + (int)(c - '0');
-        }
-        switch (op) {
-        case SF_DAY: day = v; break;
-        case SF_MON: month = v; break;
-        case SF_YEAR: year = v; break;
-        case SF_CLOCKH: clockh = v; break;
-        case SF_HOD: hod = v; break;
-        case SF_MIN: mi = v; break;
-        case SF_SEC: ss = v; break;
-        case SF_MSEC: nos = (uint32_t)v * 1000000u; break;
-        case SF_USEC: nos = (uint32_t)v * 1000u; break;
-        }
+        // DateTimeParseContext.setParsedField: a field parsed twice must agree
+        if (((has >> field) & 1u) && fv.get(field) != v) return ST_BAD;
+        has |= 1u << field;
+        fv.set_u(field, v);
     }
-    if (off > 64800 || off < -64800) return ST_BAD;                     // ZoneOffset.ofTotalSeconds
-    if (clockh >= 0) {                                                  // SMART: 0..24, 24 -> 0
-        if (clockh > 24) return ST_BAD;
-        hod = clockh == 24 ? 0 : clockh;
+    if (pos != b) return ST_BAD;  // text left over
+    auto H = [&](int f) { return ((has >> f) & 1u) != 0; };
+    auto V = [&](int f) { return (int32_t)fv.get(f); };
+    // ---- Parsed.resolve (JDK 8), SMART
+    bool have_date = false, have_time = false, plus_day = false;
+    int32_t dy = 0;
+    int dm = 0, dd = 0;
+    int64_t sod = -1;
+    if (H(SF_INSTANT)) {  // resolveInstantFields
+        int64_t off;
+        if (zone_utc || !T.zone) off = 0;
+        else if (H(SF_OFFSET)) off = V(SF_OFFSET);
+        else return ST_FALLBACK;
+        if (off > 64800 || off < -64800) return ST_BAD;
+        const int64_t inst = (int64_t)(((uint64_t)inst_hi << 32) | fv.get(SF_INSTANT));
+        if (inst > 253402300799ll) return ST_FALLBACK;  // past year 9999
+        const int64_t t = inst + off;
+        const int64_t days = t >= 0 ? t / 86400 : -((-t + 86399) / 86400);
+        civil_from_days((int32_t)days, dy, dm, dd);
+        sod = t - days * 86400;
+        have_date = true;
     }
-    if (month < 1 || month > 12 || day < 1 || day > 31) return ST_BAD;  // resolveDate
-    if (year == 0) return ST_FALLBACK;                                  // year 0: outside the 32-bit calendar
-    const int ml = month_len(year, month);
-    if (day > ml) day = ml;
-    if (mi > 59) return ST_BAD;                                         // resolveTime
-    int32_t y = year;
-    int m = month, d = day;
-    int32_t days = days_from_civil(y, m, d);
-    if (hod == 24 && mi == 0 && ss == 0 && nos == 0) {                  // SMART end of day
-        hod = 0;
-        ++days;
-        civil_from_days(days, y, m, d);
-    } else if (hod > 23 || ss > 59) {
+    if (H(SF_YEAR) && ((H(SF_MONTH) && H(SF_DOM)) || H(SF_DOY))) {  // IsoChronology.resolveDate
+        const int32_t y = V(SF_YEAR);
+        int32_t ry;
+        int rm, rd;
+        if (H(SF_MONTH) && H(SF_DOM)) {  // resolveYMD
+            const int mo = V(SF_MONTH);
+            int dom = V(SF_DOM);
+            if (mo < 1 || mo > 12 || dom < 1 || dom > 31) return ST_BAD;
+            if (y < 1 || y > 9999) return ST_FALLBACK;
+            const int ml = month_len(y, mo);
+            if (dom > ml) dom = ml;
+            ry = y; rm = mo; rd = dom;
+            has &= ~((1u << SF_MONTH) | (1u << SF_DOM));
+        } else {  // resolveYD
+            const int doy = V(SF_DOY);
+            if (doy < 1 || doy > 366) return ST_BAD;
+            if (y < 1 || y > 9999) return ST_FALLBACK;
+            if (doy == 366 && !leap(y)) return ST_BAD;
+            civil_from_days(days_from_civil(y, 1, 1) + doy - 1, ry, rm, rd);
+            has &= ~(1u << SF_DOY);
+        }
+        has &= ~(1u << SF_YEAR);
+        if (have_date && (ry != dy || rm != dm || rd != dd)) return ST_BAD;  // updateCheckConflict(date)
+        dy = ry; dm = rm; dd = rd;
+        have_date = true;
+    }
+    if (H(SF_WOY) && H(SF_YEAR)) return ST_FALLBACK;  // WeekFields.resolveWoY builds the date
+    int32_t hod = H(SF_HOD) ? V(SF_HOD) : -1, hap = -1;
+    if (H(SF_CHOD)) {  // SMART: 0..24, 24 -> 0
+        const int32_t ch = V(SF_CHOD);
+        if (ch != 0 && (ch < 1 || ch > 24)) return ST_BAD;
+        const int32_t h = ch == 24 ? 0 : ch;
+        if (hod >= 0 && hod != h) return ST_BAD;
+        hod = h;
+    }
+    if (H(SF_CHAP)) {  // SMART: 0..12, 12 -> 0
+        const int32_t ch = V(SF_CHAP);
+        if (ch != 0 && (ch < 1 || ch > 12)) return ST_BAD;
+        hap = ch == 12 ? 0 : ch;
+    }
+    bool ampm_used = false;
+    if (H(SF_AMPM) && hap >= 0) {
+        const int32_t h = V(SF_AMPM) * 12 + hap;
+        if (hod >= 0 && hod != h) return ST_BAD;
+        hod = h;
+        ampm_used = true;
+    }
+    int32_t moh = H(SF_MIN) ? V(SF_MIN) : -1, som = H(SF_SEC) ? V(SF_SEC) : -1;
+    if (sod >= 0) {  // SECOND_OF_DAY -> HOUR_OF_DAY, MINUTE_OF_HOUR, SECOND_OF_MINUTE
+        const int32_t h = (int32_t)(sod / 3600), mi = (int32_t)(sod / 60 % 60), se = (int32_t)(sod % 60);
+        if ((hod >= 0 && hod != h) || (moh >= 0 && moh != mi) || (som >= 0 && som != se)) return ST_BAD;
+        hod = h; moh = mi; som = se;
+    }
+    int32_t dow = H(SF_DOW) ? V(SF_DOW) : 0;
+    if (H(SF_ISODOW)) {  // WeekFields.ISO.dayOfWeek() replaces DAY_OF_WEEK
+        if (V(SF_ISODOW) < 1 || V(SF_ISODOW) > 7) return ST_BAD;
+        dow = V(SF_ISODOW);
+    }
+    if (H(SF_MILLI) && H(SF_MICRO)) return ST_FALLBACK;
+    int32_t nos = H(SF_MILLI) ? V(SF_MILLI) * 1000000 : H(SF_MICRO) ? V(SF_MICRO) * 1000 : -1;
+    int th = 0, tmi = 0, tse = 0;
+    if (hod >= 0 && !((moh < 0 && (som >= 0 || nos >= 0)) || (moh >= 0 && som < 0 && nos >= 0))) {
+        const int32_t m2 = moh < 0 ? 0 : moh, s2 = som < 0 ? 0 : som, n2 = nos < 0 ? 0 : nos;
+        if (m2 > 59) return ST_BAD;  // resolveTime: minute, then 24:00 end of day, then hour / second
+        if (hod == 24 && m2 == 0 && s2 == 0 && n2 == 0) { th = 0; plus_day = true; }
+        else if (hod > 23 || s2 > 59) return ST_BAD;
+        else th = hod;
+        tmi = m2;
+        tse = s2;
+        nos = n2;
+        have_time = true;
+    }
+    if (!have_date || !have_time) return ST_BAD;  // LocalDateTime.from
+    int32_t days = days_from_civil(dy, dm, dd);
+    if (plus_day) civil_from_days(++days, dy, dm, dd);
+    // crossCheck
+    if (dow && dow != iso_dow(days)) return ST_BAD;
+    if (H(SF_DOY) && V(SF_DOY) != (int32_t)(days - days_from_civil(dy, 1, 1)) + 1) return ST_BAD;
+    if (H(SF_WOY) && V(SF_WOY) != wf_week_of_year(dy, days, 1, 4)) return ST_BAD;
+    if (H(SF_WBY) && V(SF_WBY) != wf_week_based_year(dy, days, 7, 1)) return ST_BAD;
+    if (H(SF_AMPM) && !ampm_used && V(SF_AMPM) != th / 12) return ST_BAD;
+    if (hap >= 0 && !ampm_used && hap != th % 12) return ST_BAD;
+    if ((H(SF_MONTH) && V(SF_MONTH) != dm) || (H(SF_DOM) && V(SF_DOM) != dd) || (H(SF_YEAR) && V(SF_YEAR) != dy))
         return ST_BAD;
+    int off = 0;  // ZonedDateTime.from: the offset (ZoneOffset.ofTotalSeconds)
+    if (!zone_utc && T.zone) {
+        if (!H(SF_OFFSET)) return ST_BAD;
+        off = V(SF_OFFSET);
+        if (off > 64800 || off < -64800) return ST_BAD;
     }
+    if (dy < 1 || dy > 9999) return ST_FALLBACK;
     int64_t es;
-    time_fields(y, m, d, hod, mi, ss, off, days, es, local, utc);
-    epoch_ms = es * 1000 + (int64_t)(nos / 1000000u);
-    nanos = nos;
+    time_fields(dy, dm, dd, th, tmi, tse, off, days, es, local, utc);
+    epoch_ms = es * 1000 + (int64_t)(nos / 1000000);
+    nanos = (uint32_t)nos;
     return ST_OK;
 }
 

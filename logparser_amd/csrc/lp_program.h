@@ -112,27 +112,36 @@ __host__ __device__ inline ElemV load_elem(P p) {
     return e;
 }
 
-// TimeStampDissector on a TIME.STAMP token (dd/MMM/yyyy:HH:mm:ss ZZ,
-// hp/dissectors/TimeStampDissector.java:46, 404-564).
 // TimeStampDissector on a TIME.STAMP token (TK_APACHE: the fixed
 // "dd/MMM/yyyy:HH:mm:ss ZZ" of hp/dissectors/TimeStampDissector.java:46), or
 // StrfTimeStampDissector on a %{...}t token (TK_STRF,
-// hp/dissectors/StrfTimeStampDissector.java:44-70) whose strftime pattern
-// converts to fixed-width DateTimeFormatter fields
-// (hp/dissectors/StrfTimeToDateTimeFormatter.java): the value must be exactly
-// `width` bytes, op k reads its field at byte off[k].
+// hp/dissectors/StrfTimeStampDissector.java:44-70): the DateTimeFormatter
+// StrfTimeToDateTimeFormatter builds (:140-432) as a list of parser elements
+// op[k] = SE_* | field << 8 | width << 16 | arg << 24, parsed left to right
+// (lp_device.h parse_strf_time).
 enum : uint8_t { TK_APACHE = 0, TK_STRF = 1, TK_ISO = 2 };  // TK_ISO: TIME.ISO8601 ($time_iso8601)
-enum : uint8_t { SF_LIT, SF_DAY, SF_MON, SF_MONTXT, SF_YEAR, SF_CLOCKH, SF_HOD, SF_MIN, SF_SEC, SF_MSEC, SF_USEC, SF_OFF };
-constexpr int MAX_SF_OPS = 32;
+// java.time fields the conversions set (ChronoField unless noted)
+enum : uint8_t {
+    SF_YEAR, SF_MONTH, SF_DOM, SF_DOW, SF_ISODOW /* WeekFields.ISO.dayOfWeek() */, SF_DOY,
+    SF_WBY /* WeekFields.of(en_US).weekBasedYear() */, SF_WOY /* WeekFields.ISO.weekOfYear() */, SF_HOD,
+    SF_CHOD /* CLOCK_HOUR_OF_DAY */, SF_CHAP /* CLOCK_HOUR_OF_AMPM */, SF_AMPM, SF_MIN, SF_SEC, SF_MILLI, SF_MICRO,
+    SF_OFFSET, SF_INSTANT, SF_NFIELDS
+};
+// parser elements: literal char (arg), fixed-width number, 1..19-digit
+// number, padNext(2, ' ') + 1..19-digit number, 2-digit reduced value (base
+// 2000), text table (arg: ST_*), offset "+HHMM", zone text
+enum : uint8_t { SE_LIT, SE_NUM, SE_NUMV, SE_PAD2, SE_RED2, SE_TEXT, SE_OFF, SE_ZONE };
+enum : uint8_t { ST_MON_SHORT, ST_MON_FULL, ST_DOW_SHORT, ST_DOW_FULL, ST_AMPM_UP, ST_AMPM_LOW };
+constexpr int MAX_SF_OPS = 128;
 // Stage structs hold 32-bit fields only: the kernels read them with scalar
 // (dword) loads.
 struct TimeStage {
     int32_t tok;
     int32_t fmt;     // the LogFormat whose token this is
     int32_t kind;    // TK_*
-    int32_t width;   // TK_STRF: exact byte length of the value
+    int32_t zone;    // TK_STRF: the pattern has %z or %Z (else the formatter's zone is UTC)
     int32_t n_ops;
-    uint32_t op[MAX_SF_OPS], off[MAX_SF_OPS], ch[MAX_SF_OPS];  // ch: SF_LIT byte
+    uint32_t op[MAX_SF_OPS];
 };
 
 // HttpFirstLineDissector on an HTTP.FIRSTLINE token

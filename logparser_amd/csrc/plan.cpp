@@ -176,35 +176,32 @@ struct TokenTable {
     }
 };
 
-// StrfTimeToDateTimeFormatter (hp/dissectors/StrfTimeToDateTimeFormatter.java,
-// grammar StrfTime.g4) for the conversions that become fixed-width
-// DateTimeFormatter fields: %d %m %b %h %Y %H %M %S, %T (HOUR_OF_DAY:%M:%S,
-// :360-368), %F (%Y-%m-%d), %z, [%]msec_frac, [%]usec_frac, %% %t %n and
-// literal text, E/O modifiers ignored.  The pattern must give day, month,
-// year, hour, minute and second exactly once; anything else stays off the
-// device.
+// StrfTimeToDateTimeFormatter (hp/dissectors/StrfTimeToDateTimeFormatter.java
+// :140-432, grammar StrfTime.g4:40-89): the DateTimeFormatterBuilder
+// elements of each conversion (E / O modifiers ignored).  %c %C %U %w %x %X
+// %+ throw UnsupportedStrfField in the reference (no parser can be built),
+// and a variable-width number directly followed by another number switches
+// JDK's adjacent value parsing on: those stay off the device.
 static bool strf_compile(const std::string& f, TimeStage& T) {
-    int seen[16] = {0};
-    auto add = [&](int op, int w, int ch) {
-        if (T.n_ops >= MAX_SF_OPS || T.width + w > 255) return false;
-        T.op[T.n_ops] = (uint8_t)op;
-        T.off[T.n_ops] = (uint8_t)T.width;
-        T.ch[T.n_ops] = (uint8_t)ch;
-        ++T.n_ops;
-        T.width = (uint8_t)(T.width + w);
+    T.n_ops = 0;
+    T.zone = 0;
+    auto add = [&](int kind, int field, int width, int arg) {
+        if (T.n_ops >= MAX_SF_OPS) return false;
+        T.op[T.n_ops++] = (uint32_t)kind | ((uint32_t)field << 8) | ((uint32_t)width << 16) | ((uint32_t)(uint8_t)arg << 24);
         return true;
     };
-    auto fld = [&](int op, int w) { return seen[op]++ == 0 && add(op, w, 0); };
+    auto num = [&](int field, int w) { return add(SE_NUM, field, w, 0); };
+    auto lit = [&](int c) { return add(SE_LIT, 0, 1, c); };
     const size_t n = f.size();
     for (size_t i = 0; i < n;) {
         const size_t j = i + (f[i] == '%');
         if (n - j >= 9 && (f.compare(j, 9, "msec_frac") == 0 || f.compare(j, 9, "usec_frac") == 0)) {
-            if (!(f[j] == 'm' ? fld(SF_MSEC, 3) : fld(SF_USEC, 6))) return false;
+            if (!(f[j] == 'm' ? num(SF_MILLI, 3) : num(SF_MICRO, 6))) return false;
             i = j + 9;
             continue;
         }
         if (f[i] != '%') {
-            if (!add(SF_LIT, 1, (uint8_t)f[i])) return false;
+            if (!lit((uint8_t)f[i])) return false;
             ++i;
             continue;
         }
@@ -212,7 +209,7 @@ static bool strf_compile(const std::string& f, TimeStage& T) {
         char c = f[i + 1];
         size_t k = i + 1;
         if (c == '%' || c == 't' || c == 'n') {
-            if (!add(SF_LIT, 1, c == '%' ? '%' : c == 't' ? '\t' : '\n')) return false;
+            if (!lit(c == '%' ? '%' : c == 't' ? '\t' : '\n')) return false;
             i += 2;
             continue;
         }
@@ -223,24 +220,49 @@ static bool strf_compile(const std::string& f, TimeStage& T) {
         }
         bool ok;
         switch (c) {
-        case 'd': ok = fld(SF_DAY, 2); break;
-        case 'm': ok = fld(SF_MON, 2); break;
-        case 'b': case 'h': ok = fld(SF_MONTXT, 3); break;
-        case 'Y': ok = fld(SF_YEAR, 4); break;
-        case 'H': ok = fld(SF_CLOCKH, 2); break;
-        case 'M': ok = fld(SF_MIN, 2); break;
-        case 'S': ok = fld(SF_SEC, 2); break;
-        case 'T': ok = fld(SF_HOD, 2) && add(SF_LIT, 1, ':') && fld(SF_MIN, 2) && add(SF_LIT, 1, ':') && fld(SF_SEC, 2); break;
-        case 'F': ok = fld(SF_YEAR, 4) && add(SF_LIT, 1, '-') && fld(SF_MON, 2) && add(SF_LIT, 1, '-') && fld(SF_DAY, 2); break;
-        case 'z': ok = fld(SF_OFF, 5); break;
+        case 'a': ok = add(SE_TEXT, SF_DOW, 0, ST_DOW_SHORT); break;
+        case 'A': ok = add(SE_TEXT, SF_DOW, 0, ST_DOW_FULL); break;
+        case 'b': case 'h': ok = add(SE_TEXT, SF_MONTH, 0, ST_MON_SHORT); break;
+        case 'B': ok = add(SE_TEXT, SF_MONTH, 0, ST_MON_FULL); break;
+        case 'd': ok = num(SF_DOM, 2); break;
+        case 'D': ok = num(SF_MONTH, 2) && lit('/') && num(SF_DOM, 2) && lit('/') && add(SE_RED2, SF_YEAR, 2, 0); break;
+        case 'e': ok = add(SE_PAD2, SF_DOM, 2, 0); break;
+        case 'F': ok = num(SF_YEAR, 4) && lit('-') && num(SF_MONTH, 2) && lit('-') && num(SF_DOM, 2); break;
+        case 'G': ok = num(SF_WBY, 4); break;
+        case 'g': ok = add(SE_RED2, SF_WBY, 2, 0); break;
+        case 'H': ok = num(SF_CHOD, 2); break;
+        case 'I': ok = num(SF_CHAP, 2); break;
+        case 'j': ok = num(SF_DOY, 3); break;
+        case 'k': ok = add(SE_PAD2, SF_CHOD, 2, 0); break;
+        case 'l': ok = add(SE_PAD2, SF_CHAP, 2, 0); break;
+        case 'm': ok = num(SF_MONTH, 2); break;
+        case 'M': ok = num(SF_MIN, 2); break;
+        case 'p': ok = add(SE_TEXT, SF_AMPM, 0, ST_AMPM_UP); break;
+        case 'P': ok = add(SE_TEXT, SF_AMPM, 0, ST_AMPM_LOW); break;
+        case 'r': ok = num(SF_CHAP, 2) && lit(':') && num(SF_MIN, 2) && lit(':') && num(SF_SEC, 2) && lit(' ') &&
+                       add(SE_TEXT, SF_AMPM, 0, ST_AMPM_UP); break;
+        case 'R': ok = num(SF_HOD, 2) && lit(':') && num(SF_MIN, 2); break;
+        case 's': ok = add(SE_NUMV, SF_INSTANT, 19, 0); break;
+        case 'S': ok = num(SF_SEC, 2); break;
+        case 'T': ok = num(SF_HOD, 2) && lit(':') && num(SF_MIN, 2) && lit(':') && num(SF_SEC, 2); break;
+        case 'u': ok = num(SF_ISODOW, 1); break;
+        case 'V': ok = add(SE_NUMV, SF_WOY, 19, 0); break;
+        case 'W': ok = num(SF_WOY, 2); break;
+        case 'y': ok = add(SE_RED2, SF_YEAR, 2, 0); break;
+        case 'Y': ok = num(SF_YEAR, 4); break;
+        case 'z': ok = add(SE_OFF, SF_OFFSET, 5, 0); T.zone = 1; break;
+        case 'Z': ok = add(SE_ZONE, 0, 0, 0); T.zone = 1; break;
         default: ok = false; break;
         }
         if (!ok) return false;
         i = k + 1;
     }
-    if (!seen[SF_DAY] || seen[SF_MON] + seen[SF_MONTXT] != 1 || !seen[SF_YEAR]) return false;
-    if (seen[SF_CLOCKH] + seen[SF_HOD] != 1 || !seen[SF_MIN] || !seen[SF_SEC]) return false;
-    return seen[SF_MSEC] + seen[SF_USEC] <= 1;
+    for (int e = 0; e + 1 < T.n_ops; ++e) {  // adjacent value parsing
+        const int k0 = T.op[e] & 0xFF, k1 = T.op[e + 1] & 0xFF;
+        const bool num1 = k1 == SE_NUM || k1 == SE_NUMV || k1 == SE_PAD2 || k1 == SE_RED2;
+        if ((k0 == SE_NUMV || k0 == SE_PAD2) && num1) return false;
+    }
+    return true;
 }
 
 // ApacheHttpdLogFormatDissector.createAllTokenParsers (:199-638)

@@ -995,75 +995,116 @@ static instance *inst_new(dissector *d) {
 }
 
 /* ---------------------------------------------------------- strftime
- * StrfTimeToDateTimeFormatter (hp/dissectors/StrfTimeToDateTimeFormatter.java)
- * restated for the subset of StrfTime.g4 whose DateTimeFormatter is a
- * sequence of fixed-width fields: %d (DAY_OF_MONTH, 2), %m (MONTH_OF_YEAR,
- * 2), %b / %h (MONTH_OF_YEAR short text, default locale en_US: Jan..Dec),
- * %Y (YEAR, 4), %H (CLOCK_HOUR_OF_DAY, 2), %M (MINUTE_OF_HOUR, 2), %S
- * (SECOND_OF_MINUTE, 2), %T (= HOUR_OF_DAY:%M:%S, :360-368), %F (= %Y-%m-%d),
- * %z (appendOffset("+HHMM","+0000")), [%]msec_frac (MILLI_OF_SECOND, 3),
- * [%]usec_frac (MICRO_OF_SECOND, 6), %% %t %n and literal text; the E / O
- * modifiers are ignored (StrfTime.g4 MOD).  Patterns with any other
- * conversion, a field given twice, or without all of day, month, year, hour,
- * minute and second are outside the subset (ORC_UNSUPPORTED).  No %z: the
- * formatter is withZone(UTC) (:97-105). */
-enum { SF_LIT, SF_DAY, SF_MON, SF_MONTXT, SF_YEAR, SF_CLOCKH, SF_HOD, SF_MIN, SF_SEC, SF_MSEC, SF_USEC, SF_OFF };
-typedef struct { unsigned char op, off, ch; } strf_op;
-typedef struct { strf_op ops[64]; int nops, width, zone; } strf_prog;
+ * StrfTimeToDateTimeFormatter (hp/dissectors/StrfTimeToDateTimeFormatter.java
+ * :140-432, grammar StrfTime.g4:40-89) restated as the DateTimeFormatterBuilder
+ * elements each conversion appends, parsed as JDK 8's DateTimeFormatter parses
+ * them (parseCaseInsensitive, strict, default locale en_US) and resolved as
+ * JDK 8's java.time.format.Parsed.resolve does (ResolverStyle.SMART), see
+ * strf_parse below.  E / O modifiers are ignored (StrfTime.g4 MOD).
+ *   %a %A   DAY_OF_WEEK text SHORT / FULL        %b %h %B  MONTH_OF_YEAR text
+ *   %d %m   DAY_OF_MONTH / MONTH_OF_YEAR, 2       %Y       YEAR, 4
+ *   %y      YEAR reduced (2 digits, base 2000)    %D       %m/%d/%y
+ *   %e      padNext(2,' ') DAY_OF_MONTH           %F       %Y-%m-%d
+ *   %H      CLOCK_HOUR_OF_DAY, 2                  %k       padNext(2,' ') CLOCK_HOUR_OF_DAY
+ *   %I      CLOCK_HOUR_OF_AMPM, 2                 %l       padNext(2,' ') CLOCK_HOUR_OF_AMPM
+ *   %p      AMPM_OF_DAY text "AM"/"PM"            %P       AMPM_OF_DAY text "am"/"pm"
+ *   %M %S   MINUTE_OF_HOUR / SECOND_OF_MINUTE, 2  %T %R    HOUR_OF_DAY:%M[:%S]
+ *   %r      %I:%M:%S %p                           %j       DAY_OF_YEAR, 3
+ *   %s      INSTANT_SECONDS, 1..19 digits         %u       WeekFields.ISO.dayOfWeek(), 1
+ *   %V %W   WeekFields.ISO.weekOfYear(), 1..19 / 2
+ *   %G %g   WeekFields.of(en_US).weekBasedYear(), 4 / reduced 2 (base 2000)
+ *   %z      appendOffset("+HHMM", "+0000")        %Z       appendZoneText(SHORT)
+ *   [%]msec_frac / [%]usec_frac  MILLI_ / MICRO_OF_SECOND, 3 / 6
+ * %c %C %U %w %x %X %+ throw UnsupportedStrfField in the reference (the
+ * parser cannot be built): outside the restatement (ORC_UNSUPPORTED), as is
+ * a variable-width number directly followed by another number (JDK adjacent
+ * value parsing).  No %z / %Z: the formatter is withZone(UTC) (:97-105). */
+enum { SF_YEAR, SF_MONTH, SF_DOM, SF_DOW, SF_ISODOW, SF_DOY, SF_WBY, SF_WOY, SF_HOD, SF_CHOD, SF_CHAP, SF_AMPM,
+       SF_MIN, SF_SEC, SF_MILLI, SF_MICRO, SF_INSTANT, SF_OFFSET, SF_NFIELDS };
+/* elements: literal char, fixed-width number, 1..19-digit number,
+ * padNext(2,' ') + 1..19-digit number, 2-digit reduced value (base 2000),
+ * text table, offset +HHMM, zone text */
+enum { SE_LIT, SE_NUM, SE_NUMV, SE_PAD2, SE_RED2, SE_TEXT, SE_OFF, SE_ZONE };
+enum { TT_MON_SHORT, TT_MON_FULL, TT_DOW_SHORT, TT_DOW_FULL, TT_AMPM_UP, TT_AMPM_LOW };
+typedef struct { unsigned char kind, field, width, arg; } strf_el;
+typedef struct { strf_el el[96]; int nel, zone; } strf_prog;
 
-static int strf_add(strf_prog *sp, int op, int w, int ch) {
-    if (sp->nops >= 64 || sp->width + w > 200) return 0;
-    sp->ops[sp->nops].op = (unsigned char)op;
-    sp->ops[sp->nops].off = (unsigned char)sp->width;
-    sp->ops[sp->nops].ch = (unsigned char)ch;
-    sp->nops++;
-    sp->width += w;
+static int strf_add(strf_prog *sp, int kind, int field, int width, int arg) {
+    if (sp->nel >= 96) return 0;
+    strf_el *e = &sp->el[sp->nel++];
+    e->kind = (unsigned char)kind; e->field = (unsigned char)field; e->width = (unsigned char)width; e->arg = (unsigned char)arg;
     return 1;
 }
 
 static int strf_compile(const char *f, strf_prog *sp) {
     memset(sp, 0, sizeof *sp);
-    int seen[16] = {0};
     size_t n = strlen(f);
-#define SF(op, w) do { if (seen[op]++ || !strf_add(sp, op, w, 0)) return 0; } while (0)
-#define SL(c) do { if (!strf_add(sp, SF_LIT, 1, (c))) return 0; } while (0)
+#define NUM(fl, w) strf_add(sp, SE_NUM, fl, w, 0)
+#define LIT(c) strf_add(sp, SE_LIT, 0, 1, (unsigned char)(c))
     for (size_t i = 0; i < n;) {
         /* MsecFrac / UsecFrac : '%'? 'msec_frac' (longest match wins over LITERAL) */
         size_t j = i + (f[i] == '%');
         if (n - j >= 9 && (!strncmp(f + j, "msec_frac", 9) || !strncmp(f + j, "usec_frac", 9))) {
-            if (f[j] == 'm') SF(SF_MSEC, 3); else SF(SF_USEC, 6);
+            if (!(f[j] == 'm' ? NUM(SF_MILLI, 3) : NUM(SF_MICRO, 6))) return 0;
             i = j + 9;
             continue;
         }
-        if (f[i] != '%') { SL((unsigned char)f[i]); i++; continue; }
+        if (f[i] != '%') { if (!LIT(f[i])) return 0; i++; continue; }
         if (i + 1 >= n) return 0;
         char c = f[i + 1];
-        if (c == '%') { SL('%'); i += 2; continue; }
-        if (c == 't') { SL('\t'); i += 2; continue; }
-        if (c == 'n') { SL('\n'); i += 2; continue; }
+        if (c == '%') { if (!LIT('%')) return 0; i += 2; continue; }
+        if (c == 't') { if (!LIT('\t')) return 0; i += 2; continue; }
+        if (c == 'n') { if (!LIT('\n')) return 0; i += 2; continue; }
         size_t k = i + 1;
         if (c == 'E' || c == 'O') { if (i + 2 >= n) return 0; c = f[i + 2]; k++; }
+        int ok = 1;
         switch (c) {
-        case 'd': SF(SF_DAY, 2); break;
-        case 'm': SF(SF_MON, 2); break;
-        case 'b': case 'h': SF(SF_MONTXT, 3); break;
-        case 'Y': SF(SF_YEAR, 4); break;
-        case 'H': SF(SF_CLOCKH, 2); break;
-        case 'M': SF(SF_MIN, 2); break;
-        case 'S': SF(SF_SEC, 2); break;
-        case 'T': SF(SF_HOD, 2); SL(':'); SF(SF_MIN, 2); SL(':'); SF(SF_SEC, 2); break;
-        case 'F': SF(SF_YEAR, 4); SL('-'); SF(SF_MON, 2); SL('-'); SF(SF_DAY, 2); break;
-        case 'z': SF(SF_OFF, 5); sp->zone = 1; break;
-        default: return 0;
+        case 'a': ok = strf_add(sp, SE_TEXT, SF_DOW, 0, TT_DOW_SHORT); break;
+        case 'A': ok = strf_add(sp, SE_TEXT, SF_DOW, 0, TT_DOW_FULL); break;
+        case 'b': case 'h': ok = strf_add(sp, SE_TEXT, SF_MONTH, 0, TT_MON_SHORT); break;
+        case 'B': ok = strf_add(sp, SE_TEXT, SF_MONTH, 0, TT_MON_FULL); break;
+        case 'd': ok = NUM(SF_DOM, 2); break;
+        case 'D': ok = NUM(SF_MONTH, 2) && LIT('/') && NUM(SF_DOM, 2) && LIT('/') && strf_add(sp, SE_RED2, SF_YEAR, 2, 0); break;
+        case 'e': ok = strf_add(sp, SE_PAD2, SF_DOM, 2, 0); break;
+        case 'F': ok = NUM(SF_YEAR, 4) && LIT('-') && NUM(SF_MONTH, 2) && LIT('-') && NUM(SF_DOM, 2); break;
+        case 'G': ok = NUM(SF_WBY, 4); break;
+        case 'g': ok = strf_add(sp, SE_RED2, SF_WBY, 2, 0); break;
+        case 'H': ok = NUM(SF_CHOD, 2); break;
+        case 'I': ok = NUM(SF_CHAP, 2); break;
+        case 'j': ok = NUM(SF_DOY, 3); break;
+        case 'k': ok = strf_add(sp, SE_PAD2, SF_CHOD, 2, 0); break;
+        case 'l': ok = strf_add(sp, SE_PAD2, SF_CHAP, 2, 0); break;
+        case 'm': ok = NUM(SF_MONTH, 2); break;
+        case 'M': ok = NUM(SF_MIN, 2); break;
+        case 'p': ok = strf_add(sp, SE_TEXT, SF_AMPM, 0, TT_AMPM_UP); break;
+        case 'P': ok = strf_add(sp, SE_TEXT, SF_AMPM, 0, TT_AMPM_LOW); break;
+        case 'r': ok = NUM(SF_CHAP, 2) && LIT(':') && NUM(SF_MIN, 2) && LIT(':') && NUM(SF_SEC, 2) && LIT(' ') &&
+                       strf_add(sp, SE_TEXT, SF_AMPM, 0, TT_AMPM_UP); break;
+        case 'R': ok = NUM(SF_HOD, 2) && LIT(':') && NUM(SF_MIN, 2); break;
+        case 's': ok = strf_add(sp, SE_NUMV, SF_INSTANT, 19, 0); break;
+        case 'S': ok = NUM(SF_SEC, 2); break;
+        case 'T': ok = NUM(SF_HOD, 2) && LIT(':') && NUM(SF_MIN, 2) && LIT(':') && NUM(SF_SEC, 2); break;
+        case 'u': ok = NUM(SF_ISODOW, 1); break;
+        case 'V': ok = strf_add(sp, SE_NUMV, SF_WOY, 19, 0); break;
+        case 'W': ok = NUM(SF_WOY, 2); break;
+        case 'y': ok = strf_add(sp, SE_RED2, SF_YEAR, 2, 0); break;
+        case 'Y': ok = NUM(SF_YEAR, 4); break;
+        case 'z': ok = strf_add(sp, SE_OFF, SF_OFFSET, 5, 0); sp->zone = 1; break;
+        case 'Z': ok = strf_add(sp, SE_ZONE, 0, 0, 0); sp->zone = 1; break;
+        default: return 0; /* %c %C %U %w %x %X %+ (UnsupportedStrfField) or a syntax error */
         }
+        if (!ok) return 0;
         i = k + 1;
     }
-#undef SF
-#undef SL
-    if (!seen[SF_DAY] || !(seen[SF_MON] + seen[SF_MONTXT]) || !seen[SF_YEAR]) return 0;
-    if (seen[SF_MON] && seen[SF_MONTXT]) return 0;
-    if (seen[SF_CLOCKH] + seen[SF_HOD] != 1 || !seen[SF_MIN] || !seen[SF_SEC]) return 0;
-    if (seen[SF_MSEC] && seen[SF_USEC]) return 0;
+#undef NUM
+#undef LIT
+    /* adjacent value parsing (DateTimeFormatterBuilder.appendValue): a
+     * variable-width number directly followed by another number */
+    for (int e = 0; e + 1 < sp->nel; e++) {
+        const int k0 = sp->el[e].kind, k1 = sp->el[e + 1].kind;
+        const int num1 = k1 == SE_NUM || k1 == SE_NUMV || k1 == SE_PAD2 || k1 == SE_RED2;
+        if ((k0 == SE_NUMV || k0 == SE_PAD2) && num1) return 0;
+    }
     return 1;
 }
 
@@ -1583,96 +1624,279 @@ static js fmt2(parsable *ps, const char *f, int64_t a, int b, int c) {
     return js_lit(ps->a, buf);
 }
 
-/* DateTimeFormatter.parse(text, ZonedDateTime::from) with the program above,
- * parseCaseInsensitive, ResolverStyle.SMART (JDK 8 Parsed.resolveDate /
- * resolveTimeFields / resolveTime, ZoneOffset.ofTotalSeconds).  Returns 0 ok
- * (local date-time as parsed, nanos, offset seconds), 1 failure. */
+/* ---- strftime parsing: JDK 8 DateTimeFormatter.parse(text, ZonedDateTime::from)
+ * with the elements above, restated step by step.  Returns 0 ok (local
+ * date-time, nanos, offset seconds), 1 DateTimeParseException (the dissector
+ * throws DissectionFailure), 2 outside the restatement (ORC_UNSUPPORTED). */
+static const char *DOW_SHORT[] = {"Mon", "Tue", "Wed", "Thu", "Fri", "Sat", "Sun"};
+static const char *DOW_FULL[] = {"Monday", "Tuesday", "Wednesday", "Thursday", "Friday", "Saturday", "Sunday"};
+static const char *AMPM_UP[] = {"AM", "PM"};
+static const char *AMPM_LOW[] = {"am", "pm"};
+static int lower_c(int c) { return c >= 'A' && c <= 'Z' ? c + 32 : c; }
+
+/* WeekFields (java.time.temporal.WeekFields.ComputedDayOfField) of a date:
+ * first day of week sow (1 Monday .. 7 Sunday), minimal days in week 1 */
+static int dow_of(int64_t days) { return (int)(((days % 7) + 7 + 3) % 7) + 1; } /* ISO, Monday 1 */
+static int wf_start_offset(int day, int ldow, int mind) {
+    int week_start = ((day - ldow) % 7 + 7) % 7;
+    return week_start + 1 > mind ? 7 - week_start : -week_start;
+}
+static int wf_week(int offset, int day) { return (7 + offset + (day - 1)) / 7; }
+static int wf_ldow(int64_t days, int sow) { return ((dow_of(days) - sow) % 7 + 7) % 7 + 1; }
+/* weekOfYear (rangeUnit YEARS) */
+static int wf_week_of_year(int64_t y, int m, int d, int sow, int mind) {
+    int64_t days = days_from_civil(y, m, d);
+    int doy = (int)(days - days_from_civil(y, 1, 1)) + 1;
+    return wf_week(wf_start_offset(doy, wf_ldow(days, sow), mind), doy);
+}
+/* weekBasedYear */
+static int64_t wf_week_based_year(int64_t y, int m, int d, int sow, int mind) {
+    int64_t days = days_from_civil(y, m, d);
+    int doy = (int)(days - days_from_civil(y, 1, 1)) + 1;
+    int offset = wf_start_offset(doy, wf_ldow(days, sow), mind);
+    int week = wf_week(offset, doy);
+    if (week == 0) return y - 1;
+    int ylen = is_leap(y) ? 366 : 365;
+    if (week >= wf_week(offset, ylen + mind)) return y + 1;
+    return y;
+}
+
+typedef struct { int64_t v[SF_NFIELDS]; int has[SF_NFIELDS]; } strf_fields;
+/* DateTimeParseContext.setParsedField: a field parsed twice must agree */
+static int strf_set(strf_fields *f, int field, int64_t v) {
+    if (f->has[field] && f->v[field] != v) return 0;
+    f->has[field] = 1;
+    f->v[field] = v;
+    return 1;
+}
+
 static int strf_parse(const strf_prog *sp, js s, int64_t *ly, int *lm, int *ld, int *lh, int *lmi, int *ls,
                       int *nanos, int *offset_secs) {
-    if (s.n != sp->width) return 1; /* fixed-width fields: anything else leaves text or runs short */
+    strf_fields F;
+    memset(&F, 0, sizeof F);
     const int *c = s.c;
-    int day = 0, month = 0, hod = -1, clockh = -1, mi = 0, ss = 0, nos = 0, off = 0;
-    int64_t year = 0;
-    for (int k = 0; k < sp->nops; k++) {
-        const strf_op *o = &sp->ops[k];
-        const int *p = c + o->off;
-        int v = 0, w = 0;
-        switch (o->op) {
-        case SF_LIT: {
-            int x = p[0], y = o->ch;
-            if (x >= 'A' && x <= 'Z') x += 32;
-            if (y >= 'A' && y <= 'Z') y += 32;
-            if (x != y) return 1;
-            continue;
+    int pos = 0, zone_utc = 0;
+    for (int e = 0; e < sp->nel; e++) {
+        const strf_el *el = &sp->el[e];
+        switch (el->kind) {
+        case SE_LIT: /* CharLiteralPrinterParser, case-insensitive */
+            if (pos >= s.n || lower_c(c[pos]) != lower_c(el->arg)) return 1;
+            pos++;
+            break;
+        case SE_NUM: case SE_RED2: { /* NumberPrinterParser fixed width, NOT_NEGATIVE (no sign) */
+            int64_t v = 0;
+            if (pos + el->width > s.n) return 1;
+            for (int q = 0; q < el->width; q++) { int d = dig(c[pos + q]); if (d < 0) return 1; v = v * 10 + d; }
+            pos += el->width;
+            /* ReducedPrinterParser.setValue: base 2000, range 100 -> 2000 + v */
+            if (el->kind == SE_RED2) v += 2000;
+            if (!strf_set(&F, el->field, v)) return 1;
+            break;
         }
-        case SF_MONTXT: {
-            month = 0;
-            for (int m = 0; m < 12 && !month; m++) {
-                int ok = 1;
-                for (int q = 0; q < 3; q++) {
-                    int x = p[q], y = MONTH_SHORT[m][q];
-                    if (x >= 'a' && x <= 'z') x -= 32;
-                    if (y >= 'a' && y <= 'z') y -= 32;
-                    if (x != y) ok = 0;
-                }
-                if (ok) month = m + 1;
+        case SE_NUMV: { /* 1..19 digits; a sign (NORMAL for %V) is left to the reference */
+            if (pos < s.n && (c[pos] == '+' || c[pos] == '-')) return 2;
+            int q = pos;
+            int64_t v = 0;
+            while (q < s.n && q - pos < 19 && dig(c[q]) >= 0) { v = v * 10 + dig(c[q]); q++; }
+            if (q == pos) return 1;
+            if (q - pos == 19) return 2; /* 19 digits may exceed a long: outside the restatement */
+            pos = q;
+            if (!strf_set(&F, el->field, v)) return 1;
+            break;
+        }
+        case SE_PAD2: { /* PadPrinterParserDecorator(2, ' ') around a 1..19 digit number, strict */
+            if (pos >= s.n || pos + 2 > s.n) return 1;
+            int q = pos, end = pos + 2;
+            while (q < end && c[q] == ' ') q++;
+            if (q < end && (c[q] == '+' || c[q] == '-')) return 2;
+            int64_t v = 0;
+            int r = q;
+            while (r < end && dig(c[r]) >= 0) { v = v * 10 + dig(c[r]); r++; }
+            if (r == q || r != end) return 1;
+            pos = end;
+            if (!strf_set(&F, el->field, v)) return 1;
+            break;
+        }
+        case SE_TEXT: { /* TextPrinterParser: the longest entry that matches, case-insensitive */
+            const char **tab; int nt;
+            switch (el->arg) {
+            case TT_MON_SHORT: tab = MONTH_SHORT; nt = 12; break;
+            case TT_MON_FULL: tab = MONTH_FULL; nt = 12; break;
+            case TT_DOW_SHORT: tab = DOW_SHORT; nt = 7; break;
+            case TT_DOW_FULL: tab = DOW_FULL; nt = 7; break;
+            case TT_AMPM_UP: tab = AMPM_UP; nt = 2; break;
+            default: tab = AMPM_LOW; nt = 2; break;
             }
-            if (!month) return 1;
-            continue;
+            int best = -1, blen = 0;
+            for (int t = 0; t < nt; t++) {
+                int L = (int)strlen(tab[t]), ok = pos + L <= s.n;
+                for (int q = 0; ok && q < L; q++) ok = lower_c(c[pos + q]) == lower_c(tab[t][q]);
+                if (ok && L > blen) { best = t; blen = L; }
+            }
+            if (best < 0) return 1;
+            pos += blen;
+            /* values: months 1..12, days of week 1..7 (Monday 1), AM 0 / PM 1 */
+            int64_t v = (el->arg == TT_AMPM_UP || el->arg == TT_AMPM_LOW) ? best : best + 1;
+            if (!strf_set(&F, el->field, v)) return 1;
+            break;
         }
-        case SF_OFF: {
-            if (p[0] == '+' && p[1] == '0' && p[2] == '0' && p[3] == '0' && p[4] == '0') { off = 0; continue; }
-            if (p[0] != '+' && p[0] != '-') return 1;
-            int a1 = dig(p[1]), a2 = dig(p[2]), b1 = dig(p[3]), b2 = dig(p[4]);
-            if (a1 < 0 || a2 < 0 || b1 < 0 || b2 < 0) return 1;
-            int oh = a1 * 10 + a2, om = b1 * 10 + b2;
-            if (oh > 59 || om > 59) return 1;
-            off = (p[0] == '-' ? -1 : 1) * (oh * 3600 + om * 60);
-            continue;
+        case SE_OFF: { /* OffsetIdPrinterParser("+HHMM", "+0000") */
+            if (pos + 5 > s.n) return 1;
+            const int *p = c + pos;
+            int off;
+            if (p[0] == '+' && p[1] == '0' && p[2] == '0' && p[3] == '0' && p[4] == '0') off = 0;
+            else {
+                if (p[0] != '+' && p[0] != '-') return 1;
+                int a1 = dig(p[1]), a2 = dig(p[2]), b1 = dig(p[3]), b2 = dig(p[4]);
+                if (a1 < 0 || a2 < 0 || b1 < 0 || b2 < 0) return 1;
+                int oh = a1 * 10 + a2, om = b1 * 10 + b2;
+                if (oh > 59 || om > 59) return 1;
+                off = (p[0] == '-' ? -1 : 1) * (oh * 3600 + om * 60);
+            }
+            pos += 5;
+            if (!strf_set(&F, SF_OFFSET, off)) return 1;
+            break;
         }
-        case SF_YEAR: w = 4; break;
-        case SF_MSEC: w = 3; break;
-        case SF_USEC: w = 6; break;
-        default: w = 2; break;
+        case SE_ZONE: { /* ZoneTextPrinterParser: "UTC" / "GMT" (not followed by an offset) only */
+            if (pos + 3 > s.n) return 2;
+            const int *p = c + pos;
+            int utc = lower_c(p[0]) == 'u' && lower_c(p[1]) == 't' && lower_c(p[2]) == 'c';
+            int gmt = lower_c(p[0]) == 'g' && lower_c(p[1]) == 'm' && lower_c(p[2]) == 't';
+            if (!utc && !gmt) return 2;
+            if (pos + 3 < s.n && (p[3] == '+' || p[3] == '-')) return 2;
+            pos += 3;
+            zone_utc = 1;
+            break;
         }
-        for (int q = 0; q < w; q++) {
-            int d = dig(p[q]);
-            if (d < 0) return 1;
-            v = v * 10 + d;
-        }
-        switch (o->op) {
-        case SF_DAY: day = v; break;
-        case SF_MON: month = v; break;
-        case SF_YEAR: year = v; break;
-        case SF_CLOCKH: clockh = v; break;
-        case SF_HOD: hod = v; break;
-        case SF_MIN: mi = v; break;
-        case SF_SEC: ss = v; break;
-        case SF_MSEC: nos = v * 1000000; break;
-        case SF_USEC: nos = v * 1000; break;
         }
     }
-    if (off > 18 * 3600 || off < -18 * 3600) return 1;                     /* ZoneOffset.ofTotalSeconds */
-    /* resolveTimeFields: CLOCK_HOUR_OF_DAY, SMART allows 0-24, 24 -> 0 */
-    if (clockh >= 0) {
-        if (clockh != 0 && (clockh < 1 || clockh > 24)) return 1;
-        hod = clockh == 24 ? 0 : clockh;
+    if (pos != s.n) return 1; /* unparsed text */
+    /* ---- Parsed.resolve (JDK 8), SMART */
+    int has_date = 0, has_time = 0, plus_day = 0;
+    int64_t dy = 0; int dm = 0, dd = 0;
+    int th = 0, tmi = 0, tsec = 0, tnano = 0;
+    int64_t sod = -1; /* SECOND_OF_DAY from the instant */
+    /* resolveInstantFields: the zone is the parsed one, else the formatter's
+     * UTC (no %z / %Z), else OFFSET_SECONDS */
+    if (F.has[SF_INSTANT]) {
+        int64_t off;
+        if (zone_utc || !sp->zone) off = 0;
+        else if (F.has[SF_OFFSET]) off = F.v[SF_OFFSET];
+        else return 2;
+        if (off > 18 * 3600 || off < -18 * 3600) return 1;
+        const int64_t t = F.v[SF_INSTANT] + off;
+        if (F.v[SF_INSTANT] > 253402300799LL) return 2; /* beyond year 9999: outside the restatement */
+        int64_t days = t >= 0 ? t / 86400 : -((-t + 86399) / 86400);
+        civil_from_days(days, &dy, &dm, &dd);
+        has_date = 1;
+        sod = t - days * 86400;
     }
-    /* resolveDate (IsoChronology.resolveYMD, SMART) */
-    if (month < 1 || month > 12) return 1;
-    if (day < 1 || day > 31) return 1;
-    int ml = month_len(year, month);
-    if (day > ml) day = ml;
-    /* resolveTime (SMART): minute checked first, 24:00:00.0 = end of day */
-    if (mi > 59) return 1;
-    int plus_day = 0;
-    if (hod == 24 && mi == 0 && ss == 0 && nos == 0) { hod = 0; plus_day = 1; }
-    else if (hod > 23 || ss > 59) return 1;
-    if (plus_day) {
-        int64_t days = days_from_civil(year, month, day) + 1;
-        civil_from_days(days, &year, &month, &day);
+    /* resolveDateFields: IsoChronology.resolveDate (YEAR + MONTH_OF_YEAR +
+     * DAY_OF_MONTH, else YEAR + DAY_OF_YEAR; fields it does not consume stay
+     * for the cross-check) */
+    if (F.has[SF_YEAR] && ((F.has[SF_MONTH] && F.has[SF_DOM]) || F.has[SF_DOY])) {
+        int64_t y = F.v[SF_YEAR];
+        int64_t ry; int rm, rd;
+        if (y < -999999999 || y > 999999999) return 1;
+        if (F.has[SF_MONTH] && F.has[SF_DOM]) { /* resolveYMD */
+            int64_t mo = F.v[SF_MONTH], dom = F.v[SF_DOM];
+            if (mo < 1 || mo > 12 || dom < 1 || dom > 31) return 1;
+            if (y < 1 || y > 9999) return 2; /* the calendar is restated for years 1..9999 */
+            int ml = month_len(y, (int)mo);
+            if (dom > ml) dom = ml; /* SMART clamps to the month's length */
+            ry = y; rm = (int)mo; rd = (int)dom;
+            F.has[SF_MONTH] = F.has[SF_DOM] = 0;
+        } else { /* resolveYD */
+            int64_t doy = F.v[SF_DOY];
+            if (doy < 1 || doy > 366) return 1;
+            if (y < 1 || y > 9999) return 2;
+            if (doy == 366 && !is_leap(y)) return 1; /* LocalDate.ofYearDay */
+            civil_from_days(days_from_civil(y, 1, 1) + doy - 1, &ry, &rm, &rd);
+            F.has[SF_DOY] = 0;
+        }
+        F.has[SF_YEAR] = 0;
+        if (has_date && (ry != dy || rm != dm || rd != dd)) return 1; /* updateCheckConflict(date) */
+        dy = ry; dm = rm; dd = rd; has_date = 1;
     }
-    *ly = year; *lm = month; *ld = day; *lh = hod; *lmi = mi; *ls = ss; *nanos = nos; *offset_secs = off;
+    /* a week-of-year with the YEAR left: WeekFields resolves a date from it
+     * (resolveWoY): outside the restatement */
+    if (F.has[SF_WOY] && F.has[SF_YEAR]) return 2;
+    /* resolveTimeFields */
+    int64_t hod = -1, hap = -1;
+    if (F.has[SF_HOD]) hod = F.v[SF_HOD];
+#define CONFLICT_HOD(val) do { int64_t v_ = (val); if (hod >= 0 && hod != v_) return 1; hod = v_; } while (0)
+    if (F.has[SF_CHOD]) { /* SMART allows 0-24, 24 -> 0 */
+        int64_t ch = F.v[SF_CHOD];
+        if (ch != 0 && (ch < 1 || ch > 24)) return 1;
+        CONFLICT_HOD(ch == 24 ? 0 : ch);
+    }
+    if (F.has[SF_CHAP]) { /* SMART allows 0-12, 12 -> 0 */
+        int64_t ch = F.v[SF_CHAP];
+        if (ch != 0 && (ch < 1 || ch > 12)) return 1;
+        hap = ch == 12 ? 0 : ch;
+    }
+    int ampm_used = 0;
+    if (F.has[SF_AMPM] && hap >= 0) {
+        CONFLICT_HOD(F.v[SF_AMPM] * 12 + hap);
+        ampm_used = 1;
+    }
+    if (sod >= 0) { /* SECOND_OF_DAY from the instant -> HOUR_OF_DAY, MINUTE, SECOND */
+        CONFLICT_HOD(sod / 3600);
+        if (F.has[SF_MIN] && F.v[SF_MIN] != (sod / 60) % 60) return 1;
+        if (F.has[SF_SEC] && F.v[SF_SEC] != sod % 60) return 1;
+        F.v[SF_MIN] = (sod / 60) % 60; F.has[SF_MIN] = 1;
+        F.v[SF_SEC] = sod % 60; F.has[SF_SEC] = 1;
+    }
+#undef CONFLICT_HOD
+    /* the localized day-of-week (%u) replaces DAY_OF_WEEK (ComputedDayOfField.resolve, no conflict check) */
+    if (F.has[SF_ISODOW]) {
+        if (F.v[SF_ISODOW] < 1 || F.v[SF_ISODOW] > 7) return 1;
+        F.v[SF_DOW] = F.v[SF_ISODOW]; F.has[SF_DOW] = 1;
+    }
+    /* resolveTimeLenient: milli / micro to nano, hour with defaults */
+    int64_t nos = -1;
+    if (F.has[SF_MILLI] && F.has[SF_MICRO]) return 2;
+    if (F.has[SF_MILLI]) nos = F.v[SF_MILLI] * 1000000;
+    if (F.has[SF_MICRO]) nos = F.v[SF_MICRO] * 1000;
+    if (hod >= 0) {
+        int64_t moh = F.has[SF_MIN] ? F.v[SF_MIN] : -1, som = F.has[SF_SEC] ? F.v[SF_SEC] : -1;
+        if (!((moh < 0 && (som >= 0 || nos >= 0)) || (moh >= 0 && som < 0 && nos >= 0))) {
+            if (moh < 0) moh = 0;
+            if (som < 0) som = 0;
+            if (nos < 0) nos = 0;
+            /* resolveTime: MINUTE and NANO checked, 24:00 = end of day, then HOUR / SECOND */
+            if (moh > 59) return 1;
+            if (hod == 24 && moh == 0 && som == 0 && nos == 0) { th = 0; plus_day = 1; }
+            else { if (hod > 23 || som > 59) return 1; th = (int)hod; }
+            tmi = (int)moh; tsec = (int)som; tnano = (int)nos;
+            has_time = 1;
+        }
+    }
+    if (!has_date || !has_time) return 1; /* LocalDateTime.from: no date or no time */
+    if (plus_day) { int64_t dd2 = days_from_civil(dy, dm, dd) + 1; civil_from_days(dd2, &dy, &dm, &dd); }
+    /* crossCheck: the fields left against the resolved date and time */
+    const int64_t days = days_from_civil(dy, dm, dd);
+    if (F.has[SF_DOW] && F.v[SF_DOW] != dow_of(days)) return 1;
+    if (F.has[SF_DOY] && F.v[SF_DOY] != days - days_from_civil(dy, 1, 1) + 1) return 1;
+    if (F.has[SF_WOY] && F.v[SF_WOY] != wf_week_of_year(dy, dm, dd, 1, 4)) return 1;
+    if (F.has[SF_WBY] && F.v[SF_WBY] != wf_week_based_year(dy, dm, dd, 7, 1)) return 1;
+    if (F.has[SF_AMPM] && !ampm_used && F.v[SF_AMPM] != th / 12) return 1;
+    if (hap >= 0 && !ampm_used && hap != th % 12) return 1;
+    if (F.has[SF_MONTH] || F.has[SF_DOM] || F.has[SF_YEAR]) {
+        /* date fields the date did not come from (e.g. YEAR with an instant) */
+        if (F.has[SF_MONTH] && F.v[SF_MONTH] != dm) return 1;
+        if (F.has[SF_DOM] && F.v[SF_DOM] != dd) return 1;
+        if (F.has[SF_YEAR] && F.v[SF_YEAR] != dy) return 1;
+    }
+    /* ZonedDateTime.from: the zone (ZoneOffset.ofTotalSeconds when %z) */
+    int off = 0;
+    if (!zone_utc && sp->zone) {
+        if (!F.has[SF_OFFSET]) return 1;
+        off = (int)F.v[SF_OFFSET];
+        if (off > 18 * 3600 || off < -18 * 3600) return 1;
+    }
+    if (dy < 1 || dy > 9999) return 2;
+    *ly = dy; *lm = dm; *ld = dd; *lh = th; *lmi = tmi; *ls = tsec; *nanos = tnano; *offset_secs = off;
     return 0;
 }
 
@@ -1699,7 +1923,9 @@ static void d_strftime(parsable *ps, instance *in, const char *inputname) {
     strf_prog sp;
     strf_compile(in->d->param, &sp);
     int64_t y; int m, d, h, mi, sec, nanos, off;
-    if (strf_parse(&sp, s, &y, &m, &d, &h, &mi, &sec, &nanos, &off)) { ps->failed = 1; return; }
+    const int st = strf_parse(&sp, s, &y, &m, &d, &h, &mi, &sec, &nanos, &off);
+    if (st == 2) { ps->unsupported = 1; return; }
+    if (st) { ps->failed = 1; return; }
     emit_time(ps, in, inputname, y, m, d, h, mi, sec, nanos, off);
 }
 

@@ -517,7 +517,53 @@ for src, frac, digits, ms, us, ns, epoch in [
     case(src, STRF_LINE_FMT.format("%{%F %H:%M:%S." + frac + "}t"),
          "192.168.85.3 - - 2017-12-25 00:00:42." + digits + " \"GET /up.html HTTP/1.0\" 203 8 \"-\" \"HTTP-Monitor/1.1\" \"-\" t=4920",
          [tsf(f) for f in FRAC_F], expect={tsf(f): v for f, v in zip(FRAC_F, vals)})
-# (:246-349 %D %R %r %a %A %B %G %I %j %k %l %p %s %u fields: outside the restated strftime subset, left out)
+# testSpecialTimeFormatMultiFields1/2, testSpecialTimeLeadingSpaces1/2a: every convertible conversion at once
+MULTI_F = ["TIME.EPOCH:epoch", "TIME.DATE:date", "TIME.TIME:time", "TIME.YEAR:year", "TIME.MONTH:month",
+           "TIME.MONTHNAME:monthname", "TIME.YEAR:weekyear", "TIME.WEEK:weekofweekyear", "TIME.DAY:day", "TIME.HOUR:hour",
+           "TIME.MINUTE:minute", "TIME.SECOND:second", "TIME.MILLISECOND:millisecond", "TIME.DATE:date_utc",
+           "TIME.TIME:time_utc", "TIME.YEAR:year_utc", "TIME.MONTH:month_utc", "TIME.MONTHNAME:monthname_utc",
+           "TIME.YEAR:weekyear_utc", "TIME.WEEK:weekofweekyear_utc", "TIME.DAY:day_utc", "TIME.HOUR:hour_utc",
+           "TIME.MINUTE:minute_utc", "TIME.SECOND:second_utc", "TIME.MILLISECOND:millisecond_utc"]
+MULTI_FMT = "%D %F %R %T %r %a %A %b %B %d %G %h %H %I %j %k %l %m %M %p %s %S %u %Y %z"
+for src, fmt, line, vals in [
+        ("hpt/dissectors/TestTimeStampDissector.java:246-287", "%{" + MULTI_FMT + "}t",
+         "12/21/16 2016-12-21 20:50 20:50:25 08:50:25 PM Wed Wednesday Dec December 21 2016 Dec 20 08 356 20  8 12 50 PM "
+         "1482349825 25 3 2016 +0100",
+         [{"l": 1482349825000}, "2016-12-21", "20:50:25", {"l": 2016}, {"l": 12}, "December", {"l": 2016}, {"l": 51},
+          {"l": 21}, {"l": 20}, {"l": 50}, {"l": 25}, {"l": 0}, "2016-12-21", "19:50:25", {"l": 2016}, {"l": 12},
+          "December", {"l": 2016}, {"l": 51}, {"l": 21}, {"l": 19}, {"l": 50}, {"l": 25}, {"l": 0}]),
+        ("hpt/dissectors/TestTimeStampDissector.java:289-330",
+         "%h %l %u %t \"%r\" %>s %O \"%{" + MULTI_FMT + "}t\" \"%{User-Agent}i\"",
+         "127.0.0.1 - - [22/Dec/2016:00:09:54 +0100] \"GET / HTTP/1.1\" 200 3525 \"12/22/16 2016-12-22 00:09 00:09:54 "
+         "12:09:54 AM Thu Thursday Dec December 22 2016 Dec 00 12 357  0 12 12 09 AM 1482361794 54 4 2016 +0100\" "
+         "\"Mozilla/5.0 (X11; Linux x86_64) AppleWebKit/537.36 (KHTML, like Gecko) Chrome/54.0.2840.71 Safari/537.36\"",
+         [{"l": 1482361794000}, "2016-12-22", "00:09:54", {"l": 2016}, {"l": 12}, "December", {"l": 2016}, {"l": 51},
+          {"l": 22}, {"l": 0}, {"l": 9}, {"l": 54}, {"l": 0}, "2016-12-21", "23:09:54", {"l": 2016}, {"l": 12},
+          "December", {"l": 2016}, {"l": 51}, {"l": 21}, {"l": 23}, {"l": 9}, {"l": 54}, {"l": 0}])]:
+    case(src, fmt, line, [tsf(f) for f in MULTI_F] + [tsf("TIME.ZONE:timezone")],
+         expect={tsf(f): v for f, v in zip(MULTI_F, vals)}, absent=[tsf("TIME.ZONE:timezone")])
+case("hpt/dissectors/TestTimeStampDissector.java:332-341", "%{" + MULTI_FMT + "}t",
+     "12/21/16 2016-12-21 20:50 20:50:25 08:50:25 PM Wed Wednesday Dec December 21 2016 Dec 20 08 356 20  8 12 50 PM "
+     "1482349825 25 3 2016 +0100", [tsf("TIME.EPOCH:epoch")], expect={tsf("TIME.EPOCH:epoch"): {"l": 1482349825000}})
+case("hpt/dissectors/TestTimeStampDissector.java:343-352",
+     "%h %l %u %t \"%r\" %>s %O \"%{%D %F %R %T %r %a %A %b %B %d %G %h %H %I %j %k %l %m %M %p %S %u %Y %z}t\" "
+     "\"%{User-Agent}i\"",
+     "127.0.0.1 - - [01/Jan/2017:13:01:21 +0100] \"GET / HTTP/1.1\" 200 3525 \"01/01/17 2017-01-01 13:01 13:01:21 01:01:21 PM "
+     "Sun Sunday Jan January 01 2017 Jan 13 01 001 13  1 01 01 PM 21 7 2017 +0100\" \"Mozilla/5.0 (X11; Linux x86_64) "
+     "AppleWebKit/537.36 (KHTML, like Gecko) Chrome/54.0.2840.71 Safari/537.36\"",
+     [tsf("TIME.EPOCH:epoch")], expect={tsf("TIME.EPOCH:epoch"): {"l": 1483272081000}})
+# testAllStrfFieldsLowValues / HighValues (:392-510) pin what each conversion PRINTS for one ZonedDateTime
+# (CET, +01:00 on both dates); parsing the printed fields back, joined by spaces, must give that instant.
+ALL_FMT = "%a %A %b %h %B %d %D %e %F %G %g %H %I %j %k %l %m %M %p %P %r %R %s %S %T %u %V %W %y %Y %z %T.msec_frac"
+for src, text, epoch in [
+        ("hpt/dissectors/TestTimeStampDissector.java:392-443 (printed fields parsed back)",
+         "Tue Tuesday Jan Jan January 02 01/02/01  2 2001-01-02 2001 01 03 03 002  3  3 01 04 AM am 03:04:05 AM 03:04 "
+         "978401045 05 03:04:05 2 1 01 01 2001 +0100 03:04:05.678", 978401045678),
+        ("hpt/dissectors/TestTimeStampDissector.java:446-497 (printed fields parsed back)",
+         "Sun Sunday Nov Nov November 12 11/12/17 12 2017-11-12 2017 17 23 11 316 23 11 11 14 PM pm 11:14:15 PM 23:14 "
+         "1510524855 15 23:14:15 7 45 45 17 2017 +0100 23:14:15.678", 1510524855678)]:
+    case(src, "%{" + ALL_FMT + "}t", text, [tsf("TIME.EPOCH:epoch")], expect={tsf("TIME.EPOCH:epoch"): {"l": epoch}},
+         note="derived: the concatenation of the checkStrfField outputs of the same date-time")
 
 # examples/apache-flink/.../TestCase.java:37-43,86-94 (IPv6 %h, long query string); GeoIP / remapped fields skipped.
 FLINK_LINE = open(os.path.join(HERE, "flink_testcase_line.txt"), encoding="utf-8").read().rstrip("\n") \

@@ -682,3 +682,23 @@ def test_set_cookies_emulated(oracle, emu, which):
     assert e.status == 0, e.err
     s = compare(o, e, setcookie_lines(3000, 21 + which))
     assert s["ok"] > 1000 and s["fallback"] < 2000, s
+
+
+def test_strftime_conversions_emulated(oracle, emu):
+    """Every strftime conversion the reference converts (strf_corpus): the
+    device code's parse + SMART resolution against the oracle's, on printed
+    and mutated values; only the stray non-ASCII letters stay FALLBACK.
+    A variable-width number directly followed by another (JDK adjacent
+    value parsing) keeps the handle off the device, as the oracle refuses it."""
+    import strf_corpus
+    tot = {"ok": 0, "bad": 0, "fallback": 0}
+    for fmt, lines in strf_corpus.corpus(20261017, per_pattern=120):
+        o = oracle.Oracle(fmt, strf_corpus.FIELDS)
+        e = emu.Emu(fmt, strf_corpus.FIELDS)
+        s = compare(o, e, lines)
+        for k in tot:
+            tot[k] += s[k]
+        assert s["fallback"] <= len(lines) // 10, (fmt, s)
+    assert tot["ok"] > 800 and tot["bad"] > 150, tot
+    e = emu.Emu('%h [%{%k%M}t]', strf_corpus.FIELDS)
+    assert e.status == -3  # LP_E_UNSUPPORTED

@@ -712,3 +712,18 @@ def test_result_table_gpu(demolog_lines):
     # BYTESCLF is STRING_OR_LONG: a DOUBLE column finds no setter
     with pytest.raises(ValueError):
         r.table_from(res, [("BYTES:response.body.bytes", float)])
+
+
+def test_strftime_conversions_gpu(oracle):
+    """Every strftime conversion the reference converts (tests/strf_corpus.py:
+    printed and mutated values of 13 patterns, the reference's MultiFields
+    pattern among them) on the device against the oracle."""
+    import strf_corpus
+    tot = {"ok": 0, "bad": 0, "fallback": 0}
+    for fmt, lines in strf_corpus.corpus(20261017, per_pattern=400):
+        s, _ = gpu_vs_oracle(oracle, fmt, strf_corpus.FIELDS, lines)
+        for k in tot:
+            tot[k] += s[k]
+        assert s["fallback"] <= len(lines) // 10, (fmt, s)
+    print("strftime corpus on the device:", tot)
+    assert tot["ok"] > 3000 and tot["bad"] > 500, tot
