@@ -79,11 +79,32 @@ typedef struct lp_handle lp_handle;
  * receives LP_OK / LP_E_UNSUPPORTED (handle still usable) / error code. */
 lp_handle *lp_compile(const char *logformats, const char *const *paths, int n_paths,
                       int device, int *status, char *err, size_t errlen);
+
+/* Parser.addTypeRemapping(input, newType, casts) (core/Parser.java:636-677):
+ * a value delivered at path `input` is delivered again as type `type`
+ * (Parsable.addDissection, core/Parsable.java:160-176), where that type's
+ * dissectors take it further (Parser.java:446-455): e.g. a query parameter
+ * holding a URL, remapped to HTTP.URI, is dissected by HttpUriDissector on
+ * the device (the "derived" URI stages).  casts: LP_CAST_* bits of the
+ * remapped target (the reference's STRING_ONLY default is LP_CAST_STRING). */
+typedef struct lp_remap {
+    const char *input;
+    const char *type;
+    int32_t casts;
+} lp_remap;
+/* lp_compile with the parser's type remappings (n_remaps may be 0). */
+lp_handle *lp_compile_remapped(const char *logformats, const char *const *paths, int n_paths,
+                               const lp_remap *remaps, int n_remaps, int device, int *status, char *err,
+                               size_t errlen);
 void lp_free(lp_handle *h);
 
 /* Parser.getPossiblePaths(max_depth) for a logformat: '\n'-separated, sorted.
  * Returns the number of bytes written (excluding NUL) or a negative error. */
 int64_t lp_possible_paths(const char *logformats, int max_depth, char *out, size_t cap);
+/* The same with type remappings: each remapped path and what the new type's
+ * dissectors produce below it (core/Parser.java:954-962). */
+int64_t lp_possible_paths_remapped(const char *logformats, int max_depth, const lp_remap *remaps, int n_remaps,
+                                   char *out, size_t cap);
 
 /* Options (lp_set_option). */
 #define LP_OPT_FORCE_DIRECT 1  /* 1: every wave reads its lines from HBM (no LDS window);
@@ -197,9 +218,10 @@ int lp_last_bytes(lp_handle *h, uint64_t *out, int n);
  *   query stage; arena_base (u64, the line's arena region); fmt_id (u8, the
  *   routed LogFormat) with several LogFormats.
  * A ref is off | len << 32 (len 30 bits); bit 63 set: the bytes are in the
- * line's arena region, else line-relative; bit 62: '&' followed by those line
- * bytes.  Arena offsets b live in shard s = b / shard_cap, at
- * arena + shard_off[s] + (b - s * shard_cap). */
+ * line's arena region, else line-relative; bit 62: '&' followed by those
+ * bytes.  A q_params table slot whose parameter name was not requested holds
+ * ~0 (REF_SKIP) as its name ref: skip it.  Arena offsets b live in shard
+ * s = b / shard_cap, at arena + shard_off[s] + (b - s * shard_cap). */
 #define LP_ARENA_SHARDS 64
 typedef struct lp_column {
     char name[16];

@@ -109,6 +109,12 @@ def lib():
     L.lp_free.argtypes = [ctypes.c_void_p]
     L.lp_possible_paths.restype = ctypes.c_int64
     L.lp_possible_paths.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_size_t]
+    L.lp_compile_remapped.restype = ctypes.c_void_p
+    L.lp_compile_remapped.argtypes = [ctypes.c_char_p, c_char_pp, ctypes.c_int, ctypes.POINTER(LpRemap), ctypes.c_int,
+                                      ctypes.c_int, ctypes.POINTER(ctypes.c_int), ctypes.c_char_p, ctypes.c_size_t]
+    L.lp_possible_paths_remapped.restype = ctypes.c_int64
+    L.lp_possible_paths_remapped.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(LpRemap), ctypes.c_int,
+                                             ctypes.c_char_p, ctypes.c_size_t]
     L.lp_parse_batch.restype = ctypes.c_int
     L.lp_parse_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p]
     L.lp_parse_batch_at.restype = ctypes.c_int
@@ -153,11 +159,26 @@ def lib():
     return L
 
 
-def get_possible_paths(logformat, max_depth=15):
-    """Parser.getPossiblePaths(maxDepth) for a HttpdLoglineParser on logformat."""
+class LpRemap(ctypes.Structure):
+    """lp_remap: Parser.addTypeRemapping(input, type, casts)"""
+    _fields_ = [("input", ctypes.c_char_p), ("type", ctypes.c_char_p), ("casts", ctypes.c_int32)]
+
+
+def _remap_array(remaps):
+    """[(input, TYPE, casts)] -> (lp_remap array, count)"""
+    arr = (LpRemap * max(1, len(remaps)))()
+    for i, (n, t, c) in enumerate(remaps):
+        arr[i] = LpRemap(n.encode(), t.encode(), c)
+    return arr, len(remaps)
+
+
+def get_possible_paths(logformat, max_depth=15, remaps=()):
+    """Parser.getPossiblePaths(maxDepth) for a HttpdLoglineParser on logformat
+    (remaps: [(input, TYPE, casts)], its type remappings)."""
     cap = 1 << 20
     out = ctypes.create_string_buffer(cap)
-    n = lib().lp_possible_paths(logformat.encode(), max_depth, out, cap)
+    arr, n_rm = _remap_array(list(remaps))
+    n = lib().lp_possible_paths_remapped(logformat.encode(), max_depth, arr, n_rm, out, cap)
     if n < 0:
         raise InvalidDissectorException("possible paths overflow")
     return [p for p in out.value.decode().split("\n") if p]
@@ -409,53 +430,30 @@ class HttpdLoglineParser:
         """CAST_* bits of a requested "TYPE:path" (None if unknown)"""
         name = cleanup_field_value(name)
         self._ensure()
-        if name in self._remap_casts:
-            return self._remap_casts[name]
         c = lib().lp_casts(self._h, name.encode())
         return None if c < 0 else c
 
-    def _plan_fields(self):
-        """The paths the engine compiles: the requested ones, less those only a
-        type remapping delivers, plus the original paths the remapped names
-        come from."""
-        if not self._remaps:
-            return list(self.fields)
-        remapped = {t + ":" + n for n, ts in self._remaps.items() for t in ts}
-        out = [f for f in self.fields if cleanup_field_value(f) not in remapped]
-        possible = get_possible_paths(self.logformat)
-
-        def known(field):
-            pt, pn = field.split(":", 1)
-            return any(p == field or (p.endswith(".*") and p.split(":", 1)[0] == pt and
-                                      pn.startswith(p.split(":", 1)[1][:-1])) for p in possible)
-        for f in out:
-            c = cleanup_field_value(f)
-            # a path below a remapped name that only the remapped type's
-            # dissectors could deliver (Parser.java:446-455): not on the engine
-            if not known(c) and any(c.split(":", 1)[1].startswith(n + ".") for n in self._remaps):
-                raise FallbackRequired("%s: dissecting a type-remapped value is left to the reference dissector" % f)
-        for n in self._remaps:
-            for pp in possible:
-                pt, pn = pp.split(":", 1)
-                if pn == n or (pn.endswith(".*") and n.startswith(pn[:-1]) and len(n) > len(pn) - 1):
-                    out.append(pt + ":" + n)
-        return out
+    def _remap_list(self):
+        """[(input, TYPE, casts)] in a stable order"""
+        return [(n, t, self._remap_casts[t + ":" + n]) for n in sorted(self._remaps) for t in sorted(self._remaps[n])]
 
     def get_possible_paths(self, max_depth=15):
-        return get_possible_paths(self.logformat, max_depth)
+        return get_possible_paths(self.logformat, max_depth, self._remap_list())
 
     def _ensure(self):
         if self._h:
             return
         L = lib()
-        fields = self._plan_fields()
+        fields = list(self.fields)
         self._engine_fields = fields
         arr = (ctypes.c_char_p * max(1, len(fields)))()
         for i, f in enumerate(fields):
             arr[i] = f.encode()
+        rm, n_rm = _remap_array(self._remap_list())
         st = ctypes.c_int(0)
         err = ctypes.create_string_buffer(1024)
-        h = L.lp_compile(self.logformat.encode(), arr, len(fields), self.device, ctypes.byref(st), err, 1024)
+        h = L.lp_compile_remapped(self.logformat.encode(), arr, len(fields), rm, n_rm, self.device, ctypes.byref(st),
+                                  err, 1024)
         msg = err.value.decode(errors="replace")
         if not h:
             if st.value == LP_E_MISSING:

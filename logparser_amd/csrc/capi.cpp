@@ -301,7 +301,8 @@ int enqueue(lp_handle* h, bool sync_count) {
         if (hipMemcpyAsync(h->args.p, &h->host_args, sizeof(lp::DeviceArgs), hipMemcpyHostToDevice, s) != hipSuccess)
             return LP_E_DEVICE;
         lp::ParseLaunch pl{h->d_buf, nbytes, cap, (uint64_t)(h->mean_line > 0 ? h->mean_line + 0.5 : 0),
-                           P.n_elems, P.max_stack, h->force_direct, P.n_uri > 0};
+                           P.n_elems, P.max_stack, h->force_direct, P.n_uri > 0, false};
+        for (int u = 0; u < P.n_uri; ++u) pl.derived = pl.derived || P.uri[u].src_q >= 0;
         if (!pl.mean_line && cap > 0) pl.mean_line = (nbytes + cap - 1) / (uint64_t)cap;
         hipEventRecord(h->ev[2], s);
         const lp::DeviceArgs* d_args = h->args.as<lp::DeviceArgs>();
@@ -460,8 +461,18 @@ extern "C" {
 
 lp_handle* lp_compile(const char* logformats, const char* const* paths, int n_paths, int device, int* status,
                       char* err, size_t errlen) {
+    return lp_compile_remapped(logformats, paths, n_paths, nullptr, 0, device, status, err, errlen);
+}
+
+lp_handle* lp_compile_remapped(const char* logformats, const char* const* paths, int n_paths, const lp_remap* remaps,
+                               int n_remaps, int device, int* status, char* err, size_t errlen) {
     if (status) *status = LP_E_INVALID;
-    if (!logformats || (n_paths > 0 && !paths)) { set_err(err, errlen, "null argument"); return nullptr; }
+    if (!logformats || (n_paths > 0 && !paths) || (n_remaps > 0 && !remaps)) { set_err(err, errlen, "null argument"); return nullptr; }
+    std::vector<lp::Remap> rm;
+    for (int i = 0; i < n_remaps; ++i) {
+        if (!remaps[i].input || !remaps[i].type) { set_err(err, errlen, "null remapping"); return nullptr; }
+        rm.push_back(lp::Remap{remaps[i].input, remaps[i].type, (int)remaps[i].casts});
+    }
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) {
         if (status) *status = LP_E_DEVICE;
@@ -474,7 +485,7 @@ lp_handle* lp_compile(const char* logformats, const char* const* paths, int n_pa
     std::vector<std::string> f;
     for (int i = 0; i < n_paths; ++i) f.emplace_back(paths[i]);
     std::string e;
-    int st = h->plan.build(logformats, f, e);
+    int st = h->plan.build(logformats, f, e, rm);
     if (st != LP_OK && st != LP_E_UNSUPPORTED) {
         if (status) *status = st;
         set_err(err, errlen, e);
@@ -504,9 +515,20 @@ void lp_free(lp_handle* h) {
 }
 
 int64_t lp_possible_paths(const char* logformats, int max_depth, char* out, size_t cap) {
+    return lp_possible_paths_remapped(logformats, max_depth, nullptr, 0, out, cap);
+}
+
+int64_t lp_possible_paths_remapped(const char* logformats, int max_depth, const lp_remap* remaps, int n_remaps,
+                                   char* out, size_t cap) {
+    if (n_remaps > 0 && !remaps) return LP_E_INVALID;
+    std::vector<lp::Remap> rm;
+    for (int i = 0; i < n_remaps; ++i) {
+        if (!remaps[i].input || !remaps[i].type) return LP_E_INVALID;
+        rm.push_back(lp::Remap{remaps[i].input, remaps[i].type, (int)remaps[i].casts});
+    }
     std::vector<std::string> paths;
     std::string err;
-    lp::Plan::possible_paths(logformats ? logformats : "", max_depth, paths, err);
+    lp::Plan::possible_paths(logformats ? logformats : "", max_depth, paths, err, rm);
     std::string s;
     for (auto& p : paths) s += p + "\n";
     if (!out || s.size() + 1 > cap) return -(int64_t)(s.size() + 1);

@@ -38,6 +38,7 @@ struct ParseLaunch {
     int n_elems, stack_depth;
     bool force_direct;      // every wave on the direct (HBM) path: tests / diagnostics only
     bool uri;               // the program has URI stages (k_uri_lines after the parse kernel)
+    bool derived;           // ... some of them derived (type remapping: k_derived_lines after those)
 };
 // parse every line (staged waves, then the waves whose window did not fit
 // LDS on the direct path), then the URI stages (k_uri_lines, and its direct

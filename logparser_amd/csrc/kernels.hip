@@ -713,6 +713,44 @@ __global__ __launch_bounds__(PW) void k_uri_overflow(const uint8_t* __restrict__
     }
 }
 
+// Derived URI stages (type-remapped query parameters, lp_device.h
+// derived_line), after both URI kernels: one line per lane, the sources read
+// in place (the input, or the decoded value in the line's region), every
+// table and rewritten part spilled from the region's shard.  Only launched
+// for programs that have such stages.  Re-counts the wave's statuses.
+__global__ __launch_bounds__(PW) void k_derived_lines(const uint8_t* __restrict__ buf, uint64_t nbytes,
+                                                      const DeviceArgs* __restrict__ args) {
+    const Program& P = args->prog;
+    const Columns& C = args->cols;
+    const int64_t n_lines = (int64_t)C.meta->n_lines;
+    const int64_t wave = blockIdx.x;
+    if (wave * PW >= n_lines || C.meta->cap_ovf) return;
+    const WaveLines W = wave_lines(C, wave, n_lines, nbytes);
+    int st = W.active ? (int)C.status[W.li] : -1;
+    if (st == ST_OK) {
+        const int fmt = P.n_fmt > 1 ? (int)C.fmt_id[W.li] : 0;
+        const LP_G uint8_t* ls = (const LP_G uint8_t*)(buf) + W.s;
+        const uint32_t mis = (uint32_t)((uintptr_t)ls & 3);
+        const unsigned long long ab = C.arena_base[W.li];
+        const int shard = (int)(ab / C.shard_cap);
+        Arena R{C.arena + ab, 0, 0};
+        R.top = &C.meta->shard_top[16 * shard];
+        R.base = ab - (unsigned long long)shard * C.shard_cap;
+        R.limit = C.shard_cap;
+        st = derived_line(P, fmt, ls - mis, mis, crlf_len_hbm(buf, W), R, C, W.li);
+        if (R.ovf) atomicAdd(&C.meta->arena_ovf, 1ull);  // the batch is re-run with a larger arena
+        if (st != ST_OK) C.status[W.li] = (uint8_t)st;
+    }
+    const uint32_t ok = (uint32_t)__popcll(__ballot(st == ST_OK)), bad = (uint32_t)__popcll(__ballot(st == ST_BAD));
+    if (threadIdx.x == 0) {
+        LP_G uint32_t* wc = C.wave_counts + WC_WORDS * (size_t)wave;
+        const uint32_t act = wc[0];
+        wc[1] = ok;
+        wc[2] = bad;
+        wc[3] = act - ok - bad;
+    }
+}
+
 // LDS: [elements (n_elems x 16 B)][DFS stack][byte window (win_cap, a multiple of 64)][mask planes (win_cap / 4)]
 __device__ __forceinline__ void load_elems(const Program& P, Elem* s_elems) {
     for (int k = threadIdx.x; k < P.n_elems; k += PW) s_elems[k] = P.elems[k];
@@ -1098,6 +1136,7 @@ int launch_parse(const ParseLaunch& a, const DeviceArgs* d_args, const uint32_t*
     if (a.uri) {
         hipLaunchKernelGGL(k_uri_lines, dim3((unsigned)waves), dim3(PW), 0, s, a.buf, a.nbytes, d_args);
         hipLaunchKernelGGL(k_uri_overflow, dim3((unsigned)grid), dim3(PW), 0, s, a.buf, a.nbytes, d_args);
+        if (a.derived) hipLaunchKernelGGL(k_derived_lines, dim3((unsigned)waves), dim3(PW), 0, s, a.buf, a.nbytes, d_args);
     }
     int64_t rb = (waves + 255) / 256;
     if (rb > 1024) rb = 1024;

@@ -131,6 +131,7 @@ struct LineT {
     int n;
     MPtr m = MPtr{};       // planes of the 64-byte block w of b: m[NPL w .. NPL w + NPL)
     static constexpr bool has_masks = !std::is_same<MPtr, NoMasks>::value;
+    static constexpr bool in_arena = false;  // positions are line offsets
     __host__ __device__ LP_INLINE uint32_t operator[](int i) const { return b[o + i]; }
     // aligned 32-bit word w of the base (little-endian: byte k at bits 8k..8k+7)
     __host__ __device__ LP_INLINE uint32_t word(uint32_t w) const { return load_word(b + 4 * w); }
@@ -151,6 +152,22 @@ struct LineT {
 using Line = LineT<const uint8_t*>;
 using MLine = LineT<const uint8_t*, const uint64_t*>;
 using ULine = LineT<const uint8_t*, const uint64_t*, 1>;
+
+// A URI source held in the line's arena region (a decoded query value that a
+// type remapping dissects again): position q is region byte rb + q, and the
+// refs made from positions are region refs.
+template <typename Ptr>
+struct ArenaLineT : LineT<Ptr> {
+    uint32_t rb;
+    static constexpr bool in_arena = true;
+};
+
+// the ref of [x, x + n) of the source viewed by L
+template <typename LN>
+__host__ __device__ LP_INLINE uint64_t src_ref(const LN& L, int x, int n) {
+    if constexpr (LN::in_arena) return mkref(L.rb + (uint32_t)x, (uint32_t)n, true);
+    else return mkref((uint32_t)x, (uint32_t)n, false);
+}
 
 // ---- SWAR byte classes on a 32-bit word: bit 8k+7 set when byte k is in
 // the class (exact, no false positives from carries).
@@ -1804,6 +1821,7 @@ __host__ __device__ LP_INLINE bool value_is_header_name(const LN& L, int a, int 
 __host__ __device__ LP_INLINE bool uri_source(const Program& P, const LineOut& o, int u, int& a, int& b) {
     const UriStage& U = P.uri[u];
     uint32_t sp;
+    if (U.src_q >= 0) return false;  // a derived stage (k_derived_lines)
     if (U.src_tok >= 0) {
         if (o.tok_flags & (1u << U.src_tok)) return false;  // "-" -> null
         sp = o.caps.get(U.src_tok);
@@ -1821,6 +1839,7 @@ template <typename Cols>
 __host__ __device__ LP_INLINE bool uri_source_cols(const Program& P, const Cols& C, int64_t li, int u, int& a, int& b) {
     const UriStage& U = P.uri[u];
     uint32_t sp;
+    if (U.src_q >= 0) return false;  // a derived stage (k_derived_lines)
     if (U.src_tok >= 0) {
         if (C.tok_flags[li] & (1u << U.src_tok)) return false;  // "-" -> null
         sp = C.tok_span[U.src_tok][li];
@@ -2490,7 +2509,7 @@ __host__ __device__ LP_INLINE uint32_t query_finish(const Program& P, const Quer
         nref = mkref(mark, A.used - mark, true);
         A.used = (A.used + 3) & ~3u;  // the value's words start aligned
     } else {
-        nref = mkref(s, ne - s, false);
+        nref = src_ref(L, s, ne - s);
     }
     // requested?  (wantAllFields || requestedParameters.contains(name))
     bool want = Q.want_all;
@@ -2511,7 +2530,7 @@ __host__ __device__ LP_INLINE uint32_t query_finish(const Program& P, const Quer
     }
     uint64_t vref;
     if (eq < 0) vref = mkref(0, 0, false);  // no '=' -> ""
-    else if (!qp.pv) vref = mkref(eq + 1, e - eq - 1, false);
+    else if (!qp.pv) vref = src_ref(L, eq + 1, e - eq - 1);
     else vref = url_decode_value(L, eq + 1, e, A);
     slot[0] = nref;
     slot[1] = vref;
@@ -2670,7 +2689,7 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
         if (p < b && p != fa && c == ':') {
             if (p == a || !sch_ok) return ST_BAD;                                          // URISyntaxException
             flags |= UF_SCHEME;
-            scheme_ref = (int64_t)mkref(a, p - a, false);
+            scheme_ref = (int64_t)src_ref(L, a, p - a);
             ++p;
             if (!(p < b && cur.at(p) == '/')) return ST_FALLBACK;                          // opaque URI
             if (p + 1 < b && cur.at(p + 1) == '/') {
@@ -2703,7 +2722,7 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
                 }
                 if (ok) {
                     flags |= UF_HOST;
-                    host_ref = (int64_t)mkref(as, he - as, false);
+                    host_ref = (int64_t)src_ref(L, as, he - as);
                     if (pt >= 0) { flags |= UF_PORT; port = pt; }
                 }
                 ps = ae;
@@ -2721,7 +2740,7 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
     C.u_host[u][li] = (uint64_t)host_ref;
     C.u_port[u][li] = port;
     if (U.want_path) {
-        uint64_t r = mkref(ps, pend - ps, false);
+        uint64_t r = src_ref(L, ps, pend - ps);
         if (first_pct >= 0 && first_pct < pend) {  // decoded: at most the escaped length
             Arena X;
             if (!spill(A, (uint32_t)(pend - ps), X)) return ST_FALLBACK;
@@ -2741,7 +2760,7 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
             // the ref is formed before the scan below: with it formed after,
             // the gfx950 build (ROCm 7.2, -O3) delivered a wrong offset on
             // lanes whose scan ran an extra word (parity tests caught it)
-            const uint64_t amp_ref = mkref(qs0, qe - qs0, false) | REF_AMP;
+            const uint64_t amp_ref = src_ref(L, qs0, qe - qs0) | REF_AMP;
             if (!(rewr & 2u)) {
                 C.u_query[u][li] = amp_ref;
             } else {
@@ -2767,7 +2786,7 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
     if (U.want_ref && h >= 0) {
         flags |= UF_FRAG;
         // fragment = decode(normalized text after '#')
-        if (!(rewr & 1u)) C.u_frag[u][li] = mkref(h + 1, b - h - 1, false);
+        if (!(rewr & 1u)) C.u_frag[u][li] = src_ref(L, h + 1, b - h - 1);
         else {
             Arena X;  // the decoded fragment: at most one byte more than its text
             if (!spill(A, (uint32_t)(b - h), X)) return ST_FALLBACK;
@@ -2799,6 +2818,95 @@ __host__ __device__ LP_INLINE void query_pieces_serial(const Program& P, LQ&& lq
         for (uint32_t k = 0; k < o.qpend.get(qs); ++k)
             A.extra += query_piece(P, P.query[qs], L, A, (LP_G uint64_t*)(A.p + o.qlist.get(qs) + 16 * k));
     }
+}
+
+// ---- Derived URI stages: a query parameter's value that a type remapping
+// turned into an HTTP.URI (Parsable.addDissection, core/Parsable.java:160-176,
+// re-adds the value under the new type; Parser.findUsefulDissectorsFromField,
+// core/Parser.java:446-455, gave that type its dissectors).  They run after
+// the query pieces of their source are complete (k_derived_lines), one line
+// per lane, on the value's bytes in place: a line span, or the decoded
+// value in the line's arena region.
+//
+// The source: the value of the line's one occurrence of the parameter.
+// Returns 0 none (no such parameter, or an empty value: HttpUriDissector
+// does nothing for an empty input, HttpUriDissector.java:134-136), 1 found
+// (vref), 2 FALLBACK (two or more occurrences: each is dissected in turn).
+template <typename Cols>
+__host__ __device__ LP_INLINE int derived_source(const Program& P, const UriStage& U, const Cols& C, int64_t li,
+                                                 const LP_G uint8_t* line, const LP_G uint8_t* region, uint64_t& vref) {
+    const QueryStage& Q = P.query[U.src_q];
+    const uint32_t cnt = C.q_count[U.src_q][li];
+    if (cnt == 0) return 0;
+    const LP_G uint64_t* t = reinterpret_cast<const LP_G uint64_t*>(region + ref_off(C.q_params[U.src_q][li]));
+    const uint32_t no = Q.name_off[U.src_qname], nl = Q.name_len[U.src_qname];
+    int found = 0;
+    for (uint32_t k = 0; k < cnt; ++k) {
+        const uint64_t nref = t[2 * k];
+        if (nref == REF_SKIP || ref_len(nref) != nl) continue;
+        const LP_G uint8_t* np = (ref_arena(nref) ? region : line) + ref_off(nref);
+        bool same = true;
+        for (uint32_t q = 0; q < nl && same; ++q) same = np[q] == P.lit_byte((int)(no + q));
+        if (!same) continue;
+        if (++found > 1) return 2;
+        vref = t[2 * k + 1];
+    }
+    return found && ref_len(vref) > 0 ? 1 : 0;
+}
+
+// Derived stage u on source [a, b) of L: the URI stage, then its query
+// pieces one after the other.  R: the line's region with the shard's spill
+// allocator (the stage's query table and every rewritten part are spilled).
+template <typename LN, typename Cols>
+__host__ __device__ LP_INLINE int derived_stage(const Program& P, int u, const LN& L, int a, int b, Arena& R, Cols& C,
+                                                int64_t li) {
+    uint32_t usep;
+    const uint32_t need = uri_need(P, u, L, a, b, usep);
+    Arena X = R;
+    if (need && !spill(R, need, X)) return ST_FALLBACK;
+    UriOut o;
+    o.qlist.fill(0);
+    o.qpend.fill(0);
+    o.status = ST_OK;
+    int st = uri_stage(P, u, L, a, b, usep, X, C, li, o);
+    const int qs = P.uri[u].query_stage;
+    if (st == ST_OK && qs >= 0)
+        for (uint32_t k = 0; k < o.qpend.get(qs); ++k)
+            query_piece(P, P.query[qs], L, X, (LP_G uint64_t*)(X.p + o.qlist.get(qs) + 16 * k));
+    if (X.ovf) R.ovf = true;
+    return X.ovf ? ST_FALLBACK : st;
+}
+
+// The derived stages of one OK line of LogFormat fmt.  line: the line's
+// bytes (4-byte aligned base lb, line start at lb + lo, n bytes), R: its
+// region (see derived_stage).  Returns the line's status.
+template <typename Cols>
+__host__ __device__ LP_INLINE int derived_line(const Program& P, int fmt, const LP_G uint8_t* lb, uint32_t lo, int n,
+                                               Arena& R, Cols& C, int64_t li) {
+    for (int u = 0; u < P.n_uri; ++u) {
+        const UriStage& U = P.uri[u];
+        if (U.src_q < 0 || U.fmt != fmt) continue;
+        uint64_t vref = 0;
+        const int f = derived_source(P, U, C, li, lb + lo, R.p, vref);
+        if (f == 2) return ST_FALLBACK;
+        if (f == 0) {
+            C.u_flags[u][li] = 0;
+            if (U.query_stage >= 0) { C.q_count[U.query_stage][li] = 0; C.q_params[U.query_stage][li] = 0; }
+            continue;
+        }
+        const uint32_t vo = ref_off(vref), vl = ref_len(vref);
+        int st;
+        if (ref_arena(vref)) {
+            // the decoded value in the region: positions from its first byte
+            const ArenaLineT<const LP_G uint8_t*> A{{R.p + (vo & ~3u), vo & 3u, (int)vl}, vo};
+            st = derived_stage(P, u, A, 0, (int)vl, R, C, li);
+        } else {
+            const LineT<const LP_G uint8_t*> L{lb, lo, n};
+            st = derived_stage(P, u, L, (int)vo, (int)(vo + vl), R, C, li);
+        }
+        if (st != ST_OK) return st;
+    }
+    return ST_OK;
 }
 
 // Phase 2 of one line (the URI kernel): the URI stages of its LogFormat.

@@ -152,7 +152,10 @@ struct FlStage {
 };
 
 // HttpUriDissector (hp/dissectors/HttpUriDissector.java:130-233) on either a
-// token (e.g. request.referer) or the uri of a first-line stage.
+// token (e.g. request.referer), the uri of a first-line stage, or a query
+// parameter that a type remapping (core/Parser.java:446-455, Parsable.java:
+// 160-176) turned into an HTTP.URI (a "derived" stage: src_q >= 0; it runs
+// in k_derived_lines, after the query pieces of its source are complete).
 struct UriStage {
     int32_t src_tok;     // >= 0: token slot
     int32_t src_fl;      // >= 0: first-line stage (its uri)
@@ -162,6 +165,8 @@ struct UriStage {
     int32_t want_userinfo;
     int32_t query_stage; // QueryStringFieldDissector on its query, -1 none
     int32_t fmt;         // the LogFormat of its source token
+    int32_t src_q;       // >= 0: query stage whose parameter src_qname (an index into its names) is the source
+    int32_t src_qname;
 };
 
 // QueryStringFieldDissector (hp/dissectors/QueryStringFieldDissector.java:56-108)
@@ -226,9 +231,10 @@ __host__ __device__ inline uint64_t pack_cal(uint32_t y, uint32_t mo, uint32_t d
 
 // A "ref" names a byte string: bits 0..31 offset, 32..61 length, bit 63 set
 // when the bytes live in the line's arena region (else: relative to the
-// line start).  Bit 62 (REF_AMP, line refs only): the string is '&'
-// followed by the line bytes -- the HttpUriDissector rawQuery of a query
-// that needs no other rewriting, delivered without copying it.
+// line start).  Bit 62 (REF_AMP): the string is '&' followed by the bytes
+// (line or region) -- the HttpUriDissector rawQuery of a query that needs no
+// other rewriting, delivered without copying it.  A query table slot whose
+// name was not requested holds REF_SKIP (~0) as its name ref.
 constexpr uint64_t REF_ARENA = 1ull << 63;
 constexpr uint64_t REF_AMP = 1ull << 62;
 __host__ __device__ inline uint64_t mkref(uint32_t off, uint32_t len, bool arena) {

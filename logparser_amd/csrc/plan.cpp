@@ -1107,12 +1107,34 @@ void Plan::find_useful(const std::set<std::string>& possible, const std::string&
             }
         }
     }
+    // the new types of a remapped name get their dissectors too (core/Parser.java:447-455)
+    auto rm = remaps_.find(name);
+    if (rm != remaps_.end())
+        for (const auto& mt : rm->second)
+            if (!compiled_.count(mt + ":" + name)) {
+                casts_[mt + ":" + name] = CAST_S;  // "Retyped targets are ALWAYS String ONLY"
+                find_useful(possible, mt, name, false);
+            }
 }
 
-int Plan::build(const std::string& logformats, const std::vector<std::string>& fields, std::string& err) {
+int Plan::build(const std::string& logformats, const std::vector<std::string>& fields, std::string& err,
+                const std::vector<Remap>& remaps) {
     gen_ = g_plan_gen.fetch_add(1);
     int r = build_dissectors(logformats, err);
     if (r != LP_OK) return r;
+    // Parser.addTypeRemapping (core/Parser.java:664-677): input trimmed and
+    // lower-cased, type trimmed and upper-cased; the first casts given for a
+    // pair are its castsOfTargets entry
+    auto trim = [](const std::string& x) {  // String.trim: chars <= ' ' at both ends
+        size_t a = 0, b = x.size();
+        while (a < b && (uint8_t)x[a] <= ' ') ++a;
+        while (b > a && (uint8_t)x[b - 1] <= ' ') --b;
+        return x.substr(a, b - a);
+    };
+    for (const auto& m : remaps) {
+        const std::string in = lower(trim(m.input)), ty = upper(trim(m.type));
+        if (remaps_[in].insert(ty).second) casts_[ty + ":" + in] = m.casts;
+    }
     for (const auto& f : fields) needed_.insert(cleanup_field(f));
     for (const auto& d : dis_)
         if (d->outs.empty()) {
@@ -1162,7 +1184,7 @@ int Plan::build(const std::string& logformats, const std::vector<std::string>& f
 }
 
 int Plan::possible_paths(const std::string& logformats, int max_depth, std::vector<std::string>& out,
-                         std::string& err) {
+                         std::string& err, const std::vector<Remap>& remaps) {
     Plan p;
     p.build_dissectors(logformats, err);
     std::set<std::string> seen;
@@ -1181,13 +1203,20 @@ int Plan::possible_paths(const std::string& logformats, int max_depth, std::vect
         }
     };
     rec("", p.root_type_, max_depth);
+    // each remapped path and what its new type's dissectors produce below it (core/Parser.java:954-962)
+    for (const auto& m : remaps) {
+        const std::string in = lower(m.input), ty = upper(m.type);
+        seen.insert(ty + ":" + in);
+        rec(in, ty, max_depth - 1);
+    }
     out.assign(seen.begin(), seen.end());
     return LP_OK;
 }
 
 // ====================================================== device program
 namespace {
-enum Origin { O_NONE, O_TOKEN, O_FL_URI, O_FL_PROTO, O_FL_METHOD, O_URI_QUERY, O_URI_PART, O_CONV, O_TIME };
+// O_QPARAM: a query parameter's value (index: query stage * MAX_QNAMES + name index)
+enum Origin { O_NONE, O_TOKEN, O_FL_URI, O_FL_PROTO, O_FL_METHOD, O_URI_QUERY, O_URI_PART, O_CONV, O_TIME, O_QPARAM };
 }
 
 void Plan::compile_program() {
@@ -1318,10 +1347,27 @@ void Plan::compile_program() {
     if (P.max_stack > MAX_STACK) { device_ok_ = false; why_ = "too many backtracking elements"; return; }
     int cur_fmt = 0;
     auto tk = [&](int oi) { return cur_fmt * 64 + oi; };  // (format, token slot) key of the stage maps
-    // stages, walking the compiled tree from each captured token output
-    std::function<void(int, int, const std::string&, const std::string&)> walk =
-        [&](int ok, int oi, const std::string& type, const std::string& complete) {
+    // stages, walking the compiled tree from each captured token output.
+    // remapped: this visit is a type remapping's second delivery of a value
+    // (Parsable.addDissection with recursion, core/Parsable.java:160-176)
+    std::set<std::string> remap_seen;  // remapped names whose values the walk reached
+    std::function<void(int, int, const std::string&, const std::string&, bool)> walk =
+        [&](int ok, int oi, const std::string& type, const std::string& complete, bool remapped) {
             if (!device_ok_) return;
+            if (!remapped) {
+                auto rm = remaps_.find(complete);
+                if (rm != remaps_.end()) {
+                    remap_seen.insert(complete);
+                    for (const auto& mt : rm->second) {
+                        if (mt == type) {  // DissectionFailure for every line delivering the value
+                            device_ok_ = false;
+                            why_ = "type remapping to the value's own type";
+                            return;
+                        }
+                        walk(ok, oi, mt, complete, true);
+                    }
+                }
+            }
             if (!useful_.count(complete)) return;
             auto it = compiled_.find(type + ":" + complete);
             if (it == compiled_.end()) return;
@@ -1390,9 +1436,9 @@ void Plan::compile_program() {
                         fl_of_tok_[tk(oi)] = P.n_fl++;
                     }
                     fidx = fl_of_tok_[tk(oi)];
-                    walk(O_FL_URI, fidx, "HTTP.URI", complete + ".uri");
-                    walk(O_FL_PROTO, fidx, "HTTP.PROTOCOL_VERSION", complete + ".protocol");
-                    walk(O_FL_METHOD, fidx, "HTTP.METHOD", complete + ".method");
+                    walk(O_FL_URI, fidx, "HTTP.URI", complete + ".uri", false);
+                    walk(O_FL_PROTO, fidx, "HTTP.PROTOCOL_VERSION", complete + ".protocol", false);
+                    walk(O_FL_METHOD, fidx, "HTTP.METHOD", complete + ".method", false);
                     break;
                 }
                 case D_PROTOCOL:
@@ -1401,15 +1447,18 @@ void Plan::compile_program() {
                     if (ok != O_FL_PROTO && ok != O_TOKEN) { device_ok_ = false; why_ = "protocol from a derived value"; return; }
                     break;
                 case D_URI: {
-                    std::map<int, int>& m = ok == O_TOKEN ? uri_of_tok_ : uri_of_fl_;
-                    if (ok != O_TOKEN && ok != O_FL_URI) { device_ok_ = false; why_ = "URI from a derived value"; return; }
-                    const int key = ok == O_TOKEN ? tk(oi) : oi;  // first-line stages are already per format
+                    // a token, a first line's uri, or a remapped query parameter (derived stage)
+                    std::map<int, int>& m = ok == O_TOKEN ? uri_of_tok_ : ok == O_QPARAM ? uri_of_qp_ : uri_of_fl_;
+                    if (ok != O_TOKEN && ok != O_FL_URI && ok != O_QPARAM) { device_ok_ = false; why_ = "URI from a derived value"; return; }
+                    const int key = ok == O_TOKEN ? tk(oi) : oi;  // first-line / query stages are already per format
                     if (!m.count(key)) {
                         if (P.n_uri == MAX_URI) { device_ok_ = false; why_ = "too many URIs"; return; }
                         UriStage& U = P.uri[P.n_uri];
                         memset(&U, 0, sizeof U);
                         U.src_tok = ok == O_TOKEN ? (int8_t)oi : -1;
                         U.src_fl = ok == O_FL_URI ? (int8_t)oi : -1;
+                        U.src_q = ok == O_QPARAM ? oi / MAX_QNAMES : -1;
+                        U.src_qname = ok == O_QPARAM ? oi % MAX_QNAMES : 0;
                         U.query_stage = -1;
                         U.fmt = (int8_t)cur_fmt;
                         m[key] = P.n_uri++;
@@ -1420,7 +1469,7 @@ void Plan::compile_program() {
                     if (in.requested.count("path")) U.want_path = 1;
                     if (in.requested.count("ref")) U.want_ref = 1;
                     if (in.requested.count("userinfo")) U.want_userinfo = 1;
-                    walk(O_URI_QUERY, u, "HTTP.QUERYSTRING", complete + ".query");
+                    walk(O_URI_QUERY, u, "HTTP.QUERYSTRING", complete + ".query", false);
                     break;
                 }
                 case D_QUERY: {
@@ -1455,12 +1504,22 @@ void Plan::compile_program() {
                         Q.name_len[Q.n_names] = (uint8_t)r.size();
                         Q.n_names++;
                     }
+                    // a remapped parameter: its value is dissected again under the new type
+                    const int qsi = U.query_stage;
+                    for (int k = 0; k < P.query[qsi].n_names; ++k) {
+                        const std::string r((const char*)P.lit + P.query[qsi].name_off[k], P.query[qsi].name_len[k]);
+                        const std::string pc = complete + "." + r;
+                        if (!remaps_.count(pc)) continue;
+                        qname_of_[std::to_string(qsi) + ":" + r] = k;
+                        walk(O_QPARAM, qsi * MAX_QNAMES + k, "STRING", pc, false);
+                        if (!device_ok_) return;
+                    }
                     break;
                 }
                 case D_CLF2NUM: case D_NUM2CLF: case D_SECMILLIS: case D_MS2US: case D_BINIP:
                     // value-level conversions, done in the replay from the token / list item
                     if (ok != O_TOKEN && ok != O_CONV) { device_ok_ = false; why_ = "converter on a derived value"; return; }
-                    walk(O_CONV, oi, in.d->out_type, complete);
+                    walk(O_CONV, oi, in.d->out_type, complete, false);
                     break;
                 case D_UPSTREAM: {
                     // the list token's element kind (EK_UPLIST_*) proves the list
@@ -1468,7 +1527,7 @@ void Plan::compile_program() {
                     if (ok != O_TOKEN) { device_ok_ = false; why_ = "upstream list from a derived value"; return; }
                     for (int k = 0; k < 32; ++k)
                         for (const char* sfx : {".value", ".redirected"})
-                            walk(O_CONV, oi, in.d->out_type, complete + "." + std::to_string(k) + sfx);
+                            walk(O_CONV, oi, in.d->out_type, complete + "." + std::to_string(k) + sfx, false);
                     break;
                 }
                 default:
@@ -1483,9 +1542,17 @@ void Plan::compile_program() {
         for (int i = 0; i < (int)f.tokens.size(); ++i) {
             auto it = tok_slot_.find(cur_fmt * 256 + i);
             if (it == tok_slot_.end()) continue;
-            for (const auto& o : f.tokens[i].outs) walk(O_TOKEN, it->second, o.type, o.name);
+            for (const auto& o : f.tokens[i].outs) walk(O_TOKEN, it->second, o.type, o.name, false);
         }
     }
+    // a remapped name whose new type has dissectors but whose values the walk
+    // never reached (e.g. a URI part): the replay could not follow it
+    for (const auto& kv : remaps_)
+        for (const auto& mt : kv.second)
+            if (device_ok_ && compiled_.count(mt + ":" + kv.first) && !remap_seen.count(kv.first)) {
+                device_ok_ = false;
+                why_ = "type remapping of a value the device does not track: " + kv.first;
+            }
     // histogram sources: the captured status token and the first first-line stage of each format
     for (int fi = 0; fi < P.n_fmt; ++fi) {
         P.hist_status[fi] = P.hist_fl[fi] = -1;
@@ -1570,7 +1637,9 @@ namespace {
 struct EmitDec {
     std::string complete, needed;
     const std::vector<Instance>* ins = nullptr;  // further dissectors (useful intermediate)
+    const std::set<std::string>* remap = nullptr;  // the name's type remappings
     bool exact = false, wild = false;
+    bool remap_needed = false;  // a remapped delivery of the value is requested
 };
 struct EmitMemo {
     uint64_t gen = 0;
@@ -1581,7 +1650,7 @@ thread_local EmitMemo t_memo;
 }  // namespace
 
 void Plan::emit(Ctx& c, const std::string& base, const std::string& type, const std::string& name, const MVal& v,
-                const MVal* dv) const {
+                const MVal* dv, bool recursion) const {
     EmitMemo& M = t_memo;
     if (M.gen != gen_) {
         M.m.clear();
@@ -1610,9 +1679,30 @@ void Plan::emit(Ctx& c, const std::string& base, const std::string& type, const 
         }
         d.exact = needed_.count(d.needed) > 0;
         d.wild = needed_.count(wild) > 0;
+        auto rm = remaps_.find(d.complete);
+        if (rm != remaps_.end()) {
+            d.remap = &rm->second;
+            for (const auto& mt : rm->second)
+                d.remap_needed = d.remap_needed || needed_.count(mt + ":" + d.complete) ||
+                                 needed_.count(mt + (base.empty() ? ":*" : ":" + base + ".*"));
+        }
         it = M.m.emplace(M.key, std::move(d)).first;
     }
     const EmitDec& d = it->second;  // node-based map: stays valid while the row inserts more
+    if (d.remap && !recursion) {
+        // the value again under each new type, first (core/Parsable.java:160-176;
+        // a remapping to the value's own type left the whole plan to FALLBACK).
+        // Not a dissector's addDissection call: the emission list holds the
+        // original only (the caller's Parser.store replays the remapping).
+        const int ok = t_origin_kind, oi = t_origin_idx;
+        for (const auto& mt : *d.remap) {
+            t_origin_kind = ok;
+            t_origin_idx = oi;
+            emit(c, base, mt, name, v, dv, true);
+        }
+        t_origin_kind = ok;
+        t_origin_idx = oi;
+    }
     if (d.ins) {
         const int ok = t_origin_kind, oi = t_origin_idx;
         for (const auto& in : *d.ins) {
@@ -1623,7 +1713,7 @@ void Plan::emit(Ctx& c, const std::string& base, const std::string& type, const 
     }
     if (d.exact) c.rec.emplace_back(d.needed, v);
     if (d.wild) c.rec.emplace_back(d.needed, v);
-    if (d.exact || d.wild) c.em.push_back(Emission{base, type, name, v});
+    if ((d.exact || d.wild || d.remap_needed) && !recursion) c.em.push_back(Emission{base, type, name, v});
 }
 
 void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const MVal& v) const {
@@ -1633,8 +1723,8 @@ void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const 
     auto has = [&](const char* n) { return in.requested.count(n) > 0; };
     auto set_origin = [](int k, int x) { t_origin_kind = k; t_origin_idx = x; };
     auto line_ref = [&](uint64_t r) {
-        if (ref_amp(r)) {  // '&' + line bytes (rawQuery delivered without a copy)
-            c.pool.emplace_back("&" + std::string((const char*)c.line + ref_off(r), ref_len(r)));
+        if (ref_amp(r)) {  // '&' + line / region bytes (rawQuery delivered without a copy)
+            c.pool.emplace_back("&" + std::string((const char*)(ref_arena(r) ? c.arena : c.line) + ref_off(r), ref_len(r)));
             return mstr((const uint8_t*)c.pool.back().data(), (uint32_t)c.pool.back().size());
         }
         return mstr((ref_arena(r) ? c.arena : c.line) + ref_off(r), ref_len(r));
@@ -1718,7 +1808,7 @@ void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const 
     }
     case D_URI: {
         if (v.null || v.len == 0) return;
-        int u = ok == O_TOKEN ? uri_of_tok_.at(t_fmt * 64 + oi) : uri_of_fl_.at(oi);
+        int u = ok == O_TOKEN ? uri_of_tok_.at(t_fmt * 64 + oi) : ok == O_QPARAM ? uri_of_qp_.at(oi) : uri_of_fl_.at(oi);
         uint32_t fl = R.u_flags[u][i];
         if (!(fl & UF_DONE)) return;
         if (has("query") || has("path") || has("ref")) {
@@ -1773,12 +1863,17 @@ void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const 
         uint32_t cnt = R.q_count[q][i];
         uint64_t tab = R.q_params[q][i];
         const uint64_t* t = (const uint64_t*)(c.arena + ref_off(tab));
-        set_origin(O_NONE, 0);
         for (uint32_t k = 0; k < cnt; ++k) {
             if (t[2 * k] == REF_SKIP) continue;  // name not requested
             MVal nm = line_ref(t[2 * k]);
             MVal val = line_ref(t[2 * k + 1]);
-            emit(c, name, "STRING", std::string((const char*)nm.p, nm.len), val);
+            std::string pn((const char*)nm.p, nm.len);
+            set_origin(O_NONE, 0);
+            if (!qname_of_.empty()) {  // a remapped parameter: its derived URI stage follows it
+                auto qn = qname_of_.find(std::to_string(q) + ":" + pn);
+                if (qn != qname_of_.end()) set_origin(O_QPARAM, q * MAX_QNAMES + qn->second);
+            }
+            emit(c, name, "STRING", pn, val);
         }
         return;
     }

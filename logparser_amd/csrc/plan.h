@@ -118,12 +118,19 @@ struct ResultView {
 // tables extracted from the reference's sources by the CPU tests)
 std::string token_table_json(bool nginx);
 
+// Parser.addTypeRemapping(input, newType, casts) (core/Parser.java:660-677)
+struct Remap {
+    std::string input, type;
+    int casts = CAST_S;
+};
+
 class Plan {
 public:
     // returns LP_OK / LP_E_UNSUPPORTED / error; err filled on error
-    int build(const std::string& logformats, const std::vector<std::string>& fields, std::string& err);
+    int build(const std::string& logformats, const std::vector<std::string>& fields, std::string& err,
+              const std::vector<Remap>& remaps = {});
     static int possible_paths(const std::string& logformats, int max_depth, std::vector<std::string>& out,
-                              std::string& err);
+                              std::string& err, const std::vector<Remap>& remaps = {});
 
     const Program& program() const { return prog_; }
     // Parser.getCasts(name) (core/Parser.java:127-129): CAST_* bits of a
@@ -159,13 +166,14 @@ private:
     void replay(Ctx& c) const;
     // dv: the value further dissectors read (default v)
     void emit(Ctx& c, const std::string& base, const std::string& type, const std::string& name, const MVal& v,
-              const MVal* dv = nullptr) const;
+              const MVal* dv = nullptr, bool recursion = false) const;
     void run_phase(Ctx& c, const Instance& in, const std::string& name, const MVal& v) const;
 
     std::vector<std::unique_ptr<Format>> formats_;
     std::vector<std::unique_ptr<Dissector>> dis_;
     std::string root_type_ = "HTTPLOGLINE";
     std::set<std::string> needed_, useful_, located_;
+    std::map<std::string, std::set<std::string>> remaps_;  // Parser.typeRemappings: input path -> new types
     std::map<std::string, int> casts_;  // castsOfTargets
     uint64_t gen_ = 0;                  // this build's id (the replay's per-thread memo)
     std::map<std::string, std::vector<Instance>> compiled_;
@@ -178,6 +186,8 @@ private:
     std::map<int, int> time_of_tok_, fl_of_tok_, uri_of_tok_;
     std::map<int, int> uri_of_fl_;
     std::map<int, int> query_of_uri_;
+    std::map<int, int> uri_of_qp_;         // query stage * MAX_QNAMES + name index -> derived URI stage
+    std::map<std::string, int> qname_of_;  // "query stage:name" -> name index (remapped parameters)
     // replay source tracking: emission id -> (kind, stage)
     std::map<std::string, std::pair<int, int>> src_;
 };

@@ -11,10 +11,11 @@ delivers (the Parsable.addDissection stream of lp_result_emit):
     FatalErrorDuringCallOfSetterMethod;
   * type remapping (core/Parser.java:636-677, Parsable.java:160-176): a value
     delivered at a remapped name is also delivered under each new type, whose
-    casts are STRING_ONLY unless given.  The engine has no dissectors for
-    derived values, so a remapped type that some requested path would dissect
-    further is refused at setup (the whole handle then belongs to the
-    reference dissector: FallbackRequired).
+    casts are STRING_ONLY unless given.  The engine takes care of what the
+    new type's dissectors produce (lp_compile_remapped: a remapped query
+    parameter dissected as an HTTP.URI runs as a derived URI stage on the
+    device); the emissions hold the original delivery only, and this module
+    replays the remapped one into the setters.
 """
 import enum
 import inspect

@@ -954,6 +954,7 @@ struct orc_parser {
     int ncompiled;
     slist useful;     /* usefulIntermediateFields (names) */
     slist located;
+    slist rm_in, rm_type;  /* typeRemappings as (input name, new type) pairs (core/Parser.java:639-677) */
     int unsupported;
     char unsupported_why[256];
     /* for cloning */
@@ -1186,6 +1187,13 @@ static void find_useful(orc_parser *p, slist *possible, const char *sr_type, con
             free(otype);
         }
     }
+    /* the new types of a remapped name get their dissectors (core/Parser.java:447-455) */
+    for (int k = 0; k < p->rm_in.n; k++) {
+        if (strcmp(p->rm_in.v[k], sr_name) != 0) continue;
+        char *mid = xfmt("%s:%s", p->rm_type.v[k], sr_name);
+        if (!c_get(p, mid)) find_useful(p, possible, p->rm_type.v[k], sr_name, 0);
+        free(mid);
+    }
     free(srid);
 }
 
@@ -1380,8 +1388,14 @@ static void rec_add(parsable *ps, const char *name, val v) {
     ps->nrec++;
 }
 
-/* Parsable.addDissection (core/Parsable.java:142-193), no type remappings */
+/* Parsable.addDissection (core/Parsable.java:142-193): with recursion 0, a
+ * remapped name's value is first added again under each new type
+ * (:160-176; the same type is a DissectionFailure) */
+static void add_dissection_r(parsable *ps, const char *base, const char *type, const char *name, val v, int recursion);
 static void add_dissection(parsable *ps, const char *base, const char *type, const char *name, val v) {
+    add_dissection_r(ps, base, type, name, v, 0);
+}
+static void add_dissection_r(parsable *ps, const char *base, const char *type, const char *name, val v, int recursion) {
     char complete[1024], wild[1024], needed[1024];
     if (base[0] == 0) {
         snprintf(complete, sizeof complete, "%s", name);
@@ -1392,6 +1406,12 @@ static void add_dissection(parsable *ps, const char *base, const char *type, con
         snprintf(wild, sizeof wild, "%s:%s.*", type, base);
     }
     snprintf(needed, sizeof needed, "%s:%s", type, complete);
+    if (!recursion)
+        for (int k = 0; k < ps->p->rm_in.n; k++) {
+            if (strcmp(ps->p->rm_in.v[k], complete) != 0) continue;
+            if (strcmp(ps->p->rm_type.v[k], type) == 0) { ps->failed = 1; return; }
+            add_dissection_r(ps, base, ps->p->rm_type.v[k], name, v, 1);
+        }
     if (sl_has(&ps->p->useful, complete)) {
         cache_put(ps, type, complete, v);
         todo_add(ps, type, complete);
@@ -2934,10 +2954,30 @@ static void run_instance(parsable *ps, instance *in, const char *name) {
 }
 
 /* =================================================================== API */
-static orc_parser *build(const char *logformat, const char *const *fields, int nfields, char *err, int errlen, int for_paths) {
+static orc_parser *build(const char *logformat, const char *const *fields, int nfields, const char *const *rm_in,
+                         const char *const *rm_type, int n_rm, char *err, int errlen, int for_paths) {
     pthread_once(&g_re_once, init_res);
     orc_parser *p = (orc_parser *)xmalloc(sizeof(orc_parser));
     p->logformat_arg = xstrdup(logformat);
+    /* Parser.addTypeRemapping (core/Parser.java:664-677): input trimmed +
+     * lower-cased, type trimmed + upper-cased, each pair once */
+    for (int k = 0; k < n_rm; k++) {
+        char *in = xstrdup(rm_in[k]), *ty = xstrdup(rm_type[k]);
+        for (char **x = (char *[]){in, ty, NULL}; *x; x++) {
+            char *a = *x, *b = a + strlen(a);
+            while (*a && (unsigned char)*a <= ' ') a++;
+            while (b > a && (unsigned char)b[-1] <= ' ') b--;
+            memmove(*x, a, (size_t)(b - a));
+            (*x)[b - a] = 0;
+        }
+        ascii_lower(in);
+        for (char *c = ty; *c; c++) if (*c >= 'a' && *c <= 'z') *c -= 32;
+        int dup = 0;
+        for (int j = 0; j < p->rm_in.n; j++) dup |= !strcmp(p->rm_in.v[j], in) && !strcmp(p->rm_type.v[j], ty);
+        if (!dup) { sl_add(&p->rm_in, in); sl_add(&p->rm_type, ty); }
+        free(in);
+        free(ty);
+    }
     for (int i = 0; i < nfields; i++) sl_add(&p->field_args, fields[i]);
     if (build_dissectors(p, logformat, err, errlen)) { return NULL; }
     if (for_paths) return p;
@@ -3014,7 +3054,13 @@ static orc_parser *build(const char *logformat, const char *const *fields, int n
 
 orc_parser *orc_new(const char *logformat, const char *const *fields, int nfields, char *err, int errlen) {
     if (err && errlen) err[0] = 0;
-    return build(logformat, fields, nfields, err, errlen, 0);
+    return build(logformat, fields, nfields, NULL, NULL, 0, err, errlen, 0);
+}
+
+orc_parser *orc_new_remapped(const char *logformat, const char *const *fields, int nfields, const char *const *rm_in,
+                             const char *const *rm_type, int n_rm, char *err, int errlen) {
+    if (err && errlen) err[0] = 0;
+    return build(logformat, fields, nfields, rm_in, rm_type, n_rm, err, errlen, 0);
 }
 
 void orc_free(orc_parser *p) {
@@ -3218,7 +3264,7 @@ static int scmp(const void *a, const void *b) { return strcmp(*(char *const *)a,
 int orc_possible_paths(const char *logformat, int max_depth, char *out, int out_cap) {
     char err[256];
     pthread_once(&g_re_once, init_res);
-    orc_parser *p = build(logformat, NULL, 0, err, sizeof err, 1);
+    orc_parser *p = build(logformat, NULL, 0, NULL, NULL, 0, err, sizeof err, 1);
     if (!p) return -1;
     slist paths = {0};
     find_paths(p, &paths, "", p->root_type, max_depth);

@@ -9,7 +9,7 @@
  * It restates:
  *   HttpdLoglineParser.setupDissectors        HttpdLoglineParser.java:104-126
  *   Parser.assembleDissectors / parse / store core/Parser.java:237-458,716-876
- *   Parsable.addDissection                     core/Parsable.java:142-193
+ *   Parsable.addDissection (+ type remapping)  core/Parsable.java:142-193
  *   HttpdLogFormatDissector (multi-format)     HttpdLogFormatDissector.java:99-204
  *   TokenFormatDissector compile + dissect     tokenformat/TokenFormatDissector.java:127-379
  *   ApacheHttpdLogFormatDissector              ApacheHttpdLogFormatDissector.java:73-714
@@ -48,6 +48,11 @@ typedef struct orc_parser orc_parser;
  * dissector this oracle does not restate ("unsupported: ..."). */
 orc_parser *orc_new(const char *logformat, const char *const *fields, int nfields,
                     char *err, int errlen);
+/* The same with Parser.addTypeRemapping(rm_in[k], rm_type[k]) for each k
+ * (core/Parser.java:636-677, Parsable.java:160-176). */
+orc_parser *orc_new_remapped(const char *logformat, const char *const *fields, int nfields,
+                             const char *const *rm_in, const char *const *rm_type, int n_rm,
+                             char *err, int errlen);
 void orc_free(orc_parser *p);
 
 /* Parse one line (no terminator).  Writes the canonical JSON record (NUL

@@ -23,14 +23,22 @@ struct Emu {
 
 extern "C" {
 
-void* emu_new(const char* fmt, const char* const* fields, int n, int* status, char* err, int errlen) {
+// with type remappings: rm_in[k] -> rm_type[k] (STRING_ONLY casts)
+void* emu_new_remapped(const char* fmt, const char* const* fields, int n, const char* const* rm_in,
+                       const char* const* rm_type, int n_rm, int* status, char* err, int errlen) {
     Emu* e = new Emu();
     std::vector<std::string> f(fields, fields + n);
-    e->status = e->plan.build(fmt, f, e->err);
+    std::vector<Remap> rm;
+    for (int k = 0; k < n_rm; ++k) rm.push_back(Remap{rm_in[k], rm_type[k], CAST_S});
+    e->status = e->plan.build(fmt, f, e->err, rm);
     *status = e->status;
     if (err && errlen) snprintf(err, errlen, "%s%s", e->err.c_str(), e->plan.device_ok() ? "" : e->plan.unsupported_reason().c_str());
     if (e->status != 0 && e->status != -3) { delete e; return nullptr; }
     return e;
+}
+
+void* emu_new(const char* fmt, const char* const* fields, int n, int* status, char* err, int errlen) {
+    return emu_new_remapped(fmt, fields, n, nullptr, nullptr, 0, status, err, errlen);
 }
 
 void emu_free(void* h) { delete (Emu*)h; }
@@ -147,7 +155,7 @@ static int run_line(const Program& P, const LN& L, const uint8_t* base, uint32_t
     need = (need + 15) & ~15u;
     // the region, then room for spills (a shard of its own: bump counter
     // after the region, as the kernel's shard_top)
-    const uint64_t room = need + 16ull * (uint64_t)L.n + 4096;
+    const uint64_t room = need + 64ull * (uint64_t)L.n + 8192;
     R.arena.assign(room + 64, 0);
     unsigned long long top = need;
     Arena A{R.arena.data(), 0, need};
@@ -170,6 +178,16 @@ static int run_line(const Program& P, const LN& L, const uint8_t* base, uint32_t
     }
     if (A.used > need) { snprintf(out, cap, "ARENA OVERFLOW %u > %u", A.used, need); return 3; }
     if (A.ovf) { snprintf(out, cap, "ARENA SPILL OVERFLOW"); return 3; }
+    // k_derived_lines: the remapped query parameters' URI stages, on the
+    // line in the input and the values in the region
+    if (uo.status == ST_OK) {
+        Arena D{R.arena.data(), 0, 0};
+        D.top = &top;
+        D.base = 0;
+        D.limit = room;
+        uo.status = derived_line(P, o.fmt, base + (off & ~3u), off & 3u, L.n, D, C, 0);
+        if (D.ovf) { snprintf(out, cap, "ARENA SPILL OVERFLOW (derived)"); return 3; }
+    }
     o.status = uo.status;
     C.status[0] = (uint8_t)o.status;
     return 0;

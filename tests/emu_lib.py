@@ -37,6 +37,10 @@ def lib():
         L.emu_new.restype = ctypes.c_void_p
         L.emu_new.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int,
                               ctypes.POINTER(ctypes.c_int), ctypes.c_char_p, ctypes.c_int]
+        L.emu_new_remapped.restype = ctypes.c_void_p
+        L.emu_new_remapped.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int,
+                                       ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_char_p), ctypes.c_int,
+                                       ctypes.POINTER(ctypes.c_int), ctypes.c_char_p, ctypes.c_int]
         L.emu_free.argtypes = [ctypes.c_void_p]
         L.emu_parse.restype = ctypes.c_int
         L.emu_parse.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
@@ -54,15 +58,23 @@ def lib():
     return _lib
 
 
+def _cstrs(xs):
+    arr = (ctypes.c_char_p * max(1, len(xs)))()
+    for i, x in enumerate(xs):
+        arr[i] = x.encode()
+    return arr
+
+
 class Emu:
-    def __init__(self, logformat, fields):
-        arr = (ctypes.c_char_p * max(1, len(fields)))()
-        for i, f in enumerate(fields):
-            arr[i] = f.encode()
+    def __init__(self, logformat, fields, remaps=()):
+        """remaps: [(input path, new TYPE)] (Parser.addTypeRemapping)"""
+        arr = _cstrs(fields)
         self._arr = arr
+        self._rm = (_cstrs([r[0] for r in remaps]), _cstrs([r[1] for r in remaps]))
         st = ctypes.c_int(0)
         err = ctypes.create_string_buffer(512)
-        self.h = lib().emu_new(logformat.encode(), arr, len(fields), ctypes.byref(st), err, 512)
+        self.h = lib().emu_new_remapped(logformat.encode(), arr, len(fields), self._rm[0], self._rm[1], len(remaps),
+                                        ctypes.byref(st), err, 512)
         self.status = st.value
         self.err = err.value.decode()
         if not self.h:

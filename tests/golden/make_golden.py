@@ -12,9 +12,10 @@ parser-core/src/test/java/nl/basjes/parse/core/test/TestRecord.java:47-114):
              among the values delivered for that path
   "absent":  [path, ...]    the path must not be delivered at all
   "bad":     true           the line must raise DissectionFailure
+  "remaps":  [[input path, NEW TYPE], ...] the parser's addTypeRemapping calls
 Fields the reference test asserts through dissectors this build does not
-cover (cookies, GeoIP, type remappings, screen resolution) are left out and
-listed in "skipped".
+cover (GeoIP, the Flink example's own ScreenResolutionDissector) are left out
+and listed in "skipped".
 """
 import json
 import os
@@ -33,8 +34,9 @@ DISSECTOR_TESTER_SOURCES = ("EdgeCasesTest", "NginxLogFormatTest", "NginxUpstrea
                             "TestTranslators", "AllFieldsTest")
 
 
-def case(source, logformat, line, fields, expect=None, absent=(), bad=False, skipped=(), note=""):
+def case(source, logformat, line, fields, expect=None, absent=(), bad=False, skipped=(), note="", remaps=()):
     CASES.append({
+        "remaps": [list(r) for r in remaps],
         "source": source,
         "null_present": any(k in source for k in DISSECTOR_TESTER_SOURCES),
         "logformat": logformat,
@@ -565,23 +567,31 @@ for src, text, epoch in [
     case(src, "%{" + ALL_FMT + "}t", text, [tsf("TIME.EPOCH:epoch")], expect={tsf("TIME.EPOCH:epoch"): {"l": epoch}},
          note="derived: the concatenation of the checkStrfField outputs of the same date-time")
 
-# examples/apache-flink/.../TestCase.java:37-43,86-94 (IPv6 %h, long query string); GeoIP / remapped fields skipped.
+# examples/apache-flink/.../TestCase.java:37-60,86-94 (IPv6 %h, long query string, the query parameters g and r
+# remapped to HTTP.URI and dissected again, s to the example's SCREENRESOLUTION); GeoIP / screen size skipped.
 FLINK_LINE = open(os.path.join(HERE, "flink_testcase_line.txt"), encoding="utf-8").read().rstrip("\n") \
     if os.path.exists(os.path.join(HERE, "flink_testcase_line.txt")) else None
 if FLINK_LINE:
-    case("examples/apache-flink/src/test/java/nl/basjes/parse/httpdlog/flink/TestCase.java:37-43,86-94",
+    case("examples/apache-flink/src/test/java/nl/basjes/parse/httpdlog/flink/TestCase.java:37-60,86-94",
          "%h %l %u %t \"%r\" %>s %b \"%{Referer}i\" \"%{User-Agent}i\" \"%{Cookie}i\"", FLINK_LINE,
          ["IP:connection.client.host", "TIME.STAMP:request.receive.time", "TIME.EPOCH:request.receive.time.epoch",
           "HTTP.USERAGENT:request.user-agent", "STRING:request.firstline.uri.query.g", "STRING:request.firstline.uri.query.s",
-          "HTTP.COOKIE:request.cookies.bui"],
+          "HTTP.COOKIE:request.cookies.bui", "STRING:request.firstline.uri.query.g.query.promo",
+          "STRING:request.firstline.uri.query.r.query.blabla"],
          expect={"IP:connection.client.host": "2001:980:91c0:1:8d31:a232:25e5:85d",
                  "TIME.STAMP:request.receive.time": "05/Sep/2010:11:27:50 +0200",
                  "TIME.EPOCH:request.receive.time.epoch": {"l": 1283678870000},
                  "STRING:request.firstline.uri.query.s": "1280x800",
                  "HTTP.USERAGENT:request.user-agent": "Mozilla/5.0 (Macintosh; U; Intel Mac OS X 10_6_4; nl-nl) "
                                                       "AppleWebKit/533.17.8 (KHTML, like Gecko) Version/5.0.1 Safari/533.17.8",
-                 "HTTP.COOKIE:request.cookies.bui": "SomeThing"},
-         skipped=["STRING:request.firstline.uri.query.g.query.promo (type remapping)", "GeoIP fields"])
+                 "HTTP.COOKIE:request.cookies.bui": "SomeThing",
+                 # getExpectedReferrer / getExpectedGoogleQuery (:88, :92)
+                 "STRING:request.firstline.uri.query.g.query.promo":
+                     "koken-pannen_303_hs-koken-pannen-afj-120601_B3_product_1_9200000002876066",
+                 "STRING:request.firstline.uri.query.r.query.blabla": "blablawashere"},
+         remaps=[("request.firstline.uri.query.g", "HTTP.URI"), ("request.firstline.uri.query.r", "HTTP.URI"),
+                 ("request.firstline.uri.query.s", "SCREENRESOLUTION")],
+         skipped=["SCREENWIDTH / SCREENHEIGHT (the example's own ScreenResolutionDissector)", "GeoIP fields"])
 
 # --------------------------------------------------------------------- NGINX
 # hpt/nginxmodules/NginxUpstreamTest.java:49-90 (testBasicLogFormat)

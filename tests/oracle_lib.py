@@ -30,6 +30,10 @@ def lib():
         L.orc_new.restype = ctypes.c_void_p
         L.orc_new.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int,
                               ctypes.c_char_p, ctypes.c_int]
+        L.orc_new_remapped.restype = ctypes.c_void_p
+        L.orc_new_remapped.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int,
+                                       ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_char_p), ctypes.c_int,
+                                       ctypes.c_char_p, ctypes.c_int]
         L.orc_free.argtypes = [ctypes.c_void_p]
         L.orc_parse.restype = ctypes.c_int
         L.orc_parse.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
@@ -62,11 +66,14 @@ class OracleError(Exception):
 class Oracle:
     """One oracle parser (the reference's Parser is stateful: sticky format)."""
 
-    def __init__(self, logformat, fields):
+    def __init__(self, logformat, fields, remaps=()):
+        """remaps: [(input path, new TYPE)] (Parser.addTypeRemapping)"""
         L = lib()
         err = ctypes.create_string_buffer(512)
         self._fields = _fields(fields)
-        self.h = L.orc_new(logformat.encode(), self._fields, len(fields), err, 512)
+        self._rm = (_fields([r[0] for r in remaps]), _fields([r[1] for r in remaps]))
+        self.h = L.orc_new_remapped(logformat.encode(), self._fields, len(fields), self._rm[0], self._rm[1],
+                                    len(remaps), err, 512)
         if not self.h:
             raise OracleError(err.value.decode())
         self.buf = ctypes.create_string_buffer(1 << 20)

@@ -47,3 +47,16 @@ def test_compile_requires_gpu():
     p = lpa.HttpdLoglineParser("combined", ["IP:connection.client.host"])
     with pytest.raises(lpa.EngineUnavailable):
         p.parse_batch(b"1.2.3.4 - - [31/Dec/2012:23:00:44 -0700] \"GET / HTTP/1.1\" 200 1 \"-\" \"x\"\n")
+
+
+def test_possible_paths_with_remapping():
+    """Parser.getPossiblePaths with a type remapping (core/Parser.java:954-962):
+    the remapped path and what the new type's dissectors produce below it."""
+    base = set(lpa.get_possible_paths("combined"))
+    got = set(lpa.get_possible_paths("combined", remaps=[("request.firstline.uri.query.g", "HTTP.URI", 1)]))
+    assert base < got
+    for p in ["HTTP.URI:request.firstline.uri.query.g", "HTTP.HOST:request.firstline.uri.query.g.host",
+              "HTTP.QUERYSTRING:request.firstline.uri.query.g.query",
+              "STRING:request.firstline.uri.query.g.query.*"]:
+        assert p in got, p
+    assert not any("query.g" in p for p in base)

@@ -43,7 +43,7 @@ def compare(o, e, lines, allow_fallback=True):
 def test_golden_vectors_emulated(oracle, emu, vectors):
     n_checked = 0
     for c in vectors["cases"]:
-        e = emu.Emu(c["logformat"], c["fields"])
+        e = emu.Emu(c["logformat"], c["fields"], c["remaps"])
         if e.status != 0:  # not on the device: every line FALLBACK
             assert e.parse(c["line"])[0] == 2
             continue
@@ -145,10 +145,11 @@ def test_lines_in_batch_context_emulated(oracle, emu, vectors, demolog_lines):
     records as lines parsed alone."""
     groups = {}
     for c in vectors["cases"]:
-        groups.setdefault((c["logformat"], tuple(c["fields"])), []).append(c["line"].encode())
-    groups[("combined", tuple(all_paths(oracle)))] = demolog_lines[:400] + lpa.synth_combined(8, 0, 400).split(b"\n")[:-1]
-    for (fmt, fields), lines in groups.items():
-        e = emu.Emu(fmt, list(fields))
+        groups.setdefault((c["logformat"], tuple(c["fields"]), tuple(map(tuple, c["remaps"]))), []).append(
+            c["line"].encode())
+    groups[("combined", tuple(all_paths(oracle)), ())] = demolog_lines[:400] + lpa.synth_combined(8, 0, 400).split(b"\n")[:-1]
+    for (fmt, fields, remaps), lines in groups.items():
+        e = emu.Emu(fmt, list(fields), list(remaps))
         if e.status != 0:
             continue
         for pad in range(4):
@@ -702,3 +703,31 @@ def test_strftime_conversions_emulated(oracle, emu):
     assert tot["ok"] > 800 and tot["bad"] > 150, tot
     e = emu.Emu('%h [%{%k%M}t]', strf_corpus.FIELDS)
     assert e.status == -3  # LP_E_UNSUPPORTED
+
+
+def test_type_remapping_emulated(oracle, emu):
+    """Type remappings (core/Parser.java:636-677, Parsable.java:160-176): URLs
+    in query parameters / the user agent remapped to HTTP.URI, dissected by the
+    derived URI stages; exact against the oracle's restatement."""
+    import remap_corpus as rc
+    lines = rc.corpus(7, 1500)
+    o = oracle.Oracle(rc.FORMAT, rc.FIELDS, rc.REMAPS)
+    e = emu.Emu(rc.FORMAT, rc.FIELDS, rc.REMAPS)
+    assert e.status == 0, e.err
+    s = compare(o, e, lines)
+    assert s["ok"] > 750 and s["fallback"] < 0.4 * len(lines), s
+
+
+def test_type_remapping_same_type_planner(oracle, emu):
+    """A remapping to the value's own type is a DissectionFailure for every
+    line that delivers the value (core/Parsable.java:163-168): the oracle says
+    BAD for those lines; the planner leaves the program to FALLBACK."""
+    fields = ["STRING:request.firstline.uri.query.a", "HTTP.PATH:request.firstline.uri.path"]
+    rm = [("request.firstline.uri.query.a", "STRING")]
+    o = oracle.Oracle("combined", fields, rm)
+    e = emu.Emu("combined", fields, rm)
+    assert e.status == -3 and "own type" in e.err, e.err
+    base = '1.2.3.4 - - [10/Oct/2020:13:55:36 +0200] "GET %s HTTP/1.1" 200 5 "-" "x"'
+    assert o.parse(base % "/p?a=1")[0] == oracle.BAD
+    assert o.parse(base % "/p?b=1")[0] == oracle.OK
+    assert e.parse(base % "/p?b=1")[0] == 2

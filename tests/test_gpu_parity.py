@@ -22,14 +22,17 @@ def paths(oracle, fmt="combined"):
     return _PATHS[fmt]
 
 
-def gpu_vs_oracle(oracle, fmt, fields, lines, allow_fallback=True, data=None):
-    """lines: the expected lines; data: the batch buffer (default: the lines + '\n')"""
+def gpu_vs_oracle(oracle, fmt, fields, lines, allow_fallback=True, data=None, remaps=()):
+    """lines: the expected lines; data: the batch buffer (default: the lines + '\n');
+    remaps: [(input, TYPE)] type remappings of both parsers"""
     p = lpa.HttpdLoglineParser(fmt, fields)
+    for name, typ in remaps:
+        p.add_type_remapping(name, typ)
     if data is None:
         data = b"".join(l + b"\n" for l in lines)
     r = p.parse_batch(data)
     assert r.n_lines == len(lines)
-    o = oracle.Oracle(fmt, fields)
+    o = oracle.Oracle(fmt, fields, remaps)
     stats = {"ok": 0, "bad": 0, "fallback": 0}
     for i, l in enumerate(lines):
         s2 = int(r.status[i])
@@ -55,10 +58,12 @@ def gpu_vs_oracle(oracle, fmt, fields, lines, allow_fallback=True, data=None):
 def test_golden_vectors_gpu(oracle, vectors):
     groups = {}
     for c in vectors["cases"]:
-        groups.setdefault((c["logformat"], tuple(c["fields"])), []).append(c)
+        groups.setdefault((c["logformat"], tuple(c["fields"]), tuple(map(tuple, c["remaps"]))), []).append(c)
     checked, fallback, unsupported = 0, [], 0
-    for (fmt, fields), cases in groups.items():
+    for (fmt, fields, remaps), cases in groups.items():
         p = lpa.HttpdLoglineParser(fmt, list(fields))
+        for name, typ in remaps:
+            p.add_type_remapping(name, typ)
         data = b"".join(c["line"].encode() + b"\n" for c in cases)
         r = p.parse_batch(data)
         assert r.n_lines == len(cases)
@@ -727,3 +732,17 @@ def test_strftime_conversions_gpu(oracle):
         assert s["fallback"] <= len(lines) // 10, (fmt, s)
     print("strftime corpus on the device:", tot)
     assert tot["ok"] > 3000 and tot["bad"] > 500, tot
+
+
+def test_type_remapping_gpu(oracle):
+    """Parser.addTypeRemapping (core/Parser.java:636-677): query parameters
+    holding URLs (and a user agent) remapped to HTTP.URI and dissected again
+    on the device -- derived URI stages (k_derived_lines) on values in the
+    input and decoded values in the arena, a remapped parameter of a remapped
+    URL, a remapping to a type without dissectors; exact against the oracle."""
+    import remap_corpus as rc
+    lines = rc.corpus(11, 6000)
+    s, r = gpu_vs_oracle(oracle, rc.FORMAT, rc.FIELDS, lines, remaps=rc.REMAPS)
+    print("type remapping corpus:", s)
+    assert s["ok"] > 3000, s
+    assert s["fallback"] < 0.4 * len(lines), s

@@ -46,7 +46,7 @@ def test_golden_vector(oracle, vectors, idx):
     c = cases[idx]
     if c["source"].startswith("hpt/MultiLineHttpdLogParserTest"):
         pytest.skip("sequence case: covered by test_multiline_sequence")
-    o = oracle.Oracle(c["logformat"], c["fields"])
+    o = oracle.Oracle(c["logformat"], c["fields"], c["remaps"])
     st, rec = o.parse(c["line"])
     assert golden_check.check_case(c, st, rec or {}) == [], c["source"]
 
