@@ -297,7 +297,14 @@ int lp_casts(lp_handle *h, const char *target);
  * small (chars_len = bytes needed: call again); LP_E_MISSING for a path the
  * handle does not deliver; LP_E_INVALID when the path's casts (lp_casts) do
  * not include the column's type (the reference's store would call no setter).
- * threads: host threads to replay with. */
+ * threads: host threads to replay with.
+ * On a device view (r from lp_result_view, on_host 0) the table is built on
+ * the GPU from the batch still in HBM (its input must still be valid):
+ * valid / i64 / f64 / chars are then device buffers of the handle's device,
+ * the call returns once they are filled, and LP_E_UNSUPPORTED names a path
+ * whose value only the host replay derives (cookies, Set-Cookie, upstream
+ * lists, converters of converters, remapped deliveries) or a DOUBLE column of
+ * a string-valued path: build those from a host copy. */
 typedef struct lp_table_col {
     const char *path;
     int32_t kind;

@@ -356,6 +356,57 @@ class BatchResult:
                 out[path] = ((i64[:count] if typ is int else f64[:count]).copy(), ok)
         return out
 
+    def table_device(self, columns, first=0, count=None, chars_cap=None):
+        """lp_result_table on the device view: typed columns of rows [first,
+        first+count) built in HBM.  columns: [(path, str | int | float)].
+        Returns {path: (values, valid)} of torch tensors on the handle's
+        device: valid uint8 [count]; STRING columns the Arrow pair (offsets
+        int64 [count + 1], chars uint8), BIGINT int64 / DOUBLE float64 [count].
+        chars_cap: bytes allotted per STRING column (default: enough after a
+        first call that reports the need)."""
+        import torch
+        count = self.n_lines - first if count is None else count
+        dev = torch.device("cuda", self._p.device)
+        kinds = {str: CAST_STRING, int: CAST_LONG, float: CAST_DOUBLE}
+        res = LpResult()
+        L = lib()
+        rc = L.lp_result_view(self._p._h, ctypes.byref(res))
+        if rc != LP_OK:
+            raise EngineUnavailable("lp_result_view failed: %d" % rc)
+        cols = (LpTableCol * len(columns))()
+        keep = []
+        for k, (path, typ) in enumerate(columns):
+            c = cols[k]
+            c.path = path.encode()
+            c.kind = kinds[typ]
+            valid = torch.empty(max(1, count), dtype=torch.uint8, device=dev)
+            i64 = torch.empty(count + 1 if typ is str else max(1, count), dtype=torch.int64, device=dev)
+            f64 = torch.empty(max(1, count), dtype=torch.float64, device=dev)
+            chars = torch.empty(max(1, chars_cap or 1), dtype=torch.uint8, device=dev) if typ is str else None
+            c.valid, c.i64, c.f64 = valid.data_ptr(), i64.data_ptr(), f64.data_ptr()
+            if chars is not None:
+                c.chars, c.chars_cap = chars.data_ptr(), chars.numel() if chars_cap else 0
+            keep.append([valid, i64, f64, chars])
+        rc = L.lp_result_table(self._p._h, ctypes.byref(res), first, count, cols, len(columns), 0)
+        if rc == LP_E_NOMEM:
+            for k, (path, typ) in enumerate(columns):
+                if typ is str and cols[k].chars_len > cols[k].chars_cap:
+                    keep[k][3] = torch.empty(max(1, cols[k].chars_len), dtype=torch.uint8, device=dev)
+                    cols[k].chars, cols[k].chars_cap = keep[k][3].data_ptr(), keep[k][3].numel()
+            rc = L.lp_result_table(self._p._h, ctypes.byref(res), first, count, cols, len(columns), 0)
+        if rc == LP_E_UNSUPPORTED:
+            raise FallbackRequired("a column's values are derived on the host only: use table_from")
+        if rc != LP_OK:
+            raise ValueError("lp_result_table (device) failed: %d" % rc)
+        out = {}
+        for k, (path, typ) in enumerate(columns):
+            valid, i64, f64, chars = keep[k]
+            if typ is str:
+                out[path] = ((i64, chars[:cols[k].chars_len]), valid[:count])
+            else:
+                out[path] = ((i64 if typ is int else f64)[:count], valid[:count])
+        return out
+
     def record_json_from(self, res, i):
         """lp_result_record_json: the record of line i from a host copy."""
         cap = 1 << 16

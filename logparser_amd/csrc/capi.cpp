@@ -61,6 +61,7 @@ struct lp_handle {
     int device = 0;
     hipStream_t stream = nullptr;
     DevBuf input, chunk, line_off, cols, arena, meta, waves, args, route, ovf, hist;
+    DevBuf targs, tscratch;  // device table (lp_result_table on a device view)
     lp::DeviceArgs host_args{};
     lp::Columns C{};
     std::vector<ColSpec> specs;
@@ -507,7 +508,7 @@ void lp_free(lp_handle* h) {
     hipSetDevice(h->device);
     if (h->pending) hipStreamSynchronize(h->stream);
     for (auto* b : {&h->input, &h->chunk, &h->line_off, &h->cols, &h->arena, &h->meta, &h->waves, &h->args, &h->route,
-                    &h->ovf, &h->hist})
+                    &h->ovf, &h->hist, &h->targs, &h->tscratch})
         b->release();
     if (h->have_events)
         for (auto& ev : h->ev) hipEventDestroy(ev);
@@ -861,9 +862,81 @@ void table_value(void* vctx, const std::string& target, const lp::MVal& v) {
 }
 }  // namespace
 
+// lp_result_table on a device view: the columns built in HBM (table.hip)
+static int table_device(lp_handle* h, int64_t first, int64_t count, lp_table_col* cols, int n_cols) {
+    if (ensure_synced(h) != LP_OK) return LP_E_STATE;
+    if (first < 0 || count < 0 || first + count > h->n_lines || n_cols > lp::MAX_TABLE_COLS) return LP_E_INVALID;
+    auto ta = std::make_unique<lp::TableArgs>();
+    memset(ta.get(), 0, sizeof(lp::TableArgs));
+    ta->first = first;
+    ta->count = count;
+    ta->n_cols = n_cols;
+    std::string names;
+    for (int c = 0; c < n_cols; ++c) {
+        lp_table_col& C = cols[c];
+        lp::TableCol& T = ta->cols[c];
+        T.kind = C.kind;
+        if (!h->plan.table_src(C.path, T.src, names)) return LP_E_UNSUPPORTED;
+        if (C.kind == LP_CAST_DOUBLE)  // Double.parseDouble of a string stays on the host table
+            for (const auto& x : T.src) {
+                const bool long_valued = x.kind == lp::TC_NONE || x.kind == lp::TC_NULL ||
+                                         (x.kind == lp::TC_URI && x.b == lp::UP_PORT) ||
+                                         (x.kind == lp::TC_TIME && x.b != lp::TF_MONTHNAME && x.b != lp::TF_DATE &&
+                                          x.b != lp::TF_TIME);
+                if (!long_valued) return LP_E_UNSUPPORTED;
+            }
+        T.valid = C.valid;
+        T.i64 = C.i64;
+        T.f64 = C.f64;
+        T.chars = (uint8_t*)C.chars;
+    }
+    memcpy(ta->names, names.data(), names.size());
+    hipSetDevice(h->device);
+    hipStream_t s = h->stream;
+    if (!h->targs.ensure(sizeof(lp::TableArgs))) return LP_E_NOMEM;
+    const size_t scratch = lp::table_scratch_bytes(count);
+    if (!h->tscratch.ensure(scratch)) return LP_E_NOMEM;
+    if (hipMemcpyAsync(h->targs.p, ta.get(), sizeof(lp::TableArgs), hipMemcpyHostToDevice, s) != hipSuccess) return LP_E_DEVICE;
+    const lp::DeviceArgs* d_args = h->args.as<lp::DeviceArgs>();
+    const lp::TableArgs* d_targs = h->targs.as<lp::TableArgs>();
+    if (lp::launch_table_values(d_args, d_targs, *ta, h->d_buf, h->tscratch.p, h->tscratch.cap, s) != 0) return LP_E_DEVICE;
+    // the STRING columns' byte counts decide whether their bytes fit
+    std::vector<int64_t> tot(n_cols, 0);
+    for (int c = 0; c < n_cols; ++c)
+        if (cols[c].kind == LP_CAST_STRING &&
+            hipMemcpyAsync(&tot[c], cols[c].i64 + count, 8, hipMemcpyDeviceToHost, s) != hipSuccess)
+            return LP_E_DEVICE;
+    if (hipStreamSynchronize(s) != hipSuccess) return LP_E_DEVICE;
+    bool fits = true;
+    for (int c = 0; c < n_cols; ++c) {
+        if (cols[c].kind != LP_CAST_STRING) continue;
+        cols[c].chars_len = (uint64_t)tot[c];
+        if (cols[c].chars_len > cols[c].chars_cap || (tot[c] && !cols[c].chars)) fits = false;
+    }
+    if (!fits) return LP_E_NOMEM;
+    if (lp::launch_table_chars(d_args, d_targs, count, h->d_buf, s) != 0) return LP_E_DEVICE;
+    return hipStreamSynchronize(s) == hipSuccess ? LP_OK : LP_E_DEVICE;
+}
+
 int lp_result_table(lp_handle* h, const lp_result* r, int64_t first, int64_t count, lp_table_col* cols, int n_cols,
                     int threads) {
-    if (!h || !r || !cols || n_cols <= 0 || !r->on_host || !r->input) return LP_E_INVALID;
+    if (!h || !r || !cols || n_cols <= 0) return LP_E_INVALID;
+    for (int c = 0; c < n_cols; ++c) {  // the same validation in both modes
+        const lp_table_col& C = cols[c];
+        if (!C.path || !C.valid || (C.kind == LP_CAST_STRING ? !C.i64 : C.kind == LP_CAST_LONG ? !C.i64 : !C.f64))
+            return LP_E_INVALID;
+        if (C.kind != LP_CAST_STRING && C.kind != LP_CAST_LONG && C.kind != LP_CAST_DOUBLE) return LP_E_INVALID;
+        std::string p = C.path;
+        int casts = h->plan.casts(p);
+        if (casts < 0) {
+            const size_t dot = p.rfind('.');
+            if (dot != std::string::npos) casts = h->plan.casts(p.substr(0, dot) + ".*");
+        }
+        if (casts < 0) return LP_E_MISSING;
+        if (!(casts & C.kind)) return LP_E_INVALID;
+    }
+    if (!r->on_host) return table_device(h, first, count, cols, n_cols);
+    if (!r->input) return LP_E_INVALID;
     if (first < 0 || count < 0 || first + count > r->n_lines) return LP_E_INVALID;
     std::unordered_map<std::string, std::vector<int>> by_path;
     for (int c = 0; c < n_cols; ++c) {

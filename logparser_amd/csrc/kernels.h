@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include "lp_program.h"
+#include "lp_table.h"
 
 namespace lp {
 
@@ -58,5 +59,15 @@ int launch_route(const DeviceArgs* d_args, int64_t cap_lines, hipStream_t s);
 // (HIST_WORDS u64, zeroed here): layout in include/logparser_amd.h
 constexpr int HIST_WORDS = 1024;
 int launch_histograms(const DeviceArgs* d_args, const uint8_t* buf, int64_t cap_lines, uint64_t* hist, hipStream_t s);
+
+// device table (table.hip, lp_table.h): scratch bytes for count rows; the
+// values / validity / STRING offsets of rows [ta.first, ta.first + ta.count)
+// (d_targs: ta on the device; buf: the batch's input); then, once the caller
+// checked the offsets' totals against its capacities, the STRING bytes
+size_t table_scratch_bytes(int64_t count);
+int launch_table_values(const DeviceArgs* d_args, const TableArgs* d_targs, const TableArgs& ta, const uint8_t* buf,
+                        void* scratch, size_t scratch_bytes, hipStream_t s);
+int launch_table_chars(const DeviceArgs* d_args, const TableArgs* d_targs, int64_t count, const uint8_t* buf,
+                       hipStream_t s);
 
 }  // namespace lp

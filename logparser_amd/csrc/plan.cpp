@@ -1062,6 +1062,45 @@ int Plan::casts_of(const Dissector& d, const std::string& otype, const std::stri
     (void)otype;
 }
 
+bool Plan::table_src(const std::string& path, TableSrc out[MAX_FMT], std::string& names) const {
+    const size_t colon = path.find(':');
+    if (colon == std::string::npos || !device_ok_) return false;
+    const std::string type = path.substr(0, colon), name = path.substr(colon + 1);
+    for (int f = 0; f < MAX_FMT; ++f) out[f] = TableSrc{TC_NONE, 0, 0, 0};
+    for (int f = 0; f < prog_.n_fmt; ++f) {
+        auto it = tsrc_[f].find(path);
+        if (it != tsrc_[f].end()) {
+            if (it->second.kind < 0) return false;
+            out[f] = it->second;
+            continue;
+        }
+        if (thost_exact_[f].count(path)) return false;
+        // a query parameter: "STRING:<query string's name>.<parameter>" of the
+        // longest such query string
+        const std::string* best = nullptr;
+        int q = -1;
+        if (type == "STRING")
+            for (const auto& kv : tqp_[f])
+                if (name.size() > kv.first.size() + 1 && name.compare(0, kv.first.size(), kv.first) == 0 &&
+                    name[kv.first.size()] == '.' && (!best || kv.first.size() > best->size())) {
+                    best = &kv.first;
+                    q = kv.second;
+                }
+        for (const auto& h : thost_prefix_[f])
+            if ((name == h || (name.size() > h.size() && name.compare(0, h.size(), h) == 0 && name[h.size()] == '.')) &&
+                (!best || h.size() > best->size()))
+                return false;  // below a value only the replay dissects
+        if (best) {
+            if (q < 0) return false;
+            const std::string pn = name.substr(best->size() + 1);
+            if (names.size() + pn.size() > (size_t)TABLE_NAMES) return false;
+            out[f] = TableSrc{TC_QP, q, (int32_t)names.size(), (int32_t)pn.size()};
+            names += pn;
+        }
+    }
+    return true;
+}
+
 int Plan::casts(const std::string& target) const {
     auto it = casts_.find(target);
     return it == casts_.end() ? -1 : it->second;
@@ -1351,6 +1390,33 @@ void Plan::compile_program() {
     // remapped: this visit is a type remapping's second delivery of a value
     // (Parsable.addDissection with recursion, core/Parsable.java:160-176)
     std::set<std::string> remap_seen;  // remapped names whose values the walk reached
+    // the requested fields of time stage t (TimeStampDissector outputs, the
+    // replay's D_TIMESTAMP case)
+    std::function<void(const Instance&, const std::string&, int)> treg_time;
+    // device table sources (lp_table.h); a path with two different sources is left to the host
+    auto treg = [&](const std::string& path, TableSrc ts) {
+        auto& m = tsrc_[cur_fmt];
+        auto it = m.find(path);
+        if (it == m.end()) m[path] = ts;
+        else if (memcmp(&it->second, &ts, sizeof ts) != 0) it->second.kind = -1;
+    };
+    auto thost = [&](const std::string& name) { thost_prefix_[cur_fmt].insert(name); };
+    treg_time = [&](const Instance& in, const std::string& complete, int t) {
+        static const char* const fn[] = {"epoch", "day", "monthname", "month", "weekofweekyear", "weekyear", "year",
+                                         "hour", "minute", "second", "millisecond", "microsecond", "nanosecond",
+                                         "date", "time"};
+        for (const auto& r : in.requested) {
+            const bool utc = r.size() > 4 && r.compare(r.size() - 4, 4, "_utc") == 0;
+            const std::string base = utc ? r.substr(0, r.size() - 4) : r;
+            int tf = -1;
+            for (int k = 0; k < 15; ++k) if (base == fn[k]) tf = k;
+            if (tf < 0 || (utc && tf == TF_EPOCH)) continue;  // timezone: never delivered
+            std::string type;
+            for (const auto& o : in.d->outs)
+                if (o.compare(o.find(':') + 1, std::string::npos, r) == 0) type = o.substr(0, o.find(':'));
+            if (!type.empty()) treg(type + ":" + complete + "." + r, TableSrc{TC_TIME, t, tf, utc ? 1 : 0});
+        }
+    };
     std::function<void(int, int, const std::string&, const std::string&, bool)> walk =
         [&](int ok, int oi, const std::string& type, const std::string& complete, bool remapped) {
             if (!device_ok_) return;
@@ -1364,6 +1430,7 @@ void Plan::compile_program() {
                             why_ = "type remapping to the value's own type";
                             return;
                         }
+                        thost_exact_[cur_fmt].insert(mt + ":" + complete);  // the remapped delivery itself
                         walk(ok, oi, mt, complete, true);
                     }
                 }
@@ -1382,6 +1449,7 @@ void Plan::compile_program() {
                         P.time[P.n_time].kind = in.cls == D_TIMESTAMP_ISO ? TK_ISO : TK_APACHE;
                         time_of_tok_[tk(oi)] = P.n_time++;
                     }
+                    treg_time(in, complete, time_of_tok_[tk(oi)]);
                     break;
                 }
                 case D_STRFTIME: {
@@ -1404,10 +1472,12 @@ void Plan::compile_program() {
                         }
                         time_of_tok_[tk(oi)] = P.n_time++;
                     }
+                    treg_time(in, complete, time_of_tok_[tk(oi)]);
                     break;
                 }
                 case D_LOCALIZED:
                     if (ok != O_TOKEN) { device_ok_ = false; why_ = "localized time from a derived value"; return; }
+                    treg("TIME.LOCALIZEDSTRING:" + complete, TableSrc{TC_TOKEN, oi, 0, 0});
                     break;
                 case D_SETCOOKIES: {
                     // ResponseSetCookieListDissector / ResponseSetCookieDissector:
@@ -1415,6 +1485,7 @@ void Plan::compile_program() {
                     // proves HttpCookie.parse and parseExpire cannot throw (setcookie_ok)
                     if (ok != O_TOKEN) { device_ok_ = false; why_ = "Set-Cookie list from a derived value"; return; }
                     P.guard_setc[cur_fmt] |= 1 << oi;
+                    thost(complete);
                     const std::string pre = "HTTP.SETCOOKIE:" + complete + ".";
                     for (const auto& kv : compiled_)
                         if (kv.first.compare(0, pre.size(), pre) == 0) P.guard_setc_exp[cur_fmt] |= 1 << oi;
@@ -1425,6 +1496,7 @@ void Plan::compile_program() {
                     // the device proves the decode cannot fail (guard_pct)
                     if (ok != O_TOKEN) { device_ok_ = false; why_ = "cookies from a derived value"; return; }
                     P.guard_pct[cur_fmt] |= 1 << oi;
+                    thost(complete);
                     break;
                 case D_FIRSTLINE: {
                     if (ok != O_TOKEN) { device_ok_ = false; why_ = "first line from a derived value"; return; }
@@ -1436,6 +1508,9 @@ void Plan::compile_program() {
                         fl_of_tok_[tk(oi)] = P.n_fl++;
                     }
                     fidx = fl_of_tok_[tk(oi)];
+                    treg("HTTP.METHOD:" + complete + ".method", TableSrc{TC_FL, fidx, 0, 0});
+                    treg("HTTP.URI:" + complete + ".uri", TableSrc{TC_FL, fidx, 1, 0});
+                    treg("HTTP.PROTOCOL_VERSION:" + complete + ".protocol", TableSrc{TC_FL, fidx, 2, 0});
                     walk(O_FL_URI, fidx, "HTTP.URI", complete + ".uri", false);
                     walk(O_FL_PROTO, fidx, "HTTP.PROTOCOL_VERSION", complete + ".protocol", false);
                     walk(O_FL_METHOD, fidx, "HTTP.METHOD", complete + ".method", false);
@@ -1445,6 +1520,13 @@ void Plan::compile_program() {
                     // the replay splits the value (first-line protocol, or a
                     // HTTP.PROTOCOL_VERSION token such as NGINX $server_protocol)
                     if (ok != O_FL_PROTO && ok != O_TOKEN) { device_ok_ = false; why_ = "protocol from a derived value"; return; }
+                    if (ok == O_FL_PROTO) {
+                        treg("HTTP.PROTOCOL:" + complete, TableSrc{TC_PROTO, oi, 0, 0});
+                        treg("HTTP.PROTOCOL.VERSION:" + complete + ".version", TableSrc{TC_PROTO, oi, 1, 0});
+                    } else {
+                        thost_exact_[cur_fmt].insert("HTTP.PROTOCOL:" + complete);
+                        thost(complete);
+                    }
                     break;
                 case D_URI: {
                     // a token, a first line's uri, or a remapped query parameter (derived stage)
@@ -1469,6 +1551,13 @@ void Plan::compile_program() {
                     if (in.requested.count("path")) U.want_path = 1;
                     if (in.requested.count("ref")) U.want_ref = 1;
                     if (in.requested.count("userinfo")) U.want_userinfo = 1;
+                    treg("HTTP.QUERYSTRING:" + complete + ".query", TableSrc{TC_URI, u, UP_QUERY, 0});
+                    treg("HTTP.PATH:" + complete + ".path", TableSrc{TC_URI, u, UP_PATH, 0});
+                    treg("HTTP.REF:" + complete + ".ref", TableSrc{TC_URI, u, UP_REF, 0});
+                    treg("HTTP.PROTOCOL:" + complete + ".protocol", TableSrc{TC_URI, u, UP_PROTOCOL, 0});
+                    treg("HTTP.HOST:" + complete + ".host", TableSrc{TC_URI, u, UP_HOST, 0});
+                    treg("HTTP.PORT:" + complete + ".port", TableSrc{TC_URI, u, UP_PORT, 0});
+                    treg("HTTP.USERINFO:" + complete + ".userinfo", TableSrc{TC_NULL, 0, 0, 0});
                     walk(O_URI_QUERY, u, "HTTP.QUERYSTRING", complete + ".query", false);
                     break;
                 }
@@ -1478,6 +1567,7 @@ void Plan::compile_program() {
                         // split / decoded in the replay, the device proves the
                         // decode cannot fail (guard_pct, as for cookies)
                         P.guard_pct[cur_fmt] |= 1 << oi;
+                        thost(complete);
                         break;
                     }
                     if (ok != O_URI_QUERY) { device_ok_ = false; why_ = "query string from a derived value"; return; }
@@ -1491,6 +1581,10 @@ void Plan::compile_program() {
                         query_of_uri_[oi] = P.n_query++;
                     }
                     QueryStage& Q = P.query[U.query_stage];
+                    {  // two query stages delivering under one name: the host table decides
+                        auto tq = tqp_[cur_fmt].emplace(complete, U.query_stage);
+                        if (!tq.second && tq.first->second != U.query_stage) tq.first->second = -1;
+                    }
                     for (const auto& r : in.requested) {
                         if (r == "*") { Q.want_all = 1; continue; }
                         bool dup = false;
@@ -1519,12 +1613,17 @@ void Plan::compile_program() {
                 case D_CLF2NUM: case D_NUM2CLF: case D_SECMILLIS: case D_MS2US: case D_BINIP:
                     // value-level conversions, done in the replay from the token / list item
                     if (ok != O_TOKEN && ok != O_CONV) { device_ok_ = false; why_ = "converter on a derived value"; return; }
+                    if (ok == O_TOKEN && (in.cls == D_CLF2NUM || in.cls == D_NUM2CLF))
+                        treg(in.d->out_type + ":" + complete, TableSrc{in.cls == D_CLF2NUM ? TC_CLF2NUM : TC_NUM2CLF, oi, 0, 0});
+                    else
+                        thost_exact_[cur_fmt].insert(in.d->out_type + ":" + complete);
                     walk(O_CONV, oi, in.d->out_type, complete, false);
                     break;
                 case D_UPSTREAM: {
                     // the list token's element kind (EK_UPLIST_*) proves the list
                     // splits into clean items; the split is done in the replay
                     if (ok != O_TOKEN) { device_ok_ = false; why_ = "upstream list from a derived value"; return; }
+                    thost(complete);
                     for (int k = 0; k < 32; ++k)
                         for (const char* sfx : {".value", ".redirected"})
                             walk(O_CONV, oi, in.d->out_type, complete + "." + std::to_string(k) + sfx, false);
@@ -1542,7 +1641,10 @@ void Plan::compile_program() {
         for (int i = 0; i < (int)f.tokens.size(); ++i) {
             auto it = tok_slot_.find(cur_fmt * 256 + i);
             if (it == tok_slot_.end()) continue;
-            for (const auto& o : f.tokens[i].outs) walk(O_TOKEN, it->second, o.type, o.name, false);
+            for (const auto& o : f.tokens[i].outs) {
+                treg(o.type + ":" + o.name, TableSrc{TC_TOKEN, it->second, 0, 0});
+                walk(O_TOKEN, it->second, o.type, o.name, false);
+            }
         }
     }
     // a remapped name whose new type has dissectors but whose values the walk

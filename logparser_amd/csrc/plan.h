@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "lp_program.h"
+#include "lp_table.h"
 
 namespace lp {
 
@@ -153,6 +154,11 @@ public:
     // by the value's full path)
     using RecFn = void (*)(void* ctx, const std::string& target, const MVal& v);
     int rec_row(const ResultView& R, int64_t i, RecFn fn, void* ctx) const;
+    // where the device table finds a requested "TYPE:path" (lp_table.h), per
+    // LogFormat; a query parameter's name is appended to `names` (its
+    // offset / length in the source).  false: some LogFormat derives the
+    // value in the host replay only
+    bool table_src(const std::string& path, TableSrc out[MAX_FMT], std::string& names) const;
 
 private:
     int build_dissectors(const std::string& logformats, std::string& err);
@@ -188,6 +194,12 @@ private:
     std::map<int, int> query_of_uri_;
     std::map<int, int> uri_of_qp_;         // query stage * MAX_QNAMES + name index -> derived URI stage
     std::map<std::string, int> qname_of_;  // "query stage:name" -> name index (remapped parameters)
+    // device table sources per LogFormat (compile_program): exact paths, the
+    // query stages by the name of their query string, and what only the
+    // replay derives (exact paths, and names below which it derives values)
+    std::map<std::string, TableSrc> tsrc_[MAX_FMT];
+    std::map<std::string, int> tqp_[MAX_FMT];
+    std::set<std::string> thost_exact_[MAX_FMT], thost_prefix_[MAX_FMT];
     // replay source tracking: emission id -> (kind, stage)
     std::map<std::string, std::pair<int, int>> src_;
 };

@@ -1,0 +1,321 @@
+// gfx950 kernels of the device table: lp_result_table on a device view
+// (include/logparser_amd.h), the ParsedRecord / Hive SerDe output side
+// (httpdlog-inputformat/.../ParsedRecord.java:154-214: set(name, value), a
+// null ignored, the last value wins; httpdlog-serde/.../ApacheHttpdlogDeserializer.java:
+// 224-240, 295-323: STRING / BIGINT / DOUBLE columns, one row per line) built
+// from the parse kernels' SoA columns without leaving HBM:
+//
+//   k_table_values  one lane per row: each column's value from the source the
+//                   planner named (lp_table.h), the validity byte, LONG /
+//                   DOUBLE values, and each STRING value's length
+//   (scan)          the lengths -> Arrow offsets (hipCUB inclusive sum)
+//   k_table_chars   one lane per row: the STRING values' bytes at their offsets
+//
+// What each source delivers mirrors Plan::replay (plan.cpp) case by case.
+#include <hip/hip_runtime.h>
+
+#define LP_KERNEL_TU 1  // device column pointers are global-memory pointers (lp_program.h)
+
+#include <hipcub/hipcub.hpp>
+
+#include "kernels.h"
+#include "lp_device.h"
+
+namespace lp {
+
+namespace {
+
+constexpr int TB = 256;
+
+// one value: 0 none (null / not delivered), 1 bytes at p (amp: a '&' first),
+// 2 a long, 3 bytes in buf
+struct TVal {
+    int kind = 0;
+    const LP_G uint8_t* p = nullptr;
+    uint32_t n = 0;
+    bool amp = false;
+    int64_t l = 0;
+    char buf[12];
+};
+
+__constant__ char MONTH_TEXT[] = "JanuaryFebruaryMarchAprilMayJuneJulyAugustSeptemberOctoberNovemberDecember";
+__constant__ uint8_t MONTH_OFF[13] = {0, 7, 15, 20, 25, 28, 32, 36, 42, 51, 58, 66, 74};
+
+__device__ __forceinline__ void put2(char* b, int64_t v) {
+    b[0] = (char)('0' + v / 10);
+    b[1] = (char)('0' + v % 10);
+}
+
+__device__ __forceinline__ uint32_t digits(int64_t l) {
+    uint64_t u = l < 0 ? 0 - (uint64_t)l : (uint64_t)l;
+    uint32_t n = 1;
+    while (u >= 10) { u /= 10; ++n; }
+    return n + (l < 0 ? 1u : 0u);
+}
+
+__device__ __forceinline__ void write_long(LP_G uint8_t* d, int64_t l, uint32_t n) {  // n = digits(l)
+    uint64_t u = l < 0 ? 0 - (uint64_t)l : (uint64_t)l;
+    uint32_t k = n;
+    do {
+        d[--k] = (uint8_t)('0' + u % 10);
+        u /= 10;
+    } while (u);
+    if (l < 0) d[0] = '-';
+}
+
+// Long.parseLong (the host table's java_parse_long)
+__device__ bool parse_long(const LP_G uint8_t* p, uint32_t n, bool amp, int64_t& out) {
+    if (amp || n == 0) return false;
+    uint32_t k = 0;
+    bool neg = false;
+    if (p[0] == '-' || p[0] == '+') { neg = p[0] == '-'; k = 1; }
+    if (k == n) return false;
+    uint64_t v = 0;
+    for (; k < n; ++k) {
+        const uint32_t d = p[k] - '0';
+        if (d > 9) return false;
+        if (v > (0x8000000000000000ull - d) / 10) return false;  // past 2^63
+        v = v * 10 + d;
+    }
+    if (!neg && v == 0x8000000000000000ull) return false;
+    out = neg ? (int64_t)(0 - v) : (int64_t)v;
+    return true;
+}
+
+__device__ TVal tvalue(const Program& P, const Columns& C, const TableArgs& T, const TableSrc& s, int64_t i,
+                       const LP_G uint8_t* line, const LP_G uint8_t* region) {
+    TVal v;
+    auto bytes = [&](const LP_G uint8_t* p, uint32_t n) {
+        v.kind = 1;
+        v.p = p;
+        v.n = n;
+    };
+    auto span = [&](uint32_t sp) { bytes(line + (sp & 0xFFFFu), (sp >> 16) - (sp & 0xFFFFu)); };
+    auto ref = [&](uint64_t r) {
+        bytes((ref_arena(r) ? region : line) + ref_off(r), ref_len(r));
+        v.amp = ref_amp(r);
+    };
+    auto along = [&](int64_t l) {
+        v.kind = 2;
+        v.l = l;
+    };
+    switch (s.kind) {
+    case TC_TOKEN: case TC_CLF2NUM: case TC_NUM2CLF: {
+        const bool null = (C.tok_flags[i] >> s.a) & 1u;
+        if (null) {
+            if (s.kind == TC_CLF2NUM) along(0);  // ConvertCLFIntoNumber: null -> 0L
+            return v;
+        }
+        span(C.tok_span[s.a][i]);
+        if (s.kind == TC_NUM2CLF && v.n == 1 && v.p[0] == '0') v.kind = 0;  // "0" -> null
+        return v;
+    }
+    case TC_TIME: {
+        const TimeStage& TS = P.time[s.a];
+        const uint32_t sp = C.tok_span[TS.tok][i];
+        if (((C.tok_flags[i] >> TS.tok) & 1u) || (sp >> 16) <= (sp & 0xFFFFu)) return v;  // null / empty: no dissection
+        if (s.b == TF_EPOCH) { along(C.t_epoch[s.a][i]); return v; }
+        const uint64_t w = s.c ? C.t_utc[s.a][i] : C.t_local[s.a][i];
+        const int64_t Y = w & 0xFFFF, MO = (w >> 16) & 15, D = (w >> 20) & 31, H = (w >> 25) & 31, MI = (w >> 30) & 63,
+                      S = (w >> 36) & 63, WY = (w >> 42) & 0xFFFF, WK = (w >> 58) & 63;
+        const int64_t nanos = TS.kind == TK_STRF ? (int64_t)C.t_nano[s.a][i] : 0;
+        switch (s.b) {
+        case TF_DAY: along(D); break;
+        case TF_MONTH: along(MO); break;
+        case TF_WEEK: along(WK); break;
+        case TF_WEEKYEAR: along(WY); break;
+        case TF_YEAR: along(Y); break;
+        case TF_HOUR: along(H); break;
+        case TF_MINUTE: along(MI); break;
+        case TF_SECOND: along(S); break;
+        case TF_MILLI: along(nanos / 1000000); break;
+        case TF_MICRO: along(nanos / 1000); break;
+        case TF_NANO: along(nanos); break;
+        case TF_MONTHNAME:
+            v.kind = 3;
+            v.n = MONTH_OFF[MO] - MONTH_OFF[MO - 1];
+            for (uint32_t k = 0; k < v.n; ++k) v.buf[k] = MONTH_TEXT[MONTH_OFF[MO - 1] + k];
+            break;
+        case TF_DATE:  // "%04d-%02d-%02d"
+            v.kind = 3;
+            v.n = 10;
+            put2(v.buf, Y / 100);
+            put2(v.buf + 2, Y % 100);
+            v.buf[4] = '-';
+            put2(v.buf + 5, MO);
+            v.buf[7] = '-';
+            put2(v.buf + 8, D);
+            break;
+        case TF_TIME:  // "%02d:%02d:%02d"
+            v.kind = 3;
+            v.n = 8;
+            put2(v.buf, H);
+            v.buf[2] = ':';
+            put2(v.buf + 3, MI);
+            v.buf[5] = ':';
+            put2(v.buf + 6, S);
+            break;
+        default: break;
+        }
+        return v;
+    }
+    case TC_FL: {
+        const uint32_t kind = C.fl_kind[s.a][i];
+        if (kind == FL_NONE) return v;
+        if (s.b == 0) span(C.fl_method[s.a][i]);
+        else if (s.b == 1) span(C.fl_uri[s.a][i]);
+        else if (kind == FL_FULL) span(C.fl_proto[s.a][i]);  // a chopped line's protocol is null
+        return v;
+    }
+    case TC_PROTO: {  // HttpFirstLineProtocolDissector: "HTTP/x.y".split("/", 2)
+        if (C.fl_kind[s.a][i] != FL_FULL) return v;
+        span(C.fl_proto[s.a][i]);
+        if (v.n == 0 || (v.n == 1 && v.p[0] == '-')) { v.kind = 0; return v; }
+        uint32_t sl = 0;
+        while (sl < v.n && v.p[sl] != '/') ++sl;
+        if (sl == v.n) { v.kind = 0; return v; }  // no '/': both null
+        if (s.b == 0) v.n = sl;
+        else { v.p += sl + 1; v.n -= sl + 1; }
+        return v;
+    }
+    case TC_URI: {
+        const uint32_t f = C.u_flags[s.a][i];
+        if (!(f & UF_DONE)) return v;
+        switch (s.b) {
+        case UP_QUERY: ref(C.u_query[s.a][i]); break;
+        case UP_PATH: ref(C.u_path[s.a][i]); break;
+        case UP_REF: if (f & UF_FRAG) ref(C.u_frag[s.a][i]); break;
+        case UP_PROTOCOL: if ((f & UF_IS_URL) && (f & UF_SCHEME)) ref(C.u_scheme[s.a][i]); break;
+        case UP_HOST: if ((f & UF_IS_URL) && (f & UF_HOST)) ref(C.u_host[s.a][i]); break;
+        case UP_PORT: if ((f & UF_IS_URL) && (f & UF_PORT)) along(C.u_port[s.a][i]); break;
+        default: break;
+        }
+        return v;
+    }
+    case TC_QP: {  // the parameter's last occurrence (ParsedRecord: the last value wins)
+        const uint32_t cnt = C.q_count[s.a][i];
+        if (cnt == 0) return v;
+        const LP_G uint64_t* t = reinterpret_cast<const LP_G uint64_t*>(region + ref_off(C.q_params[s.a][i]));
+        for (uint32_t k = 0; k < cnt; ++k) {
+            const uint64_t nref = t[2 * k];
+            if (nref == REF_SKIP || ref_len(nref) != (uint32_t)s.c) continue;
+            const LP_G uint8_t* np = (ref_arena(nref) ? region : line) + ref_off(nref);
+            bool same = true;
+            for (int q = 0; q < s.c && same; ++q) same = np[q] == T.names[s.b + q];
+            if (same) ref(t[2 * k + 1]);
+        }
+        return v;
+    }
+    default:  // TC_NONE, TC_NULL
+        return v;
+    }
+}
+
+__device__ __forceinline__ bool row_view(const Columns& C, const uint8_t* buf, int64_t i, const LP_G uint8_t*& line,
+                                         const LP_G uint8_t*& region) {
+    if (C.status[i] != ST_OK) return false;
+    line = (const LP_G uint8_t*)buf + C.line_off[i];
+    region = C.arena + C.arena_base[i];
+    return true;
+}
+
+__global__ __launch_bounds__(TB) void k_table_values(const DeviceArgs* __restrict__ args,
+                                                     const TableArgs* __restrict__ targs, const uint8_t* buf) {
+    const Program& P = args->prog;
+    const Columns& C = args->cols;
+    const TableArgs& T = *targs;
+    const int64_t k = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (k >= T.count) return;
+    const int64_t i = T.first + k;
+    const LP_G uint8_t *line = nullptr, *region = nullptr;
+    const bool ok = row_view(C, buf, i, line, region);
+    const int fmt = ok && P.n_fmt > 1 ? (int)C.fmt_id[i] : 0;
+    for (int c = 0; c < T.n_cols; ++c) {
+        const TableCol& col = T.cols[c];
+        const TVal v = ok ? tvalue(P, C, T, col.src[fmt], i, line, region) : TVal{};
+        bool valid = v.kind != 0;
+        if (col.kind == 1) {  // STRING: its length now, its bytes after the scan
+            const uint32_t n = v.kind == 2 ? digits(v.l) : v.n + (v.amp ? 1u : 0u);
+            col.i64[k + 1] = valid ? (int64_t)n : 0;
+            if (k == 0) col.i64[0] = 0;
+        } else if (col.kind == 2) {
+            int64_t x = v.l;
+            if (v.kind == 1) valid = parse_long(v.p, v.n, v.amp, x);
+            else if (v.kind == 3) valid = false;  // month names, dates: not numbers
+            if (valid) col.i64[k] = x;
+        } else {
+            valid = v.kind == 2;  // the planner admits only long-valued sources here
+            if (valid) col.f64[k] = (double)v.l;
+        }
+        col.valid[k] = valid ? 1 : 0;
+    }
+}
+
+__global__ __launch_bounds__(TB) void k_table_chars(const DeviceArgs* __restrict__ args,
+                                                    const TableArgs* __restrict__ targs, const uint8_t* buf) {
+    const Program& P = args->prog;
+    const Columns& C = args->cols;
+    const TableArgs& T = *targs;
+    const int64_t k = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (k >= T.count) return;
+    const int64_t i = T.first + k;
+    const LP_G uint8_t *line = nullptr, *region = nullptr;
+    if (!row_view(C, buf, i, line, region)) return;
+    const int fmt = P.n_fmt > 1 ? (int)C.fmt_id[i] : 0;
+    for (int c = 0; c < T.n_cols; ++c) {
+        const TableCol& col = T.cols[c];
+        if (col.kind != 1 || !col.valid[k]) continue;
+        const TVal v = tvalue(P, C, T, col.src[fmt], i, line, region);
+        LP_G uint8_t* d = col.chars + col.i64[k];
+        if (v.kind == 2) {
+            write_long(d, v.l, digits(v.l));
+        } else if (v.kind == 3) {
+            for (uint32_t q = 0; q < v.n; ++q) d[q] = (uint8_t)v.buf[q];
+        } else {
+            if (v.amp) *d++ = '&';
+            for (uint32_t q = 0; q < v.n; ++q) d[q] = v.p[q];
+        }
+    }
+}
+
+}  // namespace
+
+size_t table_scratch_bytes(int64_t count) {
+    size_t tmp = 0;
+    hipcub::DeviceScan::InclusiveSum(nullptr, tmp, (const int64_t*)nullptr, (int64_t*)nullptr, (int)count);
+    return ((tmp + 255) & ~(size_t)255) + 8 * (size_t)count + 256;
+}
+
+int launch_table_values(const DeviceArgs* d_args, const TableArgs* d_targs, const TableArgs& ta, const uint8_t* buf,
+                        void* scratch, size_t scratch_bytes, hipStream_t s) {
+    if (ta.count > 0x7FFFFFFF) return -1;  // the scan's item count is an int
+    const int64_t n = ta.count;
+    if (n == 0) {
+        for (int c = 0; c < ta.n_cols; ++c)
+            if (ta.cols[c].kind == 1 && hipMemsetAsync(ta.cols[c].i64, 0, 8, s) != hipSuccess) return -1;
+        return 0;
+    }
+    hipLaunchKernelGGL(k_table_values, dim3((unsigned)((n + TB - 1) / TB)), dim3(TB), 0, s, d_args, d_targs, buf);
+    size_t tmp = 0;
+    hipcub::DeviceScan::InclusiveSum(nullptr, tmp, (const int64_t*)nullptr, (int64_t*)nullptr, (int)n);
+    const size_t tmp_al = (tmp + 255) & ~(size_t)255;
+    if (tmp_al + 8 * (size_t)n > scratch_bytes) return -1;
+    int64_t* sums = reinterpret_cast<int64_t*>((char*)scratch + tmp_al);
+    for (int c = 0; c < ta.n_cols; ++c) {
+        if (ta.cols[c].kind != 1) continue;
+        int64_t* off = (int64_t*)ta.cols[c].i64;
+        size_t t = tmp;
+        if (hipcub::DeviceScan::InclusiveSum(scratch, t, off + 1, sums, (int)n, s) != hipSuccess) return -1;
+        if (hipMemcpyAsync(off + 1, sums, 8 * (size_t)n, hipMemcpyDeviceToDevice, s) != hipSuccess) return -1;
+    }
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+int launch_table_chars(const DeviceArgs* d_args, const TableArgs* d_targs, int64_t count, const uint8_t* buf,
+                       hipStream_t s) {
+    if (count == 0) return 0;
+    hipLaunchKernelGGL(k_table_chars, dim3((unsigned)((count + TB - 1) / TB)), dim3(TB), 0, s, d_args, d_targs, buf);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+}  // namespace lp
