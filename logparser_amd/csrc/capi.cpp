@@ -302,7 +302,7 @@ int enqueue(lp_handle* h, bool sync_count) {
         if (hipMemcpyAsync(h->args.p, &h->host_args, sizeof(lp::DeviceArgs), hipMemcpyHostToDevice, s) != hipSuccess)
             return LP_E_DEVICE;
         lp::ParseLaunch pl{h->d_buf, nbytes, cap, (uint64_t)(h->mean_line > 0 ? h->mean_line + 0.5 : 0),
-                           P.n_elems, P.max_stack, h->force_direct, P.n_uri > 0, false};
+                           P.n_elems, P.max_stack, h->force_direct, P.n_uri > 0, false, P.n_uri, P.n_query};
         for (int u = 0; u < P.n_uri; ++u) pl.derived = pl.derived || P.uri[u].src_q >= 0;
         if (!pl.mean_line && cap > 0) pl.mean_line = (nbytes + cap - 1) / (uint64_t)cap;
         hipEventRecord(h->ev[2], s);

@@ -409,19 +409,26 @@ __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, 
 // passes' latencies), with their one-plane UEV mask; then phase 2 per lane,
 // a wave-aggregated arena allocation, and the query pieces spread over the
 // lanes.  A wave whose URI bytes do not fit runs on the direct (HBM) path.
-constexpr uint32_t URI_CAP = 12288;  // compact URI bytes per wave
+// compact URI bytes per wave: with its mask plane within the LDS share of a
+// CU running 16 waves (config 2: 7.3 KiB per wave on average, 8.3 KiB at the
+// 99th percentile; a wave needing more runs on the direct path)
+constexpr uint32_t URI_CAP = 8512;
 
 // Per lane: the line's URI sources.  sp[u] = a | b << 16 (line-relative, 0 =
-// none), cs[u] = the compact buffer offset of line byte a.
+// none), cs[u] = the compact buffer offset of line byte a.  NU: the URI
+// stages this kernel instance handles (>= P.n_uri; most programs have at
+// most two, whose per-lane arrays then take two registers each)
+template <int NU>
 struct UriLane {
     bool ok;
     int fmt;
     uint64_t ls;  // line start in the input
-    RegArr<MAX_URI> sp, cs, usep;
+    RegArr<NU> sp, cs, usep;
 };
 
-__device__ __forceinline__ UriLane uri_lane(const Program& P, const Columns& C, int64_t li, bool active) {
-    UriLane U;
+template <int NU>
+__device__ __forceinline__ UriLane<NU> uri_lane(const Program& P, const Columns& C, int64_t li, bool active) {
+    UriLane<NU> U;
     U.ok = active && C.status[li] == ST_OK;
     U.fmt = U.ok && P.n_fmt > 1 ? (int)C.fmt_id[li] : 0;
     U.ls = active ? C.line_off[li] : 0;
@@ -429,7 +436,7 @@ __device__ __forceinline__ UriLane uri_lane(const Program& P, const Columns& C, 
     U.cs.fill(0);
     U.usep.fill(0);
     if (U.ok)
-        for (int u = 0; u < P.n_uri; ++u) {
+        for (int u = 0; u < P.n_uri && u < NU; ++u) {
             int a, b;
             if (P.uri[u].fmt == U.fmt && uri_source_cols(P, C, li, u, a, b)) U.sp.set(u, mkspan(a, b));
         }
@@ -439,13 +446,14 @@ __device__ __forceinline__ UriLane uri_lane(const Program& P, const Columns& C, 
 // Phase 2, the arena allocation and the query pieces of one wave; lu(u) is
 // the lane's line view of URI stage u (valid for every lane, empty stages
 // included: the query pass reads other lanes' views).
-template <typename LU>
-__device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, UriLane& U, LU&& lu, bool active,
+template <int NU, int NQ, typename LU>
+__device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, UriLane<NU>& U, LU&& lu, bool active,
                                          int64_t li, int64_t wave, WaveCounts& WC) {
     const int lane = threadIdx.x;
+    const int nq = P.n_query < NQ ? P.n_query : NQ;
     uint32_t need = 0;
     if (U.ok)
-        for (int u = 0; u < P.n_uri; ++u) {
+        for (int u = 0; u < P.n_uri && u < NU; ++u) {
             const uint32_t s = U.sp.get(u);
             if (!s) continue;
             uint32_t ev;
@@ -470,7 +478,7 @@ __device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, Uri
     LP_PROF(26);
     uint32_t written = 0;
     unsigned long long my_region = 0;
-    UriOut o;
+    UriOutT<NQ> o;
     o.qlist.fill(0);
     o.qpend.fill(0);
     o.status = U.ok ? ST_OK : ST_BAD;
@@ -501,13 +509,13 @@ __device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, Uri
     // would leave most lanes idle while the longest query finishes), QR
     // rounds of 64 pieces at a time: their table slots loaded together, then
     // query_prep, ONE spill allocation for the batch, query_finish.
-    if (P.n_query > 0) {
+    if (nq > 0) {
         constexpr int QR = 4;
         __syncthreads();  // the table slots written in phase 2 are visible to every lane
         const bool has = U.ok && o.status == ST_OK && need != 0;
         const unsigned long long my_ab = has ? my_region : 0ull;
         uint64_t piece_ovf = 0;  // lanes whose line lost a piece for want of arena
-        for (int qs = 0; qs < P.n_query; ++qs) {
+        for (int qs = 0; qs < nq; ++qs) {
             const uint32_t np = has ? o.qpend.get(qs) : 0u;
             const uint32_t my_list = o.qlist.get(qs);
             uint32_t incl = np;
@@ -602,27 +610,24 @@ __device__ __forceinline__ u32x4 load16(const uint8_t* __restrict__ buf, uint64_
     return u32x4{w[0], w[1], w[2], w[3]};
 }
 
-__global__ __launch_bounds__(PW) void k_uri_lines(const uint8_t* __restrict__ buf, uint64_t nbytes,
-                                                  const DeviceArgs* __restrict__ args) {
-    const Program& P = args->prog;
-    const Columns& C = args->cols;
-    const int64_t n_lines = (int64_t)C.meta->n_lines;
-    const int64_t wave = blockIdx.x;
-    if (wave * PW >= n_lines || C.meta->cap_ovf) return;
-    __shared__ __attribute__((aligned(16))) uint32_t cbuf[URI_CAP / 4 + 16];
-    __shared__ uint64_t plane[URI_CAP / 64 + 1];
-    __shared__ uint8_t blk_own[URI_CAP / 16];  // the lane (line) of each gathered block
+// The URI stages of one wave on the compact path: its lines' URI bytes
+// gathered into cbuf (CAP bytes) with their UEV plane, then uri_wave.
+// Returns false, having done nothing, when the wave's bytes exceed CAP.
+template <int NU, int NQ, uint32_t CAP>
+__device__ __forceinline__ bool uri_compact(const uint8_t* __restrict__ buf, uint64_t nbytes, const Program& P,
+                                            const Columns& C, int64_t wave, int64_t n_lines, uint32_t* cbuf,
+                                            uint64_t* plane, WaveCounts& WC) {
     const int lane = threadIdx.x;
     const int64_t li = wave * PW + lane;
     const bool active = li < n_lines;
     LP_PROF(23);
-    UriLane U = uri_lane(P, C, li, active);
+    UriLane<NU> U = uri_lane<NU>(P, C, li, active);
     // one region per line: the 16-byte input blocks holding all its URI
     // sources (request URI, referer, ...: close together in a line), in
     // line order; a block keeps its alignment, so the wave gathers whole
     // aligned 16-byte blocks, consecutive lanes taking consecutive blocks
     uint64_t lo = ~0ull, hi = 0;
-    for (int u = 0; u < P.n_uri; ++u) {
+    for (int u = 0; u < P.n_uri && u < NU; ++u) {
         const uint32_t s = U.sp.get(u);
         if (!s) continue;
         lo = min(lo, U.ls + (s & 0xFFFF));
@@ -636,26 +641,24 @@ __global__ __launch_bounds__(PW) void k_uri_lines(const uint8_t* __restrict__ bu
         if (lane >= d) x += y;
     }
     const uint32_t tot = __shfl(x, 63), cb = x - nblk;  // blocks of the wave, this line's first block
-    if (16 * tot + 16 > URI_CAP) {  // the direct (HBM) path
-        if (lane == 0) C.uri_ovf_list[atomicAdd(&C.meta->uri_ovf_waves, 1ull)] = (uint32_t)wave;
-        return;
-    }
-    for (int u = 0; u < P.n_uri; ++u) {
+    if (16 * tot + 16 > CAP) return false;
+    for (int u = 0; u < P.n_uri && u < NU; ++u) {
         const uint32_t s = U.sp.get(u);
         if (s) U.cs.set(u, 16 * cb + (uint32_t)(U.ls + (s & 0xFFFF) - r0));
     }
-    for (uint32_t k = 0; k < nblk; ++k) blk_own[cb + k] = (uint8_t)lane;
-    __syncthreads();
-    // gather: block g of the wave is block g - cb[own] of line own's region;
-    // every round's load in flight before the first store
-    constexpr int GR = 12;  // rounds per batch (URI_CAP / 1024)
+    // gather: block g of the wave is block g - cb[own] of line own's region,
+    // own = the last lane whose first block is <= g; every round's load in
+    // flight before the first store
+    constexpr int GR = 9;  // rounds per batch (the main kernel's CAP / 1024, rounded up)
     uint16_t* pl16 = reinterpret_cast<uint16_t*>(plane);
     for (uint32_t g0 = 0; g0 < tot; g0 += GR * PW) {
         u32x4 v[GR];
 #pragma unroll
         for (int k = 0; k < GR; ++k) {
             const uint32_t g = g0 + (uint32_t)(k * PW + lane);
-            const int own = g < tot ? (int)blk_own[g] : 0;
+            int own = 0;
+            for (int st = 32; st; st >>= 1)
+                if (__shfl(cb, own + st) <= g) own += st;
             const uint64_t src = (uint64_t)__shfl((unsigned long long)r0, own) + 16ull * (g - __shfl(cb, own));
             v[k] = u32x4{0, 0, 0, 0};
             if (g < tot) v[k] = load16(buf, nbytes, src);
@@ -685,29 +688,51 @@ __global__ __launch_bounds__(PW) void k_uri_lines(const uint8_t* __restrict__ bu
         // line byte q lives at cbuf + cs + (q - a): origin cs - a (mod 2^32)
         return CL{(lds_bytes)cbuf, U.cs.get(u) - (s & 0xFFFFu), (int)(s >> 16), (lds_u64)plane};
     };
-    WaveCounts WC;
-    uri_wave(P, C, U, lu, active, li, wave, WC);
-    WC.store(C, wave);
+    uri_wave<NU, NQ>(P, C, U, lu, active, li, wave, WC);
+    return true;
 }
 
-// The waves k_uri_lines queued (their URI bytes exceed the compact buffer),
-// on a persistent grid: the lines' bytes are read from HBM directly.
+template <int NU, int NQ>
+__global__ __launch_bounds__(PW) void k_uri_lines(const uint8_t* __restrict__ buf, uint64_t nbytes,
+                                                  const DeviceArgs* __restrict__ args) {
+    const Program& P = args->prog;
+    const Columns& C = args->cols;
+    const int64_t n_lines = (int64_t)C.meta->n_lines;
+    const int64_t wave = blockIdx.x;
+    if (wave * PW >= n_lines || C.meta->cap_ovf) return;
+    __shared__ __attribute__((aligned(16))) uint32_t cbuf[URI_CAP / 4 + 16];
+    __shared__ uint64_t plane[URI_CAP / 64 + 1];
+    WaveCounts WC;
+    if (uri_compact<NU, NQ, URI_CAP>(buf, nbytes, P, C, wave, n_lines, cbuf, plane, WC)) WC.store(C, wave);
+    else if (threadIdx.x == 0) C.uri_ovf_list[atomicAdd(&C.meta->uri_ovf_waves, 1ull)] = (uint32_t)wave;
+}
+
+// The waves k_uri_lines queued (their URI bytes exceed its compact buffer),
+// on a persistent grid: the same path with a buffer four times as large (few
+// waves: their occupancy does not matter), and for a wave exceeding even
+// that, the lines' bytes read from HBM directly.
+constexpr uint32_t URI_CAP_OVF = 4 * URI_CAP;
+template <int NU, int NQ>
 __global__ __launch_bounds__(PW) void k_uri_overflow(const uint8_t* __restrict__ buf, uint64_t nbytes,
                                                      const DeviceArgs* __restrict__ args) {
     const Program& P = args->prog;
     const Columns& C = args->cols;
     const int64_t n_lines = (int64_t)C.meta->n_lines;
     const uint64_t nq = C.meta->uri_ovf_waves;
+    __shared__ __attribute__((aligned(16))) uint32_t cbuf[URI_CAP_OVF / 4 + 16];
+    __shared__ uint64_t plane[URI_CAP_OVF / 64 + 1];
     for (uint64_t q = blockIdx.x; q < nq; q += gridDim.x) {
         const int64_t wave = C.uri_ovf_list[q];
-        const WaveLines W = wave_lines(C, wave, n_lines, nbytes);
-        UriLane U = uri_lane(P, C, W.li, W.active);
-        const LP_G uint8_t* ls = (const LP_G uint8_t*)(buf) + W.s;
-        const uint32_t mis = (uint32_t)((uintptr_t)ls & 3);
-        const LineT<const LP_G uint8_t*> L{ls - mis, mis, crlf_len_hbm(buf, W)};
-        auto lu = [&](int) { return L; };
         WaveCounts WC;
-        uri_wave(P, C, U, lu, W.active, W.li, wave, WC);
+        if (!uri_compact<NU, NQ, URI_CAP_OVF>(buf, nbytes, P, C, wave, n_lines, cbuf, plane, WC)) {
+            const WaveLines W = wave_lines(C, wave, n_lines, nbytes);
+            UriLane<NU> U = uri_lane<NU>(P, C, W.li, W.active);
+            const LP_G uint8_t* ls = (const LP_G uint8_t*)(buf) + W.s;
+            const uint32_t mis = (uint32_t)((uintptr_t)ls & 3);
+            const LineT<const LP_G uint8_t*> L{ls - mis, mis, crlf_len_hbm(buf, W)};
+            auto lu = [&](int) { return L; };
+            uri_wave<NU, NQ>(P, C, U, lu, W.active, W.li, wave, WC);
+        }
         __syncthreads();
         WC.store(C, wave);
     }
@@ -1134,8 +1159,17 @@ int launch_parse(const ParseLaunch& a, const DeviceArgs* d_args, const uint32_t*
     hipLaunchKernelGGL(k_parse_overflow, dim3((unsigned)grid), dim3(PW), lds_ovf, s, a.buf, a.nbytes, d_args,
                        w.stk_words);
     if (a.uri) {
-        hipLaunchKernelGGL(k_uri_lines, dim3((unsigned)waves), dim3(PW), 0, s, a.buf, a.nbytes, d_args);
-        hipLaunchKernelGGL(k_uri_overflow, dim3((unsigned)grid), dim3(PW), 0, s, a.buf, a.nbytes, d_args);
+        // most programs have at most two URI and two query stages (the
+        // request URI and the referer): an instance keeping two of each
+        if (a.n_uri <= 2 && a.n_query <= 2) {
+            hipLaunchKernelGGL((k_uri_lines<2, 2>), dim3((unsigned)waves), dim3(PW), 0, s, a.buf, a.nbytes, d_args);
+            hipLaunchKernelGGL((k_uri_overflow<2, 2>), dim3((unsigned)grid), dim3(PW), 0, s, a.buf, a.nbytes, d_args);
+        } else {
+            hipLaunchKernelGGL((k_uri_lines<MAX_URI, MAX_QUERY>), dim3((unsigned)waves), dim3(PW), 0, s, a.buf,
+                               a.nbytes, d_args);
+            hipLaunchKernelGGL((k_uri_overflow<MAX_URI, MAX_QUERY>), dim3((unsigned)grid), dim3(PW), 0, s, a.buf,
+                               a.nbytes, d_args);
+        }
         if (a.derived) hipLaunchKernelGGL(k_derived_lines, dim3((unsigned)waves), dim3(PW), 0, s, a.buf, a.nbytes, d_args);
     }
     int64_t rb = (waves + 255) / 256;

@@ -556,6 +556,7 @@ __host__ __device__ LP_INLINE Bytes28 load28(const LN& L, int p) {
 // any pass could turn it into a dynamically indexed scratch-memory array.
 template <int N>
 struct RegArr {
+    static constexpr int size = N;
 #if defined(__HIP_DEVICE_COMPILE__)
     // a vector value: an element write with a wave-uniform index is one
     // VGPR-indexed move (s_set_gpr_idx), not a branch or a select chain
@@ -1786,11 +1787,14 @@ struct LineOut {
 };
 
 // A line's URI stages (the URI kernel): per query stage the piece table
-// (arena region offset) and its pending pieces.
-struct UriOut {
+// (arena region offset) and its pending pieces.  NQ: query stages the
+// kernel instance handles (the registers it keeps)
+template <int NQ>
+struct UriOutT {
     int status = ST_OK;
-    RegArr<MAX_QUERY> qlist, qpend;
+    RegArr<NQ> qlist, qpend;
 };
+using UriOut = UriOutT<MAX_QUERY>;
 
 // Last ' ' in [lo, hi], else -1 (lines with masks: the WS class, skipping TABs).
 template <typename LN>
@@ -2554,9 +2558,9 @@ __host__ __device__ LP_INLINE uint32_t query_piece(const Program& P, const Query
 }
 
 // HttpUriDissector fast path on the line bytes [a,b).  Returns status.
-template <typename LN, typename Cols>
+template <typename LN, typename Cols, typename UO>
 __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L, int a, int b, uint32_t usep, Arena& A,
-                                            Cols& C, int64_t li, UriOut& o) {
+                                            Cols& C, int64_t li, UO& o) {
     const UriStage& U = P.uri[u];
     const int qsi = U.want_query ? U.query_stage : -1;
     QueryTable T;
@@ -2912,10 +2916,11 @@ __host__ __device__ LP_INLINE int derived_line(const Program& P, int fmt, const 
 // Phase 2 of one line (the URI kernel): the URI stages of its LogFormat.
 // lu(u): the line view of stage u's source (holding at least [a, b)), with
 // sp[u] = a | b << 16 (0: no source), usep[u] its event count.
-template <typename LU, typename Cols>
-__host__ __device__ LP_INLINE void phase2(const Program& P, int fmt, LU&& lu, const RegArr<MAX_URI>& sp,
-                                          const RegArr<MAX_URI>& usep, UriOut& o, Arena& A, Cols& C, int64_t li) {
-    for (int u = 0; u < P.n_uri && o.status == ST_OK; ++u) {
+template <typename LU, typename Cols, typename SP, typename UO>
+__host__ __device__ LP_INLINE void phase2(const Program& P, int fmt, LU&& lu, const SP& sp, const SP& usep, UO& o,
+                                          Arena& A, Cols& C, int64_t li) {
+    const int nu = P.n_uri < SP::size ? P.n_uri : SP::size;  // the caller picked SP::size >= P.n_uri
+    for (int u = 0; u < nu && o.status == ST_OK; ++u) {
         if (P.uri[u].fmt != fmt) continue;  // another LogFormat's URI: nothing to write
         const uint32_t s = sp.get(u);
         const int a = (int)(s & 0xFFFF), b = (int)(s >> 16);
