@@ -48,6 +48,12 @@ def lib():
         L.orc_resilient_url_decode.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
         L.orc_token_table.restype = ctypes.c_int
         L.orc_token_table.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        L.orc_digest_lines.restype = ctypes.c_int64
+        L.orc_digest_lines.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int, ctypes.c_char_p,
+                                       ctypes.c_size_t, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]
+        L.dg_engine.restype = ctypes.c_int
+        L.dg_engine.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                ctypes.c_int, ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -136,3 +142,29 @@ def token_table(nginx):
     if n < 0:
         raise OracleError("token table buffer too small")
     return json.loads(out.value.decode("utf-8"))
+
+
+def digest_lines(logformat, fields, data, threads, max_lines):
+    """orc_digest_lines: (status u8[n], FNV-1a of each OK line's record u64[n])
+    of every '\\n'-terminated line of data, on `threads` threads."""
+    import numpy as np
+    st = np.zeros(max_lines, dtype=np.uint8)
+    h = np.zeros(max_lines, dtype=np.uint64)
+    f = _fields(fields)
+    n = lib().orc_digest_lines(logformat.encode(), f, len(fields), data, len(data), threads, max_lines,
+                               st.ctypes.data, h.ctypes.data)
+    if n < 0:
+        raise OracleError("orc_digest_lines failed: %d" % n)
+    return st[:n], h[:n]
+
+
+def digest_engine(record_json_fn, handle, res_ptr, status, threads):
+    """dg_engine: the same digest of the engine's records of a host result
+    (record_json_fn: the address of the product's lp_result_record_json)."""
+    import numpy as np
+    h = np.zeros(len(status), dtype=np.uint64)
+    st = np.ascontiguousarray(status, dtype=np.uint8)
+    rc = lib().dg_engine(record_json_fn, handle, res_ptr, st.ctypes.data, len(st), threads, h.ctypes.data)
+    if rc != 0:
+        raise OracleError("dg_engine failed: %d" % rc)
+    return h

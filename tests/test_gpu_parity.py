@@ -189,6 +189,33 @@ def test_large_batch_properties(oracle):
         assert s1 == 0 and js == r.record_json(i), i
 
 
+def test_headline_parity_every_line(oracle):
+    """Whole-batch parity at headline scale: EVERY line of a 10 M-line
+    config-2 batch (2.5 GB, all 123 paths) against the oracle.  Both sides
+    reduce a line to (status, FNV-1a of its canonical JSON record) on 16
+    host threads (oracle/digest.c); the engine side replays its records from
+    one lp_result_copy of the batch, through lp_result_record_json."""
+    import ctypes
+    import os
+    n = int(os.environ.get("LP_HEADLINE_LINES", "10000000"))
+    threads = 16
+    fields = paths(oracle)
+    data = lpa.synth_combined(20261015, 0, n)
+    p = lpa.HttpdLoglineParser("combined", fields)
+    r = p.parse_batch(data)
+    assert r.n_lines == n
+    assert r.counters == {"lines": n, "ok": n, "bad": 0, "fallback": 0}
+    buf, res = r.copy_to_host(with_input=True)
+    fn = ctypes.cast(lpa.lib().lp_result_record_json, ctypes.c_void_p).value
+    h_eng = oracle.digest_engine(fn, p._h, ctypes.addressof(res), r.status, threads)
+    st_orc, h_orc = oracle.digest_lines("combined", fields, data, threads, n + 1)
+    assert len(st_orc) == n
+    assert np.array_equal(st_orc, r.status.astype(np.uint8))
+    diff = np.nonzero(h_eng != h_orc)[0]
+    assert len(diff) == 0, (len(diff), diff[:10].tolist())
+    assert np.count_nonzero(h_eng) == n  # every line produced a record
+
+
 @pytest.mark.parametrize("staged", [True, False])
 def test_offsets_beyond_4gb(oracle, staged):
     """A 4.4 GB batch (a 1 MB block of synthetic lines repeated on the device):
@@ -611,13 +638,16 @@ def test_request_cookies_gpu(oracle, which):
               ["HTTP.COOKIE:request.cookies.session", "HTTP.COOKIE:request.cookies.theme",
                "HTTP.COOKIES:request.cookies", "STRING:request.status.last"]][which]
     s, _ = gpu_vs_oracle(oracle, COOKIE_FMT, fields, cookie_lines(20000, 11 + which))
-    assert s["ok"] > 17000 and s["fallback"] < 2000, s
+    # exactly the corpus's lines outside the device guard (7.6 % / 7.9 %: the
+    # 5 % with an invalid escape "%zz" and the 3 % with a non-ASCII value the
+    # generator plants; the same counts as the CPU emulation of the device code)
+    assert s == [{"ok": 18476, "bad": 0, "fallback": 1524}, {"ok": 18414, "bad": 0, "fallback": 1586}][which], s
 
 
 def test_querystring_token_gpu(oracle):
     from test_emu_parity import QS_FMT, querystring_lines
     s, _ = gpu_vs_oracle(oracle, QS_FMT, ["STRING:request.querystring.*"], querystring_lines(20000, 13))
-    assert s["ok"] > 18000 and s["fallback"] < 1500, s
+    assert s == {"ok": 19177, "bad": 0, "fallback": 823}, s  # 4.1 %: the planted invalid escapes
 
 
 def test_iso8601_timestamps_gpu(oracle):
@@ -640,7 +670,14 @@ def test_set_cookies_gpu(oracle, which):
     device path (guard) and the replay, against the oracle"""
     from test_emu_parity import SETCOOKIE_FMT, SETCOOKIE_FIELDS, setcookie_lines
     s, _ = gpu_vs_oracle(oracle, SETCOOKIE_FMT, SETCOOKIE_FIELDS[which], setcookie_lines(20000, 31 + which))
-    assert s["ok"] > 8000, s
+    # The corpus plants inputs outside the restated subset (Max-Age / Version,
+    # quotes, '$' / reserved names, names without '=', bad dates): 42.5 % /
+    # 46.7 % FALLBACK.  With which=0 every FALLBACK line is one the oracle
+    # refuses too (ORC_UNSUPPORTED: HttpCookie's RFC 2965 branch, parity
+    # unpinned); with which=1, 391 lines (2.0 %) are FALLBACK on the device
+    # only (an expires value outside the guard's `EEE, dd-MMM-yyyy HH:mm:ss
+    # GMT` subset: other zones / layouts, or a ',' inside a value before it).
+    assert s == [{"ok": 11503, "bad": 0, "fallback": 8497}, {"ok": 10659, "bad": 0, "fallback": 9341}][which], s
 
 
 def test_setters_and_remapping_gpu():

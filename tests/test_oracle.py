@@ -149,3 +149,26 @@ def test_setup_vectors_oracle(oracle, vectors):
         with pytest.raises(Exception) as ei:
             oracle.Oracle(c["logformat"], c["fields"])
         assert c["error"] in str(ei.value) and c["message_contains"] in str(ei.value), c["source"]
+
+
+def _fnv1a(b):
+    h = 1469598103934665603
+    for c in b:
+        h = ((h ^ c) * 1099511628211) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def test_digest_lines_matches_records(oracle):
+    """orc_digest_lines (the whole-batch parity helper) gives each line's
+    status and the FNV-1a of the same record orc_parse writes."""
+    fields = oracle.possible_paths("combined")
+    lines = [b'1.2.3.4 - - [10/Oct/2000:13:55:36 -0700] "GET /a?b=c HTTP/1.0" 200 2326 "-" "x"',
+             b'garbage line', b'5.6.7.8 - u [31/Dec/2019:23:59:59 +0100] "POST /x#f HTTP/1.1" 404 - "http://h:8/p?q" "y"']
+    data = b"".join(l + b"\n" for l in lines * 7)
+    st, h = oracle.digest_lines("combined", fields, data, 3, 100)
+    assert len(st) == 21
+    o = oracle.Oracle("combined", fields)
+    for i, l in enumerate(lines * 7):
+        s, js = o.parse_raw(l)
+        assert st[i] == s
+        assert int(h[i]) == (_fnv1a(js.encode()) if s == oracle.OK else 0)
