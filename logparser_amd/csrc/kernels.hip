@@ -351,12 +351,10 @@ __device__ __forceinline__ bool stage_window(const uint8_t* __restrict__ buf, ui
                 };
                 v[j] = u32x4{word(p), word(p + 4), word(p + 8), word(p + 12)};
             }
-            if (k < nv)
-                for (int w = 0; w < 4; ++w)
-                    bad |= swar::guard_bad(v[j][w]) & ~swar::eq(v[j][w], '\n') & ~swar::eq(v[j][w], '\r');
             *reinterpret_cast<u32x4*>(win + 16 * k) = v[j];
-            uint32_t m0, m1;
-            bcls::classify16(v[j][0], v[j][1], v[j][2], v[j][3], m0, m1);
+            uint32_t m0, m1, g = 0;
+            bcls::classify16g(v[j][0], v[j][1], v[j][2], v[j][3], m0, m1, g);
+            if (k < nv) bad |= g;
             msk16[8 * (k >> 2) + (k & 3)] = (uint16_t)m0;
             msk16[8 * (k >> 2) + 4 + (k & 3)] = (uint16_t)m1;
         }
@@ -429,24 +427,201 @@ struct UriLane {
 template <int NU>
 __device__ __forceinline__ UriLane<NU> uri_lane(const Program& P, const Columns& C, int64_t li, bool active) {
     UriLane<NU> U;
-    U.ok = active && C.status[li] == ST_OK;
-    U.fmt = U.ok && P.n_fmt > 1 ? (int)C.fmt_id[li] : 0;
-    U.ls = active ? C.line_off[li] : 0;
     U.sp.fill(0);
     U.cs.fill(0);
     U.usep.fill(0);
+    U.ok = false;
+    U.fmt = 0;
+    U.ls = 0;
+    if (!active) return U;
+    // every column read issued before the status is known (one round trip;
+    // the values of a line that is not OK are not used)
+    const uint8_t st = C.status[li];
+    const int fmt = P.n_fmt > 1 ? (int)C.fmt_id[li] : 0;
+    U.ls = C.line_off[li];
+    const uint32_t tf = C.tok_flags[li];
+    uint32_t raw[NU], kind[NU];
+    for (int u = 0; u < NU; ++u) {
+        raw[u] = 0;
+        kind[u] = FL_FULL;
+        if (u >= P.n_uri || P.uri[u].src_q >= 0) continue;
+        if (P.uri[u].src_tok >= 0) {
+            raw[u] = C.tok_span[P.uri[u].src_tok][li];
+            kind[u] = (tf >> P.uri[u].src_tok) & 1u ? FL_NONE : FL_FULL;  // "-" -> null
+        } else {
+            raw[u] = C.fl_uri[P.uri[u].src_fl][li];
+            kind[u] = C.fl_kind[P.uri[u].src_fl][li];
+        }
+    }
+    U.ok = st == ST_OK;
+    U.fmt = U.ok ? fmt : 0;
     if (U.ok)
         for (int u = 0; u < P.n_uri && u < NU; ++u) {
-            int a, b;
-            if (P.uri[u].fmt == U.fmt && uri_source_cols(P, C, li, u, a, b)) U.sp.set(u, mkspan(a, b));
+            // uri_source_cols (lp_device.h) on the values read above
+            const int a = (int)(raw[u] & 0xFFFF), b = (int)(raw[u] >> 16);
+            if (P.uri[u].fmt == U.fmt && P.uri[u].src_q < 0 && kind[u] != FL_NONE && b > a) U.sp.set(u, mkspan(a, b));
         }
     return U;
+}
+
+// k-th set bit (0-based) of m (k < popcount(m))
+__device__ __forceinline__ uint32_t select64(uint64_t m, uint32_t k) {
+    uint32_t pos = 0, v = (uint32_t)m, c = (uint32_t)__popc(v);
+    if (k >= c) { k -= c; v = (uint32_t)(m >> 32); pos = 32; }
+    c = (uint32_t)__popc(v & 0xFFFFu);
+    if (k >= c) { k -= c; v >>= 16; pos += 16; }
+    c = (uint32_t)__popc(v & 0xFFu);
+    if (k >= c) { k -= c; v >>= 8; pos += 8; }
+    c = (uint32_t)__popc(v & 0xFu);
+    if (k >= c) { k -= c; v >>= 4; pos += 4; }
+    c = (uint32_t)__popc(v & 3u);
+    if (k >= c) { k -= c; v >>= 2; pos += 2; }
+    return pos + (k >= (v & 1u) ? 1u : 0u);
+}
+__device__ __forceinline__ int lsb64(uint64_t m) { return (int)__builtin_ctzll(m); }
+__device__ __forceinline__ int msb64(uint64_t m) { return 63 - (int)__builtin_clzll(m); }
+
+// The fast walk of URI stage u (lp_device.h uri_walk_fast) for all lines of
+// the wave at once.  A line's event bytes (its UEV bits in [a, b), usep of
+// them) are numbered line after line; each round, every lane takes one event
+// of the wave: its byte, its class, and from ballots over its line's earlier
+// events in the round plus the line's carried state (the owner lane's
+// registers) what the sequential walk would know there -- whether an
+// earlier event stopped the walk, the first '&' / '?' (fa), the previous
+// query-piece boundary, the last '%' / '+'.  A boundary event that ends a
+// non-empty piece writes its table slot; at the end of each round every
+// owner lane folds its events of the round into its state.  The result per
+// lane (part: the lane's line takes part) is exactly the sequential walk's
+// state: resume, fa, first_pct, rewr bit 1, the query table (slots, count,
+// s, lp).  L: the lane's line view (compact buffer with its UEV plane);
+// A.p / A.used: the line's region and where its table starts.
+template <typename CL>
+__device__ __forceinline__ void uri_walk_coop(const Program& P, int u, const CL& L, bool part, int a, int b,
+                                              uint32_t usep, const Arena& A, UriWalk& Wk) {
+    const int lane = threadIdx.x;
+    const bool table = P.uri[u].want_query && P.uri[u].query_stage >= 0;  // uniform
+    const uint32_t cnt = part ? usep : 0u;
+    uint32_t x = cnt;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d);
+        if (lane >= d) x += y;
+    }
+    const uint32_t eb = x - cnt, E = __shfl(x, 63);
+    const uint32_t tab = (A.used + 15) & ~15u;
+    const unsigned long long reg = (unsigned long long)(uintptr_t)A.p;
+    // the owner's state (this lane's line)
+    int resume = -1, fa = -1, fpct = -1, lastB = -1, lastPP = -1;
+    uint32_t count = 0;
+    bool rw = false;
+    for (uint32_t g0 = 0; g0 < E; g0 += PW) {
+        const uint32_t g = g0 + (uint32_t)lane;
+        const bool valid = g < E;
+        int ow = 0;  // last lane whose first event is <= g
+        for (int st = 32; st; st >>= 1)
+            if (__shfl((int)eb, ow + st) <= (int)g) ow += st;
+        const uint32_t ebo = (uint32_t)__shfl((int)eb, ow);
+        const uint32_t oo = (uint32_t)__shfl((int)L.o, ow);
+        const int oa = __shfl(a, ow), ob = __shfl(b, ow);
+        // the event: the (g - ebo)-th UEV bit of the owner's [oa, ob)
+        uint32_t Aq = 0;
+        if (valid) {
+            const uint32_t A0 = oo + (uint32_t)oa, A1 = oo + (uint32_t)ob, WL = (A1 - 1) >> 6;
+            uint32_t W = A0 >> 6, k = g - ebo;
+            uint64_t m = L.mask(MC_UEV, W) & (~0ull << (A0 & 63));
+            for (;;) {
+                if (W == WL) m &= ~0ull >> (63 - ((A1 - 1) & 63));
+                const uint32_t c = (uint32_t)__popcll(m);
+                if (k < c || W >= WL) break;  // (the count came from the same plane: k < c by WL)
+                k -= c;
+                ++W;
+                m = L.mask(MC_UEV, W);
+            }
+            Aq = (W << 6) + select64(m, k);
+        }
+        const int q = (int)(Aq - oo);
+        CL Lo = L;
+        Lo.o = oo;
+        Lo.n = ob;
+        const uint32_t w = valid ? load_u32_at(Lo, q) : 0u;
+        const uint32_t c = w & 0xFFu;
+        const bool pct = c == '%';
+        const bool bad_pct = pct && (q + 2 >= ob || !is_hex((w >> 8) & 0xFFu) || !is_hex((w >> 16) & 0xFFu));
+        const bool stop = valid && (c == '#' || c == ';' || c >= 0x80 || bad_pct);
+        const bool aq = c == '&' || c == '?';
+        // the owner's state before this round
+        const int cres = __shfl(resume, ow), cfa = __shfl(fa, ow), clB = __shfl(lastB, ow), clPP = __shfl(lastPP, ow);
+        const uint32_t ccount = (uint32_t)__shfl((int)count, ow);
+        // my line's earlier events in this round: lanes [seg0, lane)
+        const int s0 = (int)ebo - (int)g0;
+        const uint64_t below = (1ull << lane) - 1ull;
+        const uint64_t seg_lt = valid ? below & (~0ull << (s0 > 0 ? s0 : 0)) : 0ull;
+        const uint64_t Bstop = __ballot(stop);
+        const bool live = valid && !stop && cres < 0 && !(Bstop & seg_lt);  // the fast walk takes this event
+        const uint64_t Baq = __ballot(live && aq);
+        const uint64_t mfa = Baq & seg_lt;
+        const int qfa = __shfl(q, mfa ? lsb64(mfa) : lane);
+        const int fa_j = cfa >= 0 ? cfa : (mfa ? qfa : -1);  // the first '&' / '?' before me
+        const bool pp = live && ((pct && !bad_pct) || c == '+');
+        const bool isB = table && live && aq && fa_j >= 0;   // a piece boundary after fa
+        const uint64_t BB = __ballot(isB), BPP = __ballot(pp);
+        const uint64_t mB = BB & seg_lt, mP = BPP & seg_lt;
+        const int qpb = __shfl(q, mB ? msb64(mB) : lane), qpp = __shfl(q, mP ? msb64(mP) : lane);
+        const bool first_piece = !mB && clB < 0;  // the previous boundary is fa
+        const int pb = mB ? qpb : (clB >= 0 ? clB : fa_j);
+        const int lpp = mP ? qpp : clPP;  // the last '%' / '+' before me
+        const int lp = first_piece ? lpp : (lpp > pb ? lpp : -1);
+        const bool emit = isB && q > pb + 1;
+        const uint64_t BE = __ballot(emit);
+        const bool rwj = live && fa_j >= 0 && ((aq && c == '?') || (!aq && !pct && uri_needs_encode(c)));
+        const uint64_t BR = __ballot(rwj);
+        const unsigned long long oreg = __shfl(reg, ow);
+        const uint32_t otab = (uint32_t)__shfl((int)tab, ow);
+        if (emit) {
+            const uint32_t idx = ccount + (uint32_t)__popcll(BE & seg_lt);
+            const uint64_t t0 = (uint64_t)(uint32_t)(pb + 1) | ((uint64_t)(uint32_t)q << 16) | ((uint64_t)(uint32_t)(lp + 1) << 48);
+            *reinterpret_cast<LP_G u32x4*>(reinterpret_cast<LP_G uint8_t*>(oreg) + otab + 16 * idx) =
+                u32x4{(uint32_t)t0, (uint32_t)(t0 >> 32), 0u, 0u};
+        }
+        // owners fold their events of this round into their state
+        const int so = (int)eb - (int)g0, eo = (int)(eb + cnt) - (int)g0;
+        const int so_c = so < 0 ? 0 : so > PW ? PW : so, eo_c = eo < 0 ? 0 : eo > PW ? PW : eo;
+        const uint64_t segm = so_c < eo_c ? ((eo_c == PW ? ~0ull : (1ull << eo_c) - 1ull) & (~0ull << so_c)) : 0ull;
+        const uint64_t ms = Bstop & segm, mf = Baq & segm, mpct = __ballot(live && pct) & segm, mb = BB & segm,
+                       mpp = BPP & segm;
+        const int q_s = __shfl(q, ms ? lsb64(ms) : lane), q_f = __shfl(q, mf ? lsb64(mf) : lane);
+        const int q_p = __shfl(q, mpct ? lsb64(mpct) : lane), q_b = __shfl(q, mb ? msb64(mb) : lane);
+        const int q_pp = __shfl(q, mpp ? msb64(mpp) : lane);
+        if (resume < 0 && ms) resume = q_s;
+        if (fa < 0 && mf) fa = q_f;
+        if (fpct < 0 && mpct) fpct = q_p;
+        if (mb) lastB = q_b;
+        if (mpp) lastPP = q_pp;
+        count += (uint32_t)__popcll(BE & segm);
+        rw = rw || (BR & segm) != 0;
+    }
+    if (!part) return;
+    Wk.resume = resume;
+    Wk.fa = fa;
+    Wk.first_pct = fpct;
+    Wk.rewr = rw ? 2u : 0u;
+    QueryTable& T = Wk.T;
+    if (table && fa >= 0) {
+        T.on = T.set = true;
+        T.maxp = usep + 1;
+        T.tab = tab;
+        T.reg = tab + 16 * T.maxp;
+        T.s = (lastB >= 0 ? lastB : fa) + 1;
+        T.count = count;
+        T.lp = lastB >= 0 ? (lastPP > lastB ? lastPP : -1) : lastPP;
+    } else {
+        T.lp = lastPP;
+    }
 }
 
 // Phase 2, the arena allocation and the query pieces of one wave; lu(u) is
 // the lane's line view of URI stage u (valid for every lane, empty stages
 // included: the query pass reads other lanes' views).
-template <int NU, int NQ, typename LU>
+template <int NU, int NQ, bool COOP, typename LU>
 __device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, UriLane<NU>& U, LU&& lu, bool active,
                                          int64_t li, int64_t wave, WaveCounts& WC) {
     const int lane = threadIdx.x;
@@ -482,6 +657,8 @@ __device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, Uri
     o.qlist.fill(0);
     o.qpend.fill(0);
     o.status = U.ok ? ST_OK : ST_BAD;
+    Arena A{C.arena, 0, 0};
+    bool live = false;  // the line's region is allocated: phase 2 runs
     if (U.ok) {
         if (!fits && need) {
             // the shard is full: the batch is re-run with a larger arena
@@ -491,17 +668,46 @@ __device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, Uri
             const unsigned long long mine = (unsigned long long)shard * C.shard_cap + wbase + x - need;
             my_region = mine;
             C.arena_base[li] = mine;  // also for an empty region: spills are region-relative
-            Arena A{C.arena + mine, 0, need};
+            A = Arena{C.arena + mine, 0, need};
             A.top = &C.meta->shard_top[16 * shard];  // spills come from the same shard
             A.base = wbase + x - need;
             A.limit = C.shard_cap;
-            phase2(P, U.fmt, lu, U.sp, U.usep, o, A, C, li);
-            if (A.ovf) {
-                o.status = ST_FALLBACK;
-                atomicAdd(&C.meta->arena_ovf, 1ull);
-            }
-            written = A.used - A.slack + A.extra;
+            live = true;
         }
+    }
+    // phase 2 (lp_device.h phase2), stage by stage for the whole wave: the
+    // compact path walks the stages' event bytes cooperatively
+    const int nu = P.n_uri < NU ? P.n_uri : NU;
+    for (int u = 0; u < nu; ++u) {
+        const bool fmt_ok = live && o.status == ST_OK && P.uri[u].fmt == U.fmt;
+        const uint32_t sp = U.sp.get(u);
+        const int a = (int)(sp & 0xFFFF), b = (int)(sp >> 16);
+        const bool part = fmt_ok && b > a;
+        if (fmt_ok && !part) {
+            C.u_flags[u][li] = 0;
+            if (P.uri[u].query_stage >= 0) { C.q_count[P.uri[u].query_stage][li] = 0; C.q_params[P.uri[u].query_stage][li] = 0; }
+        }
+        LP_PROF(10 + 2 * u);
+        UriWalk Wk;
+        if constexpr (COOP) {
+            LP_PROF(50 + 4 * u);
+            uri_walk_coop(P, u, lu(u), part, a, b, U.usep.get(u), A, Wk);
+            LP_PROF(51 + 4 * u);
+        } else if (part) {
+            uri_walk_fast(P, u, lu(u), a, b, U.usep.get(u), A, Wk);
+        }
+        if (part) {
+            const int st = uri_stage_rest(P, u, lu(u), a, b, U.usep.get(u), A, C, li, o, Wk);
+            if (st != ST_OK) o.status = st;
+        }
+        LP_PROF(11 + 2 * u);
+    }
+    if (live) {
+        if (A.ovf) {
+            o.status = ST_FALLBACK;
+            atomicAdd(&C.meta->arena_ovf, 1ull);
+        }
+        written = A.used - A.slack + A.extra;
     }
     LP_PROF(21);
     // QueryStringFieldDissector pieces of all lines of the wave, spread evenly
@@ -530,6 +736,9 @@ __device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, Uri
                 uint64_t t0[QR];
 #pragma unroll
                 for (int k = 0; k < QR; ++k) {
+                    own[k] = 0;
+                    t0[k] = 0;
+                    if (g0 + (uint32_t)(k * PW) >= tot) continue;  // no piece in this block (uniform)
                     const uint32_t g = g0 + (uint32_t)(k * PW + lane);
                     int ow = 0;  // last lane whose first pending piece index is <= g
                     for (int st = 32; st; st >>= 1)
@@ -537,13 +746,13 @@ __device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, Uri
                     own[k] = ow;
                     const uint32_t ob = __shfl(base, ow), olist = __shfl(my_list, ow);
                     const unsigned long long oab = __shfl(my_ab, ow);
-                    t0[k] = 0;
                     if (g < tot) t0[k] = *reinterpret_cast<const LP_G uint64_t*>(C.arena + oab + olist + 16 * (g - ob));
                 }
                 QPrep qp[QR];
                 uint32_t mine = 0;
 #pragma unroll
                 for (int k = 0; k < QR; ++k) {
+                    if (g0 + (uint32_t)(k * PW) >= tot) continue;
                     const uint32_t g = g0 + (uint32_t)(k * PW + lane);
                     const auto OL = owner_line(L, own[k]);  // every lane takes part in the shuffles
                     if (g < tot) qp[k] = query_prep(OL, t0[k]);
@@ -562,6 +771,7 @@ __device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, Uri
                 unsigned long long at = __shfl(rbase, 63) + x - mine;  // this lane's first piece in the shard
 #pragma unroll
                 for (int k = 0; k < QR; ++k) {
+                    if (g0 + (uint32_t)(k * PW) >= tot) continue;
                     const uint32_t g = g0 + (uint32_t)(k * PW + lane);
                     const int ow = own[k];
                     const uint32_t ob = __shfl(base, ow), olist = __shfl(my_list, ow);
@@ -688,13 +898,15 @@ __device__ __forceinline__ bool uri_compact(const uint8_t* __restrict__ buf, uin
         // line byte q lives at cbuf + cs + (q - a): origin cs - a (mod 2^32)
         return CL{(lds_bytes)cbuf, U.cs.get(u) - (s & 0xFFFFu), (int)(s >> 16), (lds_u64)plane};
     };
-    uri_wave<NU, NQ>(P, C, U, lu, active, li, wave, WC);
+    uri_wave<NU, NQ, true>(P, C, U, lu, active, li, wave, WC);
     return true;
 }
 
+// 16 waves per CU: the LDS share allows them, and __launch_bounds__(64, 4)
+// (4 waves per SIMD) keeps the registers within 128
 template <int NU, int NQ>
-__global__ __launch_bounds__(PW) void k_uri_lines(const uint8_t* __restrict__ buf, uint64_t nbytes,
-                                                  const DeviceArgs* __restrict__ args) {
+__global__ __launch_bounds__(PW, 4) void k_uri_lines(const uint8_t* __restrict__ buf, uint64_t nbytes,
+                                                     const DeviceArgs* __restrict__ args) {
     const Program& P = args->prog;
     const Columns& C = args->cols;
     const int64_t n_lines = (int64_t)C.meta->n_lines;
@@ -731,7 +943,7 @@ __global__ __launch_bounds__(PW) void k_uri_overflow(const uint8_t* __restrict__
             const uint32_t mis = (uint32_t)((uintptr_t)ls & 3);
             const LineT<const LP_G uint8_t*> L{ls - mis, mis, crlf_len_hbm(buf, W)};
             auto lu = [&](int) { return L; };
-            uri_wave<NU, NQ>(P, C, U, lu, W.active, W.li, wave, WC);
+            uri_wave<NU, NQ, false>(P, C, U, lu, W.active, W.li, wave, WC);
         }
         __syncthreads();
         WC.store(C, wave);
@@ -781,19 +993,11 @@ __device__ __forceinline__ void load_elems(const Program& P, Elem* s_elems) {
     for (int k = threadIdx.x; k < P.n_elems; k += PW) s_elems[k] = P.elems[k];
 }
 
-__global__ __launch_bounds__(PW, 2) void k_parse_lines(const uint8_t* __restrict__ buf, uint64_t nbytes,
-                                                    const DeviceArgs* __restrict__ args, uint32_t win_cap,
-                                                    uint32_t stk_words) {
-    const Program& P = args->prog;
-    const Columns& C = args->cols;
-    const int64_t n_lines = (int64_t)C.meta->n_lines;
-    const int64_t wave = blockIdx.x;
-    if (wave * PW >= n_lines || C.meta->cap_ovf) return;
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    Elem* s_elems = reinterpret_cast<Elem*>(smem);
-    WaveStack stk{reinterpret_cast<uint32_t*>(smem + 16 * P.n_elems) + threadIdx.x};
-    uint8_t* win = smem + 16 * P.n_elems + stk_words * 4;
-    uint16_t* msk16 = reinterpret_cast<uint16_t*>(win + win_cap);
+// One wave's 64 lines on the staged path (k_parse_lines), or queued for
+// k_parse_overflow when even half its window exceeds LDS.
+__device__ __forceinline__ void parse_group(const uint8_t* __restrict__ buf, uint64_t nbytes, const Program& P,
+                                            const Columns& C, const Elem* s_elems, WaveStack stk, uint8_t* win,
+                                            uint16_t* msk16, uint32_t win_cap, int64_t wave, int64_t n_lines) {
     const WaveLines W = wave_lines(C, wave, n_lines, nbytes);
     // the lines' window in one staged round; a window larger than LDS in two
     // rounds of 32 lines (lanes 0-31, then 32-63) when each half fits, else
@@ -812,7 +1016,6 @@ __global__ __launch_bounds__(PW, 2) void k_parse_lines(const uint8_t* __restrict
             return;
         }
     }
-    load_elems(P, s_elems);
     LP_PROF(0);
     WaveCounts WC;
 #pragma nounroll
@@ -828,6 +1031,23 @@ __global__ __launch_bounds__(PW, 2) void k_parse_lines(const uint8_t* __restrict
         if (r + 1 < rounds) __syncthreads();  // this round's LDS reads are done before the next staging
     }
     WC.store(C, wave);
+}
+
+__global__ __launch_bounds__(PW, 2) void k_parse_lines(const uint8_t* __restrict__ buf, uint64_t nbytes,
+                                                    const DeviceArgs* __restrict__ args, uint32_t win_cap,
+                                                    uint32_t stk_words) {
+    const Program& P = args->prog;
+    const Columns& C = args->cols;
+    const int64_t n_lines = (int64_t)C.meta->n_lines;
+    const int64_t wave = blockIdx.x;
+    if (wave * PW >= n_lines || C.meta->cap_ovf) return;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    Elem* s_elems = reinterpret_cast<Elem*>(smem);
+    WaveStack stk{reinterpret_cast<uint32_t*>(smem + 16 * P.n_elems) + threadIdx.x};
+    uint8_t* win = smem + 16 * P.n_elems + stk_words * 4;
+    uint16_t* msk16 = reinterpret_cast<uint16_t*>(win + win_cap);
+    load_elems(P, s_elems);
+    parse_group(buf, nbytes, P, C, s_elems, stk, win, msk16, win_cap, wave, n_lines);
 }
 
 // The waves k_parse_lines queued (even half their window exceeds LDS: very

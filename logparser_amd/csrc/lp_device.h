@@ -23,7 +23,7 @@ enum : int { ST_OK = 0, ST_BAD = 1, ST_FALLBACK = 2 };
 // Profiling build only (-DLP_PROFILE): wave timestamps at fixed points,
 // stored per wave (the waves of blocks [PROF_W0, PROF_W0 + PROF_WAVES)),
 // no atomics: the host averages the cycles between consecutive points.
-constexpr int PROF_WAVES = 16384, PROF_W0 = 1024, PROF_POINTS = 64;
+constexpr int PROF_WAVES = 16384, PROF_W0 = 1024, PROF_POINTS = 96;
 #if defined(LP_PROFILE) && defined(__HIP__)
 __device__ unsigned long long g_prof[PROF_WAVES * PROF_POINTS];
 #endif
@@ -52,8 +52,14 @@ __device__ __forceinline__ void lp_prof_acc(int k, unsigned long long& t0) {
 #define LP_PT_DECL
 #define LP_PACC(k)
 #endif
+// element i of the first-leaf match: its cycles accumulate in slot 64 + i
+#if defined(LP_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
+#define LP_PROF_EL_BEGIN() unsigned long long lp_el_t = clock64();
+#define LP_PROF_EL_END(i) if ((i) < 32) lp_prof_acc(64 + (i), lp_el_t);
+#else
 #define LP_PROF_EL_BEGIN()
 #define LP_PROF_EL_END(i)
+#endif
 
 // ----------------------------------------------------------- byte classes
 __host__ __device__ LP_INLINE bool is_ws(uint32_t c) { return c == ' ' || (c >= 9 && c <= 13); }      // \s
@@ -211,15 +217,19 @@ __host__ __device__ LP_INLINE int count(uint32_t m) { return __builtin_popcount(
 // ---- byte classes through two nibble look-up tables (the SIMD "shuffle"
 // classifier): class bits(b) = LO[b & 15] & HI[b >> 4], one v_perm_b32 per
 // 8-entry table half.  Bits (rectangles hi-nibble set x lo-nibble set):
-// 0 hi 2 x lo 0 (' '), 1 hi 0 x lo 9 (TAB), 2 hi 2 x lo 2 ('"'),
+// 0 hi 2 x lo 0 (' '), 1 hi 0 x lo {9,A,D} (TAB, LF, CR), 2 hi 2 x lo 2 ('"'),
 // 3 hi 2 x lo {3,5,6,B} (# % & +), 4 hi 3 x lo {B,C,E,F} (; < > ?),
 // 5 hi {5,7} x lo {B,C,D} ([ \ ] { | }), 6 hi 5 x lo E (^), 7 hi 6 x lo 0 (`).
 // QUOTE = bit 2, UEV = any bit: the URI event bytes % # & ? ; + and every
 // byte URIUtil.encode escapes (upper-case letters are not events: the query
-// stage finds a name's upper-case bytes itself, query_piece).
+// stage finds a name's upper-case bytes itself, query_piece).  LF and CR
+// share TAB's class (\s); inside a line they never occur (they end it), so
+// they only matter to the staging guard, which reads class bit 1 as "a
+// control byte the guard allows" (guard16).
+
 namespace bcls {
 constexpr uint32_t LO0 = 0x08040081u, LO1 = 0x00080800u;  // LO[0..3], LO[4..7]
-constexpr uint32_t LO2 = 0x38000200u, LO3 = 0x10502030u;  // LO[8..11], LO[12..15]
+constexpr uint32_t LO2 = 0x38020200u, LO3 = 0x10502230u;  // LO[8..11], LO[12..15]
 constexpr uint32_t HI0 = 0x100D0002u, HI1 = 0x20806000u;  // HI[0..3], HI[4..7]
 // v_perm_b32: byte i of the result = byte sel_i (0..7) of (s0:s1), s1 low
 __host__ __device__ LP_INLINE uint32_t perm(uint32_t s0, uint32_t s1, uint32_t sel) {
@@ -265,6 +275,25 @@ __host__ __device__ LP_INLINE void classify16(uint32_t w0, uint32_t w1, uint32_t
     constexpr uint32_t NW = 0xFCFCFCFCu, NQ = 0xFBFBFBFBu;
     p0 = nib(uev_hb(r0 & NW)) | (nib(uev_hb(r1 & NW)) << 4) | (nib(uev_hb(r2 & NW)) << 8) | (nib(uev_hb(r3 & NW)) << 12);
     p1 = nib(uev_hb(r0 & NQ)) | (nib(uev_hb(r1 & NQ)) << 4) | (nib(uev_hb(r2 & NQ)) << 8) | (nib(uev_hb(r3 & NQ)) << 12);
+}
+// The staging guard of a word whose class bits are r = bits(w): the high bit
+// of every byte outside printable ASCII other than TAB, LF and CR (controls
+// are the bytes < 0x20; of those, exactly TAB / LF / CR have class bit 1).
+// Equals swar::guard_bad(w) & ~eq(w, '\n') & ~eq(w, '\r').
+__host__ __device__ LP_INLINE uint32_t guard_word(uint32_t w, uint32_t r) {
+    const uint32_t lo7 = w & swar::LO7;
+    const uint32_t ctl = ~((lo7 + 0x60606060u) | w) & swar::HI;  // bytes < 0x20
+    const uint32_t ge7f = ((lo7 + 0x01010101u) | w) & swar::HI;   // bytes >= 0x7F
+    return (ctl & ~(r << 6)) | ge7f;
+}
+// classify16 and the guard of the same 16 bytes (OR of guard_word)
+__host__ __device__ LP_INLINE void classify16g(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t& p0,
+                                               uint32_t& p1, uint32_t& bad) {
+    const uint32_t r0 = bits(w0), r1 = bits(w1), r2 = bits(w2), r3 = bits(w3);
+    constexpr uint32_t NW = 0xFCFCFCFCu, NQ = 0xFBFBFBFBu;
+    p0 = nib(uev_hb(r0 & NW)) | (nib(uev_hb(r1 & NW)) << 4) | (nib(uev_hb(r2 & NW)) << 8) | (nib(uev_hb(r3 & NW)) << 12);
+    p1 = nib(uev_hb(r0 & NQ)) | (nib(uev_hb(r1 & NQ)) << 4) | (nib(uev_hb(r2 & NQ)) << 8) | (nib(uev_hb(r3 & NQ)) << 12);
+    bad |= guard_word(w0, r0) | guard_word(w1, r1) | guard_word(w2, r2) | guard_word(w3, r3);
 }
 // mask class whose members are exactly the byte c, -1 none
 __host__ __device__ LP_INLINE int class_of(uint32_t c) { return c == '"' ? (int)MC_QUOTE : -1; }
@@ -2557,25 +2586,34 @@ __host__ __device__ LP_INLINE uint32_t query_piece(const Program& P, const Query
     return query_finish(P, Q, L, A, R.p, slot, qp);
 }
 
-// HttpUriDissector fast path on the line bytes [a,b).  Returns status.
-template <typename LN, typename Cols, typename UO>
-__host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L, int a, int b, uint32_t usep, Arena& A,
-                                            Cols& C, int64_t li, UO& o) {
-    const UriStage& U = P.uri[u];
-    const int qsi = U.want_query ? U.query_stage : -1;
-    QueryTable T;
-    // ---- guards (FALLBACK when a cleanup step of the reference would change
-    // the string), one pass over the special bytes % # & ? ;
+// State of HttpUriDissector's walk over a URI's event bytes (uri_stage): the
+// guards' positions, the rawQuery rewrite bits and the query table being
+// laid out.  The fast walk (uri_walk_fast, or the wave-cooperative walk of
+// the URI kernel) takes the events up to the first '#', ';', non-ASCII byte
+// or invalid escape; uri_stage_rest continues from there (resume).
+struct UriWalk {
     int fa = -1, h = -1, nh = 0, first_pct = -1;
     // bit 0: the fragment holds '%' '?' or '&' (decoded / rewritten, not a plain span);
     // bit 1: the rawQuery is not "&" + the bytes between the first '&'/'?' and the '#'
     uint32_t rewr = 0;
-    int st = ST_OK;
-    // Fast walk over the events before the first '#' or ';' (the common
-    // bytes % & ? + and URIUtil-escaped ones, few branches); it stops
-    // at the first '#', ';' or invalid escape and the general walk below
-    // continues from there with the same state.
     int resume = -1;
+    QueryTable T;
+};
+
+// The fast walk of URI stage u over [a,b): the events before the first '#',
+// ';', non-ASCII byte or invalid escape (the common bytes % & ? + and
+// URIUtil-escaped ones, few branches).  A: the line's region (the query
+// table starts at its next 16-byte boundary).
+template <typename LN>
+__host__ __device__ LP_INLINE void uri_walk_fast(const Program& P, int u, const LN& L, int a, int b, uint32_t usep,
+                                                 Arena& A, UriWalk& Wk) {
+    const UriStage& U = P.uri[u];
+    const int qsi = U.want_query ? U.query_stage : -1;
+    QueryTable& T = Wk.T;
+    int& fa = Wk.fa;
+    int& first_pct = Wk.first_pct;
+    uint32_t& rewr = Wk.rewr;
+    int& resume = Wk.resume;
     LP_PROF(50 + 4 * u);
     for_uev_w(L, a, b, [&](int q, uint32_t w) {
         const uint32_t c = w & 0xFFu;
@@ -2607,6 +2645,24 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
         return true;
     });
     LP_PROF(51 + 4 * u);
+}
+
+// HttpUriDissector on the line bytes [a,b) after the fast walk: the general
+// walk from Wk.resume, the query table's last piece, then the URI's parts.
+// Returns status.
+template <typename LN, typename Cols, typename UO>
+__host__ __device__ LP_INLINE int uri_stage_rest(const Program& P, int u, const LN& L, int a, int b, uint32_t usep,
+                                                 Arena& A, Cols& C, int64_t li, UO& o, UriWalk& Wk) {
+    const UriStage& U = P.uri[u];
+    const int qsi = U.want_query ? U.query_stage : -1;
+    QueryTable& T = Wk.T;
+    int& fa = Wk.fa;
+    int& h = Wk.h;
+    int& nh = Wk.nh;
+    int& first_pct = Wk.first_pct;
+    uint32_t& rewr = Wk.rewr;
+    const int resume = Wk.resume;
+    int st = ST_OK;
     if (resume >= 0) for_uev(L, resume, b, [&](int q, uint32_t c) {
         // non-ASCII: URIUtil.encode keeps the UTF-8 bytes raw and the
         // dissector reads them back as US-ASCII (U+FFFD each); not on the device
@@ -2690,6 +2746,7 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
             sch_ok = sch_ok && scheme_char(c);
             ++p;
         }
+        LP_PROF(43);
         if (p < b && p != fa && c == ':') {
             if (p == a || !sch_ok) return ST_BAD;                                          // URISyntaxException
             flags |= UF_SCHEME;
@@ -2704,9 +2761,12 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
                 const int ae = find_fwd(L, as, b, [](uint32_t w) { return bcls::uev_hb(bcls::nonauth_bits(w)); });
                 if (ae < b && ae != fa && cur.at(ae) != '/' && cur.at(ae) != '#') return ST_FALLBACK;
                 if (ae == as) return ST_FALLBACK;                                          // empty authority
+                LP_PROF(44);
                 // parseServer; any failure -> registry-based authority (host null)
                 int he = jdk_ipv4(L, as, ae);
+                LP_PROF(45);
                 if (he <= as) he = jdk_hostname_swar(L, as, ae);
+                LP_PROF(46);
                 bool ok = he > as;
                 int pt = -1;
                 if (ok && he < ae) {
@@ -2724,6 +2784,7 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
                         if (ok) pt = (int)v;
                     }
                 }
+                LP_PROF(47);
                 if (ok) {
                     flags |= UF_HOST;
                     host_ref = (int64_t)src_ref(L, as, he - as);
@@ -2810,6 +2871,15 @@ __host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L
     LP_PROF(34 + 8 * u);
     C.u_flags[u][li] = flags;
     return ST_OK;
+}
+
+// HttpUriDissector fast path on the line bytes [a,b).  Returns status.
+template <typename LN, typename Cols, typename UO>
+__host__ __device__ LP_INLINE int uri_stage(const Program& P, int u, const LN& L, int a, int b, uint32_t usep, Arena& A,
+                                            Cols& C, int64_t li, UO& o) {
+    UriWalk Wk;
+    uri_walk_fast(P, u, L, a, b, usep, A, Wk);
+    return uri_stage_rest(P, u, L, a, b, usep, A, C, li, o, Wk);
 }
 
 // The pending query pieces of one line, one after the other (the test-only

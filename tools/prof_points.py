@@ -19,7 +19,7 @@ data = lpa.synth_combined(20261015, 0, n)
 t = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
 p = lpa.HttpdLoglineParser("combined", fields)
 L = lpa.lib()
-W, K = 16384, 64
+W, K = 16384, 96
 L.lp_profile_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
 buf = np.zeros(W * K, dtype=np.uint64)
 p.run(t.data_ptr(), len(data))
@@ -31,7 +31,7 @@ T = buf.reshape(W, K).astype(np.int64)
 names = {0: "start", 1: "staged", 2: "phase1 entry", 3: "guard", 4: "match", 5: "tok flags", 6: "time",
          7: "first line", 9: "phase1 exit", 10: "uri0 in", 11: "uri0 out", 12: "uri1 in",
          13: "uri1 out", 21: "phase2 exit", 22: "query pieces", 23: "uri kernel start", 24: "uri copied",
-         25: "uri plane", 26: "uri arena"}
+         25: "uri plane", 26: "uri arena", 43: "scheme", 44: "auth end", 45: "ipv4", 46: "hostname", 47: "port"}
 for u in range(2):
     for j, nm in enumerate(["pass1", "authority", "path", "query", "frag"]):
         names[30 + 8 * u + j] = "u%d %s done" % (u, nm)
@@ -41,7 +41,7 @@ for u in range(2):
     names[52 + 4 * u] = "u%d gen walk" % u
 # the parse kernel, then the URI kernel (k_uri_lines): separate orders
 orders = [[0, 1, 2, 3, 4, 5, 6, 7, 9],
-          [23, 24, 25, 26, 10, 50, 51, 52, 30, 31, 32, 33, 34, 11, 12, 54, 55, 56, 38, 39, 40, 41, 42, 13, 21, 22]]
+          [23, 24, 25, 26, 10, 50, 51, 52, 30, 31, 32, 33, 34, 11, 12, 54, 55, 56, 38, 43, 44, 45, 46, 47, 39, 40, 41, 42, 13, 21, 22]]
 print("parse ms %.3f  waves profiled %d" % (st["ms_parse"], int((T[:, 0] != 0).sum())))
 for order in orders:
     acc = {}
@@ -61,3 +61,11 @@ for order in orders:
     rows = [r for r in T if r[order[0]] and r[order[-1]]]
     if rows:
         print("  kernel total %.0f cycles per wave" % np.mean([r[order[-1]] - r[order[0]] for r in rows]))
+
+# first-leaf match cycles per element (LP_PROF_EL, slots 64 + i), k_parse_lines waves
+el = T[:, 64:96]
+rows = T[:, 0] != 0
+if rows.any():
+    m = el[rows].mean(axis=0)
+    print("first-leaf element cycles per wave:", " ".join("%d:%.0f" % (i, v) for i, v in enumerate(m) if v))
+print(p.describe())

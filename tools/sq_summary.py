@@ -8,7 +8,7 @@ d = sys.argv[1]
 vals = {}
 for f in sorted(glob.glob(d + "/p*/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        m = re.search(r"::(k_\w+)(?:<\w+>)?\(", r["Kernel_Name"])
+        m = re.search(r"::(k_\w+)(?:<[^>]*>)?\(", r["Kernel_Name"])
         k = m.group(1) if m else r["Kernel_Name"][:40]
         vals.setdefault(k, {})[r["Counter_Name"]] = float(r["Counter_Value"])
 for k, v in vals.items():
