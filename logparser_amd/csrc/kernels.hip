@@ -712,91 +712,117 @@ __device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, Uri
     LP_PROF(21);
     // QueryStringFieldDissector pieces of all lines of the wave, spread evenly
     // over the lanes (a line's pieces vary from 0 to dozens; one lane per line
-    // would leave most lanes idle while the longest query finishes), QR
-    // rounds of 64 pieces at a time: their table slots loaded together, then
-    // query_prep, ONE spill allocation for the batch, query_finish.
+    // would leave most lanes idle while the longest query finishes): the
+    // pieces of every query stage in one numbering (a lane's stage-0 pieces,
+    // then its stage-1 pieces, ...), QR blocks of 64 pieces per round: their
+    // table slots loaded together, then query_prep, ONE spill allocation for
+    // the round, query_finish.  Most waves need one round for all stages.
     if (nq > 0) {
         constexpr int QR = 4;
         __syncthreads();  // the table slots written in phase 2 are visible to every lane
         const bool has = U.ok && o.status == ST_OK && need != 0;
         const unsigned long long my_ab = has ? my_region : 0ull;
         uint64_t piece_ovf = 0;  // lanes whose line lost a piece for want of arena
-        for (int qs = 0; qs < nq; ++qs) {
-            const uint32_t np = has ? o.qpend.get(qs) : 0u;
-            const uint32_t my_list = o.qlist.get(qs);
-            uint32_t incl = np;
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t y = __shfl_up(incl, d);
-                if (lane >= d) incl += y;
+        uint32_t np = 0;
+        for (int qs = 0; qs < nq; ++qs) np += has ? o.qpend.get(qs) : 0u;
+        uint32_t incl = np;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(incl, d);
+            if (lane >= d) incl += y;
+        }
+        const uint32_t base = incl - np, tot = __shfl(incl, 63);
+        // piece j of lane ow: its query stage and its slot in ow's region;
+        // OL = ow's line view of that stage (every lane takes part in the shuffles)
+        auto piece = [&](int ow, uint32_t j, int& pq, uint32_t& soff) {
+            uint32_t cum = 0;
+            pq = 0;
+            soff = 0;
+            for (int qs = 0; qs < nq; ++qs) {
+                const uint32_t c = (uint32_t)__shfl((int)(has ? o.qpend.get(qs) : 0u), ow);
+                const uint32_t l = (uint32_t)__shfl((int)o.qlist.get(qs), ow);
+                if (j >= cum && j < cum + c) {
+                    pq = qs;
+                    soff = l + 16 * (j - cum);
+                }
+                cum += c;
             }
-            const uint32_t base = incl - np, tot = __shfl(incl, 63);
-            const auto L = lu(P.query[qs].uri);
-            for (uint32_t g0 = 0; g0 < tot; g0 += QR * PW) {
-                int own[QR];
-                uint64_t t0[QR];
+        };
+        auto owner_view = [&](int ow, int pq) {
+            auto OL = owner_line(lu(P.query[0].uri), ow);
+            for (int qs = 1; qs < nq; ++qs) {
+                const auto V = owner_line(lu(P.query[qs].uri), ow);
+                if (pq == qs) OL = V;
+            }
+            return OL;
+        };
+        for (uint32_t g0 = 0; g0 < tot; g0 += QR * PW) {
+            int own[QR], pqs[QR];
+            uint32_t soffs[QR];
+            uint64_t t0[QR];
 #pragma unroll
-                for (int k = 0; k < QR; ++k) {
-                    own[k] = 0;
-                    t0[k] = 0;
-                    if (g0 + (uint32_t)(k * PW) >= tot) continue;  // no piece in this block (uniform)
-                    const uint32_t g = g0 + (uint32_t)(k * PW + lane);
-                    int ow = 0;  // last lane whose first pending piece index is <= g
-                    for (int st = 32; st; st >>= 1)
-                        if (__shfl(base, ow + st) <= g) ow += st;
-                    own[k] = ow;
-                    const uint32_t ob = __shfl(base, ow), olist = __shfl(my_list, ow);
-                    const unsigned long long oab = __shfl(my_ab, ow);
-                    if (g < tot) t0[k] = *reinterpret_cast<const LP_G uint64_t*>(C.arena + oab + olist + 16 * (g - ob));
-                }
-                QPrep qp[QR];
-                uint32_t mine = 0;
+            for (int k = 0; k < QR; ++k) {
+                own[k] = 0;
+                pqs[k] = 0;
+                soffs[k] = 0;
+                t0[k] = 0;
+                if (g0 + (uint32_t)(k * PW) >= tot) continue;  // no piece in this block (uniform)
+                const uint32_t g = g0 + (uint32_t)(k * PW + lane);
+                int ow = 0;  // last lane whose first pending piece index is <= g
+                for (int st = 32; st; st >>= 1)
+                    if (__shfl(base, ow + st) <= g) ow += st;
+                own[k] = ow;
+                const uint32_t ob = __shfl(base, ow);
+                const unsigned long long oab = __shfl(my_ab, ow);
+                piece(ow, g - ob, pqs[k], soffs[k]);
+                if (g < tot) t0[k] = *reinterpret_cast<const LP_G uint64_t*>(C.arena + oab + soffs[k]);
+            }
+            QPrep qp[QR];
+            uint32_t mine = 0;
 #pragma unroll
-                for (int k = 0; k < QR; ++k) {
-                    if (g0 + (uint32_t)(k * PW) >= tot) continue;
-                    const uint32_t g = g0 + (uint32_t)(k * PW + lane);
-                    const auto OL = owner_line(L, own[k]);  // every lane takes part in the shuffles
-                    if (g < tot) qp[k] = query_prep(OL, t0[k]);
-                    mine += qp[k].need;
-                }
-                // the batch's spilled bytes in one allocation from the wave's
-                // shard (every owner is a line of this wave)
-                uint32_t x = mine;
-                for (int d = 1; d < 64; d <<= 1) {
-                    const uint32_t y = __shfl_up(x, d);
-                    if (lane >= d) x += y;
-                }
-                const uint32_t rtot = __shfl(x, 63);
-                unsigned long long rbase = 0;
-                if (lane == 63 && rtot) rbase = atomicAdd(&C.meta->shard_top[16 * shard], (unsigned long long)rtot);
-                unsigned long long at = __shfl(rbase, 63) + x - mine;  // this lane's first piece in the shard
+            for (int k = 0; k < QR; ++k) {
+                if (g0 + (uint32_t)(k * PW) >= tot) continue;
+                const uint32_t g = g0 + (uint32_t)(k * PW + lane);
+                const auto OL = owner_view(own[k], pqs[k]);
+                if (g < tot) qp[k] = query_prep(OL, t0[k]);
+                mine += qp[k].need;
+            }
+            // the round's spilled bytes in one allocation from the wave's
+            // shard (every owner is a line of this wave)
+            uint32_t x = mine;
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(x, d);
+                if (lane >= d) x += y;
+            }
+            const uint32_t rtot = __shfl(x, 63);
+            unsigned long long rbase = 0;
+            if (lane == 63 && rtot) rbase = atomicAdd(&C.meta->shard_top[16 * shard], (unsigned long long)rtot);
+            unsigned long long at = __shfl(rbase, 63) + x - mine;  // this lane's first piece in the shard
 #pragma unroll
-                for (int k = 0; k < QR; ++k) {
-                    if (g0 + (uint32_t)(k * PW) >= tot) continue;
-                    const uint32_t g = g0 + (uint32_t)(k * PW + lane);
-                    const int ow = own[k];
-                    const uint32_t ob = __shfl(base, ow), olist = __shfl(my_list, ow);
-                    const unsigned long long oab = __shfl(my_ab, ow);
-                    const auto OL = owner_line(L, ow);
-                    bool povf = false;
-                    if (g < tot) {
-                        LP_G uint64_t* slot = reinterpret_cast<LP_G uint64_t*>(C.arena + oab + olist + 16 * (g - ob));
-                        const unsigned long long rel = oab - (unsigned long long)shard * C.shard_cap;  // region in the shard
-                        if (qp[k].need && (at + qp[k].need > C.shard_cap || at - rel + qp[k].need > 0x7FFFFFFFull)) {
-                            slot[0] = REF_SKIP;
-                            slot[1] = 0;
-                            povf = true;
-                            atomicAdd(&C.meta->arena_ovf, 1ull);  // the batch is re-run with a larger arena
-                        } else {
-                            Arena A{C.arena + oab, (uint32_t)(at - rel), (uint32_t)(at - rel + qp[k].need)};
-                            written += query_finish(P, P.query[qs], OL, A, C.arena + oab, slot, qp[k]);
-                        }
-                        at += qp[k].need;
+            for (int k = 0; k < QR; ++k) {
+                if (g0 + (uint32_t)(k * PW) >= tot) continue;
+                const uint32_t g = g0 + (uint32_t)(k * PW + lane);
+                const int ow = own[k];
+                const unsigned long long oab = __shfl(my_ab, ow);
+                const auto OL = owner_view(ow, pqs[k]);
+                bool povf = false;
+                if (g < tot) {
+                    LP_G uint64_t* slot = reinterpret_cast<LP_G uint64_t*>(C.arena + oab + soffs[k]);
+                    const unsigned long long rel = oab - (unsigned long long)shard * C.shard_cap;  // region in the shard
+                    if (qp[k].need && (at + qp[k].need > C.shard_cap || at - rel + qp[k].need > 0x7FFFFFFFull)) {
+                        slot[0] = REF_SKIP;
+                        slot[1] = 0;
+                        povf = true;
+                        atomicAdd(&C.meta->arena_ovf, 1ull);  // the batch is re-run with a larger arena
+                    } else {
+                        Arena A{C.arena + oab, (uint32_t)(at - rel), (uint32_t)(at - rel + qp[k].need)};
+                        written += query_finish(P, P.query[pqs[k]], OL, A, C.arena + oab, slot, qp[k]);
                     }
-                    // a piece that did not fit: its line goes to FALLBACK (the
-                    // batch is re-run with a larger arena, or, when the re-runs
-                    // are spent, delivered with those lines FALLBACK)
-                    for (uint64_t m = __ballot(povf); m; m &= m - 1) piece_ovf |= 1ull << __shfl(ow, (int)__builtin_ctzll(m));
+                    at += qp[k].need;
                 }
+                // a piece that did not fit: its line goes to FALLBACK (the
+                // batch is re-run with a larger arena, or, when the re-runs
+                // are spent, delivered with those lines FALLBACK)
+                for (uint64_t m = __ballot(povf); m; m &= m - 1) piece_ovf |= 1ull << __shfl(ow, (int)__builtin_ctzll(m));
             }
         }
         if (((piece_ovf >> lane) & 1) && o.status == ST_OK) o.status = ST_FALLBACK;

@@ -2306,6 +2306,50 @@ __host__ __device__ LP_INLINE int jdk_hostname_swar(const LN& L, int a, int b) {
     return he;
 }
 
+// jdk_hostname_swar for an authority of at most 32 bytes: its bytes' classes
+// as 32-bit masks (one word load per 4 bytes, all issued together), then the
+// label rules as bit operations: every label start (a, and after each '.')
+// alnum, every label end (before each '.', and the last byte unless it is a
+// '.') not '-', the last label starting with a letter when there are several.
+// Longer authorities take jdk_hostname_swar.
+template <typename LN>
+__host__ __device__ LP_INLINE int jdk_hostname_m32(const LN& L, int a, int b) {
+    const int len = b - a;
+    if (len > 32) return jdk_hostname_swar(L, a, b);
+    const uint32_t A = L.o + (uint32_t)a, W0 = A >> 2, sh = A & 3;
+    const int nw = (int)(((A & 3) + (uint32_t)len + 3) >> 2);  // aligned words holding the bytes
+    uint32_t w[9];
+    LP_UNROLL for (int j = 0; j < 9; ++j) w[j] = j < nw ? L.word(W0 + (uint32_t)j) : 0u;
+    uint32_t alnum = 0, alpha = 0, dot = 0, dash = 0;
+    LP_UNROLL for (int j = 0; j < 8; ++j) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        const uint32_t x = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
+#else
+        const uint32_t x = (uint32_t)((((uint64_t)w[j + 1] << 32) | w[j]) >> (8 * sh));
+#endif
+        const uint32_t l = x | 0x20202020u;
+        const uint32_t al = swar::ge(l, 'a') & swar::lt(l, 'z' + 1) & ~(x & swar::HI);
+        alpha |= bcls::nib(al) << (4 * j);
+        alnum |= bcls::nib(al | swar::digit(x)) << (4 * j);
+        dot |= bcls::nib(swar::eq(x, '.')) << (4 * j);
+        dash |= bcls::nib(swar::eq(x, '-')) << (4 * j);
+    }
+    const uint32_t valid = len == 32 ? ~0u : (1u << len) - 1u;
+    const uint32_t other = ~(alnum | dot | dash) & valid;
+    const int he = other ? __builtin_ctz(other) : len;  // first byte outside alnum / '-' / '.'
+    if (he == 0) return -1;                            // no label
+    const uint32_t range = he == 32 ? ~0u : (1u << he) - 1u;
+    const uint32_t d = dot & range;
+    const uint32_t starts = (1u | (d << 1)) & range;
+    if (starts & ~alnum) return -1;                    // a label starts with '.' or '-'
+    const uint32_t ends = (d >> 1) | (((d >> (he - 1)) & 1u) ? 0u : 1u << (he - 1));
+    if (ends & dash) return -1;                        // a label ends with '-'
+    if (he < len && L[a + he] != ':') return -1;
+    const int l = 31 - __builtin_clz(starts);          // the last label's start
+    if (l > 0 && !((alpha >> l) & 1u)) return -1;
+    return a + he;
+}
+
 // java.net.URI.Parser.parseHostname on [a,b); returns end or -1 (fail)
 template <typename LN>
 __host__ __device__ LP_INLINE int jdk_hostname(const LN& L, int a, int b) {
@@ -2737,14 +2781,25 @@ __host__ __device__ LP_INLINE int uri_stage_rest(const Program& P, int u, const 
         flags |= UF_IS_URL;
         // scheme: ':' before any of "/?#" (in the normalized string '?' is at fa)
         Fwd<LN> cur(L, a);
-        bool sch_ok = is_alpha(cur.at(a));
+        bool sch_ok = true;
         int p = a;
         uint32_t c = 0;
-        while (p < b && p != fa) {
-            c = cur.at(p);
-            if (c == ':' || c == '/' || c == '#') break;
-            sch_ok = sch_ok && scheme_char(c);
-            ++p;
+        // "http://" / "https://" (no '&' / '?' among them: fa lies beyond)
+        const uint32_t s0 = b - a >= 8 ? load_u32_at(L, a) : 0u, s1 = b - a >= 8 ? load_u32_at(L, a + 4) : 0u;
+        if (s0 == 0x70747468u /* "http" */ && (s1 & 0xFFFFFFu) == 0x2F2F3Au /* "://" */) {
+            p = a + 4;
+            c = ':';
+        } else if (s0 == 0x70747468u && s1 == 0x2F2F3A73u /* "s://" */) {
+            p = a + 5;
+            c = ':';
+        } else {
+            sch_ok = is_alpha(cur.at(a));
+            while (p < b && p != fa) {
+                c = cur.at(p);
+                if (c == ':' || c == '/' || c == '#') break;
+                sch_ok = sch_ok && scheme_char(c);
+                ++p;
+            }
         }
         LP_PROF(43);
         if (p < b && p != fa && c == ':') {
@@ -2765,7 +2820,7 @@ __host__ __device__ LP_INLINE int uri_stage_rest(const Program& P, int u, const 
                 // parseServer; any failure -> registry-based authority (host null)
                 int he = jdk_ipv4(L, as, ae);
                 LP_PROF(45);
-                if (he <= as) he = jdk_hostname_swar(L, as, ae);
+                if (he <= as) he = jdk_hostname_m32(L, as, ae);
                 LP_PROF(46);
                 bool ok = he > as;
                 int pt = -1;
