@@ -167,7 +167,9 @@ int lp_counters(lp_handle *h, uint64_t *out, int n);
 
 /* Device-side timing of the last batch, in milliseconds, measured with HIP
  * events on the batch's stream: [0] whole batch, [1] line index kernels,
- * [2] parse kernel.  Returns the number of values written. */
+ * [2] parse pass (every kernel after the index), [3] of it the parse kernels
+ * (routing match + k_parse_lines + its direct path), [4] of it the URI
+ * kernels (+ the counter reduction).  Returns the number of values written. */
 int lp_last_timing(lp_handle *h, float *out_ms, int n);
 
 /* Run histograms of the last batch, computed on the device (SURVEY.md §5
@@ -200,7 +202,10 @@ int lp_last_timing(lp_handle *h, float *out_ms, int n);
 int lp_histograms(lp_handle *h, uint64_t *out, int out_on_device);
 
 /* Algorithmic bytes of the last batch: [0] input bytes read, [1] bytes of
- * SoA results + arena written (for roofline accounting). */
+ * SoA results + arena written, [2] the parse kernels' bytes (input once,
+ * line index, their columns), [3] the URI kernels' bytes (URI source bytes
+ * gathered, the per-line columns they read, their columns and arena
+ * writes) -- roofline accounting per kernel (timings [3] and [4]). */
 int lp_last_bytes(lp_handle *h, uint64_t *out, int n);
 
 /* ---- Bulk results: the SoA the kernels wrote (SURVEY.md §8(b) lp_result). ----

@@ -577,13 +577,14 @@ class HttpdLoglineParser:
             raise EngineUnavailable("lp_sync failed: %d" % rc)
         c = (ctypes.c_uint64 * 8)()
         L.lp_counters(self._h, c, 8)
-        t = (ctypes.c_float * 3)()
-        L.lp_last_timing(self._h, t, 3)
-        b = (ctypes.c_uint64 * 2)()
-        L.lp_last_bytes(self._h, b, 2)
+        t = (ctypes.c_float * 5)()
+        L.lp_last_timing(self._h, t, 5)
+        b = (ctypes.c_uint64 * 4)()
+        L.lp_last_bytes(self._h, b, 4)
         return {"lines": c[0], "ok": c[1], "bad": c[2], "fallback": c[3], "overflow_waves": c[4], "retries": c[5],
                 "arena_ovf": c[6], "uri_overflow_waves": c[7],
-                "ms_total": t[0], "ms_index": t[1], "ms_parse": t[2], "bytes_in": b[0], "bytes_out": b[1]}
+                "ms_total": t[0], "ms_index": t[1], "ms_parse": t[2], "ms_parse_kernels": t[3], "ms_uri_kernels": t[4],
+                "bytes_in": b[0], "bytes_out": b[1], "bytes_parse_kernels": b[2], "bytes_uri_kernels": b[3]}
 
     def parse(self, line, record=None):
         """Parser.parse(line) / parse(record, line) (core/Parser.java:700-756):

@@ -84,15 +84,16 @@ struct lp_handle {
     uint64_t arena_ovf = 0;        // arena overflow events of the last batch's final run (its lines FALLBACK)
     int64_t first_line = 0;        // global number of the last batch's first line
     int64_t next_line = 0;         // ... of the next batch's (lp_parse_batch continues the numbering)
-    hipEvent_t ev[4]{};
+    hipEvent_t ev[5]{};  // batch start, index done, parse start, batch end, parse kernels done
     bool have_events = false;
     uint64_t counters[4]{};
     uint64_t ovf_waves = 0;        // waves of the last batch parsed by k_parse_overflow
     uint64_t uri_ovf_waves = 0;    // ... whose URI stages ran in k_uri_overflow
     uint64_t shard_top[LP_ARENA_SHARDS]{};
     uint64_t arena_written = 0;
+    uint64_t uri_src_bytes = 0;  // URI source bytes the URI kernels read (meta counters[5])
     int retries = 0;
-    float ms[3]{};
+    float ms[5]{};
     // host copy for lp_line_record_json / lp_line_status
     bool host_valid = false;
     std::vector<uint8_t> hostbuf;
@@ -302,7 +303,7 @@ int enqueue(lp_handle* h, bool sync_count) {
         if (hipMemcpyAsync(h->args.p, &h->host_args, sizeof(lp::DeviceArgs), hipMemcpyHostToDevice, s) != hipSuccess)
             return LP_E_DEVICE;
         lp::ParseLaunch pl{h->d_buf, nbytes, cap, (uint64_t)(h->mean_line > 0 ? h->mean_line + 0.5 : 0),
-                           P.n_elems, P.max_stack, h->force_direct, P.n_uri > 0, false, P.n_uri, P.n_query};
+                           P.n_elems, P.max_stack, h->force_direct, P.n_uri > 0, false, P.n_uri, P.n_query, h->ev[4]};
         for (int u = 0; u < P.n_uri; ++u) pl.derived = pl.derived || P.uri[u].src_q >= 0;
         if (!pl.mean_line && cap > 0) pl.mean_line = (nbytes + cap - 1) / (uint64_t)cap;
         hipEventRecord(h->ev[2], s);
@@ -318,6 +319,7 @@ int enqueue(lp_handle* h, bool sync_count) {
         // every line goes back to the reference (FALLBACK)
         hipEventRecord(h->ev[2], s);
         if (cap) hipMemsetAsync(C.status, LP_LINE_FALLBACK, (size_t)cap, s);
+        hipEventRecord(h->ev[4], s);
     }
     hipEventRecord(h->ev[3], s);
     return LP_OK;
@@ -359,6 +361,7 @@ int finish(lp_handle* h) {
         if (h->plan.device_ok()) {
             for (int k = 0; k < 4; ++k) h->counters[k] = m.counters[k];
             h->arena_written = m.counters[4];
+            h->uri_src_bytes = m.counters[5];
             h->ovf_waves = m.ovf_waves;
             h->uri_ovf_waves = m.uri_ovf_waves;
         } else {
@@ -366,6 +369,7 @@ int finish(lp_handle* h) {
             h->counters[1] = h->counters[2] = 0;
             h->counters[3] = (uint64_t)n;
             h->arena_written = 0;
+            h->uri_src_bytes = 0;
         }
         for (int s = 0; s < LP_ARENA_SHARDS; ++s) h->shard_top[s] = std::min<uint64_t>(h->shard_top[s], h->shard_cap);
         const lp::Program& P = h->plan.program();
@@ -374,11 +378,13 @@ int finish(lp_handle* h) {
             h->mean_line = (double)h->nbytes / (double)n;
             h->arena_per_line = (double)top_max * LP_ARENA_SHARDS / (double)n;
         }
-        float a = 0, b = 0, c = 0;
+        float a = 0, b = 0, c = 0, d = 0, e = 0;
         hipEventElapsedTime(&a, h->ev[0], h->ev[3]);
         hipEventElapsedTime(&b, h->ev[0], h->ev[1]);
         hipEventElapsedTime(&c, h->ev[2], h->ev[3]);
-        h->ms[0] = a; h->ms[1] = b; h->ms[2] = c;
+        hipEventElapsedTime(&d, h->ev[2], h->ev[4]);
+        hipEventElapsedTime(&e, h->ev[4], h->ev[3]);
+        h->ms[0] = a; h->ms[1] = b; h->ms[2] = c; h->ms[3] = d; h->ms[4] = e;
         return LP_OK;
     }
 }
@@ -713,8 +719,8 @@ int lp_last_timing(lp_handle* h, float* out, int n) {
     if (!h || !out) return LP_E_INVALID;
     const int st = ensure_synced(h);
     if (st != LP_OK) return st;
-    for (int k = 0; k < n && k < 3; ++k) out[k] = h->ms[k];
-    return n < 3 ? n : 3;
+    for (int k = 0; k < n && k < 5; ++k) out[k] = h->ms[k];
+    return n < 5 ? n : 5;
 }
 
 int lp_last_bytes(lp_handle* h, uint64_t* out, int n) {
@@ -722,10 +728,22 @@ int lp_last_bytes(lp_handle* h, uint64_t* out, int n) {
     const int st = ensure_synced(h);
     if (st != LP_OK) return st;
     uint64_t row = 8;  // line index entry
-    for (const auto& c : h->specs) row += (uint64_t)c.esz;
-    uint64_t v[2] = {h->nbytes, (uint64_t)h->n_lines * row + h->arena_written};
-    for (int k = 0; k < n && k < 2; ++k) out[k] = v[k];
-    return n < 2 ? n : 2;
+    uint64_t row_uri = 0;  // the columns the URI kernels write
+    for (const auto& c : h->specs) {
+        row += (uint64_t)c.esz;
+        if (c.name[0] == 'u' || c.name[0] == 'q' || !strcmp(c.name, "arena_base")) row_uri += (uint64_t)c.esz;
+    }
+    const uint64_t n1 = (uint64_t)h->n_lines;
+    const lp::Program& P = h->plan.program();
+    // parse kernels: the input once, the line index, their columns;
+    // URI kernels: the gathered URI bytes, per line the status, line start,
+    // token flags and one source span per URI stage, their columns and arena
+    const uint64_t parse_b = h->nbytes + 8 * (n1 + 1) + n1 * (row - 8 - row_uri);
+    const uint64_t uri_b = P.n_uri ? h->uri_src_bytes + n1 * (1 + 8 + 4 + 4 * (uint64_t)P.n_uri) + n1 * row_uri +
+                                         h->arena_written : 0;
+    uint64_t v[4] = {h->nbytes, n1 * row + h->arena_written, parse_b, uri_b};
+    for (int k = 0; k < n && k < 4; ++k) out[k] = v[k];
+    return n < 4 ? n : 4;
 }
 
 int lp_casts(lp_handle* h, const char* target) {

@@ -41,6 +41,7 @@ struct ParseLaunch {
     bool uri;               // the program has URI stages (k_uri_lines after the parse kernel)
     bool derived;           // ... some of them derived (type remapping: k_derived_lines after those)
     int n_uri, n_query;     // URI / query stages (the URI kernel instance)
+    void* mid_event = nullptr;  // hipEvent_t recorded between the parse kernels and the URI kernels
 };
 // parse every line (staged waves, then the waves whose window did not fit
 // LDS on the direct path), then the URI stages (k_uri_lines, and its direct

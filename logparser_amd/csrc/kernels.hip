@@ -365,6 +365,7 @@ __device__ __forceinline__ bool stage_window(const uint8_t* __restrict__ buf, ui
 // Status counts of a wave's lines (lines, ok, bad, arena bytes written).
 struct WaveCounts {
     uint32_t act = 0, ok = 0, bad = 0, written = 0;
+    uint32_t gathered = 0;  // URI source bytes the URI kernel read (its roofline accounting)
     __device__ __forceinline__ void store(const Columns& C, int64_t wave) const {
         if (threadIdx.x == 0) {
             uint4 c, d;
@@ -373,7 +374,8 @@ struct WaveCounts {
             c.z = bad;
             c.w = act - ok - bad;
             d.x = written;
-            d.y = d.z = d.w = 0;
+            d.y = gathered;
+            d.z = d.w = 0;
             uint4* wc = reinterpret_cast<uint4*>(C.wave_counts + WC_WORDS * (size_t)wave);
             wc[0] = c;
             wc[1] = d;
@@ -878,6 +880,7 @@ __device__ __forceinline__ bool uri_compact(const uint8_t* __restrict__ buf, uin
     }
     const uint32_t tot = __shfl(x, 63), cb = x - nblk;  // blocks of the wave, this line's first block
     if (16 * tot + 16 > CAP) return false;
+    WC.gathered = 16 * tot;
     for (int u = 0; u < P.n_uri && u < NU; ++u) {
         const uint32_t s = U.sp.get(u);
         if (s) U.cs.set(u, 16 * cb + (uint32_t)(U.ls + (s & 0xFFFF) - r0));
@@ -1135,24 +1138,24 @@ __global__ __launch_bounds__(PW) void k_route_match(const uint8_t* __restrict__ 
     }
 }
 
-// meta->counters[0..4] += sum of the per-wave counts (lines ok bad fallback arena-bytes)
+// meta->counters[0..5] += sum of the per-wave counts (lines ok bad fallback arena-bytes URI-source-bytes)
 __global__ __launch_bounds__(256) void k_reduce_counts(const uint32_t* __restrict__ wc, Meta* __restrict__ meta) {
     const int64_t n_lines = meta->cap_ovf ? 0 : (int64_t)meta->n_lines;
     const int64_t n_waves = (n_lines + PW - 1) / PW;
-    unsigned long long a[5] = {0, 0, 0, 0, 0};
+    unsigned long long a[6] = {0, 0, 0, 0, 0, 0};
     for (int64_t w = (int64_t)blockIdx.x * 256 + threadIdx.x; w < n_waves; w += (int64_t)gridDim.x * 256) {
         const uint4 c = reinterpret_cast<const uint4*>(wc + WC_WORDS * w)[0];
         const uint4 d = reinterpret_cast<const uint4*>(wc + WC_WORDS * w)[1];
-        a[0] += c.x; a[1] += c.y; a[2] += c.z; a[3] += c.w; a[4] += d.x;
+        a[0] += c.x; a[1] += c.y; a[2] += c.z; a[3] += c.w; a[4] += d.x; a[5] += d.y;
     }
-    __shared__ unsigned long long red[5][4];
-    for (int k = 0; k < 5; ++k) {
+    __shared__ unsigned long long red[6][4];
+    for (int k = 0; k < 6; ++k) {
         unsigned long long v = a[k];
         for (int d = 32; d > 0; d >>= 1) v += __shfl_down(v, d);
         if ((threadIdx.x & 63) == 0) red[k][threadIdx.x >> 6] = v;
     }
     __syncthreads();
-    if (threadIdx.x < 5) {
+    if (threadIdx.x < 6) {
         unsigned long long v = red[threadIdx.x][0] + red[threadIdx.x][1] + red[threadIdx.x][2] + red[threadIdx.x][3];
         if (v) atomicAdd(&meta->counters[threadIdx.x], v);
     }
@@ -1394,7 +1397,10 @@ int launch_histograms(const DeviceArgs* d_args, const uint8_t* buf, int64_t cap_
 int launch_parse(const ParseLaunch& a, const DeviceArgs* d_args, const uint32_t* d_wave_counts, Meta* d_meta,
                  hipStream_t s) {
     const int64_t waves = parse_waves(a.cap_lines);
-    if (waves == 0) return 0;
+    if (waves == 0) {
+        if (a.mid_event) hipEventRecord((hipEvent_t)a.mid_event, s);
+        return 0;
+    }
     const WindowPlan w = window_plan(a);
     hipLaunchKernelGGL(k_parse_lines, dim3((unsigned)waves), dim3(PW), w.lds, s, a.buf, a.nbytes, d_args, w.cap,
                        w.stk_words);
@@ -1404,6 +1410,7 @@ int launch_parse(const ParseLaunch& a, const DeviceArgs* d_args, const uint32_t*
     const size_t lds_ovf = 16 * (size_t)a.n_elems + 4 * (size_t)w.stk_words;
     hipLaunchKernelGGL(k_parse_overflow, dim3((unsigned)grid), dim3(PW), lds_ovf, s, a.buf, a.nbytes, d_args,
                        w.stk_words);
+    if (a.mid_event) hipEventRecord((hipEvent_t)a.mid_event, s);
     if (a.uri) {
         // most programs have at most two URI and two query stages (the
         // request URI and the referer): an instance keeping two of each

@@ -278,7 +278,7 @@ enum : uint32_t {
 // Per-batch device bookkeeping (one block per handle, zeroed before each batch).
 constexpr int ARENA_SHARDS = 64;  // arena bump pointers, each owning 1/64 of the arena
 struct Meta {
-    unsigned long long counters[8];  // lines, ok, bad, fallback, arena bytes written
+    unsigned long long counters[8];  // lines, ok, bad, fallback, arena bytes written, URI source bytes read
     unsigned long long n_lines;      // lines of the batch (the line index's count)
     unsigned long long cap_ovf;      // 1: more lines than the columns hold (nothing parsed, retry)
     unsigned long long ovf_waves;    // waves queued for the direct (HBM) parse kernel

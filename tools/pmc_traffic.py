@@ -24,7 +24,7 @@ def per_kernel(path, counter):
         if r["Counter_Name"] != counter:
             continue
         name = r["Kernel_Name"]
-        m = re.search(r"::(k_\w+)(?:<\w+>)?\(", name)
+        m = re.search(r"::(k_\w+)(?:<[^>]*>)?\(", name)
         short = m.group(1) if m else name[:60]
         dur = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         rows[short].append((dur, int(r["Dispatch_Id"]), float(r["Counter_Value"]) * 1024.0))
