@@ -1680,11 +1680,13 @@ std::string Plan::describe() const {
     s += b;
     for (const auto& f : formats_) s += "format: " + f->cleaned + "\n";
     static const char* kn[] = {"LIT", "NOSPACE", "NUMBER", "CLFNUMBER", "HEXNUMBER", "CLFHEXNUMBER", "NONZERO",
-                               "ANY_GREEDY", "ANY_LAZY", "TIME_US", "CLF_IP", "IP"};
+                               "ANY_GREEDY", "ANY_LAZY", "TIME_US", "CLF_IP", "IP", "ANYCHAR", "DECIMAL", "MSEC",
+                               "NOSPACE3", "UPLIST_DEC", "UPLIST_NUM", "UPLIST_NS", "BINIP", "TIME_ISO", "CACHE_STATUS"};
+    constexpr int n_kn = (int)(sizeof kn / sizeof kn[0]);
     for (int i = 0; i < prog_.n_elems; ++i) {
         const Elem& e = prog_.elems[i];
         std::string lit = e.kind == EK_LIT ? std::string((const char*)prog_.lit + e.lit_off, e.lit_len) : "";
-        snprintf(b, sizeof b, "  elem %2d %-12s cap=%2d det=%d last=%d nlit=%d %s\n", i, kn[e.kind], e.cap, e.det,
+        snprintf(b, sizeof b, "  elem %2d %-12s cap=%2d det=%d last=%d nlit=%d %s\n", i, e.kind < n_kn ? kn[e.kind] : "?", e.cap, e.det,
                  e.last, e.nlit, e.kind == EK_LIT ? ("'" + lit + "'").c_str() : "");
         s += b;
     }
