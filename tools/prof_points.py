@@ -14,10 +14,12 @@ import torch  # noqa: E402,F401
 import logparser_amd as lpa  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 4_000_000
-fields = lpa.get_possible_paths("combined") if len(sys.argv) < 3 else sys.argv[2].split(",")
-data = lpa.synth_combined(20261015, 0, n)
+wl = int(os.environ.get("LP_WORKLOAD", "2"))  # BASELINE.json config (lp_synth workload)
+fmt = lpa.SYNTH_FORMATS[wl]
+fields = lpa.get_possible_paths(fmt) if len(sys.argv) < 3 else sys.argv[2].split(",")
+data = lpa.synth(wl, 20261015, 0, n)
 t = torch.frombuffer(bytearray(data), dtype=torch.uint8).cuda()
-p = lpa.HttpdLoglineParser("combined", fields)
+p = lpa.HttpdLoglineParser(fmt, fields)
 L = lpa.lib()
 W, K = 16384, 96
 L.lp_profile_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
