@@ -215,35 +215,66 @@ def cpu_run(oracle_lib, lpa, workload, fields, sample_lines, threads, repeats, s
             "spread_gbs": [round(len(data) / t / 1e9, 6) for t in reversed(runs)]}
 
 
-def cpu_baseline(lpa, workload, fields, sample_lines, threads, share_threads=16, repeats=3):
+def usable_cpus():
+    """CPUs this process may run on: its affinity mask, capped by a cgroup
+    CPU quota (cgroup v2 cpu.max, v1 cpu.cfs_quota_us / cpu.cfs_period_us)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        try:
+            q = float(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = float(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    if quota:
+        n = min(n, max(1, int(quota + 0.999)))
+    return max(1, n)
+
+
+def cpu_baseline(lpa, workload, fields, sample_lines, threads, repeats=3):
     """The oracle (C restatement of the reference semantics) on the GPU box's
-    host cores, on the first lines of the same workload: `threads` threads
-    (default every CPU the box reports) -- the median of `repeats` timed runs
-    -- and, beside it, the per-GPU CPU share (16 threads of the box)."""
+    host cores, on the first lines of the same workload: a sweep of thread
+    counts up to the CPUs this process may use (affinity and cgroup quota),
+    one run each; the fastest count is run `repeats` times and its median is
+    the value (every swept rate is reported, the value is at least each)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
     oracle_lib.lib()
-    threads = threads or os.cpu_count() or 1
-    full = cpu_run(oracle_lib, lpa, workload, fields, sample_lines, threads, repeats, 3)
-    share = cpu_run(oracle_lib, lpa, workload, fields, sample_lines, min(share_threads, threads), 1, 4)
+    usable = usable_cpus()
+    if threads:
+        counts = [threads]
+    else:
+        counts = sorted({c for c in (1, 4, usable // 2, usable, 2 * usable) if c >= 1})
+    sweep = {}
+    for t in counts:
+        sweep[t] = cpu_run(oracle_lib, lpa, workload, fields, sample_lines, t, 1, 2)
+    best_t = max(sweep, key=lambda t: sweep[t]["value"])
+    full = cpu_run(oracle_lib, lpa, workload, fields, sample_lines, best_t, repeats, 3)
+    if full["value"] < sweep[best_t]["value"]:  # the median of the repeats may fall below the sweep's single run
+        full = dict(sweep[best_t], spread_gbs=full["spread_gbs"] + sweep[best_t]["spread_gbs"])
     c = full["counts"]
     return {
         "value": full["value"],
         "unit": "GB/s",
         "lines_per_s": full["lines_per_s"],
-        "cores": threads,
+        "cores": best_t,
+        "usable_cpus": usable,
         "host_cpus": os.cpu_count(),
         "kind": "port",
-        "sample": "first %d lines (%.1f MB) of the config-%d workload, all %d paths, oracle/ C restatement, "
-                  "%d threads = every CPU the box reports (os.cpu_count()), one parser per thread, median of %d "
-                  "runs; ok=%d bad=%d unsupported=%d" % (
-                      full["lines"], full["bytes"] / 1e6, workload, len(fields), threads, repeats, c[1], c[2], c[3]),
+        "sample": "first %d lines (%.1f MB) of the config-%d workload, all %d paths, oracle/ C restatement, one parser "
+                  "per thread; thread sweep %s over the %d CPUs this process may use (affinity / cgroup quota; the box "
+                  "reports %d), the fastest (%d threads) as the median of %d runs; ok=%d bad=%d unsupported=%d" % (
+                      full["lines"], full["bytes"] / 1e6, workload, len(fields), counts, usable, os.cpu_count(), best_t,
+                      repeats, c[1], c[2], c[3]),
         "seconds": full["seconds"],
         "spread_gbs": full["spread_gbs"],
-        "per_gpu_share": {"value": share["value"], "unit": "GB/s", "lines_per_s": share["lines_per_s"],
-                          "cores": share["cores"], "seconds": share["seconds"],
-                          "sample": "first %d lines, %d threads (one GPU's CPU share of the box), one run"
-                                    % (share["lines"], share["cores"])},
+        "thread_sweep_gbs": {str(t): r["value"] for t, r in sorted(sweep.items())},
     }
 
 
@@ -343,7 +374,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--lines", type=int, default=100_000_000, help="lines per GPU")
     ap.add_argument("--cpu-sample-lines", type=int, default=4_000_000)
-    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = os.cpu_count())")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="CPU baseline threads (0 = sweep up to the usable CPUs)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-delivery", action="store_true", help="skip the host delivery measurement (huge batches)")
     ap.add_argument("--workload", type=int, default=2, choices=(2, 3, 4, 5), help="BASELINE.json config")
@@ -532,7 +563,7 @@ def main():
     if rank == 0 and wl != 5 and not args.no_delivery:
         result["delivery"] = host_delivery(lpa, torch, parser, stats["lines"], wl)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        log("cpu baseline (oracle, %d threads) ..." % (args.cpu_threads or os.cpu_count()))
+        log("cpu baseline (oracle, %s threads) ..." % (args.cpu_threads or "sweep of"))
         result["cpu_baseline"] = cpu_baseline(lpa, wl, fields, args.cpu_sample_lines, args.cpu_threads)
         # vs_baseline stays null: BASELINE.md publishes no number for this metric
         result["vs_cpu_baseline"] = round(result["value"] / result["cpu_baseline"]["value"], 1)

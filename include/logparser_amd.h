@@ -113,6 +113,9 @@ int64_t lp_possible_paths_remapped(const char *logformats, int max_depth, const 
                                   (default 3, 0..16); an arena still short after them degrades:
                                   the lines that did not fit are FALLBACK, lp_counters out[6] */
 #define LP_OPT_ARENA_BYTES 3   /* tests: exact arena capacity of each batch's first run (0 = estimate) */
+#define LP_OPT_CHUNK_LINES 4   /* one-format programs: lines per byte chunk the one-pass parse kernel
+                                  aims for (1..64, 0 = default 60; a chunk's 65th line onwards is
+                                  parsed from HBM by a second kernel) */
 int lp_set_option(lp_handle *h, int option, int64_t value);
 
 /* Capacity for the coming batches: columns for max_lines lines and at least
@@ -156,8 +159,10 @@ int64_t lp_line_offset(lp_handle *h, int64_t i);
  * is not OK, -100 - needed if cap is too small). */
 int64_t lp_line_record_json(lp_handle *h, int64_t i, char *out, size_t cap);
 /* out[0..3] = lines, ok, bad, fallback of the last batch (device counters);
- * diagnostics: out[4] = waves parsed by the overflow kernel (their lines'
- * window exceeded the main kernel's LDS window), out[5] = re-runs of the
+ * diagnostics: out[4] = one LogFormat: lines parsed by the direct kernel (a
+ * byte chunk's 65th line onwards, or a line ending past the chunk's LDS
+ * window); several LogFormats: waves parsed by the overflow kernel (their
+ * lines' window exceeded the main kernel's LDS window), out[5] = re-runs of the
  * batch (capacity / arena estimates exceeded), out[6] = arena overflows the
  * final run left (lines sent to FALLBACK for want of arena; 0 normally),
  * out[7] = waves whose URI bytes exceeded the URI kernel's compact buffer
@@ -166,10 +171,12 @@ int64_t lp_line_record_json(lp_handle *h, int64_t i, char *out, size_t cap);
 int lp_counters(lp_handle *h, uint64_t *out, int n);
 
 /* Device-side timing of the last batch, in milliseconds, measured with HIP
- * events on the batch's stream: [0] whole batch, [1] line index kernels,
- * [2] parse pass (every kernel after the index), [3] of it the parse kernels
- * (routing match + k_parse_lines + its direct path), [4] of it the URI
- * kernels (+ the counter reduction).  Returns the number of values written. */
+ * events on the batch's stream: [0] whole batch, [1] separate line index
+ * kernels (0 for one-LogFormat programs after a handle's first batch: their
+ * parse kernel finds the lines itself), [2] parse pass (every kernel after
+ * the index), [3] of it the parse kernels (one LogFormat: k_parse_chunks +
+ * k_parse_ovf_lines; several: routing match + k_parse_lines + its direct
+ * path), [4] of it the URI kernels (+ the counter reduction).  Returns the number of values written. */
 int lp_last_timing(lp_handle *h, float *out_ms, int n);
 
 /* Run histograms of the last batch, computed on the device (SURVEY.md §5

@@ -16,6 +16,21 @@
 #include "kernels.h"
 #include "plan.h"
 
+#if defined(LP_PROFILE)
+// profiling build: copy out (and clear) the per-wave timestamps of the parse
+// and URI kernels (PROF_WAVES x PROF_POINTS u64; the two kernel translation
+// units mark disjoint points)
+extern "C" int lp_profile_read(unsigned long long* out, int n) {
+    if (n < lp::PROF_WAVES * lp::PROF_POINTS) return -1;
+    std::vector<unsigned long long> u((size_t)lp::PROF_WAVES * lp::PROF_POINTS);
+    if (lp::prof_read_parse(out) != 0 || lp::prof_read_uri(u.data()) != 0) return -1;
+    for (size_t k = 0; k < u.size(); ++k) out[k] += u[k];
+    lp::prof_clear_parse();
+    lp::prof_clear_uri();
+    return 0;
+}
+#endif
+
 static_assert(LP_ARENA_SHARDS == lp::ARENA_SHARDS, "arena shard count of the ABI and the kernels");
 
 namespace {
@@ -51,6 +66,7 @@ struct ColSpec {
     int index;
     int esz;
     void** field;
+    int uri;  // written by the URI kernels (1) or the parse kernels (0): lp_last_bytes' per-kernel split
 };
 
 }  // namespace
@@ -61,6 +77,7 @@ struct lp_handle {
     int device = 0;
     hipStream_t stream = nullptr;
     DevBuf input, chunk, line_off, cols, arena, meta, waves, args, route, ovf, hist;
+    DevBuf cstate;  // chunked parse: look-back words, per-chunk counts, queued lines
     DevBuf targs, tscratch;  // device table (lp_result_table on a device view)
     lp::DeviceArgs host_args{};
     lp::Columns C{};
@@ -87,7 +104,9 @@ struct lp_handle {
     hipEvent_t ev[5]{};  // batch start, index done, parse start, batch end, parse kernels done
     bool have_events = false;
     uint64_t counters[4]{};
-    uint64_t ovf_waves = 0;        // waves of the last batch parsed by k_parse_overflow
+    uint32_t chunk_lines = 0;      // LP_OPT_CHUNK_LINES (0: the kernel's default)
+    bool chunked = false;          // the last batch ran the chunked parse (line index inside the parse kernel)
+    uint64_t ovf_waves = 0;        // waves of the last batch parsed by k_parse_overflow (chunked: lines by k_parse_ovf_lines)
     uint64_t uri_ovf_waves = 0;    // ... whose URI stages ran in k_uri_overflow
     uint64_t shard_top[LP_ARENA_SHARDS]{};
     uint64_t arena_written = 0;
@@ -121,22 +140,26 @@ void build_specs(lp_handle* h) {
     lp::Columns& C = h->C;
     auto& v = h->specs;
     v.clear();
-    auto add = [&](const char* nm, int idx, int esz, void* field) { v.push_back({nm, idx, esz, (void**)field}); };
+    int uri = 0;
+    auto add = [&](const char* nm, int idx, int esz, void* field) { v.push_back({nm, idx, esz, (void**)field, uri}); };
     add("status", 0, 1, &C.status);
     for (int k = 0; k < P.n_tok; ++k) add("tok_span", k, 4, &C.tok_span[k]);
     add("tok_flags", 0, 4, &C.tok_flags);
+    add("hist", 0, 4, &C.hist);
     for (int t = 0; t < P.n_time; ++t) {
         add("t_epoch", t, 8, &C.t_epoch[t]);
         add("t_local", t, 8, &C.t_local[t]);
         add("t_utc", t, 8, &C.t_utc[t]);
         if (P.time[t].kind == lp::TK_STRF) add("t_nano", t, 4, &C.t_nano[t]);  // only strftime has fractions
     }
+    for (int k = 0; k < P.n_secms; ++k) add("sm_ms", k, 8, &C.sm_ms[k]);
     for (int f = 0; f < P.n_fl; ++f) {
         add("fl_kind", f, 4, &C.fl_kind[f]);
         add("fl_method", f, 4, &C.fl_method[f]);
         add("fl_uri", f, 4, &C.fl_uri[f]);
         add("fl_proto", f, 4, &C.fl_proto[f]);
     }
+    uri = 1;  // the URI kernels' columns
     for (int u = 0; u < P.n_uri; ++u) {
         add("u_flags", u, 4, &C.u_flags[u]);
         add("u_scheme", u, 8, &C.u_scheme[u]);
@@ -150,7 +173,12 @@ void build_specs(lp_handle* h) {
         add("q_count", q, 4, &C.q_count[q]);
         add("q_params", q, 8, &C.q_params[q]);
     }
+    for (int j = 0; j < P.n_list; ++j) {
+        add("l_count", j, 4, &C.l_count[j]);
+        add("l_tab", j, 8, &C.l_tab[j]);
+    }
     add("arena_base", 0, 8, &C.arena_base);
+    uri = 0;
     if (P.n_fmt > 1) {
         add("fmt_match", 0, 2, &C.fmt_match);
         add("fmt_id", 0, 1, &C.fmt_id);
@@ -218,6 +246,9 @@ void make_view(lp_handle* h, const lp_result& r, lp::ResultView& V) {
         else if (nm == "q_count") V.q_count[i] = (const uint32_t*)p;
         else if (nm == "q_params") V.q_params[i] = (const uint64_t*)p;
         else if (nm == "arena_base") V.arena_base = (const uint64_t*)p;
+        else if (nm == "sm_ms") V.sm_ms[i] = (const int64_t*)p;
+        else if (nm == "l_count") V.l_count[i] = (const uint32_t*)p;
+        else if (nm == "l_tab") V.l_tab[i] = (const uint64_t*)p;
         else if (nm == "fmt_id") V.fmt_id = (const uint8_t*)p;
     }
     if (!V.arena) V.arena_base = nullptr;
@@ -240,6 +271,10 @@ int enqueue(lp_handle* h, bool sync_count) {
     if (hipMemsetAsync(d_meta, 0, sizeof(lp::Meta), s) != hipSuccess) return LP_E_DEVICE;
     hipEventRecord(h->ev[0], s);
     int64_t cap = h->cap_lines;
+    // one LogFormat: the parse kernel finds the lines itself (k_parse_chunks);
+    // several: the routing pass needs the line index first
+    const bool chunked = h->plan.device_ok() && P.n_fmt == 1;
+    h->chunked = chunked;
     if (sync_count) {
         // first batch of a handle: the exact line count sizes the columns
         if (!h->line_off.ensure(16)) return LP_E_NOMEM;
@@ -252,13 +287,13 @@ int enqueue(lp_handle* h, bool sync_count) {
         // headroom for the next batches of the stream (sized like the estimate below)
         cap = std::max<int64_t>(headroom((int64_t)n), h->reserve_lines);
         if (n) h->mean_line = (double)nbytes / (double)n;  // sizes this batch's LDS windows
-    } else {
+    } else if (!chunked) {
         if (!h->line_off.ensure(sizeof(uint64_t) * (size_t)(cap + 2))) return LP_E_NOMEM;
         if (lp::launch_count(h->d_buf, nbytes, d_chunk, d_nlmask, h->line_off.as<uint64_t>(), cap, d_meta, s) != 0)
             return LP_E_DEVICE;
     }
     if (!h->line_off.ensure(sizeof(uint64_t) * (size_t)(cap + 2))) return LP_E_NOMEM;
-    if (sync_count) {  // the scan ran without the line index buffer: its ends now
+    if (sync_count && !chunked) {  // the scan ran without the line index buffer: its ends now
         unsigned long long n = 0;
         hipMemcpy(&n, &d_meta->n_lines, sizeof n, hipMemcpyDeviceToHost);
         uint64_t ends[2] = {0, nbytes + 1};
@@ -268,7 +303,8 @@ int enqueue(lp_handle* h, bool sync_count) {
         if (nbytes && last != '\n' && last != '\r') hipMemcpy(h->line_off.as<uint64_t>() + n, &ends[1], 8, hipMemcpyHostToDevice);
     }
     h->cap_lines = cap;
-    if (lp::launch_offsets(d_nlmask, nbytes, d_chunk, h->line_off.as<uint64_t>(), cap, s) != 0) return LP_E_DEVICE;
+    if (!chunked && lp::launch_offsets(d_nlmask, nbytes, d_chunk, h->line_off.as<uint64_t>(), cap, s) != 0)
+        return LP_E_DEVICE;
     hipEventRecord(h->ev[1], s);
     if (!alloc_columns(h, cap)) return LP_E_NOMEM;
     // arena: ARENA_SHARDS shards of shard_cap bytes; the reservation is a
@@ -276,7 +312,7 @@ int enqueue(lp_handle* h, bool sync_count) {
     const double per = h->arena_per_line > 0 ? h->arena_per_line * 1.25 : 64.0;
     uint64_t acap = std::max<uint64_t>(h->reserve_arena, (uint64_t)(per * (double)cap) + (1u << 20));
     if (h->arena_first && h->retries == 0) acap = h->arena_first;
-    if (!h->plan.device_ok() || P.n_uri == 0) acap = 4096 * LP_ARENA_SHARDS;
+    if (!h->plan.device_ok() || (P.n_uri == 0 && P.n_list == 0)) acap = 4096 * LP_ARENA_SHARDS;
     h->shard_cap = (acap / LP_ARENA_SHARDS + 255) & ~255ull;
     if (!h->arena.ensure(h->shard_cap * LP_ARENA_SHARDS)) return LP_E_NOMEM;
     lp::Columns& C = h->C;
@@ -298,14 +334,27 @@ int enqueue(lp_handle* h, bool sync_count) {
             C.fmt_init = h->fmt_state;
         }
         if (!h->args.ensure(sizeof(lp::DeviceArgs))) return LP_E_NOMEM;
+        lp::ParseLaunch pl{h->d_buf, nbytes, cap, (uint64_t)(h->mean_line > 0 ? h->mean_line + 0.5 : 0),
+                           P.n_elems, P.max_stack, h->force_direct, P.n_uri > 0 || P.n_list > 0, false, P.n_uri, P.n_query,
+                           h->ev[4]};
+        for (int u = 0; u < P.n_uri; ++u) pl.derived = pl.derived || P.uri[u].src_q >= 0;
+        if (!pl.mean_line && cap > 0) pl.mean_line = (nbytes + cap - 1) / (uint64_t)cap;
+        pl.chunked = chunked;
+        pl.chunk_lines = h->chunk_lines;
+        if (chunked) {
+            // look-back words (zeroed), per-chunk counts, the queued line list
+            const lp::ChunkPlan cp = lp::chunk_plan(pl);
+            const size_t sb = align256(8 * (size_t)(cp.n_chunks + 1)), cb = align256(4 * lp::WC_WORDS * (size_t)(cp.n_chunks + 1));
+            if (!h->cstate.ensure(sb + cb + 4 * (size_t)(cap + 1))) return LP_E_NOMEM;
+            C.chunk_state = h->cstate.as<uint64_t>();
+            C.chunk_counts = h->cstate.as<uint32_t>(sb);
+            C.ovf_lines = h->cstate.as<uint32_t>(sb + cb);
+            if (hipMemsetAsync(C.chunk_state, 0, sb, s) != hipSuccess) return LP_E_DEVICE;
+        }
         h->host_args.prog = P;
         h->host_args.cols = C;
         if (hipMemcpyAsync(h->args.p, &h->host_args, sizeof(lp::DeviceArgs), hipMemcpyHostToDevice, s) != hipSuccess)
             return LP_E_DEVICE;
-        lp::ParseLaunch pl{h->d_buf, nbytes, cap, (uint64_t)(h->mean_line > 0 ? h->mean_line + 0.5 : 0),
-                           P.n_elems, P.max_stack, h->force_direct, P.n_uri > 0, false, P.n_uri, P.n_query, h->ev[4]};
-        for (int u = 0; u < P.n_uri; ++u) pl.derived = pl.derived || P.uri[u].src_q >= 0;
-        if (!pl.mean_line && cap > 0) pl.mean_line = (nbytes + cap - 1) / (uint64_t)cap;
         hipEventRecord(h->ev[2], s);
         const lp::DeviceArgs* d_args = h->args.as<lp::DeviceArgs>();
         if (P.n_fmt > 1) {
@@ -313,7 +362,7 @@ int enqueue(lp_handle* h, bool sync_count) {
             // then the scan of the sticky active format
             if (lp::launch_route_match(pl, d_args, s) != 0 || lp::launch_route(d_args, cap, s) != 0) return LP_E_DEVICE;
         }
-        if (lp::launch_parse(pl, d_args, C.wave_counts, d_meta, s) != 0) return LP_E_DEVICE;
+        if (lp::launch_parse(pl, d_args, C, s) != 0) return LP_E_DEVICE;
     } else {
         // the requested paths need a dissector that is not on the device:
         // every line goes back to the reference (FALLBACK)
@@ -328,6 +377,8 @@ int enqueue(lp_handle* h, bool sync_count) {
 // Wait for the batch, read its bookkeeping; when its line count or arena
 // need outgrew the buffers, re-run it with exact sizes.
 int finish(lp_handle* h) {
+    int cap_reruns = 0;    // re-runs for a short line capacity: always (the re-run has the exact count)
+    int arena_reruns = 0;  // ... for a short arena: at most LP_OPT_MAX_RETRIES
     for (;;) {
         if (hipStreamSynchronize(h->stream) != hipSuccess) return LP_E_DEVICE;
         lp::Meta m;
@@ -338,9 +389,15 @@ int finish(lp_handle* h) {
             top_max = std::max<uint64_t>(top_max, h->shard_top[s]);
         }
         const int64_t n = (int64_t)m.n_lines;
-        if (h->plan.device_ok() && (m.cap_ovf || m.arena_ovf) && h->retries < h->max_retries) {
+        // LP_OPT_MAX_RETRIES bounds the arena re-runs only: a short arena has
+        // a fallback (its lines go FALLBACK), a short line capacity has none
+        const bool cap_rerun = m.cap_ovf && cap_reruns < 2;
+        const bool arena_rerun = !m.cap_ovf && m.arena_ovf && arena_reruns < h->max_retries;
+        if (h->plan.device_ok() && (cap_rerun || arena_rerun)) {
             // exact sizes: the line count, every shard as large as the largest
             // request (shard tops count what was asked for, also past the end)
+            if (cap_rerun) ++cap_reruns;
+            else ++arena_reruns;
             ++h->retries;
             h->cap_lines = std::max<int64_t>(n, h->cap_lines);
             if (n > 0) h->mean_line = (double)h->nbytes / (double)n;
@@ -362,7 +419,7 @@ int finish(lp_handle* h) {
             for (int k = 0; k < 4; ++k) h->counters[k] = m.counters[k];
             h->arena_written = m.counters[4];
             h->uri_src_bytes = m.counters[5];
-            h->ovf_waves = m.ovf_waves;
+            h->ovf_waves = h->chunked ? m.ovf_lines : m.ovf_waves;
             h->uri_ovf_waves = m.uri_ovf_waves;
         } else {
             h->counters[0] = (uint64_t)n;
@@ -547,6 +604,10 @@ int lp_set_option(lp_handle* h, int option, int64_t value) {
     if (!h) return LP_E_INVALID;
     switch (option) {
     case LP_OPT_FORCE_DIRECT: h->force_direct = value != 0; return LP_OK;
+    case LP_OPT_CHUNK_LINES:
+        if (value < 0 || value > 64) return LP_E_INVALID;
+        h->chunk_lines = (uint32_t)value;
+        return LP_OK;
     case LP_OPT_MAX_RETRIES:
         if (value < 0 || value > 16) return LP_E_INVALID;
         h->max_retries = (int)value;
@@ -731,7 +792,7 @@ int lp_last_bytes(lp_handle* h, uint64_t* out, int n) {
     uint64_t row_uri = 0;  // the columns the URI kernels write
     for (const auto& c : h->specs) {
         row += (uint64_t)c.esz;
-        if (c.name[0] == 'u' || c.name[0] == 'q' || !strcmp(c.name, "arena_base")) row_uri += (uint64_t)c.esz;
+        if (c.uri) row_uri += (uint64_t)c.esz;
     }
     const uint64_t n1 = (uint64_t)h->n_lines;
     const lp::Program& P = h->plan.program();
@@ -739,7 +800,7 @@ int lp_last_bytes(lp_handle* h, uint64_t* out, int n) {
     // URI kernels: the gathered URI bytes, per line the status, line start,
     // token flags and one source span per URI stage, their columns and arena
     const uint64_t parse_b = h->nbytes + 8 * (n1 + 1) + n1 * (row - 8 - row_uri);
-    const uint64_t uri_b = P.n_uri ? h->uri_src_bytes + n1 * (1 + 8 + 4 + 4 * (uint64_t)P.n_uri) + n1 * row_uri +
+    const uint64_t uri_b = P.has_phase2() ? h->uri_src_bytes + n1 * (1 + 8 + 4 + 4 * (uint64_t)P.n_uri) + n1 * row_uri +
                                          h->arena_written : 0;
     uint64_t v[4] = {h->nbytes, n1 * row + h->arena_written, parse_b, uri_b};
     for (int k = 0; k < n && k < 4; ++k) out[k] = v[k];
@@ -953,7 +1014,13 @@ int lp_result_table(lp_handle* h, const lp_result* r, int64_t first, int64_t cou
         if (casts < 0) return LP_E_MISSING;
         if (!(casts & C.kind)) return LP_E_INVALID;
     }
-    if (!r->on_host) return table_device(h, first, count, cols, n_cols);
+    if (!r->on_host) {
+        // a device view is only good for the batch the handle holds now
+        if (!h->valid || r->n_lines != h->n_lines || r->first_line != h->first_line || r->input != h->d_buf ||
+            r->line_off != h->line_off.as<uint64_t>())
+            return LP_E_STATE;
+        return table_device(h, first, count, cols, n_cols);
+    }
     if (!r->input) return LP_E_INVALID;
     if (first < 0 || count < 0 || first + count > r->n_lines) return LP_E_INVALID;
     std::unordered_map<std::string, std::vector<int>> by_path;

@@ -42,13 +42,40 @@ struct ParseLaunch {
     bool derived;           // ... some of them derived (type remapping: k_derived_lines after those)
     int n_uri, n_query;     // URI / query stages (the URI kernel instance)
     void* mid_event = nullptr;  // hipEvent_t recorded between the parse kernels and the URI kernels
+    bool chunked = false;       // one-format program: k_parse_chunks builds the line index itself
+    uint32_t chunk_lines = 0;   // lines per byte chunk the chunked kernel aims for (0: default)
 };
-// parse every line (staged waves, then the waves whose window did not fit
-// LDS on the direct path), then the URI stages (k_uri_lines, and its direct
-// path), then meta->counters[0..4] += lines, ok, bad, fallback, arena bytes
-// written (C.ovf_list and C.uri_ovf_list: parse_waves(cap_lines) + 1 entries each)
-int launch_parse(const ParseLaunch& a, const DeviceArgs* d_args, const uint32_t* d_wave_counts, Meta* d_meta,
-                 hipStream_t s);
+// The chunked parse kernel's geometry: cb input bytes per chunk (one wave
+// each), an LDS window of win_cap bytes (the chunk, 64 bytes before it, the
+// tail of its last line), n_chunks chunks.
+struct ChunkPlan {
+    uint32_t cb, win_cap, stk_words;
+    int waves_per_cu;
+    size_t lds;
+    int64_t n_chunks;
+};
+ChunkPlan chunk_plan(const ParseLaunch& a);
+// parse every line, then the URI stages (k_uri_lines, and its direct path),
+// then meta->counters[0..4] += lines, ok, bad, fallback, arena bytes written.
+// Chunked (a.chunked): k_parse_chunks writes the line index, meta->n_lines /
+// cap_ovf and the lines' rows, k_parse_ovf_lines the lines it queued
+// (C.chunk_state zeroed, C.chunk_counts: chunk_plan().n_chunks records,
+// C.ovf_lines: cap_lines entries).  Otherwise the line index exists and the
+// staged waves, then the waves whose window did not fit LDS, run
+// (C.ovf_list and C.uri_ovf_list: parse_waves(cap_lines) + 1 entries each).
+// C: the host copy of the columns the device holds.
+int launch_parse(const ParseLaunch& a, const DeviceArgs* d_args, const Columns& C, hipStream_t s);
+// the URI kernels of a launch (uri.hip)
+int launch_uri(const ParseLaunch& a, const DeviceArgs* d_args, hipStream_t s);
+// meta->counters[0..5] += the sum of n_entries count records (per_group: of
+// 64-line groups, only those holding the batch's meta->n_lines lines)
+int launch_reduce_counts(const uint32_t* d_wave_counts, int64_t n_entries, bool per_group, Meta* d_meta, hipStream_t s);
+#if defined(LP_PROFILE)
+int prof_read_parse(unsigned long long* out);
+int prof_clear_parse();
+int prof_read_uri(unsigned long long* out);
+int prof_clear_uri();
+#endif
 // sticky routing pass 1: C.fmt_match of every line
 int launch_route_match(const ParseLaunch& a, const DeviceArgs* d_args, hipStream_t s);
 // sticky routing pass 2: C.fmt_match -> C.fmt_id (C.fmt_chunk: fmt_chunks()+1 words, the

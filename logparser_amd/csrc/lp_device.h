@@ -23,9 +23,8 @@ enum : int { ST_OK = 0, ST_BAD = 1, ST_FALLBACK = 2 };
 // Profiling build only (-DLP_PROFILE): wave timestamps at fixed points,
 // stored per wave (the waves of blocks [PROF_W0, PROF_W0 + PROF_WAVES)),
 // no atomics: the host averages the cycles between consecutive points.
-constexpr int PROF_WAVES = 16384, PROF_W0 = 1024, PROF_POINTS = 96;
 #if defined(LP_PROFILE) && defined(__HIP__)
-__device__ unsigned long long g_prof[PROF_WAVES * PROF_POINTS];
+static __device__ unsigned long long g_prof[PROF_WAVES * PROF_POINTS];  // one per kernel translation unit
 #endif
 #if defined(LP_PROFILE) && defined(__HIP_DEVICE_COMPILE__)
 __device__ __forceinline__ void lp_prof_mark(int k) {
@@ -107,13 +106,14 @@ __device__ LP_INLINE uint32_t load_word(const LP_G uint8_t* p) {
 #endif
 
 // ---- byte-class bitmasks (1 bit per byte, one 64-bit word per 64 bytes),
-// built once per LDS window by the staging pass of the parse kernel, so the
-// per-line scanners walk 64 bytes per step instead of 4.  Exact for TAB and
-// printable ASCII (every other byte sends its line to FALLBACK before any
-// scanner runs).  Three classes in two bit planes (QUOTE and WS are disjoint
-// subsets of UEV): P0 = UEV minus WS, P1 = UEV minus QUOTE, so QUOTE =
-// P0 & ~P1, WS = P1 & ~P0, UEV = P0 | P1.  The planes of 64-byte block w are
-// the 16 bytes at 16 w (one 128-bit LDS read).
+// built once per LDS window by the staging pass of a kernel, so the per-line
+// scanners walk 64 bytes per step instead of 4.  The parse kernels' windows
+// carry two planes (NPL = 2): P0 = QUOTE ('"'), P1 = WS (the bytes <= 0x20:
+// exactly ' ' and TAB inside a line the guard passes, whose other control
+// bytes send it to FALLBACK before any scanner runs); the planes of 64-byte
+// block w are the 16 bytes at 16 w (one 128-bit LDS read).  The URI kernel's
+// compact buffer carries the one UEV plane (NPL = 1).  Phase 1 never asks
+// for UEV, the URI stages never for QUOTE / WS.
 enum : int {
     MC_QUOTE = 0,  // '"'
     MC_UEV = 1,    // URI events: % # & ? ; + and the bytes URIUtil.encode escapes (not '=', not A-Z)
@@ -150,8 +150,7 @@ struct LineT {
         if constexpr (NPL == 1) {
             return mask_load(m + w);  // c == MC_UEV (the only class of a one-plane line)
         } else {
-            const uint64_t p0 = mask_load(m + 2 * w), p1 = mask_load(m + 2 * w + 1);
-            return c == MC_QUOTE ? (p0 & ~p1) : c == MC_WS ? (p1 & ~p0) : (p0 | p1);
+            return mask_load(m + 2 * w + (c == MC_QUOTE ? 0 : 1));  // QUOTE / WS (no UEV plane, see above)
         }
     }
 };
@@ -267,33 +266,57 @@ __host__ __device__ LP_INLINE uint32_t nonauth_bits(uint32_t w) {
 // bytes with bit 7 set -> 4-bit mask (byte k -> bit k)
 __host__ __device__ LP_INLINE uint32_t nib(uint32_t hb) { return (((hb >> 7) * 0x204081u) >> 21) & 15u; }
 __host__ __device__ LP_INLINE uint32_t uev_hb(uint32_t r) { return (((r & swar::LO7) + swar::LO7) | r) & swar::HI; }
-// 16 bytes (4 little-endian words) -> the 16-bit masks of the two planes
-// (P0: a class bit other than ' ' / TAB, P1: a class bit other than '"')
-__host__ __device__ LP_INLINE void classify16(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t& p0,
-                                              uint32_t& p1) {
-    const uint32_t r0 = bits(w0), r1 = bits(w1), r2 = bits(w2), r3 = bits(w3);
-    constexpr uint32_t NW = 0xFCFCFCFCu, NQ = 0xFBFBFBFBu;
-    p0 = nib(uev_hb(r0 & NW)) | (nib(uev_hb(r1 & NW)) << 4) | (nib(uev_hb(r2 & NW)) << 8) | (nib(uev_hb(r3 & NW)) << 12);
-    p1 = nib(uev_hb(r0 & NQ)) | (nib(uev_hb(r1 & NQ)) << 4) | (nib(uev_hb(r2 & NQ)) << 8) | (nib(uev_hb(r3 & NQ)) << 12);
+// 16 bytes (4 little-endian words) -> the 16-bit UEV mask (the URI kernel's one plane)
+__host__ __device__ LP_INLINE uint32_t pack16(uint32_t h0, uint32_t h1, uint32_t h2, uint32_t h3);
+__host__ __device__ LP_INLINE uint32_t classify16u(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+    return pack16(uev_hb(bits(w0)), uev_hb(bits(w1)), uev_hb(bits(w2)), uev_hb(bits(w3)));
 }
-// The staging guard of a word whose class bits are r = bits(w): the high bit
-// of every byte outside printable ASCII other than TAB, LF and CR (controls
-// are the bytes < 0x20; of those, exactly TAB / LF / CR have class bit 1).
-// Equals swar::guard_bad(w) & ~eq(w, '\n') & ~eq(w, '\r').
-__host__ __device__ LP_INLINE uint32_t guard_word(uint32_t w, uint32_t r) {
-    const uint32_t lo7 = w & swar::LO7;
-    const uint32_t ctl = ~((lo7 + 0x60606060u) | w) & swar::HI;  // bytes < 0x20
-    const uint32_t ge7f = ((lo7 + 0x01010101u) | w) & swar::HI;   // bytes >= 0x7F
-    return (ctl & ~(r << 6)) | ge7f;
+// The parse kernels' staging classifier (SWAR on the 4 little-endian words
+// of 16 bytes): p0 = QUOTE, p1 = WS (bytes <= 0x20) as 16-bit masks, lf /
+// other = the '\n' bytes / the control bytes other than '\n' (TAB, '\r',
+// ...: rare; the caller resolves them), bad |= the bytes >= 0x7F.  The
+// high-bit-per-byte masks are packed with v_dot4_u32_u8 (bytes 0x80 or 0
+// times the bit weights 1, 2, 4, 8): two per 8 mask bits.
+__host__ __device__ LP_INLINE uint32_t pack16(uint32_t h0, uint32_t h1, uint32_t h2, uint32_t h3) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const uint32_t lo = __builtin_amdgcn_udot4(h1, 0x80402010u, __builtin_amdgcn_udot4(h0, 0x08040201u, 0u, false), false);
+    const uint32_t hi = __builtin_amdgcn_udot4(h3, 0x80402010u, __builtin_amdgcn_udot4(h2, 0x08040201u, 0u, false), false);
+    return (lo >> 7) | (hi << 1);  // lo, hi = 0x80 x (8-bit mask)
+#else
+    return nib(h0) | (nib(h1) << 4) | (nib(h2) << 8) | (nib(h3) << 12);
+#endif
 }
-// classify16 and the guard of the same 16 bytes (OR of guard_word)
-__host__ __device__ LP_INLINE void classify16g(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t& p0,
-                                               uint32_t& p1, uint32_t& bad) {
-    const uint32_t r0 = bits(w0), r1 = bits(w1), r2 = bits(w2), r3 = bits(w3);
-    constexpr uint32_t NW = 0xFCFCFCFCu, NQ = 0xFBFBFBFBu;
-    p0 = nib(uev_hb(r0 & NW)) | (nib(uev_hb(r1 & NW)) << 4) | (nib(uev_hb(r2 & NW)) << 8) | (nib(uev_hb(r3 & NW)) << 12);
-    p1 = nib(uev_hb(r0 & NQ)) | (nib(uev_hb(r1 & NQ)) << 4) | (nib(uev_hb(r2 & NQ)) << 8) | (nib(uev_hb(r3 & NQ)) << 12);
-    bad |= guard_word(w0, r0) | guard_word(w1, r1) | guard_word(w2, r2) | guard_word(w3, r3);
+__host__ __device__ LP_INLINE void classify16p(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t& p0,
+                                               uint32_t& p1, uint32_t& bad, uint32_t& lf, uint32_t& other) {
+    const uint32_t w[4] = {w0, w1, w2, w3};
+    uint32_t q[4], le[4], l[4], o = 0, hi = 0;
+    LP_UNROLL for (int k = 0; k < 4; ++k) {
+        const uint32_t lo7 = w[k] & swar::LO7;
+        le[k] = ~((lo7 + 0x5F5F5F5Fu) | w[k]) & swar::HI;         // bytes <= 0x20
+        const uint32_t lt = ~((lo7 + 0x60606060u) | w[k]) & swar::HI;  // bytes < 0x20
+        hi |= ((lo7 + 0x01010101u) | w[k]) & swar::HI;             // bytes >= 0x7F
+        q[k] = swar::eq(w[k], '"');
+        l[k] = swar::eq(w[k], '\n');
+        o |= lt & ~l[k];
+    }
+    p0 = pack16(q[0], q[1], q[2], q[3]);
+    p1 = pack16(le[0], le[1], le[2], le[3]);
+    lf = pack16(l[0], l[1], l[2], l[3]);
+    bad |= hi;
+    other = o;
+}
+// the guard of 16 bytes holding control bytes other than '\n' (classify16p's
+// `other`): the controls other than TAB / LF / CR, and the '\r' mask
+__host__ __device__ LP_INLINE void classify16c(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t& bad,
+                                               uint32_t& cr) {
+    const uint32_t w[4] = {w0, w1, w2, w3};
+    uint32_t c[4];
+    LP_UNROLL for (int k = 0; k < 4; ++k) {
+        const uint32_t lt = ~(((w[k] & swar::LO7) + 0x60606060u) | w[k]) & swar::HI;
+        c[k] = swar::eq(w[k], '\r');
+        bad |= lt & ~(c[k] | swar::eq(w[k], '\n') | swar::eq(w[k], '\t'));
+    }
+    cr = pack16(c[0], c[1], c[2], c[3]);
 }
 // mask class whose members are exactly the byte c, -1 none
 __host__ __device__ LP_INLINE int class_of(uint32_t c) { return c == '"' ? (int)MC_QUOTE : -1; }
@@ -307,8 +330,8 @@ inline void build_masks(const uint8_t* buf, uint32_t n, uint64_t* masks) {
     for (uint32_t k = 0; 16 * k < n; ++k) {
         uint32_t w[4];
         for (int j = 0; j < 4; ++j) __builtin_memcpy(&w[j], buf + 16 * k + 4 * j, 4);
-        uint32_t a, b;
-        bcls::classify16(w[0], w[1], w[2], w[3], a, b);
+        uint32_t a, b, bad = 0, lf, other;
+        bcls::classify16p(w[0], w[1], w[2], w[3], a, b, bad, lf, other);
         const int sh = 16 * (k & 3);
         masks[2 * (k >> 2)] |= (uint64_t)a << sh;
         masks[2 * (k >> 2) + 1] |= (uint64_t)b << sh;
@@ -321,9 +344,7 @@ inline void build_uev_plane(const uint8_t* buf, uint32_t n, uint64_t* plane) {
     for (uint32_t k = 0; 16 * k < n; ++k) {
         uint32_t w[4];
         for (int j = 0; j < 4; ++j) __builtin_memcpy(&w[j], buf + 16 * k + 4 * j, 4);
-        uint32_t a, b;
-        bcls::classify16(w[0], w[1], w[2], w[3], a, b);
-        plane[k >> 2] |= (uint64_t)(a | b) << (16 * (k & 3));
+        plane[k >> 2] |= (uint64_t)bcls::classify16u(w[0], w[1], w[2], w[3]) << (16 * (k & 3));
     }
 }
 
@@ -1813,6 +1834,14 @@ struct LineOut {
     RegArr<MAX_TOK> caps;
     uint32_t tok_flags;
     RegArr<MAX_FL> fl_kind, fl_method, fl_uri, fl_proto;
+    // time stage t's results (bit t of tdone: delivered), written with the
+    // row by write_line (the chunked kernel knows the line's number only
+    // after phase 1)
+    uint32_t tdone;
+    RegArr<MAX_TIME> ep_lo, ep_hi, lo_lo, lo_hi, ut_lo, ut_hi, nano;
+    uint32_t hist;  // run-histogram word of an OK line (hist_word)
+    uint32_t smdone;  // SECOND_MILLIS stage s delivered (bit s)
+    RegArr<MAX_SECMS> sm_lo, sm_hi;
 };
 
 // A line's URI stages (the URI kernel): per query stage the piece table
@@ -2027,6 +2056,159 @@ __host__ __device__ LP_INLINE bool setcookie_ok(const LN& L, int a, int b, bool 
     return true;
 }
 
+// ---- ConvertSecondsWithMillisStringDissector
+// (translate/ConvertSecondsWithMillisStringDissector.java:33-40):
+// value.split("\\.", 2), Long.parseLong of both, seconds * 1000 +
+// milliseconds (the fraction read as an integer: "1.5" -> 1005), Java long
+// arithmetic (wraps).  The element kinds deliver digits '.' digits of at
+// most 18 digits each (decimal_at), so neither parse can throw.
+template <typename LN>
+__host__ __device__ LP_INLINE int64_t secms_value(const LN& L, int a, int b) {
+    uint64_t sec = 0, frac = 0;
+    int q = a;
+    for (; q < b && L[q] != '.'; ++q) sec = sec * 10u + (L[q] - '0');
+    for (++q; q < b; ++q) frac = frac * 10u + (L[q] - '0');
+    return (int64_t)(sec * 1000u + frac);
+}
+
+// ---- UpstreamListDissector.dissect (nginxmodules/UpstreamListDissector.java:79-125):
+// servers = value.split(", "); per server parts = server.split(": "); item
+// k's value = parts[0].trim(), redirected = (parts.length == 1 ? parts[0] :
+// parts[1]).trim().  Java String.split (limit 0): trailing empty pieces are
+// dropped, a value without the separator is itself the one piece (even
+// empty); String.trim drops bytes <= ' ' at both ends.  Calls f(k, va, vb,
+// ra, rb) for every item in order (trimmed line positions) and returns the
+// item count, -1 for a server that splits into no parts (": " pairs only: an
+// ArrayIndexOutOfBoundsException in the reference; the element kinds send
+// such lines to FALLBACK).
+template <typename LN>
+__host__ __device__ LP_INLINE int sep_at(const LN& L, int q, int e, uint32_t c0) {  // c0 then ' ' at q
+    return q + 1 < e && L[q] == c0 && L[q + 1] == ' ';
+}
+template <typename LN, typename F>
+__host__ __device__ LP_INLINE int uplist_items(const LN& L, int a, int b, F&& f) {
+    auto next_sep = [&](int q, int e, uint32_t c0) {
+        while (q + 1 < e && !sep_at(L, q, e, c0)) ++q;
+        return q + 1 < e ? q : e;
+    };
+    auto strip = [&](int s, int e, uint32_t c0) {  // drop the separators of trailing empty pieces
+        while (e - s >= 2 && L[e - 2] == c0 && L[e - 1] == ' ') e -= 2;
+        return e;
+    };
+    auto trim = [&](int& s, int& e) {
+        while (s < e && L[s] <= ' ') ++s;
+        while (e > s && L[e - 1] <= ' ') --e;
+    };
+    int t = b;
+    if (next_sep(a, b, ',') < b) {
+        t = strip(a, b, ',');
+        if (t == a) return 0;  // only empty servers
+    }
+    int k = 0;
+    for (int s0 = a;;) {
+        const int e0 = next_sep(s0, t, ',');
+        const int x0 = next_sep(s0, e0, ':');
+        int va = s0, vb = x0, ra = s0, rb = x0;
+        if (x0 < e0) {
+            // more than one part unless everything after the first ": " is empty pieces
+            const int r1 = strip(x0 + 2, e0, ':');
+            if (r1 > x0 + 2) {
+                ra = x0 + 2;
+                rb = next_sep(x0 + 2, e0, ':');
+            } else if (x0 == s0) {
+                return -1;  // no parts at all
+            }
+        }
+        trim(va, vb);
+        trim(ra, rb);
+        f(k, va, vb, ra, rb);
+        ++k;
+        if (e0 >= t) break;
+        s0 = e0 + 2;
+    }
+    return k;
+}
+
+// ---- run histograms (lp_histograms, SURVEY.md §5 counters): one word per
+// OK line, reduced on demand: bits 0..15 token k present (not "-" and not
+// empty), bits 16..25 the response status code (100..599; 0: another value
+// or null; 1023: the format has no status token), bits 26..30 the request
+// method (0..14 the names below, 15 another, 16 none; 31: the format has no
+// first-line stage).
+constexpr int HIST_METHOD_OTHER = 15, HIST_METHOD_NONE = 16;
+// GET POST HEAD PUT DELETE OPTIONS PATCH CONNECT TRACE PROPFIND MKCOL COPY MOVE LOCK UNLOCK
+template <typename LN>
+__host__ __device__ LP_INLINE int hist_method(const LN& L, int a, int b) {
+    if (b <= a) return HIST_METHOD_NONE;  // no method (null or empty first line, or neither regex matched)
+    const int n = b - a;
+    if (n > 9) return HIST_METHOD_OTHER;
+    const uint32_t w0 = load_u32_at(L, a) & (n >= 4 ? ~0u : (1u << (8 * n)) - 1u);
+    const uint32_t w1 = n > 4 ? load_u32_at(L, a + 4) & (n >= 8 ? ~0u : (1u << (8 * (n - 4))) - 1u) : 0u;
+    const uint32_t w2 = n > 8 ? L[a + 8] : 0u;
+    auto W = [](char c0, char c1, char c2, char c3) {
+        return (uint32_t)(uint8_t)c0 | ((uint32_t)(uint8_t)c1 << 8) | ((uint32_t)(uint8_t)c2 << 16) | ((uint32_t)(uint8_t)c3 << 24);
+    };
+    switch (n) {
+    case 3:
+        if (w0 == W('G', 'E', 'T', 0)) return 0;
+        if (w0 == W('P', 'U', 'T', 0)) return 3;
+        break;
+    case 4:
+        if (w0 == W('P', 'O', 'S', 'T')) return 1;
+        if (w0 == W('H', 'E', 'A', 'D')) return 2;
+        if (w0 == W('C', 'O', 'P', 'Y')) return 11;
+        if (w0 == W('M', 'O', 'V', 'E')) return 12;
+        if (w0 == W('L', 'O', 'C', 'K')) return 13;
+        break;
+    case 5:
+        if (w0 == W('P', 'A', 'T', 'C') && w1 == 'H') return 6;
+        if (w0 == W('T', 'R', 'A', 'C') && w1 == 'E') return 8;
+        if (w0 == W('M', 'K', 'C', 'O') && w1 == 'L') return 10;
+        break;
+    case 6:
+        if (w0 == W('D', 'E', 'L', 'E') && w1 == W('T', 'E', 0, 0)) return 4;
+        if (w0 == W('U', 'N', 'L', 'O') && w1 == W('C', 'K', 0, 0)) return 14;
+        break;
+    case 7:
+        if (w0 == W('O', 'P', 'T', 'I') && w1 == W('O', 'N', 'S', 0)) return 5;
+        if (w0 == W('C', 'O', 'N', 'N') && w1 == W('E', 'C', 'T', 0)) return 7;
+        break;
+    case 8:
+        if (w0 == W('P', 'R', 'O', 'P') && w1 == W('F', 'I', 'N', 'D')) return 9;
+        break;
+    default: break;
+    }
+    (void)w2;
+    return HIST_METHOD_OTHER;
+}
+template <typename LN>
+__host__ __device__ LP_INLINE uint32_t hist_word(const Program& P, const LN& L, const LineOut& o) {
+    uint32_t present = 0;
+    o.caps.each([&](int k, uint32_t sp) {
+        if (k < P.n_tok && !((o.tok_flags >> k) & 1u) && (sp >> 16) > (sp & 0xFFFFu)) present |= 1u << k;
+    });
+    const int sk = P.hist_status[o.fmt];
+    uint32_t code = sk >= 0 ? 0u : 1023u;  // 1023: the format has no status token (no count)
+    if (sk >= 0 && !((o.tok_flags >> sk) & 1u)) {
+        const uint32_t sp = o.caps.get(sk);
+        const int a = (int)(sp & 0xFFFFu), b = (int)(sp >> 16);
+        if (b - a == 3) {
+            const uint32_t d0 = L[a] - '0', d1 = L[a + 1] - '0', d2 = L[a + 2] - '0';
+            if (d0 < 10 && d1 < 10 && d2 < 10) code = d0 * 100 + d1 * 10 + d2;
+            if (code < 100 || code > 599) code = 0;
+        }
+    }
+    uint32_t m = HIST_METHOD_NONE;
+    const int f = P.hist_fl[o.fmt];
+    if (f >= 0) {
+        const uint32_t sp = o.fl_method.get(f);
+        m = (uint32_t)hist_method(L, (int)(sp & 0xFFFFu), (int)(sp >> 16));
+    } else {
+        m = 31;  // the format has no first-line stage: no method count
+    }
+    return present | (code << 16) | (m << 26);
+}
+
 // Phase 1: guard, match, tokens, time, first line (the parse kernel).
 // clean: the caller already proved every byte of the line passes the
 // fast-path guard (the kernel checks the whole staged window at once).
@@ -2036,6 +2218,8 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
     o.status = ST_OK;
     o.fmt = fmt;
     o.tok_flags = 0;
+    o.tdone = 0;
+    o.smdone = 0;
     o.caps.fill(0);
     o.fl_kind.fill(FL_NONE);
     o.fl_method.fill(0);
@@ -2133,11 +2317,16 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
             if (b == a || (o.tok_flags & (1u << k))) continue;
             const int st = parse_strf_time(T, L, a, b, ep, lo, ut, ns);
             if (st != ST_OK) { o.status = st; return; }
-            C.t_nano[t][li] = ns;
         }
-        C.t_epoch[t][li] = ep;
-        C.t_local[t][li] = lo;
-        C.t_utc[t][li] = ut;
+        // t is wave-uniform: indexed register writes
+        o.tdone |= 1u << t;
+        o.ep_lo.set_u(t, (uint32_t)(uint64_t)ep);
+        o.ep_hi.set_u(t, (uint32_t)((uint64_t)ep >> 32));
+        o.lo_lo.set_u(t, (uint32_t)lo);
+        o.lo_hi.set_u(t, (uint32_t)(lo >> 32));
+        o.ut_lo.set_u(t, (uint32_t)ut);
+        o.ut_hi.set_u(t, (uint32_t)(ut >> 32));
+        o.nano.set_u(t, ns);
     }
     LP_PROF(6);
     // HttpFirstLineDissector: ^([a-zA-Z-_]+) (.*) (HTTP/[0-9]+\.[0-9]+)$ else ^([a-zA-Z-_]+) (.*)$
@@ -2178,6 +2367,18 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
             o.fl_proto.set(f, 0);
         }
     }
+    // ConvertSecondsWithMillisStringDissector on this format's SECOND_MILLIS tokens
+    for (int sm = 0; sm < P.n_secms; ++sm) {
+        if (P.secms[sm].fmt != fmt) continue;
+        const int k = P.secms[sm].tok;
+        if ((o.tok_flags >> k) & 1u) continue;  // "-" never matches the token kinds; nothing to convert
+        const uint32_t sp = o.caps.get(k);
+        const int64_t ms = secms_value(L, (int)(sp & 0xFFFFu), (int)(sp >> 16));
+        o.smdone |= 1u << sm;
+        o.sm_lo.set_u(sm, (uint32_t)(uint64_t)ms);
+        o.sm_hi.set_u(sm, (uint32_t)((uint64_t)ms >> 32));
+    }
+    o.hist = hist_word(P, L, o);
     LP_PROF(7);
 }
 
@@ -3068,10 +3269,67 @@ __host__ __device__ LP_INLINE void write_line(const Program& P, const LineOut& o
     if (o.status != ST_OK) return;
     o.caps.each([&](int k, uint32_t v) { if (k < P.n_tok) C.tok_span[k][li] = v; });
     C.tok_flags[li] = o.tok_flags;
+    if (C.hist) C.hist[li] = o.hist;
     o.fl_kind.each([&](int f, uint32_t v) { if (f < P.n_fl) C.fl_kind[f][li] = v; });
     o.fl_method.each([&](int f, uint32_t v) { if (f < P.n_fl) C.fl_method[f][li] = v; });
     o.fl_uri.each([&](int f, uint32_t v) { if (f < P.n_fl) C.fl_uri[f][li] = v; });
     o.fl_proto.each([&](int f, uint32_t v) { if (f < P.n_fl) C.fl_proto[f][li] = v; });
+    for (int t = 0; t < P.n_time; ++t) {
+        if (!((o.tdone >> t) & 1u)) continue;
+        C.t_epoch[t][li] = (int64_t)(((uint64_t)o.ep_hi.get(t) << 32) | o.ep_lo.get(t));
+        C.t_local[t][li] = ((uint64_t)o.lo_hi.get(t) << 32) | o.lo_lo.get(t);
+        C.t_utc[t][li] = ((uint64_t)o.ut_hi.get(t) << 32) | o.ut_lo.get(t);
+        if (P.time[t].kind == TK_STRF) C.t_nano[t][li] = o.nano.get(t);
+    }
+    for (int sm = 0; sm < P.n_secms; ++sm)
+        if ((o.smdone >> sm) & 1u) C.sm_ms[sm][li] = (int64_t)(((uint64_t)o.sm_hi.get(sm) << 32) | o.sm_lo.get(sm));
+}
+
+// ---- the upstream list stages of one OK line (phase 2, after its URI
+// stages: the item tables follow the URI stages' tables in the line's
+// region).  L: a view of the line holding at least the list tokens.
+// list_need: the region bytes the line's lists take; list_fill writes the
+// tables and the l_count / l_tab columns.
+template <typename LN, typename Cols>
+__host__ __device__ LP_INLINE uint32_t list_need(const Program& P, int fmt, const LN& L, const Cols& C, int64_t li) {
+    uint32_t need = 0;
+    for (int j = 0; j < P.n_list; ++j) {
+        const ListStage& S = P.list[j];
+        if (S.fmt != fmt) continue;
+        const uint32_t sp = C.tok_span[S.tok][li];
+        const int n = uplist_items(L, (int)(sp & 0xFFFFu), (int)(sp >> 16), [](int, int, int, int, int) {});
+        if (n > 0) need += 8 + (uint32_t)n * (S.secms ? LIST_ENT_MS : LIST_ENT);
+    }
+    return need;
+}
+template <typename LN, typename Cols>
+__host__ __device__ LP_INLINE bool list_fill(const Program& P, int fmt, const LN& L, Arena& A, Cols& C, int64_t li) {
+    for (int j = 0; j < P.n_list; ++j) {
+        const ListStage& S = P.list[j];
+        if (S.fmt != fmt) continue;
+        const uint32_t sp = C.tok_span[S.tok][li];
+        const int a = (int)(sp & 0xFFFFu), b = (int)(sp >> 16);
+        const uint32_t ent = S.secms ? LIST_ENT_MS : LIST_ENT;
+        const int n = uplist_items(L, a, b, [](int, int, int, int, int) {});
+        if (n < 0) return false;
+        const uint32_t off = (A.used + 7u) & ~7u;
+        if (n > 0 && off + (uint32_t)n * ent > A.cap) return false;
+        if (n > 0) A.used = off + (uint32_t)n * ent;
+        LP_G uint8_t* tab = A.p + off;
+        uplist_items(L, a, b, [&](int k, int va, int vb, int ra, int rb) {
+            LP_G uint32_t* e32 = reinterpret_cast<LP_G uint32_t*>(tab + (uint32_t)k * ent);
+            e32[0] = mkspan((uint32_t)va, (uint32_t)vb);
+            e32[1] = mkspan((uint32_t)ra, (uint32_t)rb);
+            if (S.secms) {
+                LP_G int64_t* e64 = reinterpret_cast<LP_G int64_t*>(tab + (uint32_t)k * ent + 8);
+                e64[0] = secms_value(L, va, vb);
+                e64[1] = secms_value(L, ra, rb);
+            }
+        });
+        C.l_count[j][li] = (uint32_t)n;
+        C.l_tab[j][li] = n > 0 ? mkref(off, (uint32_t)n * ent, true) : 0ull;
+    }
+    return true;
 }
 
 }  // namespace lp

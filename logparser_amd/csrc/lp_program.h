@@ -31,6 +31,9 @@
 
 namespace lp {
 
+// profiling build (-DLP_PROFILE, lp_device.h): per-wave timestamps of waves [PROF_W0, PROF_W0 + PROF_WAVES)
+constexpr int PROF_WAVES = 16384, PROF_W0 = 1024, PROF_POINTS = 96;
+
 constexpr int MAX_ELEMS = 96;
 constexpr int MAX_FMT = 8;        // LogFormats of one HttpdLogFormatDissector (sticky routing)
 constexpr int MAX_FMT_ELEMS = 64; // elements of one LogFormat (6-bit DFS stack index)
@@ -44,6 +47,8 @@ constexpr int MAX_QUERY = 8;
 constexpr int MAX_QNAMES = 32;   // explicitly requested query parameter names
 constexpr int MAX_LINE = 8191;   // longer lines -> FALLBACK (13-bit offsets)
 constexpr int MAX_STACK = 16;    // DFS choice points
+constexpr int MAX_SECMS = 4;     // SECOND_MILLIS token conversions (ConvertSecondsWithMillisStringDissector)
+constexpr int MAX_LIST = 4;      // NGINX upstream lists (UpstreamListDissector)
 
 // Element kinds = the token regexes of the Apache table
 // (hp/dissectors/tokenformat/TokenParser.java:35-59).
@@ -178,6 +183,28 @@ struct QueryStage {
     uint32_t name_len[MAX_QNAMES];
 };
 
+// ConvertSecondsWithMillisStringDissector on a captured token
+// (translate/ConvertSecondsWithMillisStringDissector.java:33-40): "S.F" ->
+// S * 1000 + F (the fraction read as an integer); phase 1 writes the int64.
+struct SecmsStage {
+    int32_t tok;
+    int32_t fmt;
+};
+
+// UpstreamListDissector on a captured list token
+// (nginxmodules/UpstreamListDissector.java:79-125): the items of
+// split(", "), each server's split(": ") parts trimmed.  The URI kernel
+// writes per line the item count and, in the line's arena region, one entry
+// per item: the value and redirected spans (u32, line-relative), then for
+// SECOND_MILLIS lists both as milliseconds (i64).
+struct ListStage {
+    int32_t tok;
+    int32_t fmt;
+    int32_t secms;  // the items are SECOND_MILLIS (their conversions are stored too)
+    int32_t pad;
+};
+constexpr uint32_t LIST_ENT = 8, LIST_ENT_MS = 24;  // entry bytes without / with the milliseconds
+
 // Stages (time / first line / URI) belong to one LogFormat: a line runs the
 // stages of the format it was routed to.  Token slot k of a line is the k-th
 // captured token of that line's format.
@@ -207,13 +234,18 @@ struct Program {
     // dissects (every "expires" must then parse)
     int32_t guard_setc[MAX_FMT];
     int32_t guard_setc_exp[MAX_FMT];
-    int32_t pad_[2];
+    int32_t n_secms, n_list;
+    SecmsStage secms[MAX_SECMS];
+    ListStage list[MAX_LIST];
     Elem elems[MAX_ELEMS];
     TimeStage time[MAX_TIME];
     FlStage fl[MAX_FL];
     UriStage uri[MAX_URI];
     QueryStage query[MAX_QUERY];
     alignas(4) uint8_t lit[MAX_LIT];
+    // phase 2 runs (the URI kernel): URI stages or upstream list stages, whose
+    // results live in the line's arena region
+    __host__ __device__ bool has_phase2() const { return n_uri > 0 || n_list > 0; }
     // literal pool byte i, read as a dword (scalar load for a uniform index)
     __host__ __device__ uint32_t lit_byte(int i) const {
         return (reinterpret_cast<const uint32_t*>(lit)[i >> 2] >> (8 * (i & 3))) & 0xFFu;
@@ -285,7 +317,8 @@ struct Meta {
     unsigned long long arena_ovf;    // lines whose arena allocation did not fit its shard (retry)
     unsigned long long fmt_state;    // routed LogFormat after the batch's last line
     unsigned long long uri_ovf_waves;// waves whose URI bytes exceed the URI kernel's compact buffer (direct path)
-    unsigned long long pad[2];
+    unsigned long long ovf_lines;    // lines the chunked parse kernel queued for the direct kernel
+    unsigned long long pad[1];
     unsigned long long shard_top[ARENA_SHARDS * 16];  // bump pointer of shard s at [16 s] (own 128-B line)
 };
 
@@ -294,6 +327,7 @@ struct Columns {
     const LP_G uint64_t* line_off; // [n+1]
     LP_G uint32_t* tok_span[MAX_TOK];
     LP_G uint32_t* tok_flags;      // bit k: value "-" (null); bit 16+k: value == "0"
+    LP_G uint32_t* hist;           // run-histogram word of an OK line (lp_device.h hist_word)
     LP_G int64_t* t_epoch[MAX_TIME];
     LP_G uint64_t* t_local[MAX_TIME];
     LP_G uint64_t* t_utc[MAX_TIME];
@@ -311,6 +345,9 @@ struct Columns {
     LP_G uint64_t* u_frag[MAX_URI];
     LP_G uint32_t* q_count[MAX_QUERY]; // params are (name ref, value ref) pairs in the arena
     LP_G uint64_t* q_params[MAX_QUERY];// ref to the param table in the arena
+    LP_G int64_t* sm_ms[MAX_SECMS];    // SECOND_MILLIS stage s: the token as milliseconds
+    LP_G uint32_t* l_count[MAX_LIST];  // upstream list stage j: items
+    LP_G uint64_t* l_tab[MAX_LIST];    // ... region ref of its item table (ListStage)
     LP_G uint64_t* arena_base;         // [n]
     // sticky multi-format routing (Program::n_fmt > 1)
     LP_G uint16_t* fmt_match;          // [n] bit f: format f matches; bit 8+f: undecided on the device
@@ -323,6 +360,12 @@ struct Columns {
     LP_G uint32_t* ovf_list;             // waves for the direct parse kernel
     LP_G uint32_t* uri_ovf_list;         // waves for the direct URI kernel
     LP_G uint32_t* wave_counts;          // [n_waves][WC_WORDS] lines ok bad fallback written (reduced after the launch)
+    // chunked parse (one-format programs: the line index built inside the
+    // parse kernel): per byte chunk the decoupled look-back word, its status
+    // counts, and the lines queued for the direct kernel
+    LP_G uint64_t* chunk_state;          // [n_chunks] aggregate / inclusive line counts
+    LP_G uint32_t* chunk_counts;         // [n_chunks][WC_WORDS]
+    LP_G uint32_t* ovf_lines;            // [cap_lines] line numbers
     int64_t cap_lines;                   // lines the columns hold
 };
 

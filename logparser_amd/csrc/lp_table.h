@@ -23,6 +23,9 @@ enum : int32_t {
     TC_URI,        // a = URI stage, b = UP_* part
     TC_QP,         // a = query stage, b / c = offset / length of the name in TableArgs::names (the last occurrence)
     TC_NULL,       // always null (HttpUriDissector's userinfo)
+    TC_SECMS,      // a = SECOND_MILLIS stage: its milliseconds (b = 1: x 1000, MICROSECONDS)
+    TC_LIST,       // a = upstream list stage, b = item, c = 0 value / 1 redirected
+    TC_LIST_MS,    // a = SECOND_MILLIS list stage, b = item, c bit 0: redirected, bit 1: MICROSECONDS
 };
 enum : int32_t { TF_EPOCH, TF_DAY, TF_MONTHNAME, TF_MONTH, TF_WEEK, TF_WEEKYEAR, TF_YEAR, TF_HOUR, TF_MINUTE,
                  TF_SECOND, TF_MILLI, TF_MICRO, TF_NANO, TF_DATE, TF_TIME };

@@ -1255,7 +1255,12 @@ int Plan::possible_paths(const std::string& logformats, int max_depth, std::vect
 // ====================================================== device program
 namespace {
 // O_QPARAM: a query parameter's value (index: query stage * MAX_QNAMES + name index)
-enum Origin { O_NONE, O_TOKEN, O_FL_URI, O_FL_PROTO, O_FL_METHOD, O_URI_QUERY, O_URI_PART, O_CONV, O_TIME, O_QPARAM };
+// O_SECMS: a SECOND_MILLIS stage's milliseconds (index: the stage); O_LITEM /
+// O_LITEMMS: an upstream list item's value / its milliseconds (index:
+// item << 3 | redirected << 2 | list stage, item_code below)
+enum Origin { O_NONE, O_TOKEN, O_FL_URI, O_FL_PROTO, O_FL_METHOD, O_URI_QUERY, O_URI_PART, O_CONV, O_TIME, O_QPARAM,
+              O_SECMS, O_LITEM, O_LITEMMS };
+int item_code(int j, int k, int redirected) { return (k << 3) | (redirected << 2) | j; }
 }
 
 void Plan::compile_program() {
@@ -1610,9 +1615,40 @@ void Plan::compile_program() {
                     }
                     break;
                 }
-                case D_CLF2NUM: case D_NUM2CLF: case D_SECMILLIS: case D_MS2US: case D_BINIP:
+                case D_SECMILLIS:
+                    // ConvertSecondsWithMillisStringDissector: phase 1 converts a
+                    // token (a SECOND_MILLIS stage), the URI kernel every item of
+                    // a SECOND_MILLIS upstream list (its table holds both)
+                    if (ok == O_TOKEN) {
+                        auto st = secms_of_tok_.find(tk(oi));
+                        if (st == secms_of_tok_.end()) {
+                            if (P.n_secms == MAX_SECMS) { device_ok_ = false; why_ = "too many SECOND_MILLIS values"; return; }
+                            P.secms[P.n_secms] = SecmsStage{oi, cur_fmt};
+                            st = secms_of_tok_.emplace(tk(oi), P.n_secms++).first;
+                        }
+                        treg(in.d->out_type + ":" + complete, TableSrc{TC_SECMS, st->second, 0, 0});
+                        walk(O_SECMS, st->second, in.d->out_type, complete, false);
+                    } else if (ok == O_LITEM) {
+                        if (!P.list[oi & 3].secms) { device_ok_ = false; why_ = "SECOND_MILLIS of a non-time list"; return; }
+                        treg(in.d->out_type + ":" + complete, TableSrc{TC_LIST_MS, oi & 3, oi >> 3, (oi >> 2) & 1});
+                        walk(O_LITEMMS, oi, in.d->out_type, complete, false);
+                    } else {
+                        device_ok_ = false;
+                        why_ = "SECOND_MILLIS converter on a derived value";
+                        return;
+                    }
+                    break;
+                case D_MS2US:
+                    // ConvertMillisecondsIntoMicroseconds on a device millisecond value
+                    if (ok == O_SECMS) treg(in.d->out_type + ":" + complete, TableSrc{TC_SECMS, oi, 1, 0});
+                    else if (ok == O_LITEMMS) treg(in.d->out_type + ":" + complete, TableSrc{TC_LIST_MS, oi & 3, oi >> 3, ((oi >> 2) & 1) | 2});
+                    else if (ok == O_TOKEN || ok == O_CONV) thost_exact_[cur_fmt].insert(in.d->out_type + ":" + complete);
+                    else { device_ok_ = false; why_ = "converter on a derived value"; return; }
+                    walk(O_CONV, oi, in.d->out_type, complete, false);
+                    break;
+                case D_CLF2NUM: case D_NUM2CLF: case D_BINIP:
                     // value-level conversions, done in the replay from the token / list item
-                    if (ok != O_TOKEN && ok != O_CONV) { device_ok_ = false; why_ = "converter on a derived value"; return; }
+                    if (ok != O_TOKEN && ok != O_CONV && ok != O_LITEM) { device_ok_ = false; why_ = "converter on a derived value"; return; }
                     if (ok == O_TOKEN && (in.cls == D_CLF2NUM || in.cls == D_NUM2CLF))
                         treg(in.d->out_type + ":" + complete, TableSrc{in.cls == D_CLF2NUM ? TC_CLF2NUM : TC_NUM2CLF, oi, 0, 0});
                     else
@@ -1620,13 +1656,23 @@ void Plan::compile_program() {
                     walk(O_CONV, oi, in.d->out_type, complete, false);
                     break;
                 case D_UPSTREAM: {
-                    // the list token's element kind (EK_UPLIST_*) proves the list
-                    // splits into clean items; the split is done in the replay
+                    // UpstreamListDissector: the URI kernel splits the list (the
+                    // token's element kind, EK_UPLIST_*, proves it splits cleanly)
+                    // into an item table in the line's region
                     if (ok != O_TOKEN) { device_ok_ = false; why_ = "upstream list from a derived value"; return; }
-                    thost(complete);
+                    auto st = list_of_tok_.find(tk(oi));
+                    if (st == list_of_tok_.end()) {
+                        if (P.n_list == MAX_LIST) { device_ok_ = false; why_ = "too many upstream lists"; return; }
+                        P.list[P.n_list] = ListStage{oi, cur_fmt, in.d->out_type == "SECOND_MILLIS" ? 1 : 0, 0};
+                        st = list_of_tok_.emplace(tk(oi), P.n_list++).first;
+                    }
+                    const int j = st->second;
                     for (int k = 0; k < 32; ++k)
-                        for (const char* sfx : {".value", ".redirected"})
-                            walk(O_CONV, oi, in.d->out_type, complete + "." + std::to_string(k) + sfx, false);
+                        for (int vr = 0; vr < 2; ++vr) {
+                            const std::string item = complete + "." + std::to_string(k) + (vr ? ".redirected" : ".value");
+                            treg(in.d->out_type + ":" + item, TableSrc{TC_LIST, j, k, vr});
+                            walk(O_LITEM, item_code(j, k, vr), in.d->out_type, item, false);
+                        }
                     break;
                 }
                 default:
@@ -1991,15 +2037,21 @@ void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const 
     }
     case D_SECMILLIS: {
         // ConvertSecondsWithMillisStringDissector (translate/ConvertSecondsWithMillisStringDissector.java:33-40):
-        // "S.F" -> S * 1000 + Long.parseLong(F); the token / list item kinds
-        // guarantee digits '.' digits of at most 18 digits each
-        uint32_t d = 0;
-        while (d < v.len && v.p[d] != '.') ++d;
-        int64_t sec = 0, ms = 0;
-        for (uint32_t k = 0; k < d; ++k) sec = sec * 10 + (v.p[k] - '0');
-        for (uint32_t k = d + 1; k < v.len; ++k) ms = ms * 10 + (v.p[k] - '0');
-        set_origin(O_CONV, oi);
-        emit(c, name, in.d->out_type, "", mlong((int64_t)((uint64_t)sec * 1000u + (uint64_t)ms)));
+        // "S.F" -> S * 1000 + Long.parseLong(F), converted on the device: a
+        // token by phase 1 (sm_ms), an upstream list item by the URI kernel
+        // (its table entry)
+        int64_t ms = 0;
+        if (ok == O_TOKEN) {
+            ms = R.sm_ms[secms_of_tok_.at(t_fmt * 64 + oi)][i];
+        } else if (ok == O_LITEM) {
+            const int j = oi & 3, k = oi >> 3, vr = (oi >> 2) & 1;
+            const uint8_t* tab = c.arena + ref_off(R.l_tab[j][i]);
+            memcpy(&ms, tab + (size_t)k * LIST_ENT_MS + 8 + 8 * vr, 8);
+        } else {
+            return;  // not reached: the planner keeps such programs off the device
+        }
+        set_origin(ok == O_TOKEN ? O_SECMS : O_LITEMMS, ok == O_TOKEN ? secms_of_tok_.at(t_fmt * 64 + oi) : oi);
+        emit(c, name, in.d->out_type, "", mlong(ms));
         return;
     }
     case D_MS2US: {
@@ -2011,44 +2063,22 @@ void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const 
     case D_UPSTREAM: {
         // UpstreamListDissector.dissect (nginxmodules/UpstreamListDissector.java:79-125):
         // servers = value.split(", "); parts = server.split(": "); outputs
-        // parts[0].trim() and (parts.length == 1 ? parts[0] : parts[1]).trim().
-        // String.split drops trailing empty pieces (an all-empty split is
-        // empty); the device sends a server whose parts would be empty (an
-        // ArrayIndexOutOfBoundsException in the reference) to FALLBACK.
+        // parts[0].trim() and (parts.length == 1 ? parts[0] : parts[1]).trim(),
+        // split on the device (lp_device.h uplist_items): the URI kernel's
+        // item table in the line's region (value / redirected spans)
         if (v.null) return;
-        auto trim = [](const uint8_t* p, uint32_t n) {
-            uint32_t a = 0, b = n;
-            while (a < b && p[a] <= ' ') ++a;
-            while (b > a && p[b - 1] <= ' ') --b;
-            return mstr(p + a, b - a);
-        };
-        // Java String.split(two-char literal), limit 0: pieces as (offset, length)
-        auto split2 = [](const uint8_t* p, uint32_t n, uint8_t c0, uint8_t c1) {
-            std::vector<std::pair<uint32_t, uint32_t>> out;
-            uint32_t from = 0;
-            for (uint32_t q = 0; q + 1 < n; ++q)
-                if (p[q] == c0 && p[q + 1] == c1) {
-                    out.emplace_back(from, q - from);
-                    from = q + 2;
-                    ++q;
-                }
-            out.emplace_back(from, n - from);
-            if (out.size() > 1)  // no separator: the input itself, even when empty
-                while (!out.empty() && out.back().second == 0) out.pop_back();
-            return out;
-        };
-        int k = 0;
-        for (const auto& sv : split2(v.p, v.len, ',', ' ')) {
-            const uint8_t* sp = v.p + sv.first;
-            const auto parts = split2(sp, sv.second, ':', ' ');
-            if (parts.empty()) return;  // not reached: the device sent the line to FALLBACK
-            MVal orig = trim(sp + parts[0].first, parts[0].second);
-            MVal redir = parts.size() == 1 ? orig : trim(sp + parts[1].first, parts[1].second);
-            set_origin(O_CONV, oi);
-            emit(c, name, in.d->out_type, std::to_string(k) + ".value", orig);
-            set_origin(O_CONV, oi);
-            emit(c, name, in.d->out_type, std::to_string(k) + ".redirected", redir);
-            ++k;
+        const int j = list_of_tok_.at(t_fmt * 64 + oi);
+        const uint32_t n = R.l_count[j][i];
+        const uint32_t ent = prog_.list[j].secms ? LIST_ENT_MS : LIST_ENT;
+        const uint8_t* tab = n ? c.arena + ref_off(R.l_tab[j][i]) : nullptr;
+        for (uint32_t k = 0; k < n; ++k) {
+            uint32_t sp[2];
+            memcpy(sp, tab + (size_t)k * ent, 8);
+            for (int vr = 0; vr < 2; ++vr) {
+                set_origin(O_LITEM, item_code(j, (int)k, vr));
+                emit(c, name, in.d->out_type, std::to_string(k) + (vr ? ".redirected" : ".value"),
+                     mstr(c.line + (sp[vr] & 0xFFFFu), (sp[vr] >> 16) - (sp[vr] & 0xFFFFu)));
+            }
         }
         return;
     }

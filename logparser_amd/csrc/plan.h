@@ -103,6 +103,9 @@ struct ResultView {
     const int32_t* u_port[MAX_URI] = {};
     const uint32_t* q_count[MAX_QUERY] = {};
     const uint64_t* q_params[MAX_QUERY] = {};
+    const int64_t* sm_ms[MAX_SECMS] = {};
+    const uint32_t* l_count[MAX_LIST] = {};
+    const uint64_t* l_tab[MAX_LIST] = {};
     const uint8_t* fmt_id = nullptr;      // multi-format programs: the routed LogFormat per line
     // the bytes of line i's arena region
     const uint8_t* region(int64_t i) const {
@@ -190,6 +193,7 @@ private:
     std::map<int, int> tok_slot_;          // format * 256 + token index -> slot
     // stage maps keyed by format * 64 + slot (token stages) or stage index
     std::map<int, int> time_of_tok_, fl_of_tok_, uri_of_tok_;
+    std::map<int, int> secms_of_tok_, list_of_tok_;  // SECOND_MILLIS / upstream list stages
     std::map<int, int> uri_of_fl_;
     std::map<int, int> query_of_uri_;
     std::map<int, int> uri_of_qp_;         // query stage * MAX_QNAMES + name index -> derived URI stage

@@ -192,6 +192,21 @@ __device__ TVal tvalue(const Program& P, const Columns& C, const TableArgs& T, c
         }
         return v;
     }
+    case TC_SECMS:  // ConvertSecondsWithMillisStringDissector (+ ConvertMillisecondsIntoMicroseconds)
+        if (!((C.tok_flags[i] >> P.secms[s.a].tok) & 1u)) along(s.b ? (int64_t)((uint64_t)C.sm_ms[s.a][i] * 1000u) : C.sm_ms[s.a][i]);
+        return v;
+    case TC_LIST: case TC_LIST_MS: {  // UpstreamListDissector item b (its table in the line's region)
+        if ((uint32_t)s.b >= C.l_count[s.a][i]) return v;
+        const uint32_t ent = P.list[s.a].secms ? LIST_ENT_MS : LIST_ENT;
+        const LP_G uint8_t* e = region + ref_off(C.l_tab[s.a][i]) + (uint32_t)s.b * ent;
+        if (s.kind == TC_LIST) {
+            span(reinterpret_cast<const LP_G uint32_t*>(e)[s.c & 1]);
+        } else {
+            const int64_t ms = reinterpret_cast<const LP_G int64_t*>(e + 8)[s.c & 1];
+            along((s.c & 2) ? (int64_t)((uint64_t)ms * 1000u) : ms);
+        }
+        return v;
+    }
     case TC_QP: {  // the parameter's last occurrence (ParsedRecord: the last value wins)
         const uint32_t cnt = C.q_count[s.a][i];
         if (cnt == 0) return v;
@@ -211,11 +226,13 @@ __device__ TVal tvalue(const Program& P, const Columns& C, const TableArgs& T, c
     }
 }
 
-__device__ __forceinline__ bool row_view(const Columns& C, const uint8_t* buf, int64_t i, const LP_G uint8_t*& line,
-                                         const LP_G uint8_t*& region) {
+// the row's line and arena region (a program without URI stages writes no
+// region: nothing refers to one)
+__device__ __forceinline__ bool row_view(const Program& P, const Columns& C, const uint8_t* buf, int64_t i,
+                                         const LP_G uint8_t*& line, const LP_G uint8_t*& region) {
     if (C.status[i] != ST_OK) return false;
     line = (const LP_G uint8_t*)buf + C.line_off[i];
-    region = C.arena + C.arena_base[i];
+    region = P.has_phase2() ? C.arena + C.arena_base[i] : C.arena;
     return true;
 }
 
@@ -228,7 +245,7 @@ __global__ __launch_bounds__(TB) void k_table_values(const DeviceArgs* __restric
     if (k >= T.count) return;
     const int64_t i = T.first + k;
     const LP_G uint8_t *line = nullptr, *region = nullptr;
-    const bool ok = row_view(C, buf, i, line, region);
+    const bool ok = row_view(P, C, buf, i, line, region);
     const int fmt = ok && P.n_fmt > 1 ? (int)C.fmt_id[i] : 0;
     for (int c = 0; c < T.n_cols; ++c) {
         const TableCol& col = T.cols[c];
@@ -260,7 +277,7 @@ __global__ __launch_bounds__(TB) void k_table_chars(const DeviceArgs* __restrict
     if (k >= T.count) return;
     const int64_t i = T.first + k;
     const LP_G uint8_t *line = nullptr, *region = nullptr;
-    if (!row_view(C, buf, i, line, region)) return;
+    if (!row_view(P, C, buf, i, line, region)) return;
     const int fmt = P.n_fmt > 1 ? (int)C.fmt_id[i] : 0;
     for (int c = 0; c < T.n_cols; ++c) {
         const TableCol& col = T.cols[c];

@@ -95,6 +95,9 @@ struct Store {
     std::vector<std::vector<int64_t>> t_epoch;
     std::vector<std::vector<uint64_t>> t_local, t_utc, u_scheme, u_host, u_path, u_query, u_frag, q_params;
     std::vector<std::vector<int32_t>> u_port;
+    std::vector<std::vector<int64_t>> sm_ms;
+    std::vector<std::vector<uint32_t>> l_count;
+    std::vector<std::vector<uint64_t>> l_tab;
 };
 
 // The URI kernel's view of one URI source [a, b) of the line at base + off:
@@ -134,7 +137,7 @@ static int run_line(const Program& P, const LN& L, const uint8_t* base, uint32_t
     }
     phase1(P, P.elems, L, o, stk, C, 0, false, P.n_fmt > 1 ? (int)fmt_state : 0);
     write_line(P, o, C, 0);
-    if (o.status != ST_OK || P.n_uri == 0) return 0;
+    if (o.status != ST_OK || !P.has_phase2()) return 0;
     // the URI kernel: its sources from the columns phase 1 wrote
     RegArr<MAX_URI> sp, usep;
     sp.fill(0);
@@ -152,6 +155,9 @@ static int run_line(const Program& P, const LN& L, const uint8_t* base, uint32_t
         else need += uri_need(P, u, L, a, b, ev);
         usep.set(u, ev);
     }
+    // the upstream list stages read the line itself (the URI kernel: from HBM)
+    const Line LH{base, off, L.n};
+    need += list_need(P, o.fmt, LH, C, 0);
     need = (need + 15) & ~15u;
     // the region, then room for spills (a shard of its own: bump counter
     // after the region, as the kernel's shard_top)
@@ -176,6 +182,7 @@ static int run_line(const Program& P, const LN& L, const uint8_t* base, uint32_t
         phase2(P, o.fmt, lu, sp, usep, uo, A, C, 0);
         if (uo.status == ST_OK) query_pieces_serial(P, lu, uo, A);
     }
+    if (uo.status == ST_OK && !list_fill(P, o.fmt, LH, A, C, 0)) uo.status = ST_FALLBACK;
     if (A.used > need) { snprintf(out, cap, "ARENA OVERFLOW %u > %u", A.used, need); return 3; }
     if (A.ovf) { snprintf(out, cap, "ARENA SPILL OVERFLOW"); return 3; }
     // k_derived_lines: the remapped query parameters' URI stages, on the
@@ -217,6 +224,9 @@ static int parse_impl(Emu* e, const char* line, int len, const uint8_t* base, ui
     R.q_count.assign(MAX_QUERY, std::vector<uint32_t>(1));
     R.q_params.assign(MAX_QUERY, std::vector<uint64_t>(1));
     R.arena_base.assign(1, 0);
+    R.sm_ms.assign(MAX_SECMS, std::vector<int64_t>(1));
+    R.l_count.assign(MAX_LIST, std::vector<uint32_t>(1));
+    R.l_tab.assign(MAX_LIST, std::vector<uint64_t>(1));
     Columns C;
     memset(&C, 0, sizeof C);
     C.status = R.status.data();
@@ -231,6 +241,9 @@ static int parse_impl(Emu* e, const char* line, int len, const uint8_t* base, ui
         C.u_frag[u] = R.u_frag[u].data();
     }
     for (int q = 0; q < MAX_QUERY; ++q) { C.q_count[q] = R.q_count[q].data(); C.q_params[q] = R.q_params[q].data(); }
+    for (int k = 0; k < MAX_SECMS; ++k) C.sm_ms[k] = R.sm_ms[k].data();
+    for (int j = 0; j < MAX_LIST; ++j) { C.l_count[j] = R.l_count[j].data(); C.l_tab[j] = R.l_tab[j].data(); }
+    C.arena_base = R.arena_base.data();
     LineOut o;
     uint32_t stk[MAX_STACK];
     int st = 0;
@@ -268,6 +281,8 @@ static int parse_impl(Emu* e, const char* line, int len, const uint8_t* base, ui
         V.u_frag[u] = R.u_frag[u].data();
     }
     for (int q = 0; q < MAX_QUERY; ++q) { V.q_count[q] = R.q_count[q].data(); V.q_params[q] = R.q_params[q].data(); }
+    for (int k = 0; k < MAX_SECMS; ++k) V.sm_ms[k] = R.sm_ms[k].data();
+    for (int j = 0; j < MAX_LIST; ++j) { V.l_count[j] = R.l_count[j].data(); V.l_tab[j] = R.l_tab[j].data(); }
     V.fmt_id = R.fmt_id.empty() ? nullptr : R.fmt_id.data();
     std::string js = e->plan.record_json(V, 0);
     if ((int)js.size() + 1 > cap) return -1;

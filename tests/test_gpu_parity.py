@@ -857,8 +857,9 @@ def test_device_table_gpu(demolog_lines):
 
 def test_device_table_other_configs_gpu():
     """The device table on configs 3 (strftime), 4 (NGINX upstream: its list
-    items and converted times stay host-only) and 5 (three LogFormats, rows of
-    formats without a path empty), and on type-remapped paths"""
+    items and converted times from the URI kernel's item tables and phase 1's
+    millisecond columns) and 5 (three LogFormats, rows of formats without a
+    path empty), and on type-remapped paths"""
     import remap_corpus as rc
     cases = [(wl, lpa.SYNTH_FORMATS[wl], lpa.synth(wl, 5, 0, 20000), ()) for wl in (3, 4, 5)]
     rlines = rc.corpus(3, 3000)
@@ -881,8 +882,6 @@ def test_device_table_other_configs_gpu():
             # name), so two stages deliver there and the host table keeps their order
             assert all(h in ("HTTP.URI:" + rc.REMAPS[0][0], "SOMETAG:request.firstline.uri.query.tag") or
                        ".url.query.next." in h for h in host_only), host_only
-        elif wl in (4, 5):  # NGINX upstream list items, SECOND_MILLIS conversions, the binary IP: replay only
-            assert all(any(k in h for k in ("upstream", "MILLISECONDS", "MICROSECONDS", "request.time", "IP:"))
-                       for h in host_only), host_only
-        else:
+        else:  # every path of configs 3-5 from device columns (NGINX upstream list items and the
+            # SECOND_MILLIS -> MILLISECONDS -> MICROSECONDS conversions included)
             assert host_only == [], host_only
