@@ -153,6 +153,7 @@ void build_specs(lp_handle* h) {
         if (P.time[t].kind == lp::TK_STRF) add("t_nano", t, 4, &C.t_nano[t]);  // only strftime has fractions
     }
     for (int k = 0; k < P.n_secms; ++k) add("sm_ms", k, 8, &C.sm_ms[k]);
+    for (int k = 0; k < P.n_binip; ++k) add("bip", k, 4, &C.bip[k]);
     for (int f = 0; f < P.n_fl; ++f) {
         add("fl_kind", f, 4, &C.fl_kind[f]);
         add("fl_method", f, 4, &C.fl_method[f]);
@@ -176,6 +177,10 @@ void build_specs(lp_handle* h) {
     for (int j = 0; j < P.n_list; ++j) {
         add("l_count", j, 4, &C.l_count[j]);
         add("l_tab", j, 8, &C.l_tab[j]);
+    }
+    for (int j = 0; j < P.n_pair; ++j) {
+        add("p_count", j, 4, &C.p_count[j]);
+        add("p_tab", j, 8, &C.p_tab[j]);
     }
     add("arena_base", 0, 8, &C.arena_base);
     uri = 0;
@@ -249,6 +254,9 @@ void make_view(lp_handle* h, const lp_result& r, lp::ResultView& V) {
         else if (nm == "sm_ms") V.sm_ms[i] = (const int64_t*)p;
         else if (nm == "l_count") V.l_count[i] = (const uint32_t*)p;
         else if (nm == "l_tab") V.l_tab[i] = (const uint64_t*)p;
+        else if (nm == "bip") V.bip[i] = (const uint32_t*)p;
+        else if (nm == "p_count") V.p_count[i] = (const uint32_t*)p;
+        else if (nm == "p_tab") V.p_tab[i] = (const uint64_t*)p;
         else if (nm == "fmt_id") V.fmt_id = (const uint8_t*)p;
     }
     if (!V.arena) V.arena_base = nullptr;
@@ -312,7 +320,7 @@ int enqueue(lp_handle* h, bool sync_count) {
     const double per = h->arena_per_line > 0 ? h->arena_per_line * 1.25 : 64.0;
     uint64_t acap = std::max<uint64_t>(h->reserve_arena, (uint64_t)(per * (double)cap) + (1u << 20));
     if (h->arena_first && h->retries == 0) acap = h->arena_first;
-    if (!h->plan.device_ok() || (P.n_uri == 0 && P.n_list == 0)) acap = 4096 * LP_ARENA_SHARDS;
+    if (!h->plan.device_ok() || !P.has_phase2()) acap = 4096 * LP_ARENA_SHARDS;
     h->shard_cap = (acap / LP_ARENA_SHARDS + 255) & ~255ull;
     if (!h->arena.ensure(h->shard_cap * LP_ARENA_SHARDS)) return LP_E_NOMEM;
     lp::Columns& C = h->C;
@@ -335,7 +343,7 @@ int enqueue(lp_handle* h, bool sync_count) {
         }
         if (!h->args.ensure(sizeof(lp::DeviceArgs))) return LP_E_NOMEM;
         lp::ParseLaunch pl{h->d_buf, nbytes, cap, (uint64_t)(h->mean_line > 0 ? h->mean_line + 0.5 : 0),
-                           P.n_elems, P.max_stack, h->force_direct, P.n_uri > 0 || P.n_list > 0, false, P.n_uri, P.n_query,
+                           P.n_elems, P.max_stack, h->force_direct, P.has_phase2(), false, P.n_uri, P.n_query,
                            h->ev[4]};
         for (int u = 0; u < P.n_uri; ++u) pl.derived = pl.derived || P.uri[u].src_q >= 0;
         if (!pl.mean_line && cap > 0) pl.mean_line = (nbytes + cap - 1) / (uint64_t)cap;
@@ -955,14 +963,18 @@ static int table_device(lp_handle* h, int64_t first, int64_t count, lp_table_col
         lp_table_col& C = cols[c];
         lp::TableCol& T = ta->cols[c];
         T.kind = C.kind;
-        if (!h->plan.table_src(C.path, T.src, names)) return LP_E_UNSUPPORTED;
+        if (!h->plan.table_src(C.path, T.src, names, T.alt)) return LP_E_UNSUPPORTED;
         if (C.kind == LP_CAST_DOUBLE)  // Double.parseDouble of a string stays on the host table
-            for (const auto& x : T.src) {
+            for (int f = 0; f < 2 * lp::MAX_FMT; ++f) {
+                const lp::TableSrc& x = f < lp::MAX_FMT ? T.src[f] : T.alt[f - lp::MAX_FMT];
                 const bool long_valued = x.kind == lp::TC_NONE || x.kind == lp::TC_NULL ||
                                          (x.kind == lp::TC_URI && x.b == lp::UP_PORT) ||
                                          (x.kind == lp::TC_TIME && x.b != lp::TF_MONTHNAME && x.b != lp::TF_DATE &&
-                                          x.b != lp::TF_TIME);
-                if (!long_valued) return LP_E_UNSUPPORTED;
+                                          x.b != lp::TF_TIME) ||
+                                         x.kind == lp::TC_SECMS || x.kind == lp::TC_LIST_MS;
+                // a SECOND_MILLIS list item: digits '.' digits, parsed on the device (decimal_to_double)
+                const bool decimal = x.kind == lp::TC_LIST && h->plan.program().list[x.a].secms;
+                if (!long_valued && !decimal) return LP_E_UNSUPPORTED;
             }
         T.valid = C.valid;
         T.i64 = C.i64;

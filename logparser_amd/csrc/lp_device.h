@@ -1842,6 +1842,8 @@ struct LineOut {
     uint32_t hist;  // run-histogram word of an OK line (hist_word)
     uint32_t smdone;  // SECOND_MILLIS stage s delivered (bit s)
     RegArr<MAX_SECMS> sm_lo, sm_hi;
+    uint32_t bipdone;  // BinaryIP stage b delivered (bit b)
+    RegArr<MAX_BINIP> bip;
 };
 
 // A line's URI stages (the URI kernel): per query stage the piece table
@@ -2220,6 +2222,7 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
     o.tok_flags = 0;
     o.tdone = 0;
     o.smdone = 0;
+    o.bipdone = 0;
     o.caps.fill(0);
     o.fl_kind.fill(FL_NONE);
     o.fl_method.fill(0);
@@ -2377,6 +2380,17 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
         o.smdone |= 1u << sm;
         o.sm_lo.set_u(sm, (uint32_t)(uint64_t)ms);
         o.sm_hi.set_u(sm, (uint32_t)((uint64_t)ms >> 32));
+    }
+    // BinaryIPDissector: "\xHH" x 4 (the element kind EK_BINIP proved the shape)
+    for (int bs = 0; bs < P.n_binip; ++bs) {
+        if (P.binip[bs].fmt != fmt) continue;
+        const uint32_t sp = o.caps.get(P.binip[bs].tok);
+        const int a = (int)(sp & 0xFFFFu);
+        if ((sp >> 16) - (uint32_t)a != 16u) continue;
+        uint32_t v = 0;
+        for (int k = 0; k < 4; ++k) v |= (hexv(L[a + 4 * k + 2]) * 16u + hexv(L[a + 4 * k + 3])) << (8 * k);
+        o.bipdone |= 1u << bs;
+        o.bip.set_u(bs, v);
     }
     o.hist = hist_word(P, L, o);
     LP_PROF(7);
@@ -3283,6 +3297,8 @@ __host__ __device__ LP_INLINE void write_line(const Program& P, const LineOut& o
     }
     for (int sm = 0; sm < P.n_secms; ++sm)
         if ((o.smdone >> sm) & 1u) C.sm_ms[sm][li] = (int64_t)(((uint64_t)o.sm_hi.get(sm) << 32) | o.sm_lo.get(sm));
+    for (int bs = 0; bs < P.n_binip; ++bs)
+        if ((o.bipdone >> bs) & 1u) C.bip[bs][li] = o.bip.get(bs);
 }
 
 // ---- the upstream list stages of one OK line (phase 2, after its URI
@@ -3328,6 +3344,134 @@ __host__ __device__ LP_INLINE bool list_fill(const Program& P, int fmt, const LN
         });
         C.l_count[j][li] = (uint32_t)n;
         C.l_tab[j][li] = n > 0 ? mkref(off, (uint32_t)n * ent, true) : 0ull;
+    }
+    return true;
+}
+
+// ---- name / value pieces (PairStage): f(ns, ne, vs, ve, eq) for every
+// piece of [a, b) in order (eq: the piece has a '='; [vs, ve) its value).
+//   PK_COOKIE (RequestCookieListDissector.dissect, :79-110): Pattern("; ").split
+//     (trailing empty pieces dropped), an empty piece skipped, name = the part
+//     before the first '=' trimmed, value = the trimmed rest;
+//   PK_QUERY (QueryStringFieldDissector.dissect, :76-108): split("&") (trailing
+//     empty pieces dropped), an empty piece skipped, name = the part before the
+//     first '=' (not trimmed), value = the rest.
+// (Names are lower-cased and values resilientUrlDecode'd by the caller; the
+// phase-1 guard proved them ASCII with every '%' before two hex digits.)
+template <typename LN, typename F>
+__host__ __device__ LP_INLINE int pair_pieces(const LN& L, int a, int b, int kind, F&& f) {
+    const bool ck = kind == PK_COOKIE;
+    auto is_sep = [&](int q, int e) { return ck ? sep_at(L, q, e, ';') : (q < e && L[q] == '&'); };
+    const int sl = ck ? 2 : 1;
+    bool any = false;
+    for (int q = a; q < b && !any; ++q) any = is_sep(q, b);
+    int t = b;
+    if (any) {
+        while (t - a >= sl && is_sep(t - sl, t)) t -= sl;
+        if (t == a) return 0;
+    }
+    int k = 0;
+    for (int s0 = a;;) {
+        int e0 = s0;
+        while (e0 < t && !is_sep(e0, t)) ++e0;
+        if (e0 > s0) {
+            int eq = s0;
+            while (eq < e0 && L[eq] != '=') ++eq;
+            int ns = s0, ne = eq, vs = eq < e0 ? eq + 1 : e0, ve = e0;
+            if (ck) {
+                while (ns < ne && L[ns] <= ' ') ++ns;
+                while (ne > ns && L[ne - 1] <= ' ') --ne;
+                while (vs < ve && L[vs] <= ' ') ++vs;
+                while (ve > vs && L[ve - 1] <= ' ') --ve;
+            }
+            f(ns, ne, vs, ve, eq < e0);
+            ++k;
+        }
+        if (e0 >= t) break;
+        s0 = e0 + sl;
+    }
+    return k;
+}
+template <typename LN>
+__host__ __device__ LP_INLINE bool has_upper(const LN& L, int a, int b) {
+    for (int q = a; q < b; ++q)
+        if (L[q] - 'A' < 26u) return true;
+    return false;
+}
+template <typename LN>
+__host__ __device__ LP_INLINE bool has_escape(const LN& L, int a, int b) {
+    for (int q = a; q < b; ++q)
+        if (L[q] == '%' || L[q] == '+') return true;
+    return false;
+}
+// region bytes of the line's pair stages: the piece tables and the names /
+// values they rewrite (a decoded value is never longer than its source)
+template <typename LN, typename Cols>
+__host__ __device__ LP_INLINE uint32_t pair_need(const Program& P, int fmt, const LN& L, const Cols& C, int64_t li) {
+    uint32_t need = 0;
+    for (int j = 0; j < P.n_pair; ++j) {
+        const PairStage& S = P.pair[j];
+        if (S.fmt != fmt || ((C.tok_flags[li] >> S.tok) & 1u)) continue;
+        const uint32_t sp = C.tok_span[S.tok][li];
+        uint32_t bytes = 0;
+        const int n = pair_pieces(L, (int)(sp & 0xFFFFu), (int)(sp >> 16), S.kind, [&](int ns, int ne, int vs, int ve, bool) {
+            if (has_upper(L, ns, ne)) bytes += (uint32_t)(ne - ns) + 3;
+            if (has_escape(L, vs, ve)) bytes += (uint32_t)(ve - vs) + 3;
+        });
+        if (n > 0) need += 8 + 16 * (uint32_t)n + bytes;
+    }
+    return need;
+}
+template <typename LN, typename Cols>
+__host__ __device__ LP_INLINE bool pair_fill(const Program& P, int fmt, const LN& L, Arena& A, Cols& C, int64_t li) {
+    for (int j = 0; j < P.n_pair; ++j) {
+        const PairStage& S = P.pair[j];
+        if (S.fmt != fmt) continue;
+        if ((C.tok_flags[li] >> S.tok) & 1u) {  // "-": null, nothing is dissected
+            C.p_count[j][li] = 0;
+            C.p_tab[j][li] = 0;
+            continue;
+        }
+        const uint32_t sp = C.tok_span[S.tok][li];
+        const int a = (int)(sp & 0xFFFFu), b = (int)(sp >> 16);
+        const int n = pair_pieces(L, a, b, S.kind, [](int, int, int, int, bool) {});
+        const uint32_t off = (A.used + 7u) & ~7u;
+        if (n > 0) {
+            if (off + 16u * (uint32_t)n > A.cap) return false;
+            A.used = off + 16u * (uint32_t)n;
+        }
+        LP_G uint64_t* const tab = reinterpret_cast<LP_G uint64_t*>(A.p + off);
+        bool ok = true;
+        uint32_t k = 0;  // the piece's entry (an index: the table pointer stays fixed)
+        pair_pieces(L, a, b, S.kind, [&](int ns, int ne, int vs, int ve, bool eq) {
+            const uint32_t e = 2u * k++;
+            if (!ok) return;
+            uint64_t nref = src_ref(L, ns, ne - ns), vref = mkref(0, 0, false);
+            if (has_upper(L, ns, ne)) {
+                if (A.used + (uint32_t)(ne - ns) > A.cap) { ok = false; return; }
+                const uint32_t st = A.used;
+                for (int q = ns; q < ne; ++q) {
+                    const uint32_t c = L[q];
+                    A.put(c - 'A' < 26u ? (c | 32u) : c);
+                }
+                nref = mkref(st, A.used - st, true);
+                A.used = (A.used + 3u) & ~3u;
+            }
+            if (eq) {
+                if (has_escape(L, vs, ve)) {
+                    if (A.used + (uint32_t)(ve - vs) + 3 > A.cap) { ok = false; return; }
+                    vref = url_decode_value(L, vs, ve, A);
+                    A.used = (A.used + 3u) & ~3u;
+                } else {
+                    vref = src_ref(L, vs, ve - vs);
+                }
+            }
+            tab[e] = nref;
+            tab[e + 1] = vref;
+        });
+        if (!ok) return false;
+        C.p_count[j][li] = (uint32_t)n;
+        C.p_tab[j][li] = n > 0 ? mkref(off, 16u * (uint32_t)n, true) : 0ull;
     }
     return true;
 }

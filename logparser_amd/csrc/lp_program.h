@@ -49,6 +49,8 @@ constexpr int MAX_LINE = 8191;   // longer lines -> FALLBACK (13-bit offsets)
 constexpr int MAX_STACK = 16;    // DFS choice points
 constexpr int MAX_SECMS = 4;     // SECOND_MILLIS token conversions (ConvertSecondsWithMillisStringDissector)
 constexpr int MAX_LIST = 4;      // NGINX upstream lists (UpstreamListDissector)
+constexpr int MAX_BINIP = 2;     // NGINX $binary_remote_addr values (BinaryIPDissector)
+constexpr int MAX_PAIR = 4;      // request cookie headers / raw-token query strings
 
 // Element kinds = the token regexes of the Apache table
 // (hp/dissectors/tokenformat/TokenParser.java:35-59).
@@ -205,6 +207,31 @@ struct ListStage {
 };
 constexpr uint32_t LIST_ENT = 8, LIST_ENT_MS = 24;  // entry bytes without / with the milliseconds
 
+// Name / value pieces of a captured token, split by the URI kernel into a
+// table in the line's region, 16 bytes per piece: the name ref (lower-cased
+// copy spilled when it has upper-case letters) and the value ref (decoded
+// copy spilled when it has '%' / '+').
+//   PK_COOKIE: RequestCookieListDissector (dissectors/RequestCookieListDissector.java:79-110)
+//   PK_QUERY:  QueryStringFieldDissector on a raw token (%q, $args;
+//              dissectors/QueryStringFieldDissector.java:76-108)
+enum : int32_t { PK_COOKIE = 0, PK_QUERY = 1 };
+struct PairStage {
+    int32_t tok;
+    int32_t fmt;
+    int32_t kind;
+    int32_t pad;
+};
+
+// NginxHttpdLogFormatDissector.BinaryIPDissector on a captured
+// $binary_remote_addr token (hp/NginxHttpdLogFormatDissector.java:151-178):
+// "\xHH" x 4 -> the four bytes; phase 1 writes them as one u32 (byte k of
+// the address in bits 8k..8k+7), delivered as the bytes read as Java
+// (signed) bytes joined by '.'.
+struct BinipStage {
+    int32_t tok;
+    int32_t fmt;
+};
+
 // Stages (time / first line / URI) belong to one LogFormat: a line runs the
 // stages of the format it was routed to.  Token slot k of a line is the k-th
 // captured token of that line's format.
@@ -234,9 +261,11 @@ struct Program {
     // dissects (every "expires" must then parse)
     int32_t guard_setc[MAX_FMT];
     int32_t guard_setc_exp[MAX_FMT];
-    int32_t n_secms, n_list;
+    int32_t n_secms, n_list, n_binip, n_pair;
     SecmsStage secms[MAX_SECMS];
     ListStage list[MAX_LIST];
+    BinipStage binip[MAX_BINIP];
+    PairStage pair[MAX_PAIR];
     Elem elems[MAX_ELEMS];
     TimeStage time[MAX_TIME];
     FlStage fl[MAX_FL];
@@ -245,7 +274,7 @@ struct Program {
     alignas(4) uint8_t lit[MAX_LIT];
     // phase 2 runs (the URI kernel): URI stages or upstream list stages, whose
     // results live in the line's arena region
-    __host__ __device__ bool has_phase2() const { return n_uri > 0 || n_list > 0; }
+    __host__ __device__ bool has_phase2() const { return n_uri > 0 || n_list > 0 || n_pair > 0; }
     // literal pool byte i, read as a dword (scalar load for a uniform index)
     __host__ __device__ uint32_t lit_byte(int i) const {
         return (reinterpret_cast<const uint32_t*>(lit)[i >> 2] >> (8 * (i & 3))) & 0xFFu;
@@ -348,6 +377,9 @@ struct Columns {
     LP_G int64_t* sm_ms[MAX_SECMS];    // SECOND_MILLIS stage s: the token as milliseconds
     LP_G uint32_t* l_count[MAX_LIST];  // upstream list stage j: items
     LP_G uint64_t* l_tab[MAX_LIST];    // ... region ref of its item table (ListStage)
+    LP_G uint32_t* bip[MAX_BINIP];     // BinaryIP stage b: the address bytes
+    LP_G uint32_t* p_count[MAX_PAIR];  // name / value pieces of pair stage j
+    LP_G uint64_t* p_tab[MAX_PAIR];    // ... region ref of its piece table (PairStage)
     LP_G uint64_t* arena_base;         // [n]
     // sticky multi-format routing (Program::n_fmt > 1)
     LP_G uint16_t* fmt_match;          // [n] bit f: format f matches; bit 8+f: undecided on the device

@@ -26,6 +26,8 @@ enum : int32_t {
     TC_SECMS,      // a = SECOND_MILLIS stage: its milliseconds (b = 1: x 1000, MICROSECONDS)
     TC_LIST,       // a = upstream list stage, b = item, c = 0 value / 1 redirected
     TC_LIST_MS,    // a = SECOND_MILLIS list stage, b = item, c bit 0: redirected, bit 1: MICROSECONDS
+    TC_BINIP,      // a = BinaryIP stage: its bytes as signed decimals joined by '.'
+    TC_PAIR,       // a = pair stage (cookie / raw query), b / c = offset / length of the name in TableArgs::names (the last occurrence)
 };
 enum : int32_t { TF_EPOCH, TF_DAY, TF_MONTHNAME, TF_MONTH, TF_WEEK, TF_WEEKYEAR, TF_YEAR, TF_HOUR, TF_MINUTE,
                  TF_SECOND, TF_MILLI, TF_MICRO, TF_NANO, TF_DATE, TF_TIME };
@@ -42,6 +44,10 @@ struct TableCol {
     int32_t kind;  // LP_CAST_STRING 1 / LONG 2 / DOUBLE 4
     int32_t pad;
     TableSrc src[MAX_FMT];
+    // an earlier delivery of the same path (TC_NONE: none): the row's value
+    // when src delivers none (ParsedRecord: a null is ignored, the last value
+    // wins) -- a token that a converter of another token delivers again
+    TableSrc alt[MAX_FMT];
     LP_G uint8_t* valid;
     LP_G int64_t* i64;   // STRING: offsets [count + 1]; LONG: values
     LP_G double* f64;

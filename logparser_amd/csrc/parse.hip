@@ -309,7 +309,7 @@ __global__ __launch_bounds__(PW, 2) void k_parse_chunks(const uint8_t* __restric
     // phase 1 before the line numbers are known (its row is written after)
     LineOut o;
     o.status = ST_OK;
-    o.tdone = 0;
+    o.tdone = o.smdone = o.bipdone = 0;
     LP_PROF(1);
     if (lds_line) phase1(P, s_elems, L, o, stk, C, 0, S.clean, 0);
     LP_PROF(9);

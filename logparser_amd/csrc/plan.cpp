@@ -1062,16 +1062,23 @@ int Plan::casts_of(const Dissector& d, const std::string& otype, const std::stri
     (void)otype;
 }
 
-bool Plan::table_src(const std::string& path, TableSrc out[MAX_FMT], std::string& names) const {
+bool Plan::table_src(const std::string& path, TableSrc out[MAX_FMT], std::string& names, TableSrc* alt) const {
     const size_t colon = path.find(':');
     if (colon == std::string::npos || !device_ok_) return false;
     const std::string type = path.substr(0, colon), name = path.substr(colon + 1);
     for (int f = 0; f < MAX_FMT; ++f) out[f] = TableSrc{TC_NONE, 0, 0, 0};
+    if (alt)
+        for (int f = 0; f < MAX_FMT; ++f) alt[f] = TableSrc{TC_NONE, 0, 0, 0};
     for (int f = 0; f < prog_.n_fmt; ++f) {
         auto it = tsrc_[f].find(path);
         if (it != tsrc_[f].end()) {
             if (it->second.kind < 0) return false;
             out[f] = it->second;
+            auto at = talt_[f].find(path);
+            if (at != talt_[f].end()) {
+                if (!alt) return false;
+                alt[f] = at->second;
+            }
             continue;
         }
         if (thost_exact_[f].count(path)) return false;
@@ -1086,6 +1093,26 @@ bool Plan::table_src(const std::string& path, TableSrc out[MAX_FMT], std::string
                     best = &kv.first;
                     q = kv.second;
                 }
+        // a cookie / raw query parameter: "<TYPE>:<token path>.<name>" of a pair stage
+        const std::string* pbest = nullptr;
+        int ps = -1;
+        for (const auto& kv : tpair_[f]) {
+            const size_t c2 = kv.first.find(':');
+            const std::string ktype = kv.first.substr(0, c2), kname = kv.first.substr(c2 + 1);
+            if (ktype == type && name.size() > kname.size() + 1 && name.compare(0, kname.size(), kname) == 0 &&
+                name[kname.size()] == '.' && (!pbest || kname.size() > pbest->size() - (c2 + 1))) {
+                pbest = &kv.first;
+                ps = kv.second;
+            }
+        }
+        if (pbest) {
+            if (ps < 0) return false;
+            const std::string pn = name.substr(pbest->size() - pbest->find(':'));
+            if (names.size() + pn.size() > (size_t)TABLE_NAMES) return false;
+            out[f] = TableSrc{TC_PAIR, ps, (int32_t)names.size(), (int32_t)pn.size()};
+            names += pn;
+            continue;
+        }
         for (const auto& h : thost_prefix_[f])
             if ((name == h || (name.size() > h.size() && name.compare(0, h.size(), h) == 0 && name[h.size()] == '.')) &&
                 (!best || h.size() > best->size()))
@@ -1398,12 +1425,25 @@ void Plan::compile_program() {
     // the requested fields of time stage t (TimeStampDissector outputs, the
     // replay's D_TIMESTAMP case)
     std::function<void(const Instance&, const std::string&, int)> treg_time;
-    // device table sources (lp_table.h); a path with two different sources is left to the host
+    // device table sources (lp_table.h).  A path two sources deliver: a token
+    // and a value derived from another token (e.g. NGINX $remote_addr and
+    // $binary_remote_addr, both IP:connection.client.host) -- the root
+    // dissector delivers every token before any derived value, so the
+    // derived one is the later delivery (the value, when it has one) and the
+    // token the earlier (alt); any other pair is left to the host table.
     auto treg = [&](const std::string& path, TableSrc ts) {
         auto& m = tsrc_[cur_fmt];
+        auto& am = talt_[cur_fmt];
         auto it = m.find(path);
-        if (it == m.end()) m[path] = ts;
-        else if (memcmp(&it->second, &ts, sizeof ts) != 0) it->second.kind = -1;
+        if (it == m.end()) { m[path] = ts; return; }
+        if (memcmp(&it->second, &ts, sizeof ts) == 0 || it->second.kind < 0) return;
+        const TableSrc cur = it->second;
+        if (!am.count(path) && (cur.kind == TC_TOKEN) != (ts.kind == TC_TOKEN)) {
+            am[path] = cur.kind == TC_TOKEN ? cur : ts;
+            it->second = cur.kind == TC_TOKEN ? ts : cur;
+        } else {
+            it->second.kind = -1;
+        }
     };
     auto thost = [&](const std::string& name) { thost_prefix_[cur_fmt].insert(name); };
     treg_time = [&](const Instance& in, const std::string& complete, int t) {
@@ -1421,6 +1461,19 @@ void Plan::compile_program() {
                 if (o.compare(o.find(':') + 1, std::string::npos, r) == 0) type = o.substr(0, o.find(':'));
             if (!type.empty()) treg(type + ":" + complete + "." + r, TableSrc{TC_TIME, t, tf, utc ? 1 : 0});
         }
+    };
+    // a pair stage (cookie header / raw query string) on token slot oi of the
+    // current format; its pieces are "<key>.<name>" in the device table
+    auto add_pair = [&](int oi, int kind, const std::string& key) {
+        auto st = pair_of_tok_.find(tk(oi));
+        if (st == pair_of_tok_.end()) {
+            if (P.n_pair == MAX_PAIR) { device_ok_ = false; why_ = "too many cookie / query string tokens"; return false; }
+            P.pair[P.n_pair] = PairStage{oi, cur_fmt, kind, 0};
+            st = pair_of_tok_.emplace(tk(oi), P.n_pair++).first;
+        }
+        auto tp = tpair_[cur_fmt].emplace(key, st->second);  // two stages under one name: the host table decides
+        if (!tp.second && tp.first->second != st->second) tp.first->second = -1;
+        return true;
     };
     std::function<void(int, int, const std::string&, const std::string&, bool)> walk =
         [&](int ok, int oi, const std::string& type, const std::string& complete, bool remapped) {
@@ -1496,13 +1549,15 @@ void Plan::compile_program() {
                         if (kv.first.compare(0, pre.size(), pre) == 0) P.guard_setc_exp[cur_fmt] |= 1 << oi;
                     break;
                 }
-                case D_COOKIES:
-                    // RequestCookieListDissector: split and decoded in the replay;
-                    // the device proves the decode cannot fail (guard_pct)
+                case D_COOKIES: {
+                    // RequestCookieListDissector: split, lower-cased and decoded by
+                    // the URI kernel (a pair stage); the phase-1 guard proves the
+                    // decode cannot fail (guard_pct)
                     if (ok != O_TOKEN) { device_ok_ = false; why_ = "cookies from a derived value"; return; }
                     P.guard_pct[cur_fmt] |= 1 << oi;
-                    thost(complete);
+                    if (!add_pair(oi, PK_COOKIE, "HTTP.COOKIE:" + complete)) return;
                     break;
+                }
                 case D_FIRSTLINE: {
                     if (ok != O_TOKEN) { device_ok_ = false; why_ = "first line from a derived value"; return; }
                     int fidx;
@@ -1569,10 +1624,11 @@ void Plan::compile_program() {
                 case D_QUERY: {
                     if (ok == O_TOKEN) {
                         // a HTTP.QUERYSTRING token (%q, $args, $query_string):
-                        // split / decoded in the replay, the device proves the
-                        // decode cannot fail (guard_pct, as for cookies)
+                        // split, lower-cased and decoded by the URI kernel (a pair
+                        // stage); the phase-1 guard proves the decode cannot fail
+                        // (guard_pct, as for cookies)
                         P.guard_pct[cur_fmt] |= 1 << oi;
-                        thost(complete);
+                        if (!add_pair(oi, PK_QUERY, "STRING:" + complete)) return;
                         break;
                     }
                     if (ok != O_URI_QUERY) { device_ok_ = false; why_ = "query string from a derived value"; return; }
@@ -1646,7 +1702,21 @@ void Plan::compile_program() {
                     else { device_ok_ = false; why_ = "converter on a derived value"; return; }
                     walk(O_CONV, oi, in.d->out_type, complete, false);
                     break;
-                case D_CLF2NUM: case D_NUM2CLF: case D_BINIP:
+                case D_BINIP:
+                    if (ok == O_TOKEN) {
+                        // BinaryIPDissector: phase 1 converts the token (a BinaryIP stage)
+                        auto st = binip_of_tok_.find(tk(oi));
+                        if (st == binip_of_tok_.end()) {
+                            if (P.n_binip == MAX_BINIP) { device_ok_ = false; why_ = "too many binary IP values"; return; }
+                            P.binip[P.n_binip] = BinipStage{oi, cur_fmt};
+                            st = binip_of_tok_.emplace(tk(oi), P.n_binip++).first;
+                        }
+                        treg(in.d->out_type + ":" + complete, TableSrc{TC_BINIP, st->second, 0, 0});
+                        walk(O_CONV, oi, in.d->out_type, complete, false);
+                        break;
+                    }
+                    [[fallthrough]];
+                case D_CLF2NUM: case D_NUM2CLF:
                     // value-level conversions, done in the replay from the token / list item
                     if (ok != O_TOKEN && ok != O_CONV && ok != O_LITEM) { device_ok_ = false; why_ = "converter on a derived value"; return; }
                     if (ok == O_TOKEN && (in.cls == D_CLF2NUM || in.cls == D_NUM2CLF))
@@ -1866,6 +1936,27 @@ void Plan::emit(Ctx& c, const std::string& base, const std::string& type, const 
     if ((d.exact || d.wild || d.remap_needed) && !recursion) c.em.push_back(Emission{base, type, name, v});
 }
 
+// The pieces of pair stage j for line c.i, in order, delivered under `type`
+// (the requested names only, or all with "*").
+void Plan::emit_pairs(Ctx& c, const Instance& in, const std::string& name, const char* type, int j) const {
+    const ResultView& R = c.R;
+    const uint32_t n = R.p_count[j][c.i];
+    if (!n) return;
+    const bool all = in.requested.count("*") > 0;
+    const uint8_t* tab = c.arena + ref_off(R.p_tab[j][c.i]);
+    auto at = [&](uint64_t r) { return mstr((ref_arena(r) ? c.arena : c.line) + ref_off(r), ref_len(r)); };
+    t_origin_kind = O_NONE;
+    t_origin_idx = 0;
+    for (uint32_t k = 0; k < n; ++k) {
+        uint64_t e[2];
+        memcpy(e, tab + 16 * (size_t)k, 16);
+        const MVal nm = at(e[0]);
+        const std::string pn((const char*)nm.p, nm.len);
+        if (!all && !in.requested.count(pn)) continue;
+        emit(c, name, type, pn, at(e[1]));
+    }
+}
+
 void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const MVal& v) const {
     const ResultView& R = c.R;
     const int64_t i = c.i;
@@ -1984,29 +2075,9 @@ void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const 
         if (ok == O_TOKEN) {
             // QueryStringFieldDissector.dissect (dissectors/QueryStringFieldDissector.java:75-104)
             // on a raw token: split("&") (trailing empty pieces dropped), names
-            // lower-cased (not trimmed), values resilientUrlDecode'd (the
-            // device's guard: ASCII, every '%' followed by two hex digits)
-            const bool all = has("*");
-            std::vector<std::pair<uint32_t, uint32_t>> parts;
-            uint32_t from = 0;
-            for (uint32_t q = 0; q < v.len; ++q)
-                if (v.p[q] == '&') { parts.emplace_back(from, q); from = q + 1; }
-            parts.emplace_back(from, v.len);
-            if (parts.size() > 1)
-                while (!parts.empty() && parts.back().second == parts.back().first) parts.pop_back();
-            set_origin(O_NONE, 0);
-            for (const auto& pr : parts) {
-                const uint8_t* sp = v.p + pr.first;
-                const uint32_t n = pr.second - pr.first;
-                if (n == 0) continue;
-                uint32_t eq = 0;
-                while (eq < n && sp[eq] != '=') ++eq;
-                std::string nm((const char*)sp, eq);
-                for (auto& ch : nm) if (ch >= 'A' && ch <= 'Z') ch = char(ch + 32);
-                if (!all && !has(nm.c_str())) continue;
-                c.pool.emplace_back(eq < n ? latin1_url_decode(sp + eq + 1, n - eq - 1) : std::string());
-                emit(c, name, "STRING", nm, mstr((const uint8_t*)c.pool.back().data(), (uint32_t)c.pool.back().size()));
-            }
+            // lower-cased (not trimmed), values resilientUrlDecode'd -- the URI
+            // kernel's piece table (lp_device.h pair_pieces / pair_fill)
+            emit_pairs(c, in, name, "STRING", pair_of_tok_.at(t_fmt * 64 + oi));
             return;
         }
         int q = query_of_uri_.at(oi);
@@ -2086,43 +2157,10 @@ void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const 
         // RequestCookieListDissector.dissect (dissectors/RequestCookieListDissector.java:79-110):
         // Pattern("; ").split (trailing empty pieces dropped), name = the part
         // before the first '=' trimmed and lower-cased (just a name: value ""),
-        // value = Utils.resilientUrlDecode of the trimmed rest.  The device's
-        // guard proved the header ASCII with every '%' followed by two hex
-        // digits: each %XX is the Latin-1 char U+00XX, '+' a space.
+        // value = Utils.resilientUrlDecode of the trimmed rest -- the URI
+        // kernel's piece table (lp_device.h pair_pieces / pair_fill)
         if (v.null || v.len == 0) return;
-        const bool all = has("*");
-        auto trim = [](const uint8_t* p, uint32_t& a, uint32_t& b) {
-            while (a < b && p[a] <= ' ') ++a;
-            while (b > a && p[b - 1] <= ' ') --b;
-        };
-        std::vector<std::pair<uint32_t, uint32_t>> parts;
-        uint32_t from = 0;
-        for (uint32_t q = 0; q + 1 < v.len; ++q)
-            if (v.p[q] == ';' && v.p[q + 1] == ' ') { parts.emplace_back(from, q); from = q + 2; ++q; }
-        parts.emplace_back(from, v.len);
-        if (parts.size() > 1)
-            while (!parts.empty() && parts.back().second == parts.back().first) parts.pop_back();
-        set_origin(O_NONE, 0);
-        for (const auto& pr : parts) {
-            const uint8_t* s = v.p + pr.first;
-            const uint32_t n = pr.second - pr.first;
-            uint32_t eq = 0;
-            while (eq < n && s[eq] != '=') ++eq;
-            uint32_t na = 0, nb = eq;
-            if (eq == n && n == 0) continue;
-            trim(s, na, nb);
-            std::string nm((const char*)s + na, nb - na);
-            for (auto& ch : nm) if (ch >= 'A' && ch <= 'Z') ch = char(ch + 32);
-            if (!all && !has(nm.c_str())) continue;
-            std::string val;
-            if (eq < n) {
-                uint32_t va = eq + 1, vb = n;
-                trim(s, va, vb);
-                val = latin1_url_decode(s + va, vb - va);
-            }
-            c.pool.emplace_back(std::move(val));
-            emit(c, name, "HTTP.COOKIE", nm, mstr((const uint8_t*)c.pool.back().data(), (uint32_t)c.pool.back().size()));
-        }
+        emit_pairs(c, in, name, "HTTP.COOKIE", pair_of_tok_.at(t_fmt * 64 + oi));
         return;
     }
     case D_SETCOOKIES: {
@@ -2227,18 +2265,13 @@ void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const 
     }
     case D_BINIP: {
         // NginxHttpdLogFormatDissector.BinaryIPDissector (:151-178): "\\xHH" x 4
-        // (the token kind proves the shape) -> the four bytes as Java (signed)
-        // bytes joined by '.'
-        if (v.null || v.len != 16) return;
+        // -> the four bytes as Java (signed) bytes joined by '.'; the bytes
+        // from phase 1 (a BinaryIP stage)
+        if (v.null || v.len != 16 || ok != O_TOKEN) return;
+        const uint32_t x = R.bip[binip_of_tok_.at(t_fmt * 64 + oi)][i];
         char ip[32];
-        int b[4];
-        for (int k = 0; k < 4; ++k) {
-            const uint8_t* h = v.p + 4 * k + 2;
-            auto hv = [](uint8_t ch) { return ch <= '9' ? ch - '0' : (ch | 32) - 'a' + 10; };
-            const int x = hv(h[0]) * 16 + hv(h[1]);
-            b[k] = x >= 128 ? x - 256 : x;
-        }
-        const int n = snprintf(ip, sizeof ip, "%d.%d.%d.%d", b[0], b[1], b[2], b[3]);
+        const int n = snprintf(ip, sizeof ip, "%d.%d.%d.%d", (int)(int8_t)(x & 0xFF), (int)(int8_t)((x >> 8) & 0xFF),
+                               (int)(int8_t)((x >> 16) & 0xFF), (int)(int8_t)(x >> 24));
         set_origin(O_CONV, oi);
         c.pool.emplace_back(ip, (size_t)n);
         emit(c, name, in.d->out_type, "", mstr((const uint8_t*)c.pool.back().data(), (uint32_t)n));

@@ -106,6 +106,9 @@ struct ResultView {
     const int64_t* sm_ms[MAX_SECMS] = {};
     const uint32_t* l_count[MAX_LIST] = {};
     const uint64_t* l_tab[MAX_LIST] = {};
+    const uint32_t* bip[MAX_BINIP] = {};
+    const uint32_t* p_count[MAX_PAIR] = {};
+    const uint64_t* p_tab[MAX_PAIR] = {};
     const uint8_t* fmt_id = nullptr;      // multi-format programs: the routed LogFormat per line
     // the bytes of line i's arena region
     const uint8_t* region(int64_t i) const {
@@ -161,7 +164,9 @@ public:
     // LogFormat; a query parameter's name is appended to `names` (its
     // offset / length in the source).  false: some LogFormat derives the
     // value in the host replay only
-    bool table_src(const std::string& path, TableSrc out[MAX_FMT], std::string& names) const;
+    // alt (optional): per LogFormat the earlier delivery used when out's
+    // delivers no value (TC_NONE: none)
+    bool table_src(const std::string& path, TableSrc out[MAX_FMT], std::string& names, TableSrc* alt = nullptr) const;
 
 private:
     int build_dissectors(const std::string& logformats, std::string& err);
@@ -177,6 +182,7 @@ private:
     void emit(Ctx& c, const std::string& base, const std::string& type, const std::string& name, const MVal& v,
               const MVal* dv = nullptr, bool recursion = false) const;
     void run_phase(Ctx& c, const Instance& in, const std::string& name, const MVal& v) const;
+    void emit_pairs(Ctx& c, const Instance& in, const std::string& name, const char* type, int j) const;
 
     std::vector<std::unique_ptr<Format>> formats_;
     std::vector<std::unique_ptr<Dissector>> dis_;
@@ -193,7 +199,9 @@ private:
     std::map<int, int> tok_slot_;          // format * 256 + token index -> slot
     // stage maps keyed by format * 64 + slot (token stages) or stage index
     std::map<int, int> time_of_tok_, fl_of_tok_, uri_of_tok_;
-    std::map<int, int> secms_of_tok_, list_of_tok_;  // SECOND_MILLIS / upstream list stages
+    std::map<int, int> secms_of_tok_, list_of_tok_, binip_of_tok_;  // SECOND_MILLIS / upstream list / BinaryIP stages
+    std::map<int, int> pair_of_tok_;       // cookie / raw query string stages
+    std::map<std::string, int> tpair_[MAX_FMT];  // device table: "TYPE:<token path>" -> pair stage
     std::map<int, int> uri_of_fl_;
     std::map<int, int> query_of_uri_;
     std::map<int, int> uri_of_qp_;         // query stage * MAX_QNAMES + name index -> derived URI stage
@@ -203,6 +211,7 @@ private:
     // replay derives (exact paths, and names below which it derives values)
     std::map<std::string, TableSrc> tsrc_[MAX_FMT];
     std::map<std::string, int> tqp_[MAX_FMT];
+    std::map<std::string, TableSrc> talt_[MAX_FMT];  // the earlier delivery of a path two sources deliver
     std::set<std::string> thost_exact_[MAX_FMT], thost_prefix_[MAX_FMT];
     // replay source tracking: emission id -> (kind, stage)
     std::map<std::string, std::pair<int, int>> src_;

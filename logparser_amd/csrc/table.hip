@@ -35,7 +35,7 @@ struct TVal {
     uint32_t n = 0;
     bool amp = false;
     int64_t l = 0;
-    char buf[12];
+    char buf[20];  // formatted values (dates, times, month names, binary IPs)
 };
 
 __constant__ char MONTH_TEXT[] = "JanuaryFebruaryMarchAprilMayJuneJulyAugustSeptemberOctoberNovemberDecember";
@@ -80,6 +80,48 @@ __device__ bool parse_long(const LP_G uint8_t* p, uint32_t n, bool amp, int64_t&
     if (!neg && v == 0x8000000000000000ull) return false;
     out = neg ? (int64_t)(0 - v) : (int64_t)v;
     return true;
+}
+
+// Double.parseDouble of "I.F" (digits '.' digits, each at most 18 digits:
+// a SECOND_MILLIS upstream list item, UpstreamModule's element kind):
+// correctly rounded, as Java's parse (IEEE round half to even).  S = I *
+// 10^f + F and the value is S / 10^f: exact by one IEEE division when S <
+// 2^53 and f <= 22 (both operands exact); else the quotient's 54-55
+// leading bits by binary long division in 128-bit integers (S < 2^120),
+// rounded with the remainder as the sticky bit.
+__device__ double decimal_to_double(const LP_G uint8_t* p, uint32_t n) {
+    typedef unsigned __int128 u128;
+    uint64_t I = 0, F = 0;
+    uint32_t q = 0;
+    int f = 0;
+    for (; q < n && p[q] != '.'; ++q) I = I * 10u + (p[q] - '0');
+    for (++q; q < n; ++q, ++f) F = F * 10u + (p[q] - '0');
+    u128 D = 1;
+    for (int k = 0; k < f; ++k) D *= 10u;
+    const u128 S = (u128)I * D + F;
+    if (S == 0) return 0.0;
+    if (S < ((u128)1 << 53) && f <= 22) return (double)(uint64_t)S / (double)(uint64_t)D;
+    auto bitlen = [](u128 x) {
+        const uint64_t hi = (uint64_t)(x >> 64), lo = (uint64_t)x;
+        return hi ? 128 - __builtin_clzll(hi) : lo ? 64 - __builtin_clzll(lo) : 0;
+    };
+    const int k = 54 - (bitlen(S) - bitlen(D));  // S * 2^k / D in [2^53, 2^55)
+    u128 N = S, Dn = D;
+    if (k >= 0) N <<= k;
+    else Dn <<= -k;
+    uint64_t quo = 0;
+    for (int b = 55; b >= 0; --b) {
+        const u128 t = Dn << b;
+        if (N >= t) {
+            N -= t;
+            quo |= 1ull << b;
+        }
+    }
+    const int shift = quo >= (1ull << 54) ? 2 : 1;  // keep 53 significant bits
+    const uint64_t half = 1ull << (shift - 1), r = quo & ((1ull << shift) - 1);
+    uint64_t m = quo >> shift;
+    if (r > half || (r == half && (N != 0 || (m & 1u)))) ++m;
+    return ldexp((double)m, shift - k);
 }
 
 __device__ TVal tvalue(const Program& P, const Columns& C, const TableArgs& T, const TableSrc& s, int64_t i,
@@ -195,6 +237,22 @@ __device__ TVal tvalue(const Program& P, const Columns& C, const TableArgs& T, c
     case TC_SECMS:  // ConvertSecondsWithMillisStringDissector (+ ConvertMillisecondsIntoMicroseconds)
         if (!((C.tok_flags[i] >> P.secms[s.a].tok) & 1u)) along(s.b ? (int64_t)((uint64_t)C.sm_ms[s.a][i] * 1000u) : C.sm_ms[s.a][i]);
         return v;
+    case TC_BINIP: {  // BinaryIPDissector: "%d.%d.%d.%d" of the signed bytes
+        const uint32_t sp = C.tok_span[P.binip[s.a].tok][i];
+        if ((sp >> 16) - (sp & 0xFFFFu) != 16u) return v;
+        const uint32_t x = C.bip[s.a][i];
+        v.kind = 3;
+        v.n = 0;
+        for (int k = 0; k < 4; ++k) {
+            int b = (int)(int8_t)((x >> (8 * k)) & 0xFF);
+            if (k) v.buf[v.n++] = '.';
+            if (b < 0) { v.buf[v.n++] = '-'; b = -b; }
+            if (b >= 100) v.buf[v.n++] = (char)('0' + b / 100);
+            if (b >= 10) v.buf[v.n++] = (char)('0' + (b / 10) % 10);
+            v.buf[v.n++] = (char)('0' + b % 10);
+        }
+        return v;
+    }
     case TC_LIST: case TC_LIST_MS: {  // UpstreamListDissector item b (its table in the line's region)
         if ((uint32_t)s.b >= C.l_count[s.a][i]) return v;
         const uint32_t ent = P.list[s.a].secms ? LIST_ENT_MS : LIST_ENT;
@@ -204,6 +262,19 @@ __device__ TVal tvalue(const Program& P, const Columns& C, const TableArgs& T, c
         } else {
             const int64_t ms = reinterpret_cast<const LP_G int64_t*>(e + 8)[s.c & 1];
             along((s.c & 2) ? (int64_t)((uint64_t)ms * 1000u) : ms);
+        }
+        return v;
+    }
+    case TC_PAIR: {  // the cookie / parameter's last occurrence in the pair stage's piece table
+        const uint32_t cnt = C.p_count[s.a][i];
+        const LP_G uint64_t* t = reinterpret_cast<const LP_G uint64_t*>(region + ref_off(C.p_tab[s.a][i]));
+        for (uint32_t k = 0; k < cnt; ++k) {
+            const uint64_t nref = t[2 * k];
+            if (ref_len(nref) != (uint32_t)s.c) continue;
+            const LP_G uint8_t* np = (ref_arena(nref) ? region : line) + ref_off(nref);
+            bool same = true;
+            for (int q = 0; q < s.c && same; ++q) same = np[q] == T.names[s.b + q];
+            if (same) ref(t[2 * k + 1]);
         }
         return v;
     }
@@ -249,20 +320,35 @@ __global__ __launch_bounds__(TB) void k_table_values(const DeviceArgs* __restric
     const int fmt = ok && P.n_fmt > 1 ? (int)C.fmt_id[i] : 0;
     for (int c = 0; c < T.n_cols; ++c) {
         const TableCol& col = T.cols[c];
-        const TVal v = ok ? tvalue(P, C, T, col.src[fmt], i, line, region) : TVal{};
-        bool valid = v.kind != 0;
-        if (col.kind == 1) {  // STRING: its length now, its bytes after the scan
-            const uint32_t n = v.kind == 2 ? digits(v.l) : v.n + (v.amp ? 1u : 0u);
-            col.i64[k + 1] = valid ? (int64_t)n : 0;
+        bool valid = false;
+        int64_t x = 0;
+        double d = 0.0;
+        // the later delivery, then (a value that is none for the column) the earlier
+        for (int pass = 0; pass < 2 && ok && !valid; ++pass) {
+            const TableSrc& sc = pass ? col.alt[fmt] : col.src[fmt];
+            if (pass && sc.kind == TC_NONE) break;
+            const TVal v = tvalue(P, C, T, sc, i, line, region);
+            valid = v.kind != 0;
+            if (col.kind == 1) {  // STRING: its length now, its bytes after the scan
+                x = v.kind == 2 ? digits(v.l) : v.n + (v.amp ? 1u : 0u);
+            } else if (col.kind == 2) {
+                x = v.l;
+                if (v.kind == 1) valid = parse_long(v.p, v.n, v.amp, x);
+                else if (v.kind == 3) valid = false;  // month names, dates: not numbers
+            } else {
+                // the planner admits long-valued sources and SECOND_MILLIS list items here
+                if (v.kind == 1 && sc.kind == TC_LIST) d = decimal_to_double(v.p, v.n);
+                else if (v.kind == 2) d = (double)v.l;
+                else valid = false;
+            }
+        }
+        if (col.kind == 1) {
+            col.i64[k + 1] = valid ? x : 0;
             if (k == 0) col.i64[0] = 0;
         } else if (col.kind == 2) {
-            int64_t x = v.l;
-            if (v.kind == 1) valid = parse_long(v.p, v.n, v.amp, x);
-            else if (v.kind == 3) valid = false;  // month names, dates: not numbers
             if (valid) col.i64[k] = x;
-        } else {
-            valid = v.kind == 2;  // the planner admits only long-valued sources here
-            if (valid) col.f64[k] = (double)v.l;
+        } else if (valid) {
+            col.f64[k] = d;
         }
         col.valid[k] = valid ? 1 : 0;
     }
@@ -282,7 +368,8 @@ __global__ __launch_bounds__(TB) void k_table_chars(const DeviceArgs* __restrict
     for (int c = 0; c < T.n_cols; ++c) {
         const TableCol& col = T.cols[c];
         if (col.kind != 1 || !col.valid[k]) continue;
-        const TVal v = tvalue(P, C, T, col.src[fmt], i, line, region);
+        TVal v = tvalue(P, C, T, col.src[fmt], i, line, region);
+        if (v.kind == 0) v = tvalue(P, C, T, col.alt[fmt], i, line, region);  // the earlier delivery
         LP_G uint8_t* d = col.chars + col.i64[k];
         if (v.kind == 2) {
             write_long(d, v.l, digits(v.l));

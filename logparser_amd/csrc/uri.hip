@@ -233,14 +233,18 @@ __device__ __forceinline__ void uri_wave(const uint8_t* __restrict__ buf, const 
     // upstream list stages (UpstreamListDissector): their item tables follow
     // the URI stages' in the line's region; the list tokens are read from
     // HBM (they lie outside the gathered URI bytes; a few words each)
+    // (and the name / value pieces of cookie headers and raw query strings)
     int lend = 0;
-    if (U.ok)
+    if (U.ok) {
         for (int j = 0; j < P.n_list; ++j)
             if (P.list[j].fmt == U.fmt) lend = max(lend, (int)(C.tok_span[P.list[j].tok][li] >> 16));
+        for (int j = 0; j < P.n_pair; ++j)
+            if (P.pair[j].fmt == U.fmt) lend = max(lend, (int)(C.tok_span[P.pair[j].tok][li] >> 16));
+    }
     const LP_G uint8_t* lsp = (const LP_G uint8_t*)buf + U.ls;
     const uint32_t lmis = (uint32_t)((uintptr_t)lsp & 3);
     const LineT<const LP_G uint8_t*> LH{lsp - lmis, lmis, lend};
-    if (lend) need += list_need(P, U.fmt, LH, C, li);
+    if (lend) need += list_need(P, U.fmt, LH, C, li) + pair_need(P, U.fmt, LH, C, li);
     need = (need + 15) & ~15u;
     // wave-aggregated arena allocation from the wave's shard
     uint32_t x = need;
@@ -308,7 +312,8 @@ __device__ __forceinline__ void uri_wave(const uint8_t* __restrict__ buf, const 
         }
         LP_PROF(11 + 2 * u);
     }
-    if (live && lend && o.status == ST_OK && !list_fill(P, U.fmt, LH, A, C, li)) o.status = ST_FALLBACK;
+    if (live && lend && o.status == ST_OK && (!list_fill(P, U.fmt, LH, A, C, li) || !pair_fill(P, U.fmt, LH, A, C, li)))
+        o.status = ST_FALLBACK;
     if (live) {
         if (A.ovf) {
             o.status = ST_FALLBACK;

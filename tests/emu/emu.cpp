@@ -98,6 +98,8 @@ struct Store {
     std::vector<std::vector<int64_t>> sm_ms;
     std::vector<std::vector<uint32_t>> l_count;
     std::vector<std::vector<uint64_t>> l_tab;
+    std::vector<std::vector<uint32_t>> bip, p_count;
+    std::vector<std::vector<uint64_t>> p_tab;
 };
 
 // The URI kernel's view of one URI source [a, b) of the line at base + off:
@@ -157,7 +159,7 @@ static int run_line(const Program& P, const LN& L, const uint8_t* base, uint32_t
     }
     // the upstream list stages read the line itself (the URI kernel: from HBM)
     const Line LH{base, off, L.n};
-    need += list_need(P, o.fmt, LH, C, 0);
+    need += list_need(P, o.fmt, LH, C, 0) + pair_need(P, o.fmt, LH, C, 0);
     need = (need + 15) & ~15u;
     // the region, then room for spills (a shard of its own: bump counter
     // after the region, as the kernel's shard_top)
@@ -182,7 +184,7 @@ static int run_line(const Program& P, const LN& L, const uint8_t* base, uint32_t
         phase2(P, o.fmt, lu, sp, usep, uo, A, C, 0);
         if (uo.status == ST_OK) query_pieces_serial(P, lu, uo, A);
     }
-    if (uo.status == ST_OK && !list_fill(P, o.fmt, LH, A, C, 0)) uo.status = ST_FALLBACK;
+    if (uo.status == ST_OK && (!list_fill(P, o.fmt, LH, A, C, 0) || !pair_fill(P, o.fmt, LH, A, C, 0))) uo.status = ST_FALLBACK;
     if (A.used > need) { snprintf(out, cap, "ARENA OVERFLOW %u > %u", A.used, need); return 3; }
     if (A.ovf) { snprintf(out, cap, "ARENA SPILL OVERFLOW"); return 3; }
     // k_derived_lines: the remapped query parameters' URI stages, on the
@@ -227,6 +229,9 @@ static int parse_impl(Emu* e, const char* line, int len, const uint8_t* base, ui
     R.sm_ms.assign(MAX_SECMS, std::vector<int64_t>(1));
     R.l_count.assign(MAX_LIST, std::vector<uint32_t>(1));
     R.l_tab.assign(MAX_LIST, std::vector<uint64_t>(1));
+    R.bip.assign(MAX_BINIP, std::vector<uint32_t>(1));
+    R.p_count.assign(MAX_PAIR, std::vector<uint32_t>(1));
+    R.p_tab.assign(MAX_PAIR, std::vector<uint64_t>(1));
     Columns C;
     memset(&C, 0, sizeof C);
     C.status = R.status.data();
@@ -243,6 +248,8 @@ static int parse_impl(Emu* e, const char* line, int len, const uint8_t* base, ui
     for (int q = 0; q < MAX_QUERY; ++q) { C.q_count[q] = R.q_count[q].data(); C.q_params[q] = R.q_params[q].data(); }
     for (int k = 0; k < MAX_SECMS; ++k) C.sm_ms[k] = R.sm_ms[k].data();
     for (int j = 0; j < MAX_LIST; ++j) { C.l_count[j] = R.l_count[j].data(); C.l_tab[j] = R.l_tab[j].data(); }
+    for (int k = 0; k < MAX_BINIP; ++k) C.bip[k] = R.bip[k].data();
+    for (int j = 0; j < MAX_PAIR; ++j) { C.p_count[j] = R.p_count[j].data(); C.p_tab[j] = R.p_tab[j].data(); }
     C.arena_base = R.arena_base.data();
     LineOut o;
     uint32_t stk[MAX_STACK];
@@ -283,6 +290,8 @@ static int parse_impl(Emu* e, const char* line, int len, const uint8_t* base, ui
     for (int q = 0; q < MAX_QUERY; ++q) { V.q_count[q] = R.q_count[q].data(); V.q_params[q] = R.q_params[q].data(); }
     for (int k = 0; k < MAX_SECMS; ++k) V.sm_ms[k] = R.sm_ms[k].data();
     for (int j = 0; j < MAX_LIST; ++j) { V.l_count[j] = R.l_count[j].data(); V.l_tab[j] = R.l_tab[j].data(); }
+    for (int k = 0; k < MAX_BINIP; ++k) V.bip[k] = R.bip[k].data();
+    for (int j = 0; j < MAX_PAIR; ++j) { V.p_count[j] = R.p_count[j].data(); V.p_tab[j] = R.p_tab[j].data(); }
     V.fmt_id = R.fmt_id.empty() ? nullptr : R.fmt_id.data();
     std::string js = e->plan.record_json(V, 0);
     if ((int)js.size() + 1 > cap) return -1;

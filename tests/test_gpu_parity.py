@@ -861,11 +861,20 @@ def test_device_table_other_configs_gpu():
     millisecond columns) and 5 (three LogFormats, rows of formats without a
     path empty), and on type-remapped paths"""
     import remap_corpus as rc
+    from test_emu_parity import COOKIE_FMT, QS_FMT, UPSTREAM_FMT, cookie_lines, querystring_lines, upstream_lines
     cases = [(wl, lpa.SYNTH_FORMATS[wl], lpa.synth(wl, 5, 0, 20000), ()) for wl in (3, 4, 5)]
+    # request cookies and raw-token query strings (the URI kernel's pair stages), upstream address /
+    # status lists and the binary IP (its list stages, phase 1's BinaryIP stage)
+    extra = {COOKIE_FMT: ["HTTP.COOKIE:request.cookies.session", "HTTP.COOKIE:request.cookies.theme"],
+             QS_FMT: ["STRING:request.querystring.aap", "STRING:request.querystring.res"]}
+    for fmt, lines in ((COOKIE_FMT, cookie_lines(5000, 21)), (QS_FMT, querystring_lines(5000, 22)),
+                       (UPSTREAM_FMT, upstream_lines(5000, 23))):
+        cases.append((6, fmt, b"".join(l + b"\n" for l in lines), ()))
     rlines = rc.corpus(3, 3000)
     cases.append((0, rc.FORMAT, b"".join(l + b"\n" for l in rlines), rc.REMAPS))
     for wl, fmt, data, remaps in cases:
         fields = [f for f in lpa.get_possible_paths(fmt) if not f.endswith("*")] if not remaps else rc.FIELDS
+        fields = fields + extra.get(fmt, [])
         p = lpa.HttpdLoglineParser(fmt, fields)
         for n, t in remaps:
             p.add_type_remapping(n, t)
@@ -882,6 +891,7 @@ def test_device_table_other_configs_gpu():
             # name), so two stages deliver there and the host table keeps their order
             assert all(h in ("HTTP.URI:" + rc.REMAPS[0][0], "SOMETAG:request.firstline.uri.query.tag") or
                        ".url.query.next." in h for h in host_only), host_only
-        else:  # every path of configs 3-5 from device columns (NGINX upstream list items and the
-            # SECOND_MILLIS -> MILLISECONDS -> MICROSECONDS conversions included)
+        else:  # every path of configs 3-5 and of the cookie / query-string / upstream corpora from device
+            # columns (list items, SECOND_MILLIS -> MILLISECONDS -> MICROSECONDS, binary IPs, cookies, raw
+            # query parameters included)
             assert host_only == [], host_only
