@@ -142,6 +142,26 @@ def split_stream(lpa, torch, buf, front, nbytes, workload, lines_per_rank, rank,
     return (start, end - start), first, pos
 
 
+def newline_batches(buf, off, nbytes, batch_bytes, probe=1 << 20):
+    """[(offset, bytes)] pieces of buf[off, off + nbytes) of about batch_bytes
+    each, every cut just after a '\n' (a line boundary whatever the
+    terminators around it); one piece when batch_bytes is 0."""
+    if not batch_bytes or nbytes <= batch_bytes:
+        return [(off, nbytes)]
+    out, a, end = [], off, off + nbytes
+    while end - a > batch_bytes:
+        c = a + batch_bytes
+        w = bytes(buf[c:min(end, c + probe)].cpu().numpy())
+        k = w.find(b"\n")
+        if k < 0:
+            break  # a line longer than the probe: the rest stays one piece
+        out.append((a, c + k + 1 - a))
+        a = c + k + 1
+    if end > a:
+        out.append((a, end - a))
+    return out
+
+
 def pcie_inclusive(torch, parser, buf, batches, max_bytes):
     """Host-resident batches (pinned), the rate a caller handing over host
     buffers sees (never the headline):
@@ -294,20 +314,35 @@ def device_table(lpa, torch, parser, n_lines):
     if not cols:
         return None
     t = r.table_device(cols)  # sizes the STRING columns' bytes
-    cap = max(int(v[0][1].numel()) for p, v in t.items() if dict(cols)[p] is str) + 16
+    caps = {p: int(v[0][1].numel()) + 16 for p, v in t.items() if dict(cols)[p] is str}
     del t
+    # the output buffers allocated (and touched) before the timed call: the
+    # timed region is lp_result_table alone (the three kernels and the scans)
+    bufs = r.table_buffers(cols, chars_cap=caps)
+    for b in bufs:
+        for x in b:
+            if x is not None:
+                x.zero_()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    t = r.table_device(cols, chars_cap=cap)
+    t = r.table_device(cols, buffers=bufs)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    ph = r.table_timing()
     nbytes = sum(int(v[0][1].numel()) if dict(cols)[p] is str else 0 for p, v in t.items())
-    del t
+    # k_table_chars: each STRING byte read once (input / arena) and written once
+    chars_gbs = 2 * nbytes / (ph["chars"] / 1e3) / 1e9 if ph["chars"] > 0 else None
+    del t, bufs
     n_lines = r.n_lines  # the handle's last batch
     return {"table_rows_per_s_device": round(n_lines / dt, 1), "table_seconds_device": round(dt, 4),
+            "table_phase_ms": {k: round(v, 3) for k, v in ph.items()},
+            "table_rows_per_s_kernels": round(n_lines / (sum(ph.values()) / 1e3), 1) if sum(ph.values()) > 0 else None,
+            "table_chars_gbs": round(chars_gbs, 1) if chars_gbs else None,
+            "table_chars_roofline_frac": round(chars_gbs / HBM_PEAK_GBS, 3) if chars_gbs else None,
             "table_columns": [c for c, _ in cols], "table_string_bytes": nbytes,
             "table_sample_device": "lp_result_table on the device view of the timed batch (%d lines, %d columns: "
-                                   "values, Arrow offsets and bytes in HBM)" % (n_lines, len(cols))}
+                                   "values, Arrow offsets and bytes in HBM; output buffers allocated before the "
+                                   "timed call; phases by HIP events)" % (n_lines, len(cols))}
 
 
 def host_delivery(lpa, torch, parser, n_lines, workload, sample=100000):
@@ -407,16 +442,17 @@ def main():
     fields = lpa.get_possible_paths(fmt) if args.fields == "all" else args.fields.split(",")
     log("rank %d/%d: generating %d lines (config %d, seed %d) on %s" % (rank, world, args.lines, wl, SEEDS[wl], device))
     batch_mb = args.batch_mb if args.batch_mb is not None else (1024 if wl == 5 else 0)
-    front = (256 << 20) if (world > 1 and wl != 5) else 0
+    front = (256 << 20) if world > 1 else 0
     buf, nbytes, batches = generate_to_device(lpa, torch, wl, rank * args.lines, args.lines, device,
-                                              batch_bytes=batch_mb << 20, front=front)
+                                              batch_bytes=0 if world > 1 else batch_mb << 20, front=front)
     split = None
-    if world > 1 and wl != 5 and not batch_mb:
-        # one stream, newline-aligned Hadoop splits (config 5 keeps one corpus
-        # per rank: its sticky format state would need the k-state scan of
-        # SURVEY.md 8(e) across the splits)
+    if world > 1:
+        # one stream, newline-aligned Hadoop splits.  Config 5 too: its
+        # LogFormats are mutually exclusive, so the sticky
+        # format state a split starts with changes no line's result
+        # (tests/test_multirank.py checks this against the oracle)
         (soff, sbytes), first, cuts = split_stream(lpa, torch, buf, front, nbytes, wl, args.lines, rank, device)
-        batches = [(soff, sbytes)]
+        batches = newline_batches(buf, soff, sbytes, batch_mb << 20)
         nbytes = sbytes
         split = {"first_line": first, "byte_cuts": cuts}
         log("rank %d split: lines [%d, %d), bytes [%d, %d)" % (rank, first[rank], first[rank + 1], cuts[rank],
@@ -526,7 +562,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": pmc_traffic(args.pmc_json, stats["lines"], lpa.LIB_PATH) if with_pmc else None,
-            "kernel": "k_parse_lines",
+            "kernel": "k_parse_chunks" if len(fmt.split("\n")) == 1 else "k_parse_lines",
             "ms_per_launch": round(avg_pk, 3),
             "algorithmic_bytes_per_launch": int(pk_bytes),
             "bytes_per_line": round(pk_bytes / max(1, stats["lines"]), 1),
@@ -537,7 +573,7 @@ def main():
                 "traffic": pmc_traffic(args.pmc_json, stats["lines"], lpa.LIB_PATH, "k_uri_lines") if with_pmc else None,
             },
             "parse_pass": {
-                "kernels": "k_parse_lines + k_uri_lines (+ their direct paths, counter reduction)",
+                "kernels": "k_parse_chunks / k_parse_lines + k_uri_lines (+ their overflow paths, counter reduction)",
                 "ms": round(avg_parse, 3), "achieved": round(pass_gbs, 1), "frac": round(pass_gbs / HBM_PEAK_GBS, 4),
                 "algorithmic_bytes": int(algo_bytes), "bytes_per_line": round(algo_bytes / max(1, stats["lines"]), 1),
             },

@@ -114,7 +114,7 @@ int64_t lp_possible_paths_remapped(const char *logformats, int max_depth, const 
                                   the lines that did not fit are FALLBACK, lp_counters out[6] */
 #define LP_OPT_ARENA_BYTES 3   /* tests: exact arena capacity of each batch's first run (0 = estimate) */
 #define LP_OPT_CHUNK_LINES 4   /* one-format programs: lines per byte chunk the one-pass parse kernel
-                                  aims for (1..64, 0 = default 60; a chunk's 65th line onwards is
+                                  aims for (1..64, 0 = default 54; a chunk's 65th line onwards is
                                   parsed from HBM by a second kernel) */
 int lp_set_option(lp_handle *h, int option, int64_t value);
 
@@ -176,7 +176,10 @@ int lp_counters(lp_handle *h, uint64_t *out, int n);
  * parse kernel finds the lines itself), [2] parse pass (every kernel after
  * the index), [3] of it the parse kernels (one LogFormat: k_parse_chunks +
  * k_parse_ovf_lines; several: routing match + k_parse_lines + its direct
- * path), [4] of it the URI kernels (+ the counter reduction).  Returns the number of values written. */
+ * path), [4] of it the URI kernels (+ the counter reduction); then the last
+ * complete lp_result_table on a device view: [5] k_table_values, [6] the
+ * STRING columns' offset scans, [7] k_table_chars.  Returns the number of
+ * values written. */
 int lp_last_timing(lp_handle *h, float *out_ms, int n);
 
 /* Run histograms of the last batch, computed on the device (SURVEY.md §5

@@ -33,7 +33,7 @@ LIB_PATH = os.environ.get("LOGPARSER_AMD_LIB") or os.path.join(_HERE, "_lib", "l
 LP_OK, LP_E_INVALID, LP_E_MISSING, LP_E_UNSUPPORTED, LP_E_DEVICE, LP_E_NOMEM, LP_E_STATE = 0, -1, -2, -3, -4, -5, -6
 LINE_OK, LINE_BAD, LINE_FALLBACK = 0, 1, 2
 BUF_HOST, BUF_DEVICE = 0, 1
-OPT_FORCE_DIRECT, OPT_MAX_RETRIES, OPT_ARENA_BYTES = 1, 2, 3
+OPT_FORCE_DIRECT, OPT_MAX_RETRIES, OPT_ARENA_BYTES, OPT_CHUNK_LINES = 1, 2, 3, 4
 ARENA_SHARDS = 64
 
 
@@ -356,17 +356,34 @@ class BatchResult:
                 out[path] = ((i64[:count] if typ is int else f64[:count]).copy(), ok)
         return out
 
-    def table_device(self, columns, first=0, count=None, chars_cap=None):
+    def table_buffers(self, columns, count=None, chars_cap=None):
+        """Device buffers for table_device(columns, buffers=...): per column
+        [valid, i64 (STRING offsets / BIGINT values), f64 (DOUBLE), chars]
+        (None where the kind has none); chars_cap: an int for every STRING
+        column or {path: bytes}."""
+        import torch
+        count = self.n_lines if count is None else count
+        dev = torch.device("cuda", self._p.device)
+        keep = []
+        for path, typ in columns:
+            cap = chars_cap.get(path, 1) if isinstance(chars_cap, dict) else (chars_cap or 1)
+            keep.append([torch.empty(max(1, count), dtype=torch.uint8, device=dev),
+                         torch.empty(count + 1 if typ is str else max(1, count), dtype=torch.int64, device=dev)
+                         if typ is not float else None,
+                         torch.empty(max(1, count), dtype=torch.float64, device=dev) if typ is float else None,
+                         torch.empty(max(1, cap), dtype=torch.uint8, device=dev) if typ is str else None])
+        return keep
+
+    def table_device(self, columns, first=0, count=None, chars_cap=None, buffers=None):
         """lp_result_table on the device view: typed columns of rows [first,
         first+count) built in HBM.  columns: [(path, str | int | float)].
         Returns {path: (values, valid)} of torch tensors on the handle's
         device: valid uint8 [count]; STRING columns the Arrow pair (offsets
         int64 [count + 1], chars uint8), BIGINT int64 / DOUBLE float64 [count].
         chars_cap: bytes allotted per STRING column (default: enough after a
-        first call that reports the need)."""
-        import torch
+        first call that reports the need); buffers: table_buffers(...) to
+        fill instead of fresh ones."""
         count = self.n_lines - first if count is None else count
-        dev = torch.device("cuda", self._p.device)
         kinds = {str: CAST_STRING, int: CAST_LONG, float: CAST_DOUBLE}
         res = LpResult()
         L = lib()
@@ -374,21 +391,22 @@ class BatchResult:
         if rc != LP_OK:
             raise EngineUnavailable("lp_result_view failed: %d" % rc)
         cols = (LpTableCol * len(columns))()
-        keep = []
+        keep = buffers if buffers is not None else self.table_buffers(columns, count, chars_cap)
         for k, (path, typ) in enumerate(columns):
             c = cols[k]
             c.path = path.encode()
             c.kind = kinds[typ]
-            valid = torch.empty(max(1, count), dtype=torch.uint8, device=dev)
-            i64 = torch.empty(count + 1 if typ is str else max(1, count), dtype=torch.int64, device=dev)
-            f64 = torch.empty(max(1, count), dtype=torch.float64, device=dev)
-            chars = torch.empty(max(1, chars_cap or 1), dtype=torch.uint8, device=dev) if typ is str else None
-            c.valid, c.i64, c.f64 = valid.data_ptr(), i64.data_ptr(), f64.data_ptr()
+            valid, i64, f64, chars = keep[k]
+            c.valid = valid.data_ptr()
+            c.i64 = i64.data_ptr() if i64 is not None else 0
+            c.f64 = f64.data_ptr() if f64 is not None else 0
             if chars is not None:
-                c.chars, c.chars_cap = chars.data_ptr(), chars.numel() if chars_cap else 0
-            keep.append([valid, i64, f64, chars])
+                c.chars = chars.data_ptr()
+                c.chars_cap = chars.numel() if (chars_cap or buffers is not None) else 0
         rc = L.lp_result_table(self._p._h, ctypes.byref(res), first, count, cols, len(columns), 0)
         if rc == LP_E_NOMEM:
+            import torch
+            dev = torch.device("cuda", self._p.device)
             for k, (path, typ) in enumerate(columns):
                 if typ is str and cols[k].chars_len > cols[k].chars_cap:
                     keep[k][3] = torch.empty(max(1, cols[k].chars_len), dtype=torch.uint8, device=dev)
@@ -402,10 +420,17 @@ class BatchResult:
         for k, (path, typ) in enumerate(columns):
             valid, i64, f64, chars = keep[k]
             if typ is str:
-                out[path] = ((i64, chars[:cols[k].chars_len]), valid[:count])
+                out[path] = ((i64[:count + 1], chars[:cols[k].chars_len]), valid[:count])
             else:
                 out[path] = ((i64 if typ is int else f64)[:count], valid[:count])
         return out
+
+    def table_timing(self):
+        """HIP-event ms of the last device lp_result_table's phases:
+        {"values": k_table_values, "scans": offset scans, "chars": k_table_chars}"""
+        t = (ctypes.c_float * 8)()
+        lib().lp_last_timing(self._p._h, t, 8)
+        return {"values": t[5], "scans": t[6], "chars": t[7]}
 
     def record_json_from(self, res, i):
         """lp_result_record_json: the record of line i from a host copy."""

@@ -102,6 +102,8 @@ struct lp_handle {
     int64_t first_line = 0;        // global number of the last batch's first line
     int64_t next_line = 0;         // ... of the next batch's (lp_parse_batch continues the numbering)
     hipEvent_t ev[5]{};  // batch start, index done, parse start, batch end, parse kernels done
+    hipEvent_t tev[4]{}; // device table: start, values kernel done, scans done, bytes done
+    float tms[3] = {0, 0, 0};  // the last device table's values / scans / bytes phases
     bool have_events = false;
     uint64_t counters[4]{};
     uint32_t chunk_lines = 0;      // LP_OPT_CHUNK_LINES (0: the kernel's default)
@@ -568,6 +570,7 @@ lp_handle* lp_compile_remapped(const char* logformats, const char* const* paths,
     build_specs(h.get());
     if (hipSetDevice(device) != hipSuccess) { if (status) *status = LP_E_DEVICE; return nullptr; }
     for (auto& ev : h->ev) hipEventCreate(&ev);
+    for (auto& ev : h->tev) hipEventCreate(&ev);
     h->have_events = true;
     if (!h->meta.ensure(sizeof(lp::Meta))) { if (status) *status = LP_E_NOMEM; return nullptr; }
     if (status) *status = st;
@@ -583,6 +586,7 @@ void lp_free(lp_handle* h) {
         b->release();
     if (h->have_events)
         for (auto& ev : h->ev) hipEventDestroy(ev);
+        for (auto& ev : h->tev) hipEventDestroy(ev);
     delete h;
 }
 
@@ -789,7 +793,8 @@ int lp_last_timing(lp_handle* h, float* out, int n) {
     const int st = ensure_synced(h);
     if (st != LP_OK) return st;
     for (int k = 0; k < n && k < 5; ++k) out[k] = h->ms[k];
-    return n < 5 ? n : 5;
+    for (int k = 5; k < n && k < 8; ++k) out[k] = h->tms[k - 5];
+    return n < 8 ? n : 8;
 }
 
 int lp_last_bytes(lp_handle* h, uint64_t* out, int n) {
@@ -990,7 +995,10 @@ static int table_device(lp_handle* h, int64_t first, int64_t count, lp_table_col
     if (hipMemcpyAsync(h->targs.p, ta.get(), sizeof(lp::TableArgs), hipMemcpyHostToDevice, s) != hipSuccess) return LP_E_DEVICE;
     const lp::DeviceArgs* d_args = h->args.as<lp::DeviceArgs>();
     const lp::TableArgs* d_targs = h->targs.as<lp::TableArgs>();
-    if (lp::launch_table_values(d_args, d_targs, *ta, h->d_buf, h->tscratch.p, h->tscratch.cap, s) != 0) return LP_E_DEVICE;
+    hipEventRecord(h->tev[0], s);
+    if (lp::launch_table_values(d_args, d_targs, *ta, h->d_buf, h->tscratch.p, h->tscratch.cap, s, h->tev[1]) != 0)
+        return LP_E_DEVICE;
+    hipEventRecord(h->tev[2], s);
     // the STRING columns' byte counts decide whether their bytes fit
     std::vector<int64_t> tot(n_cols, 0);
     for (int c = 0; c < n_cols; ++c)
@@ -1005,8 +1013,17 @@ static int table_device(lp_handle* h, int64_t first, int64_t count, lp_table_col
         if (cols[c].chars_len > cols[c].chars_cap || (tot[c] && !cols[c].chars)) fits = false;
     }
     if (!fits) return LP_E_NOMEM;
-    if (lp::launch_table_chars(d_args, d_targs, count, h->d_buf, s) != 0) return LP_E_DEVICE;
-    return hipStreamSynchronize(s) == hipSuccess ? LP_OK : LP_E_DEVICE;
+    if (lp::launch_table_chars(d_args, d_targs, *ta, h->d_buf, s) != 0) return LP_E_DEVICE;
+    hipEventRecord(h->tev[3], s);
+    if (hipStreamSynchronize(s) != hipSuccess) return LP_E_DEVICE;
+    float a = 0, b = 0, c = 0;
+    hipEventElapsedTime(&a, h->tev[0], h->tev[1]);
+    hipEventElapsedTime(&b, h->tev[1], h->tev[2]);
+    hipEventElapsedTime(&c, h->tev[2], h->tev[3]);
+    h->tms[0] = a;
+    h->tms[1] = b;
+    h->tms[2] = c;
+    return LP_OK;
 }
 
 int lp_result_table(lp_handle* h, const lp_result* r, int64_t first, int64_t count, lp_table_col* cols, int n_cols,

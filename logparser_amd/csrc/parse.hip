@@ -544,7 +544,7 @@ ChunkPlan chunk_plan(const ParseLaunch& a) {
     const uint64_t fixed = 16 * (uint64_t)a.n_elems + 4 * (uint64_t)c.stk_words + 16 * ((4 * MAXS + 15) / 16);
     const uint64_t per8 = 8 + MC_N;  // LDS bytes per 8 window bytes (window + mask planes)
     const uint64_t mean = a.mean_line ? a.mean_line : 256;
-    const uint64_t lines = a.chunk_lines ? a.chunk_lines : 60;
+    const uint64_t lines = a.chunk_lines ? a.chunk_lines : 54;  // measured best (tools/chunk_sweep.py): 8 waves per CU on config 2
     const uint64_t oh = std::max<uint64_t>(512, ((2 * mean + 63) & ~63ull));
     uint64_t cb = ((lines * mean) + 63) & ~63ull;
     if (cb < 1024) cb = 1024;

@@ -9,7 +9,8 @@
 //                   planner named (lp_table.h), the validity byte, LONG /
 //                   DOUBLE values, and each STRING value's length
 //   (scan)          the lengths -> Arrow offsets (hipCUB inclusive sum)
-//   k_table_chars   one lane per row: the STRING values' bytes at their offsets
+//   k_table_chars   one wave per 64 rows of a STRING column: the column's
+//                   bytes of those rows, written 4-byte word by word
 //
 // What each source delivers mirrors Plan::replay (plan.cpp) case by case.
 #include <hip/hip_runtime.h>
@@ -354,30 +355,133 @@ __global__ __launch_bounds__(TB) void k_table_values(const DeviceArgs* __restric
     }
 }
 
-__global__ __launch_bounds__(TB) void k_table_chars(const DeviceArgs* __restrict__ args,
-                                                    const TableArgs* __restrict__ targs, const uint8_t* buf) {
+// The STRING columns' bytes, destination-major: one wave per 64 rows of one
+// STRING column (grid y = the column's rank among the STRING columns).  The
+// wave's rows fill one contiguous byte range of the column ([off[k0],
+// off[k0 + 64]), Arrow offsets), so the wave walks that range 256 bytes per
+// step, lane l on its 4-byte word: each byte's row by a binary search over
+// the rows' offsets in LDS, its source byte from the input / arena (a value's
+// bytes), the wave's LDS scratch (formatted longs, dates, binary IPs) or the
+// '&' of a raw query string, and one aligned 4-byte store per full word
+// (byte stores only at the range's two ends, whose words the neighbouring
+// waves share).  Consecutive lanes read consecutive source bytes of a row and
+// write consecutive words: the traffic is coalesced both ways.
+constexpr int CW = 4;    // waves per block
+constexpr int FMTB = 24; // scratch bytes per row (a long's 20 characters at most)
+
+__global__ __launch_bounds__(64 * CW) void k_table_chars(const DeviceArgs* __restrict__ args,
+                                                         const TableArgs* __restrict__ targs, const uint8_t* buf) {
     const Program& P = args->prog;
     const Columns& C = args->cols;
     const TableArgs& T = *targs;
-    const int64_t k = (int64_t)blockIdx.x * TB + threadIdx.x;
-    if (k >= T.count) return;
-    const int64_t i = T.first + k;
-    const LP_G uint8_t *line = nullptr, *region = nullptr;
-    if (!row_view(P, C, buf, i, line, region)) return;
-    const int fmt = P.n_fmt > 1 ? (int)C.fmt_id[i] : 0;
-    for (int c = 0; c < T.n_cols; ++c) {
-        const TableCol& col = T.cols[c];
-        if (col.kind != 1 || !col.valid[k]) continue;
-        TVal v = tvalue(P, C, T, col.src[fmt], i, line, region);
-        if (v.kind == 0) v = tvalue(P, C, T, col.alt[fmt], i, line, region);  // the earlier delivery
-        LP_G uint8_t* d = col.chars + col.i64[k];
-        if (v.kind == 2) {
-            write_long(d, v.l, digits(v.l));
-        } else if (v.kind == 3) {
-            for (uint32_t q = 0; q < v.n; ++q) d[q] = (uint8_t)v.buf[q];
-        } else {
-            if (v.amp) *d++ = '&';
-            for (uint32_t q = 0; q < v.n; ++q) d[q] = v.p[q];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    __shared__ uint32_t s_off[CW][65];
+    __shared__ uint32_t s_flag[CW][64];
+    __shared__ uint64_t s_src[CW][64];
+    __shared__ uint8_t s_fmt[CW][64 * FMTB];
+    // the column: the blockIdx.y-th STRING column
+    int c = -1;
+    for (int j = 0, r = 0; j < T.n_cols; ++j)
+        if (T.cols[j].kind == 1 && r++ == (int)blockIdx.y) c = j;
+    const int64_t k0 = ((int64_t)blockIdx.x * CW + wv) * 64;
+    if (c < 0 || k0 >= T.count) return;  // wave-uniform; only wave-level LDS sharing below
+    const TableCol& col = T.cols[c];
+    const int64_t kend = k0 + 64 < T.count ? k0 + 64 : T.count;
+    const int nrows = (int)(kend - k0);
+    const int64_t k = k0 + lane;
+    const uint64_t D0 = (uint64_t)col.i64[k0], D1 = (uint64_t)col.i64[kend];
+    uint32_t flag = 0;  // bit 0: bytes in the scratch; bit 1: a leading '&'
+    uint64_t src = 0;
+    if (k < kend && col.valid[k]) {
+        const LP_G uint8_t *line = nullptr, *region = nullptr;
+        if (row_view(P, C, buf, T.first + k, line, region)) {
+            const int fmt = P.n_fmt > 1 ? (int)C.fmt_id[T.first + k] : 0;
+            TVal v = tvalue(P, C, T, col.src[fmt], T.first + k, line, region);
+            if (v.kind == 0) v = tvalue(P, C, T, col.alt[fmt], T.first + k, line, region);  // the earlier delivery
+            uint8_t* f = &s_fmt[wv][lane * FMTB];
+            if (v.kind == 2) {
+                uint64_t u = v.l < 0 ? 0 - (uint64_t)v.l : (uint64_t)v.l;
+                const uint32_t n = digits(v.l);
+                uint32_t q = n;
+                do {
+                    f[--q] = (uint8_t)('0' + u % 10);
+                    u /= 10;
+                } while (u);
+                if (v.l < 0) f[0] = '-';
+                flag = 1;
+            } else if (v.kind == 3) {
+                for (uint32_t q = 0; q < v.n; ++q) f[q] = (uint8_t)v.buf[q];
+                flag = 1;
+            } else {
+                src = (uint64_t)(uintptr_t)v.p;
+                flag = v.amp ? 2u : 0u;
+            }
+        }
+    }
+    if (lane < nrows) {
+        s_off[wv][lane] = (uint32_t)((uint64_t)col.i64[k] - D0);
+        s_flag[wv][lane] = flag;
+        s_src[wv][lane] = src;
+    }
+    if (lane == 0) s_off[wv][nrows] = (uint32_t)(D1 - D0);
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (D1 == D0) return;
+    const uint32_t total = (uint32_t)(D1 - D0);
+    const uint32_t* off = s_off[wv];
+    // 4-byte words of the destination: offsets congruent to -mis mod 4
+    const uint32_t mis = (uint32_t)((uintptr_t)col.chars & 3u);
+    const uint64_t A0 = D0 - ((D0 + mis) & 3u);
+    LP_G uint8_t* const out = col.chars;
+    // U words per lane per step: every source byte load of the step is in
+    // flight before the first store
+    constexpr int U = 4;
+    for (uint64_t a0 = A0; a0 < D1; a0 += 256 * U) {
+        uint32_t word[U], have[U];
+        uint8_t bv[U][4];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t d = a0 + 256ull * u + 4ull * (uint64_t)lane;
+            have[u] = 0;
+            if (!(d < D1 && d + 4 > D0)) continue;
+            const uint32_t t0 = d < D0 ? (uint32_t)(D0 - d) : 0u;
+            const uint32_t x0 = (uint32_t)(d + t0 - D0);  // the first byte in range, relative
+            int r = 0;
+            for (int st = 32; st; st >>= 1)
+                if (r + st < nrows && off[r + st] <= x0) r += st;
+            uint32_t nxt = off[r + 1], beg = off[r], fl = s_flag[wv][r];
+            uint64_t sp = s_src[wv][r];
+#pragma unroll
+            for (uint32_t t = 0; t < 4; ++t) {
+                const uint32_t x = x0 + t - t0;
+                if (t < t0 || x >= total) continue;
+                while (x >= nxt) {  // the next non-empty row
+                    ++r;
+                    beg = nxt;
+                    nxt = off[r + 1];
+                    fl = s_flag[wv][r];
+                    sp = s_src[wv][r];
+                }
+                const uint32_t o = x - beg;
+                if (fl & 1u) bv[u][t] = s_fmt[wv][r * FMTB + o];
+                else if ((fl & 2u) && o == 0) bv[u][t] = '&';
+                else bv[u][t] = reinterpret_cast<const LP_G uint8_t*>((uintptr_t)sp)[o - (fl >> 1)];
+                have[u] |= 1u << t;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t d = a0 + 256ull * u + 4ull * (uint64_t)lane;
+            word[u] = 0;
+#pragma unroll
+            for (uint32_t t = 0; t < 4; ++t)
+                if ((have[u] >> t) & 1u) word[u] |= (uint32_t)bv[u][t] << (8 * t);
+            if (have[u] == 15u) {
+                *reinterpret_cast<LP_G uint32_t*>(out + d) = word[u];
+            } else if (have[u]) {
+                for (uint32_t t = 0; t < 4; ++t)
+                    if ((have[u] >> t) & 1u) out[d + t] = (uint8_t)(word[u] >> (8 * t));
+            }
         }
     }
 }
@@ -391,7 +495,7 @@ size_t table_scratch_bytes(int64_t count) {
 }
 
 int launch_table_values(const DeviceArgs* d_args, const TableArgs* d_targs, const TableArgs& ta, const uint8_t* buf,
-                        void* scratch, size_t scratch_bytes, hipStream_t s) {
+                        void* scratch, size_t scratch_bytes, hipStream_t s, hipEvent_t mid) {
     if (ta.count > 0x7FFFFFFF) return -1;  // the scan's item count is an int
     const int64_t n = ta.count;
     if (n == 0) {
@@ -400,6 +504,7 @@ int launch_table_values(const DeviceArgs* d_args, const TableArgs* d_targs, cons
         return 0;
     }
     hipLaunchKernelGGL(k_table_values, dim3((unsigned)((n + TB - 1) / TB)), dim3(TB), 0, s, d_args, d_targs, buf);
+    if (mid) hipEventRecord(mid, s);  // the values kernel done: the scans follow
     size_t tmp = 0;
     hipcub::DeviceScan::InclusiveSum(nullptr, tmp, (const int64_t*)nullptr, (int64_t*)nullptr, (int)n);
     const size_t tmp_al = (tmp + 255) & ~(size_t)255;
@@ -415,10 +520,14 @@ int launch_table_values(const DeviceArgs* d_args, const TableArgs* d_targs, cons
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-int launch_table_chars(const DeviceArgs* d_args, const TableArgs* d_targs, int64_t count, const uint8_t* buf,
+int launch_table_chars(const DeviceArgs* d_args, const TableArgs* d_targs, const TableArgs& ta, const uint8_t* buf,
                        hipStream_t s) {
-    if (count == 0) return 0;
-    hipLaunchKernelGGL(k_table_chars, dim3((unsigned)((count + TB - 1) / TB)), dim3(TB), 0, s, d_args, d_targs, buf);
+    int n_str = 0;
+    for (int c = 0; c < ta.n_cols; ++c) n_str += ta.cols[c].kind == 1 ? 1 : 0;
+    if (ta.count == 0 || n_str == 0) return 0;
+    const int64_t waves = (ta.count + 63) / 64;
+    hipLaunchKernelGGL(k_table_chars, dim3((unsigned)((waves + CW - 1) / CW), (unsigned)n_str), dim3(64 * CW), 0, s,
+                       d_args, d_targs, buf);
     return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

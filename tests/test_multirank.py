@@ -184,17 +184,18 @@ def test_two_rank_gloo_stream_split():
     assert first == [0, len(corpora.split_hadoop(stream[:pos[1]])), 3000]
 
 
-def _bench_split_worker(rank, world, port, L, out):
+def _bench_split_worker(rank, world, port, L, out, wl=2, batch_bytes=0):
     """bench.py's split of one synthetic stream (CPU tensors for the HBM buffer)"""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import bench
-    home = lpa.synth(2, bench.SEEDS[2], rank * L, L)
+    home = lpa.synth(wl, bench.SEEDS[wl], rank * L, L)
     front = 1 << 20
     buf = torch.zeros(front + len(home) + (1 << 20), dtype=torch.uint8)
     buf[front:front + len(home)] = torch.frombuffer(bytearray(home), dtype=torch.uint8)
-    (off, nb), first, cuts = bench.split_stream(lpa, torch, buf, front, len(home), 2, L, rank, None)
-    out[rank] = (bytes(buf[off:off + nb].numpy()), first, cuts)
+    (off, nb), first, cuts = bench.split_stream(lpa, torch, buf, front, len(home), wl, L, rank, None)
+    pieces = bench.newline_batches(buf, off, nb, batch_bytes)
+    out[rank] = (bytes(buf[off:off + nb].numpy()), first, cuts, [bytes(buf[a:a + n].numpy()) for a, n in pieces])
     dist.barrier()
     dist.destroy_process_group()
 
@@ -217,3 +218,42 @@ def test_bench_stream_split_gloo():
         assert out[r][0] == stream[a:b], r
         assert out[r][2][r] == a
     assert out[0][1][-1] == world * L
+
+
+@pytest.mark.timeout(600)
+def test_bench_stream_split_config5_gloo(oracle):
+    """bench.py --gpus 2 --workload 5: one config-5 stream in Hadoop splits,
+    each split cut into newline-aligned batches.  The splits and batches tile
+    the stream, and (the LogFormats being mutually exclusive) every line's
+    result from a parser that starts at a split or batch boundary equals the
+    result of one parser over the whole stream (the sticky format state at a
+    boundary changes nothing) -- checked with the oracle."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    import corpora
+    oracle_lib = oracle
+    L, world = 1200, 2
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.spawn(_bench_split_worker, args=(world, _free_port(), L, out, 5, 64 << 10), nprocs=world, join=True)
+    stream = lpa.synth(5, bench.SEEDS[5], 0, world * L)
+    want = line_aligned_ranges(stream, world)
+    for r in range(world):
+        a, b = want[r]
+        assert out[r][0] == stream[a:b], r
+        assert b"".join(out[r][3]) == out[r][0] and len(out[r][3]) > 1, r
+        assert all(p.endswith(b"\n") for p in out[r][3][:-1]), r
+    assert out[0][1][-1] == world * L
+    fmt = lpa.SYNTH_FORMATS[5]
+    fields = [f for f in oracle_lib.possible_paths(fmt) if "firstline" in f or "status" in f or "epoch" in f][:24]
+    whole = oracle_lib.Oracle(fmt, fields)
+    ref = [whole.parse_raw(x) for x in corpora.split_hadoop(stream)]
+    got = []
+    for r in range(world):
+        for piece in out[r][3]:
+            o = oracle_lib.Oracle(fmt, fields)  # a fresh sticky state at every boundary
+            got += [o.parse_raw(x) for x in corpora.split_hadoop(piece)]
+    assert len(got) == len(ref) == world * L
+    assert got == ref
+    assert sum(1 for st, _ in ref if st == oracle_lib.OK) > 0.9 * len(ref)
