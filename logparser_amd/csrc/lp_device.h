@@ -773,6 +773,19 @@ __host__ __device__ LP_INLINE int lit_first(const Program& P, const LN& L, const
     }
 }
 
+// lit_last out of line, for the candidate enumerators of elements that only
+// some programs have (a literal-aware [^\s]* / NGINX "$request"): inlined,
+// its code reshapes the register allocation of every program's kernel
+template <typename LN>
+#if defined(__HIP_DEVICE_COMPILE__)
+__device__ __noinline__
+#else
+inline
+#endif
+int lit_last_call(const Program& P, const LN& L, const ElemV& e, int hi, int lo) {
+    return lit_last(P, L, e, hi, lo);
+}
+
 // End of the digit run starting at p (p if none).
 template <typename LN>
 __host__ __device__ LP_INLINE int digits_end(const LN& L, int p) {
@@ -888,7 +901,16 @@ __host__ __device__ LP_INLINE int uplist_ns_end(const Program& P, const ElemV& e
 template <typename LN>
 __host__ __device__ LP_INLINE int cand_first(const Program& P, const ElemV& e, const LN& L, int p) {
     switch (e.kind) {
-    case EK_NOSPACE: return find_ws(L, p, L.n);
+    case EK_NOSPACE: {
+        // [^\s]* gives its ends longest first (cand_next: one shorter); when a
+        // shorter end can meet the following literal (not det: the literal
+        // starts with a non-space byte, e.g. the '"' of a quoted NGINX
+        // field), the longest end that the literal follows is the first that
+        // can succeed
+        const int q = find_ws(L, p, L.n);
+        if (e.det || e.last || !e.nlit) return q;
+        return lit_last_call(P, L, e, q, p);
+    }
     case EK_NUMBER: { int q = find_fwd(L, p, L.n, [](uint32_t w) { return ~swar::digit(w) & swar::HI; }); return q > p ? q : -1; }
     case EK_CLFNUMBER: {
         int q = find_fwd(L, p, L.n, [](uint32_t w) { return ~swar::digit(w) & swar::HI; });
@@ -937,12 +959,18 @@ __host__ __device__ LP_INLINE int cand_first(const Program& P, const ElemV& e, c
         return d - p > 18 ? -2 : d + 4;
     }
     case EK_NOSPACE3: {
-        // only the maximal first and second runs can be followed by ' '
+        // only the maximal first and second runs can be followed by ' '; the
+        // third run's ends come longest first (cand_next: one shorter), and
+        // with a following literal the first that the literal follows is the
+        // first that can succeed (NGINX "$request": the longest end takes the
+        // closing '"' too and fails at the literal '" ')
         const int q1 = find_ws(L, p, L.n);
         if (q1 >= L.n || L[q1] != ' ') return -1;
         const int q2 = find_ws(L, q1 + 1, L.n);
         if (q2 >= L.n || L[q2] != ' ') return -1;
-        return find_ws(L, q2 + 1, L.n);
+        const int q3 = find_ws(L, q2 + 1, L.n);
+        if (e.last || !e.nlit) return q3;
+        return lit_last_call(P, L, e, q3, q2 + 1);
     }
     case EK_UPLIST_DEC: return uplist_at(L, p, true);
     case EK_UPLIST_NUM: return uplist_at(L, p, false);

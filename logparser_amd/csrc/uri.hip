@@ -215,10 +215,9 @@ __device__ __forceinline__ void uri_walk_coop(const Program& P, int u, const CL&
 // Phase 2, the arena allocation and the query pieces of one wave; lu(u) is
 // the lane's line view of URI stage u (valid for every lane, empty stages
 // included: the query pass reads other lanes' views).
-template <int NU, int NQ, bool COOP, typename LU>
-__device__ __forceinline__ void uri_wave(const uint8_t* __restrict__ buf, const Program& P, const Columns& C,
-                                         UriLane<NU>& U, LU&& lu, bool active, int64_t li, int64_t wave,
-                                         WaveCounts& WC) {
+template <int NU, int NQ, bool COOP, typename LU, typename LL>
+__device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, UriLane<NU>& U, LU&& lu, LL&& ll,
+                                         bool active, int64_t li, int64_t wave, WaveCounts& WC) {
     const int lane = threadIdx.x;
     const int nq = P.n_query < NQ ? P.n_query : NQ;
     uint32_t need = 0;
@@ -231,9 +230,9 @@ __device__ __forceinline__ void uri_wave(const uint8_t* __restrict__ buf, const 
             U.usep.set(u, ev);
         }
     // upstream list stages (UpstreamListDissector): their item tables follow
-    // the URI stages' in the line's region; the list tokens are read from
-    // HBM (they lie outside the gathered URI bytes; a few words each)
-    // (and the name / value pieces of cookie headers and raw query strings)
+    // the URI stages' in the line's region (and the name / value pieces of
+    // cookie headers and raw query strings); ll(lend) views the list / pair
+    // token bytes (gathered into LDS beside the URI bytes, or in HBM)
     int lend = 0;
     if (U.ok) {
         for (int j = 0; j < P.n_list; ++j)
@@ -241,9 +240,7 @@ __device__ __forceinline__ void uri_wave(const uint8_t* __restrict__ buf, const 
         for (int j = 0; j < P.n_pair; ++j)
             if (P.pair[j].fmt == U.fmt) lend = max(lend, (int)(C.tok_span[P.pair[j].tok][li] >> 16));
     }
-    const LP_G uint8_t* lsp = (const LP_G uint8_t*)buf + U.ls;
-    const uint32_t lmis = (uint32_t)((uintptr_t)lsp & 3);
-    const LineT<const LP_G uint8_t*> LH{lsp - lmis, lmis, lend};
+    const auto LH = ll(lend);
     if (lend) need += list_need(P, U.fmt, LH, C, li) + pair_need(P, U.fmt, LH, C, li);
     need = (need + 15) & ~15u;
     // wave-aggregated arena allocation from the wave's shard
@@ -474,13 +471,44 @@ __device__ __forceinline__ bool uri_compact(const uint8_t* __restrict__ buf, uin
         hi = max(hi, U.ls + (s >> 16));
     }
     const uint64_t r0 = hi ? lo & ~15ull : 0;
-    const uint32_t nblk = hi ? (uint32_t)((((hi + 15) & ~15ull) - r0) >> 4) : 0u;
-    uint32_t x = nblk;
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d);
-        if (lane >= d) x += y;
+    const uint32_t nb1 = hi ? (uint32_t)((((hi + 15) & ~15ull) - r0) >> 4) : 0u;
+    // the line's list / pair tokens (upstream lists, cookie headers, raw
+    // query strings): a second region of blocks after the URI ones
+    const bool lists = P.n_list > 0 || P.n_pair > 0;  // wave-uniform
+    uint64_t l0 = ~0ull, l1 = 0;
+    if (lists && U.ok) {
+        auto add = [&](int tok) {
+            const uint32_t s = C.tok_span[tok][li];
+            if ((s >> 16) > (s & 0xFFFFu)) {
+                l0 = min(l0, U.ls + (s & 0xFFFFu));
+                l1 = max(l1, U.ls + (s >> 16));
+            }
+        };
+        for (int j = 0; j < P.n_list; ++j)
+            if (P.list[j].fmt == U.fmt) add(P.list[j].tok);
+        for (int j = 0; j < P.n_pair; ++j)
+            if (P.pair[j].fmt == U.fmt) add(P.pair[j].tok);
     }
-    const uint32_t tot = __shfl(x, 63), cb = x - nblk;  // blocks of the wave, this line's first block
+    const uint64_t q0 = l1 ? l0 & ~15ull : 0;
+    const uint32_t nb2 = l1 ? (uint32_t)((((l1 + 15) & ~15ull) - q0) >> 4) : 0u;
+    auto blocks = [&](uint32_t n, uint32_t& first) {  // the wave's block count, this line's first block
+        uint32_t x = n;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d);
+            if (lane >= d) x += y;
+        }
+        first = x - n;
+        return (uint32_t)__shfl(x, 63);
+    };
+    uint32_t cb;
+    uint32_t tot = blocks(nb1 + nb2, cb);
+    // the list / pair tokens in LDS when the wave's bytes fit with them, else
+    // read from HBM (only the URI bytes decide whether the wave fits)
+    bool lin = lists;
+    if (lists && 16 * tot + 16 > CAP) {
+        lin = false;
+        tot = blocks(nb1, cb);
+    }
     if (16 * tot + 16 > CAP) return false;
     WC.gathered = 16 * tot;
     for (int u = 0; u < P.n_uri && u < NU; ++u) {
@@ -500,7 +528,13 @@ __device__ __forceinline__ bool uri_compact(const uint8_t* __restrict__ buf, uin
             int own = 0;
             for (int st = 32; st; st >>= 1)
                 if (__shfl(cb, own + st) <= g) own += st;
-            const uint64_t src = (uint64_t)__shfl((unsigned long long)r0, own) + 16ull * (g - __shfl(cb, own));
+            const uint32_t j = g - (uint32_t)__shfl(cb, own);  // block j of line own's regions
+            uint64_t src = (uint64_t)__shfl((unsigned long long)r0, own) + 16ull * j;
+            if (lin) {  // (every lane in the shuffles: a permute reads no value from an inactive lane)
+                const uint32_t n1 = (uint32_t)__shfl(nb1, own);
+                const uint64_t s1 = (uint64_t)__shfl((unsigned long long)q0, own);
+                if (j >= n1) src = s1 + 16ull * (j - n1);
+            }
             v[k] = u32x4{0, 0, 0, 0};
             if (g < tot) v[k] = load16(buf, nbytes, src);
         }
@@ -527,7 +561,14 @@ __device__ __forceinline__ bool uri_compact(const uint8_t* __restrict__ buf, uin
         // line byte q lives at cbuf + cs + (q - a): origin cs - a (mod 2^32)
         return CL{(lds_bytes)cbuf, U.cs.get(u) - (s & 0xFFFFu), (int)(s >> 16), (lds_u64)plane};
     };
-    uri_wave<NU, NQ, true>(buf, P, C, U, lu, active, li, wave, WC);
+    // line byte q of a list / pair token at cbuf + 16 (cb + nb1) + (q - (q0 - ls))
+    // (flat addressing: one view type for the LDS copy and the input)
+    const uint8_t* lsp = buf + U.ls;
+    const uint32_t lmis = (uint32_t)((uintptr_t)lsp & 3);
+    const uint8_t* lbase = lin ? reinterpret_cast<const uint8_t*>(cbuf) : lsp - lmis;
+    const uint32_t lorig = lin ? 16 * (cb + nb1) + (uint32_t)(U.ls - q0) : lmis;
+    auto ll = [&](int lend) { return LineT<const uint8_t*>{lbase, lorig, lend}; };
+    uri_wave<NU, NQ, true>(P, C, U, lu, ll, active, li, wave, WC);
     return true;
 }
 
@@ -572,7 +613,10 @@ __global__ __launch_bounds__(PW) void k_uri_overflow(const uint8_t* __restrict__
             const uint32_t mis = (uint32_t)((uintptr_t)ls & 3);
             const LineT<const LP_G uint8_t*> L{ls - mis, mis, crlf_len_hbm(buf, W)};
             auto lu = [&](int) { return L; };
-            uri_wave<NU, NQ, false>(buf, P, C, U, lu, W.active, W.li, wave, WC);
+            auto ll = [&](int lend) {
+                return LineT<const uint8_t*>{reinterpret_cast<const uint8_t*>(ls - mis), mis, lend};
+            };
+            uri_wave<NU, NQ, false>(P, C, U, lu, ll, W.active, W.li, wave, WC);
         }
         __syncthreads();
         WC.store(C, wave);
