@@ -191,13 +191,13 @@ struct WaveCounts {
 
 // Phase 1 of one wave's lines (match, tokens, time, first line) and their
 // rows; adds the lines' counts to WC.  The URI stages run in k_uri_lines.
-template <typename LN>
+template <bool MULTI, typename LN>
 __device__ __forceinline__ void parse_wave(const Program& P, const Elem* elems, const Columns& C, const LN& L,
                                            bool active, int64_t li, WaveStack stk, bool clean, WaveCounts& WC) {
     LineOut o;
     o.status = ST_OK;
     LP_PROF(1);
-    if (active) phase1(P, elems, L, o, stk, C, li, clean, P.n_fmt > 1 ? (int)C.fmt_id[li] : 0);
+    if (active) phase1<MULTI>(P, elems, L, o, stk, C, li, clean, P.n_fmt > 1 ? (int)C.fmt_id[li] : 0);
     LP_PROF(9);
     if (active) write_line(P, o, C, li);
     if (active && !P.has_phase2()) C.arena_base[li] = 0;  // no URI kernel: an empty region for every line

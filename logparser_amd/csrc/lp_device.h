@@ -1251,6 +1251,29 @@ __host__ __device__ LP_INLINE bool match_first_leaf(const Program& P, const LN& 
     return ok && pos == L.n;
 }
 
+// The same first leaf for a lane of a several-format program: the lane's
+// own format's elements (LDS in the kernel, a lane-dependent index), caps
+// set by a select chain.  false also when an element needs the DFS's
+// resolution (-2): match_line decides.
+template <typename LN, typename EL, typename Caps>
+__host__ __device__ LP_INLINE bool match_first_leaf_lane(const Program& P, const EL& elems, int ne, const LN& L,
+                                                         Caps& caps) {
+    int pos = 0;
+    for (int i = 0; i < ne; ++i) {
+        const ElemV e = load_elem(elems + i);
+        if (e.kind == EK_LIT) {
+            if (!lit_at(P, L, pos, e)) return false;
+            pos += e.lit_len;
+        } else {
+            const int c = cand_first(P, e, L, pos);
+            if (c < 0) return false;
+            if (e.cap >= 0) caps.set(e.cap, mkspan(pos, c));
+            pos = c;
+        }
+    }
+    return pos == L.n;
+}
+
 struct NoCaps {
     __host__ __device__ LP_INLINE void set(int, uint32_t) {}
 };
@@ -1360,6 +1383,12 @@ __host__ __device__ LP_INLINE uint32_t fmt_match_word(const Program& P, const EL
     for (int f = 0; f < P.n_fmt; ++f) {
         const int e0 = P.fmt_elem0[f], ne = P.fmt_elem0[f + 1] - e0;
         if (quotes < P.fmt_quotes[f] || !fmt_tail_ok(P, elems + e0, ne, L)) continue;
+        // the DFS's first leaf decides most lines of the format (exact: its
+        // first complete match); the backtracking DFS the rest
+        if (match_first_leaf_lane(P, elems + e0, ne, L, nc)) {
+            m |= 1u << f;
+            continue;
+        }
         const int st = match_line(P, elems + e0, ne, L, nc, stk);
         m |= st == ST_OK ? (1u << f) : st == ST_FALLBACK ? (256u << f) : 0u;
     }
@@ -2242,7 +2271,11 @@ __host__ __device__ LP_INLINE uint32_t hist_word(const Program& P, const LN& L, 
 // Phase 1: guard, match, tokens, time, first line (the parse kernel).
 // clean: the caller already proved every byte of the line passes the
 // fast-path guard (the kernel checks the whole staged window at once).
-template <typename LN, typename EL, typename Stk, typename Cols>
+// MULTI: a kernel of several-format programs (k_parse_lines): the lanes of
+// a wave hold lines of different LogFormats, so the stages run by slot (the
+// k-th time / first-line stage of each lane's own format together) and the
+// first leaf is walked per lane.
+template <bool MULTI = false, typename LN, typename EL, typename Stk, typename Cols>
 __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, const LN& L, LineOut& o, Stk stk, Cols& C,
                                           int64_t li, bool clean = false, int fmt = 0) {
     o.status = ST_OK;
@@ -2272,7 +2305,14 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
     // Lines the first leaf does not match skip the DFS when the format's
     // quote count or line tail already rules them out (exact; malformed
     // lines would otherwise backtrack while the rest of the wave waits).
-    int st = P.n_fmt == 1 && match_first_leaf(P, L, o.caps) ? ST_OK : ST_BAD;
+    int st = ST_BAD;
+    if constexpr (MULTI) {
+        const int e0 = P.fmt_elem0[fmt], ne = P.fmt_elem0[fmt + 1] - e0;
+        if (match_first_leaf_lane(P, elems + e0, ne, L, o.caps)) st = ST_OK;
+        else o.caps.fill(0);  // the DFS sets its own
+    } else {
+        if (P.n_fmt == 1 && match_first_leaf(P, L, o.caps)) st = ST_OK;
+    }
     if (st != ST_OK) {
         const int e0 = P.fmt_elem0[fmt], ne = P.fmt_elem0[fmt + 1] - e0;
         if (P.n_fmt == 1 && (!fmt_tail_ok(P, elems + e0, ne, L) || count_quotes(L) < P.fmt_quotes[fmt])) st = ST_BAD;
@@ -2328,10 +2368,18 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
         }
     }
     LP_PROF(5);
-    // TimeStampDissector
-    for (int t = 0; t < P.n_time; ++t) {
+    // TimeStampDissector (MULTI: slot s = the s-th stage of the lane's format)
+    for (int s = 0; s < P.n_time; ++s) {
+        int t = s;
+        if constexpr (MULTI) {
+            t = -1;
+            for (int u = 0, c = 0; u < P.n_time; ++u)
+                if (P.time[u].fmt == fmt) { if (c == s) t = u; ++c; }
+            if (t < 0) continue;
+        } else {
+            if (P.time[t].fmt != fmt) continue;
+        }
         const TimeStage& T = P.time[t];
-        if (T.fmt != fmt) continue;
         const int k = T.tok;
         const uint32_t sp = o.caps.get(k);
         const int a = sp & 0xFFFF, b = sp >> 16;
@@ -2349,20 +2397,37 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
             const int st = parse_strf_time(T, L, a, b, ep, lo, ut, ns);
             if (st != ST_OK) { o.status = st; return; }
         }
-        // t is wave-uniform: indexed register writes
         o.tdone |= 1u << t;
-        o.ep_lo.set_u(t, (uint32_t)(uint64_t)ep);
-        o.ep_hi.set_u(t, (uint32_t)((uint64_t)ep >> 32));
-        o.lo_lo.set_u(t, (uint32_t)lo);
-        o.lo_hi.set_u(t, (uint32_t)(lo >> 32));
-        o.ut_lo.set_u(t, (uint32_t)ut);
-        o.ut_hi.set_u(t, (uint32_t)(ut >> 32));
-        o.nano.set_u(t, ns);
+        if constexpr (MULTI) {  // t differs between lanes: select chains
+            o.ep_lo.set(t, (uint32_t)(uint64_t)ep);
+            o.ep_hi.set(t, (uint32_t)((uint64_t)ep >> 32));
+            o.lo_lo.set(t, (uint32_t)lo);
+            o.lo_hi.set(t, (uint32_t)(lo >> 32));
+            o.ut_lo.set(t, (uint32_t)ut);
+            o.ut_hi.set(t, (uint32_t)(ut >> 32));
+            o.nano.set(t, ns);
+        } else {  // t is wave-uniform: indexed register writes
+            o.ep_lo.set_u(t, (uint32_t)(uint64_t)ep);
+            o.ep_hi.set_u(t, (uint32_t)((uint64_t)ep >> 32));
+            o.lo_lo.set_u(t, (uint32_t)lo);
+            o.lo_hi.set_u(t, (uint32_t)(lo >> 32));
+            o.ut_lo.set_u(t, (uint32_t)ut);
+            o.ut_hi.set_u(t, (uint32_t)(ut >> 32));
+            o.nano.set_u(t, ns);
+        }
     }
     LP_PROF(6);
     // HttpFirstLineDissector: ^([a-zA-Z-_]+) (.*) (HTTP/[0-9]+\.[0-9]+)$ else ^([a-zA-Z-_]+) (.*)$
-    for (int f = 0; f < P.n_fl; ++f) {
-        if (P.fl[f].fmt != fmt) continue;
+    for (int s = 0; s < P.n_fl; ++s) {
+        int f = s;
+        if constexpr (MULTI) {
+            f = -1;
+            for (int u = 0, c = 0; u < P.n_fl; ++u)
+                if (P.fl[u].fmt == fmt) { if (c == s) f = u; ++c; }
+            if (f < 0) continue;
+        } else {
+            if (P.fl[f].fmt != fmt) continue;
+        }
         int k = P.fl[f].tok;
         if (o.tok_flags & (1u << k)) continue;                // null
         const uint32_t sp0 = o.caps.get(k);

@@ -375,7 +375,7 @@ __global__ __launch_bounds__(PW) void k_parse_ovf_lines(const uint8_t* __restric
         const LP_G uint8_t* ls = (const LP_G uint8_t*)(buf) + s;
         const uint32_t mis = (uint32_t)((uintptr_t)ls & 3);
         const LineT<const LP_G uint8_t*> L{ls - mis, mis, n};
-        parse_wave(P, s_elems, C, L, active, li, stk, false, WC);
+        parse_wave<false>(P, s_elems, C, L, active, li, stk, false, WC);
     }
     if (!P.has_phase2() && threadIdx.x == 0 && WC.act) {
         atomicAdd(&C.meta->counters[0], (unsigned long long)WC.act);
@@ -421,7 +421,7 @@ __device__ __forceinline__ void parse_group(const uint8_t* __restrict__ buf, uin
         const int n = mine ? crlf_len(W.n, W.n > 0 ? win[W.e - 1 - a] : 0u) : 0;
         const LineT<lds_bytes, lds_u64> L{(lds_bytes)win, mine ? (uint32_t)(W.s - a) : 0u, n,
                                           (lds_u64)reinterpret_cast<uint64_t*>(msk16)};
-        parse_wave(P, s_elems, C, L, mine, W.li, stk, clean, WC);
+        parse_wave<true>(P, s_elems, C, L, mine, W.li, stk, clean, WC);
         if (r + 1 < rounds) __syncthreads();  // this round's LDS reads are done before the next staging
     }
     WC.store(C, wave);
@@ -466,7 +466,7 @@ __global__ __launch_bounds__(PW) void k_parse_overflow(const uint8_t* __restrict
         const LP_G uint8_t* ls = (const LP_G uint8_t*)(buf) + W.s;
         const uint32_t mis = (uint32_t)((uintptr_t)ls & 3);
         const LineT<const LP_G uint8_t*> L{ls - mis, mis, crlf_len_hbm(buf, W)};
-        parse_wave(P, s_elems, C, L, W.active, W.li, stk, false, WC);
+        parse_wave<true>(P, s_elems, C, L, W.active, W.li, stk, false, WC);
         __syncthreads();
         WC.store(C, wave);
     }

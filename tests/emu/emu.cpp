@@ -137,7 +137,8 @@ static int run_line(const Program& P, const LN& L, const uint8_t* base, uint32_t
         fmt_state = fmt_apply(fmt_table(m, P.n_fmt), fmt_state);
         R.fmt_id.assign(1, (uint8_t)fmt_state);
     }
-    phase1(P, P.elems, L, o, stk, C, 0, false, P.n_fmt > 1 ? (int)fmt_state : 0);
+    if (P.n_fmt > 1) phase1<true>(P, P.elems, L, o, stk, C, 0, false, (int)fmt_state);  // as k_parse_lines
+    else phase1<false>(P, P.elems, L, o, stk, C, 0, false, 0);
     write_line(P, o, C, 0);
     if (o.status != ST_OK || !P.has_phase2()) return 0;
     // the URI kernel: its sources from the columns phase 1 wrote
