@@ -351,6 +351,12 @@ int enqueue(lp_handle* h, bool sync_count) {
         if (!pl.mean_line && cap > 0) pl.mean_line = (nbytes + cap - 1) / (uint64_t)cap;
         pl.chunked = chunked;
         pl.chunk_lines = h->chunk_lines;
+        pl.lit_aware = false;
+        for (int i = 0; i < P.n_elems; ++i) {
+            const lp::ElemV e = lp::load_elem(P.elems + i);
+            if (e.nlit && !e.last && ((e.kind == lp::EK_NOSPACE && !e.det) || e.kind == lp::EK_NOSPACE3))
+                pl.lit_aware = true;
+        }
         if (chunked) {
             // look-back words (zeroed), per-chunk counts, the queued line list
             const lp::ChunkPlan cp = lp::chunk_plan(pl);

@@ -44,6 +44,8 @@ struct ParseLaunch {
     void* mid_event = nullptr;  // hipEvent_t recorded between the parse kernels and the URI kernels
     bool chunked = false;       // one-format program: k_parse_chunks builds the line index itself
     uint32_t chunk_lines = 0;   // lines per byte chunk the chunked kernel aims for (0: default)
+    bool lit_aware = true;      // the program has a [^\s]* / "$request" element a shorter end of which can meet
+                                // its literal (the chunked kernel's instance with literal-aware first candidates)
 };
 // The chunked parse kernel's geometry: cb input bytes per chunk (one wave
 // each), an LDS window of win_cap bytes (the chunk, 64 bytes before it, the

@@ -898,7 +898,7 @@ __host__ __device__ LP_INLINE int uplist_ns_end(const Program& P, const ElemV& e
 // First candidate end of element e at position p (exact leftmost-first
 // order), -1 = none, -2 = FALLBACK.  '.' runs to the end of the line: the
 // fast-path guard already rejected every line terminator.
-template <typename LN>
+template <bool LA = true, typename LN>
 __host__ __device__ LP_INLINE int cand_first(const Program& P, const ElemV& e, const LN& L, int p) {
     switch (e.kind) {
     case EK_NOSPACE: {
@@ -908,7 +908,7 @@ __host__ __device__ LP_INLINE int cand_first(const Program& P, const ElemV& e, c
         // field), the longest end that the literal follows is the first that
         // can succeed
         const int q = find_ws(L, p, L.n);
-        if (e.det || e.last || !e.nlit) return q;
+        if (!LA || e.det || e.last || !e.nlit) return q;
         return lit_last_call(P, L, e, q, p);
     }
     case EK_NUMBER: { int q = find_fwd(L, p, L.n, [](uint32_t w) { return ~swar::digit(w) & swar::HI; }); return q > p ? q : -1; }
@@ -969,7 +969,7 @@ __host__ __device__ LP_INLINE int cand_first(const Program& P, const ElemV& e, c
         const int q2 = find_ws(L, q1 + 1, L.n);
         if (q2 >= L.n || L[q2] != ' ') return -1;
         const int q3 = find_ws(L, q2 + 1, L.n);
-        if (e.last || !e.nlit) return q3;
+        if (!LA || e.last || !e.nlit) return q3;
         return lit_last_call(P, L, e, q3, q2 + 1);
     }
     case EK_UPLIST_DEC: return uplist_at(L, p, true);
@@ -1229,7 +1229,7 @@ __host__ __device__ LP_INLINE int match_line(const Program& P, const EL& elems, 
 // a one-format program, elements read from the Program with a uniform
 // index.  true: the line matches along that leaf (then it is the DFS's
 // result: its first complete match); false: decide with match_line.
-template <typename LN, typename Caps>
+template <bool LA = true, typename LN, typename Caps>
 __host__ __device__ LP_INLINE bool match_first_leaf(const Program& P, const LN& L, Caps& caps) {
     int pos = 0;
     bool ok = true;
@@ -1241,7 +1241,7 @@ __host__ __device__ LP_INLINE bool match_first_leaf(const Program& P, const LN& 
             ok = ok && lit_at(P, L, pos, e);
             pos += e.lit_len;
         } else if (ok) {
-            const int c = cand_first(P, e, L, pos);
+            const int c = cand_first<LA>(P, e, L, pos);
             ok = c >= 0;
             if (e.cap >= 0) caps.set_u(e.cap, mkspan(pos, c));  // e.cap is uniform
             pos = ok ? c : pos;
@@ -2271,11 +2271,15 @@ __host__ __device__ LP_INLINE uint32_t hist_word(const Program& P, const LN& L, 
 // Phase 1: guard, match, tokens, time, first line (the parse kernel).
 // clean: the caller already proved every byte of the line passes the
 // fast-path guard (the kernel checks the whole staged window at once).
+// LA: the literal-aware first candidates of [^\s]* / NGINX "$request"
+// (cand_first) in the first leaf; a kernel instance without them serves the
+// programs that have no such element (the code would reshape every
+// program's register allocation).
 // MULTI: a kernel of several-format programs (k_parse_lines): the lanes of
 // a wave hold lines of different LogFormats, so the stages run by slot (the
 // k-th time / first-line stage of each lane's own format together) and the
 // first leaf is walked per lane.
-template <bool MULTI = false, typename LN, typename EL, typename Stk, typename Cols>
+template <bool MULTI = false, bool LA = true, typename LN, typename EL, typename Stk, typename Cols>
 __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, const LN& L, LineOut& o, Stk stk, Cols& C,
                                           int64_t li, bool clean = false, int fmt = 0) {
     o.status = ST_OK;
@@ -2311,7 +2315,7 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
         if (match_first_leaf_lane(P, elems + e0, ne, L, o.caps)) st = ST_OK;
         else o.caps.fill(0);  // the DFS sets its own
     } else {
-        if (P.n_fmt == 1 && match_first_leaf(P, L, o.caps)) st = ST_OK;
+        if (P.n_fmt == 1 && match_first_leaf<LA>(P, L, o.caps)) st = ST_OK;
     }
     if (st != ST_OK) {
         const int e0 = P.fmt_elem0[fmt], ne = P.fmt_elem0[fmt + 1] - e0;

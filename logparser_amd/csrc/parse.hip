@@ -77,13 +77,20 @@ __device__ __forceinline__ ChunkScan stage_chunk(const uint8_t* __restrict__ buf
             *reinterpret_cast<u32x4*>(win + 16 * k) = v;
         }
     }
+    // window-relative 32-bit positions (a window is at most 48 KiB); the
+    // rounds inside [t_lo, t_hi) and the input (all but the first and the
+    // last) skip the boundary masks
+    const uint32_t nrel = nbytes - w0 < 16ull * (uint64_t)(nv4 + 1) ? (uint32_t)(nbytes - w0) : 16u * (uint32_t)(nv4 + 1);
+    const uint32_t tl = (uint32_t)(t_lo - w0), th = (uint32_t)(t_hi - w0);
     uint32_t bad = 0;
     uint32_t run = first;        // starts numbered so far (wave-uniform)
-    uint64_t end_term = ~0ull;   // this lane's first terminator >= t_hi
+    uint32_t end_rel = ~0u;      // this lane's first terminator >= t_hi (relative)
     u32x4 vn = lane < nv4 ? *reinterpret_cast<const u32x4*>(win + 16 * lane) : u32x4{0, 0, 0, 0};
     for (int k0 = 0; k0 < nv4; k0 += PW) {  // wave-uniform rounds: every lane joins the ballots
         const int k = k0 + lane;
-        const uint64_t p = w0 + 16ull * k;
+        const uint32_t q = 16u * (uint32_t)k;
+        const uint32_t r0 = 16u * (uint32_t)k0, r1 = r0 + 16u * PW;
+        const bool inner = r0 >= tl && r1 <= th && r1 <= nrel && k0 + PW <= nv;  // wave-uniform
         uint32_t tm = 0;
         const u32x4 v = vn;
         if (k + PW < nv4) vn = *reinterpret_cast<const u32x4*>(win + 16 * (k + PW));  // the next round's piece
@@ -98,23 +105,31 @@ __device__ __forceinline__ ChunkScan stage_chunk(const uint8_t* __restrict__ buf
                 bcls::classify16c(v[0], v[1], v[2], v[3], g, cr);
                 if (cr) {
                     // "\r\n": the '\n' ends the line; a lone '\r' does (term_bits)
+                    const uint64_t p = w0 + q;
                     uint32_t next_lf = lf >> 1;
                     if ((cr & 0x8000u) && p + 16 < nbytes && buf[p + 16] == '\n') next_lf |= 0x8000u;
                     tm |= cr & ~next_lf;
                 }
             }
-            if (k < nv) bad |= g;
-            if (p + 16 > nbytes) tm &= nbytes > p ? (1u << (uint32_t)(nbytes - p)) - 1u : 0u;
+            if (inner) {
+                bad |= g;
+            } else {
+                if (k < nv) bad |= g;
+                if (q + 16 > nrel) tm &= nrel > q ? (1u << (nrel - q)) - 1u : 0u;
+            }
         }
         // terminators in [t_lo, t_hi): line starts; the first at or after t_hi: the end
-        uint32_t ms = tm, me = 0;
-        if (p < t_lo) ms &= t_lo - p >= 16 ? 0u : ~0u << (uint32_t)(t_lo - p);
-        if (p + 16 > t_hi) {
-            const uint32_t lo = t_hi > p ? (1u << (uint32_t)(t_hi - p)) - 1u : 0u;
-            me = tm & ~lo;
-            ms &= lo;
+        uint32_t ms = tm;
+        if (!inner) {
+            uint32_t me = 0;
+            if (q < tl) ms &= tl - q >= 16 ? 0u : ~0u << (tl - q);
+            if (q + 16 > th) {
+                const uint32_t lo = th > q ? (1u << (th - q)) - 1u : 0u;
+                me = tm & ~lo;
+                ms &= lo;
+            }
+            if (me) end_rel = min(end_rel, q + (uint32_t)__builtin_ctz(me));
         }
-        if (me) end_term = min(end_term, p + (uint64_t)__builtin_ctz(me));
         // rank of this lane's first start in the round: the counts (0..16) of
         // the lanes below it, bit plane by bit plane (ballot + mbcnt; no
         // cross-lane permutes in the loop)
@@ -131,16 +146,13 @@ __device__ __forceinline__ ChunkScan stage_chunk(const uint8_t* __restrict__ buf
         uint32_t r = run + excl;
         run += tot;
         for (uint32_t m = ms; m; m &= m - 1, ++r)
-            if (r < (uint32_t)MAXS) starts[r] = (uint32_t)(p - w0) + (uint32_t)__builtin_ctz(m) + 1u;
+            if (r < (uint32_t)MAXS) starts[r] = q + (uint32_t)__builtin_ctz(m) + 1u;
     }
     ChunkScan S;
     S.count = run;
     // wave minimum of the end terminator
-    for (int d = 32; d > 0; d >>= 1) {
-        const uint64_t o = __shfl_xor(end_term, d);
-        end_term = o < end_term ? o : end_term;
-    }
-    S.end_term = end_term;
+    for (int d = 32; d > 0; d >>= 1) end_rel = min(end_rel, (uint32_t)__shfl_xor((int)end_rel, d));
+    S.end_term = end_rel == ~0u ? ~0ull : w0 + end_rel;
     S.clean = !__any(bad != 0);
     return S;
 }
@@ -251,6 +263,7 @@ __device__ __noinline__ void chunk_excess(const uint8_t* __restrict__ buf, uint6
 // Block 0: the scanner; block c + 1: chunk c of cb bytes, one wave.  LDS:
 // [elements][DFS stack][starts][window (win_cap)][mask planes (win_cap / 4)].
 // direct: every line goes to the direct kernel (LP_OPT_FORCE_DIRECT, tests).
+template <bool LA>
 __global__ __launch_bounds__(PW, 2) void k_parse_chunks(const uint8_t* __restrict__ buf, uint64_t nbytes,
                                                      const DeviceArgs* __restrict__ args, uint32_t cb, uint32_t win_cap,
                                                      uint32_t stk_words, int direct) {
@@ -311,7 +324,7 @@ __global__ __launch_bounds__(PW, 2) void k_parse_chunks(const uint8_t* __restric
     o.status = ST_OK;
     o.tdone = o.smdone = o.bipdone = 0;
     LP_PROF(1);
-    if (lds_line) phase1(P, s_elems, L, o, stk, C, 0, S.clean, 0);
+    if (lds_line) phase1<false, LA>(P, s_elems, L, o, stk, C, 0, S.clean, 0);
     LP_PROF(9);
     const uint64_t base = chunk_base(C.chunk_state, c, S.count);
     LP_PROF(61);
@@ -600,8 +613,14 @@ int launch_parse(const ParseLaunch& a, const DeviceArgs* d_args, const Columns& 
         // one pass: line index + phase 1, then the queued lines from HBM
         const ChunkPlan cp = chunk_plan(a);
         if (cp.n_chunks > 0) {
-            hipLaunchKernelGGL(k_parse_chunks, dim3((unsigned)cp.n_chunks + 1), dim3(PW), cp.lds, s, a.buf, a.nbytes,
-                               d_args, cp.cb, cp.win_cap, cp.stk_words, a.force_direct ? 1 : 0);
+            // the instance per program shape: literal-aware first candidates
+            // only for programs that have such an element
+            if (a.lit_aware)
+                hipLaunchKernelGGL(k_parse_chunks<true>, dim3((unsigned)cp.n_chunks + 1), dim3(PW), cp.lds, s, a.buf,
+                                   a.nbytes, d_args, cp.cb, cp.win_cap, cp.stk_words, a.force_direct ? 1 : 0);
+            else
+                hipLaunchKernelGGL(k_parse_chunks<false>, dim3((unsigned)cp.n_chunks + 1), dim3(PW), cp.lds, s, a.buf,
+                                   a.nbytes, d_args, cp.cb, cp.win_cap, cp.stk_words, a.force_direct ? 1 : 0);
             const size_t lds_ovf = 16 * (size_t)a.n_elems + 4 * (size_t)cp.stk_words;
             hipLaunchKernelGGL(k_parse_ovf_lines, dim3((unsigned)grid), dim3(PW), lds_ovf, s, a.buf, a.nbytes, d_args,
                                cp.stk_words);
