@@ -285,7 +285,22 @@ int enqueue(lp_handle* h, bool sync_count) {
     // several: the routing pass needs the line index first
     const bool chunked = h->plan.device_ok() && P.n_fmt == 1;
     h->chunked = chunked;
-    if (sync_count) {
+    if (sync_count && chunked) {
+        // first batch of a one-format handle: the line length of an 8 MiB
+        // prefix sizes the columns (no pass over the whole input; a short
+        // estimate sets cap_ovf and finish() re-runs with the exact count)
+        const uint64_t pre = std::min<uint64_t>(nbytes, 8ull << 20);
+        if (!h->line_off.ensure(16)) return LP_E_NOMEM;
+        if (lp::launch_count(h->d_buf, pre, d_chunk, d_nlmask, h->line_off.as<uint64_t>(), -1, d_meta, s) != 0)
+            return LP_E_DEVICE;
+        unsigned long long n = 0;
+        if (hipMemcpyAsync(&n, &d_meta->n_lines, sizeof n, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess || hipMemsetAsync(d_meta, 0, sizeof(lp::Meta), s) != hipSuccess)
+            return LP_E_DEVICE;
+        const double mean = n ? (double)pre / (double)n : (double)std::max<uint64_t>(pre, 1);
+        cap = std::max<int64_t>(headroom((int64_t)((double)nbytes / mean * 1.02)), h->reserve_lines);
+        h->mean_line = mean;  // sizes this batch's LDS windows
+    } else if (sync_count) {
         // first batch of a handle: the exact line count sizes the columns
         if (!h->line_off.ensure(16)) return LP_E_NOMEM;
         if (lp::launch_count(h->d_buf, nbytes, d_chunk, d_nlmask, h->line_off.as<uint64_t>(), -1, d_meta, s) != 0)
