@@ -240,8 +240,7 @@ __device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, Uri
         for (int j = 0; j < P.n_pair; ++j)
             if (P.pair[j].fmt == U.fmt) lend = max(lend, (int)(C.tok_span[P.pair[j].tok][li] >> 16));
     }
-    const auto LH = ll(lend);
-    if (lend) need += list_need(P, U.fmt, LH, C, li) + pair_need(P, U.fmt, LH, C, li);
+    if (lend) ll(lend, [&](const auto& LH) { need += list_need(P, U.fmt, LH, C, li) + pair_need(P, U.fmt, LH, C, li); });
     need = (need + 15) & ~15u;
     // wave-aggregated arena allocation from the wave's shard
     uint32_t x = need;
@@ -309,8 +308,11 @@ __device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, Uri
         }
         LP_PROF(11 + 2 * u);
     }
-    if (live && lend && o.status == ST_OK && (!list_fill(P, U.fmt, LH, A, C, li) || !pair_fill(P, U.fmt, LH, A, C, li)))
-        o.status = ST_FALLBACK;
+    if (live && lend && o.status == ST_OK) {
+        bool filled = true;
+        ll(lend, [&](const auto& LH) { filled = list_fill(P, U.fmt, LH, A, C, li) && pair_fill(P, U.fmt, LH, A, C, li); });
+        if (!filled) o.status = ST_FALLBACK;
+    }
     if (live) {
         if (A.ovf) {
             o.status = ST_FALLBACK;
@@ -561,13 +563,16 @@ __device__ __forceinline__ bool uri_compact(const uint8_t* __restrict__ buf, uin
         // line byte q lives at cbuf + cs + (q - a): origin cs - a (mod 2^32)
         return CL{(lds_bytes)cbuf, U.cs.get(u) - (s & 0xFFFFu), (int)(s >> 16), (lds_u64)plane};
     };
-    // line byte q of a list / pair token at cbuf + 16 (cb + nb1) + (q - (q0 - ls))
-    // (flat addressing: one view type for the LDS copy and the input)
-    const uint8_t* lsp = buf + U.ls;
+    // line byte q of a list / pair token at cbuf + 16 (cb + nb1) + (q - (q0 - ls)),
+    // or in place in the input; ll(lend, f) runs f on the view (lin is
+    // wave-uniform: LDS or global loads, never flat ones)
+    const LP_G uint8_t* lsp = (const LP_G uint8_t*)buf + U.ls;
     const uint32_t lmis = (uint32_t)((uintptr_t)lsp & 3);
-    const uint8_t* lbase = lin ? reinterpret_cast<const uint8_t*>(cbuf) : lsp - lmis;
-    const uint32_t lorig = lin ? 16 * (cb + nb1) + (uint32_t)(U.ls - q0) : lmis;
-    auto ll = [&](int lend) { return LineT<const uint8_t*>{lbase, lorig, lend}; };
+    const uint32_t lorig = 16 * (cb + nb1) + (uint32_t)(U.ls - q0);
+    auto ll = [&](int lend, auto&& f) {
+        if (lin) f(LineT<lds_bytes>{(lds_bytes)cbuf, lorig, lend});
+        else f(LineT<const LP_G uint8_t*>{lsp - lmis, lmis, lend});
+    };
     uri_wave<NU, NQ, true>(P, C, U, lu, ll, active, li, wave, WC);
     return true;
 }
@@ -613,9 +618,7 @@ __global__ __launch_bounds__(PW) void k_uri_overflow(const uint8_t* __restrict__
             const uint32_t mis = (uint32_t)((uintptr_t)ls & 3);
             const LineT<const LP_G uint8_t*> L{ls - mis, mis, crlf_len_hbm(buf, W)};
             auto lu = [&](int) { return L; };
-            auto ll = [&](int lend) {
-                return LineT<const uint8_t*>{reinterpret_cast<const uint8_t*>(ls - mis), mis, lend};
-            };
+            auto ll = [&](int lend, auto&& f) { f(LineT<const LP_G uint8_t*>{ls - mis, mis, lend}); };
             uri_wave<NU, NQ, false>(P, C, U, lu, ll, W.active, W.li, wave, WC);
         }
         __syncthreads();
