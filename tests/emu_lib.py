@@ -26,7 +26,11 @@ def build(force=False):
         return
     os.makedirs(os.path.dirname(LIB), exist_ok=True)
     flags = ["-O1"] + SAN_FLAGS if ASAN else ["-O2"]
-    subprocess.run(["g++", "-std=c++17", "-g", "-fPIC", "-shared", "-o", LIB] + flags + SRCS, check=True)
+    # built under a private name and renamed into place: parallel test
+    # workers never load a half-written library
+    tmp = "%s.%d.tmp" % (LIB, os.getpid())
+    subprocess.run(["g++", "-std=c++17", "-g", "-fPIC", "-shared", "-o", tmp] + flags + SRCS, check=True)
+    os.replace(tmp, LIB)
 
 
 def lib():
