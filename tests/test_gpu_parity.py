@@ -899,3 +899,39 @@ def test_device_table_other_configs_gpu():
             # columns (list items, SECOND_MILLIS -> MILLISECONDS -> MICROSECONDS, binary IPs, cookies, raw
             # query parameters included)
             assert host_only == [], host_only
+
+
+@pytest.mark.gpu
+def test_chunk_geometry_gpu(oracle):
+    """The one-pass parse kernel's byte chunks (LP_OPT_CHUNK_LINES): the same
+    results whatever the chunk size -- chunks of a few lines, chunks holding
+    more than 64 lines (runs of very short lines: chunk_excess and
+    k_parse_ovf_lines), lines longer than a chunk's window, CRLF / lone-CR
+    terminators and a last line without one.  The default geometry is
+    checked line by line against the oracle, every other one against it."""
+    import corpora
+    rng = random.Random(7)
+    base = lpa.synth_combined(20261020, 0, 6000).split(b"\n")[:-1]
+    lines = []
+    for i, l in enumerate(base):
+        lines.append(l)
+        if i % 500 == 7:
+            lines += [b"x"] * rng.randrange(100, 300)  # > 64 line starts in one chunk
+        if i % 700 == 11:
+            lines.append(l[:-1] + b"a" * rng.randrange(3000, 7000) + b'"')  # longer than a window
+    data = corpora.crlf_join(lines, 5)  # the last line unterminated
+    want = corpora.split_hadoop(data)
+    assert want == lines
+    fields = paths(oracle)
+    s, r0 = gpu_vs_oracle(oracle, "combined", fields, lines, data=data)
+    assert s["ok"] > 5900, s
+    recs0 = [r0.record_json(i) if int(r0.status[i]) == lpa.LINE_OK else None for i in range(len(lines))]
+    for cl in (1, 17, 64):
+        p = lpa.HttpdLoglineParser("combined", fields, options={lpa.OPT_CHUNK_LINES: cl})
+        r = p.parse_batch(data)
+        assert r.n_lines == len(lines), (cl, r.n_lines, len(lines))
+        assert (r.status == r0.status).all(), (cl, int(np.argmax(r.status != r0.status)))
+        for i in range(len(lines)):
+            if recs0[i] is not None:
+                assert r.record_json(i) == recs0[i], (cl, i)
+        assert r.counters == r0.counters, cl
