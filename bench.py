@@ -432,10 +432,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs (never used by the driver): LP_BENCH_DEVICE puts every
+    # rank on one GPU, LP_BENCH_BACKEND=gloo replaces RCCL, so the N-rank
+    # path can run on a one-GPU box
+    if os.environ.get("LP_BENCH_DEVICE"):
+        local = int(os.environ["LP_BENCH_DEVICE"])
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        backend = os.environ.get("LP_BENCH_BACKEND", "nccl")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(backend)
 
     wl = args.workload
     fmt = lpa.SYNTH_FORMATS[wl]
