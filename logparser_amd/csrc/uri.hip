@@ -21,6 +21,14 @@ namespace {
 // CU running 16 waves (config 2: 7.3 KiB per wave on average, 8.3 KiB at the
 // 99th percentile; a wave needing more runs on the direct path)
 constexpr uint32_t URI_CAP = 8512;
+// query pieces per lane per round of the piece pass; gather rounds per batch
+// (experiment builds override them: make exp XFLAGS=-DLP_URI_QR=...)
+#ifndef LP_URI_QR
+#define LP_URI_QR 4
+#endif
+#ifndef LP_URI_GR
+#define LP_URI_GR 9
+#endif
 
 // Per lane: the line's URI sources.  sp[u] = a | b << 16 (line-relative, 0 =
 // none), cs[u] = the compact buffer offset of line byte a.  NU: the URI
@@ -329,7 +337,7 @@ __device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, Uri
     // table slots loaded together, then query_prep, ONE spill allocation for
     // the round, query_finish.  Most waves need one round for all stages.
     if (nq > 0) {
-        constexpr int QR = 4;
+        constexpr int QR = LP_URI_QR;
         __syncthreads();  // the table slots written in phase 2 are visible to every lane
         const bool has = U.ok && o.status == ST_OK && need != 0;
         const unsigned long long my_ab = has ? my_region : 0ull;
@@ -520,7 +528,7 @@ __device__ __forceinline__ bool uri_compact(const uint8_t* __restrict__ buf, uin
     // gather: block g of the wave is block g - cb[own] of line own's region,
     // own = the last lane whose first block is <= g; every round's load in
     // flight before the first store
-    constexpr int GR = 9;  // rounds per batch (the main kernel's CAP / 1024, rounded up)
+    constexpr int GR = LP_URI_GR;  // rounds per batch (the main kernel's CAP / 1024, rounded up)
     uint16_t* pl16 = reinterpret_cast<uint16_t*>(plane);
     for (uint32_t g0 = 0; g0 < tot; g0 += GR * PW) {
         u32x4 v[GR];
