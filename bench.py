@@ -283,7 +283,8 @@ def cpu_baseline(lpa, workload, fields, sample_lines, threads, repeats=3):
         "value": full["value"],
         "unit": "GB/s",
         "lines_per_s": full["lines_per_s"],
-        "cores": best_t,
+        "cores": min(best_t, usable),  # CPUs the run could occupy (threads beyond them time-share)
+        "threads": best_t,
         "usable_cpus": usable,
         "host_cpus": os.cpu_count(),
         "kind": "port",
@@ -402,6 +403,25 @@ def pmc_traffic(path, n_lines, lib_path, kernel="k_parse_chunks"):
         return None
 
 
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`bench.py --gpus N` started as one plain process (WORLD_SIZE unset):
+    run N rank processes, one per GPU, through torch.distributed.run as a
+    CHILD process (the parent has made no GPU call and never execs), and
+    exit with its status."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % n,
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + list(argv)
+    log("bench: launching %d ranks: %s" % (n, " ".join(cmd)))
+    return subprocess.call(cmd, env=dict(os.environ))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -422,29 +442,54 @@ def main():
                     help="tools/pmc_traffic.py summary of separate rocprofv3 --pmc passes; fills roofline.traffic "
                          "when it was taken on this workload with this exact engine build")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # the first action, before torch or any GPU call: N rank processes
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
 
     import torch
     import torch.distributed as dist
 
-    import logparser_amd as lpa
-    from logparser_amd.shard import max_over_ranks, reduce_counters
-
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench: --gpus %d but WORLD_SIZE=%d (one rank per GPU)" % (args.gpus, world))
     # rehearsal knobs (never used by the driver): LP_BENCH_DEVICE puts every
     # rank on one GPU, LP_BENCH_BACKEND=gloo replaces RCCL, so the N-rank
-    # path can run on a one-GPU box
+    # path can run on a one-GPU box; LP_BENCH_DRYRUN stops every rank right
+    # after the process group is up, before any GPU call (CPU tests of the
+    # launcher)
+    dry = bool(os.environ.get("LP_BENCH_DRYRUN"))
+    backend = None
+    if world > 1:
+        backend = "gloo" if dry else os.environ.get("LP_BENCH_BACKEND", "nccl")
+    if dry:
+        if world > 1:
+            dist.init_process_group(backend)
+            world = dist.get_world_size()
+            dist.barrier()
+            dist.destroy_process_group()
+        print(json.dumps({"dryrun": True, "rank": rank, "world_size": world, "gpus": args.gpus,
+                          "backend": backend}), flush=True)
+        return
+
+    import logparser_amd as lpa
+    from logparser_amd.shard import max_over_ranks, reduce_counters
+
     if os.environ.get("LP_BENCH_DEVICE"):
         local = int(os.environ["LP_BENCH_DEVICE"])
     torch.cuda.set_device(local)
     device = torch.device("cuda", local)
     if world > 1:
-        backend = os.environ.get("LP_BENCH_BACKEND", "nccl")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=device)
         else:
             dist.init_process_group(backend)
+        world = dist.get_world_size()
+        if world != args.gpus:
+            raise SystemExit("bench: process group has %d ranks, --gpus %d" % (world, args.gpus))
 
     wl = args.workload
     fmt = lpa.SYNTH_FORMATS[wl]
@@ -558,8 +603,11 @@ def main():
                               "makes its lines longer than the reference demo log's 230.5 B: lines_per_s is the "
                               "length-independent figure" if wl == 2 else "incl. the terminator",
             "parallelism": ("dp%d (one stream in Hadoop newline-aligned splits: all_gather of chunk sizes, "
-                            "all-reduce of the cuts; RCCL counter all-reduce)" % world) if split is not None else
-                           "dp%d (one corpus per rank; RCCL counter all-reduce)" % world,
+                            "all-reduce of the cuts; %s counter all-reduce per step)"
+                            % (world, "RCCL" if backend == "nccl" else backend)) if split is not None else
+                           "dp1 (one rank: no collective)",
+            "world_size": world,
+            "backend": backend,
             "batches_per_step": len(batches),
         },
         "status_counts": {k: int(stats[k]) for k in ("lines", "ok", "bad", "fallback")},

@@ -109,9 +109,12 @@ int64_t lp_possible_paths_remapped(const char *logformats, int max_depth, const 
 /* Options (lp_set_option). */
 #define LP_OPT_FORCE_DIRECT 1  /* 1: every wave reads its lines from HBM (no LDS window);
                                   diagnostics and tests of the direct path only */
-#define LP_OPT_MAX_RETRIES 2   /* re-runs of a batch whose line / arena estimates were short
-                                  (default 3, 0..16); an arena still short after them degrades:
-                                  the lines that did not fit are FALLBACK, lp_counters out[6] */
+#define LP_OPT_MAX_RETRIES 2   /* re-runs of a batch whose ARENA estimate was short (default 3,
+                                  0..16); an arena still short after them degrades: the lines
+                                  that did not fit are FALLBACK, lp_counters out[6].  A short
+                                  line capacity is always re-run with the exact count (at most
+                                  twice, not bounded by this option): nothing is parsed without
+                                  columns for every line */
 #define LP_OPT_ARENA_BYTES 3   /* tests: exact arena capacity of each batch's first run (0 = estimate) */
 #define LP_OPT_CHUNK_LINES 4   /* one-format programs: lines per byte chunk the one-pass parse kernel
                                   aims for (1..64, 0 = default 54; a chunk's 65th line onwards is
@@ -123,8 +126,9 @@ int lp_set_option(lp_handle *h, int option, int64_t value);
  * With it (or after a first batch, whose line count sizes the buffers)
  * lp_parse_batch enqueues the whole batch without waiting for the device; a
  * batch that outgrows the buffers is re-run with exact sizes inside lp_sync
- * (at most LP_OPT_MAX_RETRIES times; an arena still short then sends the
- * lines that did not fit to FALLBACK instead of failing the batch). */
+ * (a short arena at most LP_OPT_MAX_RETRIES times, after which the lines that
+ * did not fit go to FALLBACK instead of failing the batch; a short line
+ * capacity at most twice, with the exact count). */
 int lp_reserve(lp_handle *h, int64_t max_lines, uint64_t arena_bytes);
 
 /* Parse every line of buf[0, nbytes), Hadoop LineRecordReader semantics
@@ -316,10 +320,13 @@ int lp_casts(lp_handle *h, const char *target);
  * On a device view (r from lp_result_view, on_host 0) the table is built on
  * the GPU from the batch still in HBM (its input must still be valid):
  * valid / i64 / f64 / chars are then device buffers of the handle's device,
- * the call returns once they are filled, and LP_E_UNSUPPORTED names a path
- * whose value only the host replay derives (cookies, Set-Cookie, upstream
- * lists, converters of converters, remapped deliveries) or a DOUBLE column of
- * a string-valued path: build those from a host copy. */
+ * the call returns once they are filled.  Request cookies, raw-token query
+ * strings, upstream list items (N.value / N.redirected, SECOND_MILLIS in ms and
+ * us), BinaryIP and the first line / URI / query values are device columns.
+ * LP_E_UNSUPPORTED names a path whose value only the host replay derives
+ * (Set-Cookie values and attributes, a converter applied to an already
+ * converted value) or a DOUBLE column of a string-valued path
+ * (Double.parseDouble): build those from a host copy. */
 typedef struct lp_table_col {
     const char *path;
     int32_t kind;

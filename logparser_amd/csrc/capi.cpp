@@ -603,11 +603,12 @@ void lp_free(lp_handle* h) {
     hipSetDevice(h->device);
     if (h->pending) hipStreamSynchronize(h->stream);
     for (auto* b : {&h->input, &h->chunk, &h->line_off, &h->cols, &h->arena, &h->meta, &h->waves, &h->args, &h->route,
-                    &h->ovf, &h->hist, &h->targs, &h->tscratch})
+                    &h->ovf, &h->hist, &h->cstate, &h->targs, &h->tscratch})
         b->release();
-    if (h->have_events)
+    if (h->have_events) {
         for (auto& ev : h->ev) hipEventDestroy(ev);
         for (auto& ev : h->tev) hipEventDestroy(ev);
+    }
     delete h;
 }
 

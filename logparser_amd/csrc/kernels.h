@@ -61,7 +61,7 @@ ChunkPlan chunk_plan(const ParseLaunch& a);
 // then meta->counters[0..4] += lines, ok, bad, fallback, arena bytes written.
 // Chunked (a.chunked): k_parse_chunks writes the line index, meta->n_lines /
 // cap_ovf and the lines' rows, k_parse_ovf_lines the lines it queued
-// (C.chunk_state zeroed, C.chunk_counts: chunk_plan().n_chunks records,
+// (C.chunk_state: n_chunks + 1 words zeroed, C.chunk_counts: chunk_plan().n_chunks records,
 // C.ovf_lines: cap_lines entries).  Otherwise the line index exists and the
 // staged waves, then the waves whose window did not fit LDS, run
 // (C.ovf_list and C.uri_ovf_list: parse_waves(cap_lines) + 1 entries each).

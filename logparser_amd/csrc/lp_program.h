@@ -262,6 +262,10 @@ struct Program {
     int32_t guard_setc[MAX_FMT];
     int32_t guard_setc_exp[MAX_FMT];
     int32_t n_secms, n_list, n_binip, n_pair;
+    // one LogFormat whose elements all have a speculative first-leaf rule
+    // (lp_device.h match_spec_leaf): the kernels try it before the exact
+    // first leaf
+    int32_t spec_leaf;
     SecmsStage secms[MAX_SECMS];
     ListStage list[MAX_LIST];
     BinipStage binip[MAX_BINIP];
@@ -395,7 +399,7 @@ struct Columns {
     // chunked parse (one-format programs: the line index built inside the
     // parse kernel): per byte chunk the decoupled look-back word, its status
     // counts, and the lines queued for the direct kernel
-    LP_G uint64_t* chunk_state;          // [n_chunks] aggregate / inclusive line counts
+    LP_G uint64_t* chunk_state;          // [n_chunks] aggregate / inclusive line counts, [n_chunks] the wave ticket
     LP_G uint32_t* chunk_counts;         // [n_chunks][WC_WORDS]
     LP_G uint32_t* ovf_lines;            // [cap_lines] line numbers
     int64_t cap_lines;                   // lines the columns hold

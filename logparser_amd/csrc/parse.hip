@@ -260,8 +260,13 @@ __device__ __noinline__ void chunk_excess(const uint8_t* __restrict__ buf, uint6
     }
 }
 
-// Block 0: the scanner; block c + 1: chunk c of cb bytes, one wave.  LDS:
-// [elements][DFS stack][starts][window (win_cap)][mask planes (win_cap / 4)].
+// Ticket 0: the scanner; ticket c + 1: chunk c of cb bytes, one wave.  The
+// role comes from an atomic ticket (chunk_state[n_chunks], zeroed with the
+// look-back words), not from blockIdx: a wave only ever waits for the scanner
+// and for chunks whose tickets were taken before its own, i.e. by waves that
+// are already resident, so every wait ends whatever order the dispatcher
+// starts the workgroups in (the decoupled look-back rule).
+// LDS: [elements][DFS stack][starts][window (win_cap)][mask planes (win_cap / 4)].
 // direct: every line goes to the direct kernel (LP_OPT_FORCE_DIRECT, tests).
 template <bool LA>
 __global__ __launch_bounds__(PW, 2) void k_parse_chunks(const uint8_t* __restrict__ buf, uint64_t nbytes,
@@ -270,11 +275,15 @@ __global__ __launch_bounds__(PW, 2) void k_parse_chunks(const uint8_t* __restric
     const Program& P = args->prog;
     const Columns& C = args->cols;
     const int64_t n_chunks = (int64_t)((nbytes + cb - 1) / cb);
-    if (blockIdx.x == 0) {
+    uint32_t ticket = 0;
+    if (threadIdx.x == 0)
+        ticket = (uint32_t)__hip_atomic_fetch_add(&C.chunk_state[n_chunks], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ticket = (uint32_t)__builtin_amdgcn_readfirstlane((int)ticket);
+    if (ticket == 0) {
         chunk_scanner(C.chunk_state, n_chunks);
         return;
     }
-    const int64_t c = (int64_t)blockIdx.x - 1;
+    const int64_t c = (int64_t)ticket - 1;
     const uint64_t c0 = (uint64_t)c * cb;
     if (c0 >= nbytes) return;
     const uint64_t c1 = c0 + cb < nbytes ? c0 + cb : nbytes;

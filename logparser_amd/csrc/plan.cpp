@@ -1416,6 +1416,20 @@ void Plan::compile_program() {
         if (depth > P.max_stack) P.max_stack = depth;
     }
     if (P.max_stack > MAX_STACK) { device_ok_ = false; why_ = "too many backtracking elements"; return; }
+    // the speculative first leaf (match_spec_leaf) covers these element kinds
+    // (for the others it would only walk part of the line and give up)
+    P.spec_leaf = P.n_fmt == 1;
+    for (int i = 0; i < P.n_elems; ++i) {
+        const Elem& e = P.elems[i];
+        switch (e.kind) {
+        case EK_LIT: case EK_NOSPACE: case EK_TIME_US: break;
+        case EK_NUMBER: case EK_CLFNUMBER: case EK_HEXNUMBER: case EK_CLFHEXNUMBER: case EK_NONZERO:
+            if (!e.last && !(e.nlit && e.det)) P.spec_leaf = 0;
+            break;
+        case EK_ANY_GREEDY: case EK_ANY_LAZY: break;
+        default: P.spec_leaf = 0; break;
+        }
+    }
     int cur_fmt = 0;
     auto tk = [&](int oi) { return cur_fmt * 64 + oi; };  // (format, token slot) key of the stage maps
     // stages, walking the compiled tree from each captured token output.

@@ -34,6 +34,7 @@ typedef struct {
     const char *buf;
     const int64_t *starts; /* line k = [starts[k], starts[k + 1] - 1) */
     int64_t from, to;
+    int64_t warm_from; /* lines [warm_from, from) parsed first, results dropped */
     uint8_t *status;
     uint64_t *hash;
     int err;
@@ -46,7 +47,21 @@ static void *orc_thread(void *arg) {
     if (!p) { j->err = 1; return NULL; }
     const int cap = 1 << 20;
     char *out = (char *)malloc((size_t)cap);
-    for (int64_t k = j->from; k < j->to; k++) {
+    /* several LogFormats: the parser's sticky active format
+     * (HttpdLogFormatDissector.java:173-204) at line `from` is the one a
+     * single parser over the whole buffer would hold when the warm-up lines
+     * hold a line that exactly one format matches (the state after such a
+     * line does not depend on the state before it) -- with mutually
+     * exclusive formats, any OK line */
+    int warm_ok = j->warm_from == j->from;
+    for (int64_t k = j->warm_from; k < j->from; k++) {
+        const int64_t a = j->starts[k], b = j->starts[k + 1] - 1;
+        const int st = orc_parse(p, j->buf + a, (int)(b - a), out, cap);
+        if (st < 0) { j->err = 2; break; }
+        if (st == ORC_OK) warm_ok = 1;
+    }
+    if (!warm_ok) j->err = 4;
+    for (int64_t k = j->from; k < j->to && !j->err; k++) {
         const int64_t a = j->starts[k], b = j->starts[k + 1] - 1;
         const int st = orc_parse(p, j->buf + a, (int)(b - a), out, cap);
         if (st < 0) { j->err = 2; break; }
@@ -58,12 +73,16 @@ static void *orc_thread(void *arg) {
     return NULL;
 }
 
-/* Every '\n'-terminated line of buf (one LogFormat, so one fresh parser per
- * thread is the reference's own per-thread Parser): status (ORC_*) and the
- * record digest per line.  Returns the line count, -1 when more than
- * max_lines, -2 on a parser error. */
-int64_t orc_digest_lines(const char *logformat, const char *const *fields, int nfields, const char *buf,
-                         size_t nbytes, int nthreads, int64_t max_lines, uint8_t *status, uint64_t *hash) {
+/* Every '\n'-terminated line of buf: status (ORC_*) and the record digest
+ * per line.  One LogFormat: one fresh parser per thread is the reference's
+ * own per-thread Parser (warmup 0).  Several LogFormats (sticky active
+ * format): each thread's parser first runs over the `warmup` lines before
+ * its range, which must hold an OK line (see orc_thread; formats that are
+ * mutually exclusive).  Returns the line count, -1 when more than
+ * max_lines, -2 on a parser error, -4 when a warm-up held no OK line. */
+int64_t orc_digest_lines_w(const char *logformat, const char *const *fields, int nfields, const char *buf,
+                           size_t nbytes, int nthreads, int64_t max_lines, int64_t warmup, uint8_t *status,
+                           uint64_t *hash) {
     int64_t n = 0;
     for (const char *q = buf; (q = (const char *)memchr(q, '\n', nbytes - (size_t)(q - buf))) != NULL; q++) n++;
     if (n > max_lines) return -1;
@@ -76,8 +95,9 @@ int64_t orc_digest_lines(const char *logformat, const char *const *fields, int n
     orc_job *jobs = (orc_job *)calloc((size_t)nthreads, sizeof(orc_job));
     pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)nthreads);
     for (int t = 0; t < nthreads; t++) {
-        jobs[t] = (orc_job){logformat, fields, nfields, buf, starts, n * t / nthreads, n * (t + 1) / nthreads,
-                            status, hash, 0};
+        const int64_t from = n * t / nthreads;
+        jobs[t] = (orc_job){logformat, fields, nfields, buf, starts, from, n * (t + 1) / nthreads,
+                            from > warmup ? from - warmup : 0, status, hash, 0};
         pthread_create(&th[t], NULL, orc_thread, &jobs[t]);
     }
     int err = 0;
@@ -88,7 +108,12 @@ int64_t orc_digest_lines(const char *logformat, const char *const *fields, int n
     free(jobs);
     free(th);
     free(starts);
-    return err ? -2 : n;
+    return err ? (err & 4 ? -4 : -2) : n;
+}
+
+int64_t orc_digest_lines(const char *logformat, const char *const *fields, int nfields, const char *buf,
+                         size_t nbytes, int nthreads, int64_t max_lines, uint8_t *status, uint64_t *hash) {
+    return orc_digest_lines_w(logformat, fields, nfields, buf, nbytes, nthreads, max_lines, 0, status, hash);
 }
 
 /* ---------------------------------------------------------------- engine */

@@ -5,6 +5,7 @@
 // stages can be diffed against the oracle in the CPU test suite.  It is never
 // part of the product: the product library (liblogparser_amd.so) only runs
 // this logic inside the HIP kernel and fails when no GPU is present.
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -20,6 +21,16 @@ struct Emu {
     std::string err;
     uint32_t fmt_state = 0;  // sticky active LogFormat (HttpdLogFormatDissector), carried line to line
 };
+
+// the kernel instance a one-format program runs in (capi.cpp enqueue: the
+// literal-aware first candidates only for programs that have such elements)
+static bool lit_aware(const Program& P) {
+    for (int i = 0; i < P.n_elems; ++i) {
+        const ElemV e = load_elem(P.elems + i);
+        if (e.nlit && !e.last && ((e.kind == EK_NOSPACE && !e.det) || e.kind == EK_NOSPACE3)) return true;
+    }
+    return false;
+}
 
 extern "C" {
 
@@ -75,6 +86,38 @@ int emu_parse_in(void* h, const char* buf, int64_t start, int len, char* out, in
 }
 
 void emu_set_masks(int on) { g_masks_fwd(on); }
+
+// The speculative first leaf against the exact one on a line (staged as in
+// parse_impl's masked window): 0 the speculation declined, 1 both matched
+// with identical captures, 2 the speculation matched and the first leaf did
+// not (or their captures differ) -- never allowed; -1 not applicable.
+int emu_spec_check(void* h, const char* line, int len) {
+    Emu* e = (Emu*)h;
+    if (!e->plan.device_ok()) return -1;
+    const Program& P = e->plan.program();
+    if (!P.spec_leaf || lit_aware(P)) return -1;
+    const uint32_t off = (uint32_t)(len * 5 + 1) & 3u;
+    std::vector<uint8_t> buf(off, 0xFF);
+    buf.insert(buf.end(), line, line + len);
+    buf.push_back('\n');
+    const uint32_t hi = (off + (uint32_t)len + 4) & ~3u;
+    const uint32_t wn = (hi + 63) & ~63u;
+    std::vector<uint64_t> wbuf(wn / 8 + 8, ~0ull);
+    memcpy(wbuf.data(), buf.data(), std::min<size_t>(buf.size(), hi));
+    std::vector<uint64_t> masks(MC_N * (wn / 64));
+    build_masks((const uint8_t*)wbuf.data(), wn, masks.data());
+    MLine L{(const uint8_t*)wbuf.data(), off, len, masks.data()};
+    RegArr<MAX_TOK> c1, c2;
+    c1.fill(0);
+    c2.fill(0);
+    const bool s = match_spec_leaf(P, L, c1);
+    if (!s) return 0;
+    const bool f = match_first_leaf<false>(P, L, c2);
+    if (!f) return 2;
+    for (int k = 0; k < MAX_TOK; ++k)
+        if (c1.get(k) != c2.get(k)) return 2;
+    return 1;
+}
 
 // the planner's token table (plan.cpp) as canonical JSON; returns its length
 int emu_token_table(int nginx, char* out, int cap) {
@@ -138,7 +181,8 @@ static int run_line(const Program& P, const LN& L, const uint8_t* base, uint32_t
         R.fmt_id.assign(1, (uint8_t)fmt_state);
     }
     if (P.n_fmt > 1) phase1<true>(P, P.elems, L, o, stk, C, 0, false, (int)fmt_state);  // as k_parse_lines
-    else phase1<false>(P, P.elems, L, o, stk, C, 0, false, 0);
+    else if (lit_aware(P)) phase1<false, true>(P, P.elems, L, o, stk, C, 0, false, 0);  // as k_parse_chunks<true>
+    else phase1<false, false>(P, P.elems, L, o, stk, C, 0, false, 0);            // as k_parse_chunks<false>
     write_line(P, o, C, 0);
     if (o.status != ST_OK || !P.has_phase2()) return 0;
     // the URI kernel: its sources from the columns phase 1 wrote

@@ -51,6 +51,10 @@ def lib():
         L.orc_digest_lines.restype = ctypes.c_int64
         L.orc_digest_lines.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int, ctypes.c_char_p,
                                        ctypes.c_size_t, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]
+        L.orc_digest_lines_w.restype = ctypes.c_int64
+        L.orc_digest_lines_w.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int,
+                                         ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int64,
+                                         ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]
         L.dg_engine.restype = ctypes.c_int
         L.dg_engine.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                 ctypes.c_int, ctypes.c_void_p]
@@ -144,15 +148,17 @@ def token_table(nginx):
     return json.loads(out.value.decode("utf-8"))
 
 
-def digest_lines(logformat, fields, data, threads, max_lines):
-    """orc_digest_lines: (status u8[n], FNV-1a of each OK line's record u64[n])
-    of every '\\n'-terminated line of data, on `threads` threads."""
+def digest_lines(logformat, fields, data, threads, max_lines, warmup=0):
+    """orc_digest_lines_w: (status u8[n], FNV-1a of each OK line's record u64[n])
+    of every '\\n'-terminated line of data, on `threads` threads (several
+    LogFormats: each thread's parser warmed up on the `warmup` lines before
+    its range, see oracle/digest.c)."""
     import numpy as np
     st = np.zeros(max_lines, dtype=np.uint8)
     h = np.zeros(max_lines, dtype=np.uint64)
     f = _fields(fields)
-    n = lib().orc_digest_lines(logformat.encode(), f, len(fields), data, len(data), threads, max_lines,
-                               st.ctypes.data, h.ctypes.data)
+    n = lib().orc_digest_lines_w(logformat.encode(), f, len(fields), data, len(data), threads, max_lines, warmup,
+                                 st.ctypes.data, h.ctypes.data)
     if n < 0:
         raise OracleError("orc_digest_lines failed: %d" % n)
     return st[:n], h[:n]

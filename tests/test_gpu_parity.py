@@ -216,6 +216,68 @@ def test_headline_parity_every_line(oracle):
     assert np.count_nonzero(h_eng) == n  # every line produced a record
 
 
+def _newline_batches(data, batch_bytes):
+    """[(start, end)) pieces of about batch_bytes, each cut just after a '\\n'
+    (bench.newline_batches on a host buffer)"""
+    out, a = [], 0
+    while len(data) - a > batch_bytes:
+        c = data.index(b"\n", a + batch_bytes) + 1
+        out.append((a, c))
+        a = c
+    if a < len(data):
+        out.append((a, len(data)))
+    return out
+
+
+@pytest.mark.parametrize("workload", [3, 4, 5])
+def test_every_line_parity_other_configs(oracle, workload):
+    """Every line of a 2 M-line batch of BASELINE configs 3, 4 and 5 against
+    the oracle, by (status, FNV-1a of the record) digests on 16 host threads
+    (oracle/digest.c): config 3 with its 5 % malformed lines (status BAD must
+    agree line by line), config 4's NGINX upstream format, and config 5's
+    three-format corpus streamed through ONE handle in newline-aligned 48 MiB
+    batches (about 10), so the sticky routing state crosses batches as in the
+    timed bench run (the oracle side: one parser per thread, each warmed up
+    on the 2000 lines before its range, digest.c).  No FALLBACK is allowed
+    on these workloads (configs 3-5 are inside the device subset)."""
+    import ctypes
+    import os
+    seeds = {3: 20261016, 4: 20261017, 5: 20261018}
+    n = int(os.environ.get("LP_OTHER_CONFIG_LINES", "2000000"))
+    threads = 16
+    fmt = lpa.SYNTH_FORMATS[workload]
+    fields = paths(oracle, fmt)
+    data = lpa.synth(workload, seeds[workload], 0, n)
+    assert data.count(b"\n") == n
+    p = lpa.HttpdLoglineParser(fmt, fields)
+    fn = ctypes.cast(lpa.lib().lp_result_record_json, ctypes.c_void_p).value
+    pieces = _newline_batches(data, 48 << 20) if workload == 5 else [(0, len(data))]
+    if workload == 5:
+        assert len(pieces) >= 8
+    st_eng, h_eng = [], []
+    for a, b in pieces:
+        r = p.parse_batch(data[a:b])
+        assert r.n_lines == data.count(b"\n", a, b)
+        assert r.counters["fallback"] == 0, r.counters
+        buf, res = r.copy_to_host(with_input=True)
+        st_eng.append(r.status.astype(np.uint8).copy())
+        h_eng.append(oracle.digest_engine(fn, p._h, ctypes.addressof(res), r.status, threads))
+        del buf, res
+    st_eng, h_eng = np.concatenate(st_eng), np.concatenate(h_eng)
+    st_orc, h_orc = oracle.digest_lines(fmt, fields, data, threads, n + 1, warmup=2000 if workload == 5 else 0)
+    assert len(st_orc) == n == len(st_eng)
+    bad = np.nonzero(st_orc != st_eng)[0]
+    assert len(bad) == 0, (len(bad), bad[:10].tolist(), st_orc[bad[:10]].tolist(), st_eng[bad[:10]].tolist())
+    diff = np.nonzero(h_eng != h_orc)[0]
+    assert len(diff) == 0, (len(diff), diff[:10].tolist())
+    n_ok = int(np.count_nonzero(st_eng == oracle.OK))
+    assert np.count_nonzero(h_eng) == n_ok
+    if workload == 3:  # the malformed 5 % are BAD on both sides
+        assert 0.03 * n < n - n_ok < 0.07 * n, n - n_ok
+    else:
+        assert n_ok == n
+
+
 @pytest.mark.parametrize("staged", [True, False])
 def test_offsets_beyond_4gb(oracle, staged):
     """A 4.4 GB batch (a 1 MB block of synthetic lines repeated on the device):

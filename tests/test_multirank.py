@@ -257,3 +257,33 @@ def test_bench_stream_split_config5_gloo(oracle):
     assert len(got) == len(ref) == world * L
     assert got == ref
     assert sum(1 for st, _ in ref if st == oracle_lib.OK) > 0.9 * len(ref)
+
+
+def test_bench_gpus_flag_launches_ranks():
+    """`python bench.py --gpus N` (WORLD_SIZE unset) starts N rank processes
+    itself (torch.distributed.run as a child process, before any GPU call);
+    LP_BENCH_DRYRUN stops each rank right after its process group is up, so
+    the launcher path runs on CPU (gloo) up to its pre-GPU point."""
+    import json
+    import re
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["LP_BENCH_DRYRUN"] = "1"
+    for n in (1, 3):
+        p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(n)], env=env,
+                           capture_output=True, text=True, timeout=240)
+        assert p.returncode == 0, p.stderr[-2000:]
+        # the ranks share one stdout: pick the objects out wherever they landed
+        lines = [json.loads(x) for x in re.findall(r'\{"dryrun"[^{}]*\}', p.stdout)]
+        assert sorted(x["rank"] for x in lines) == list(range(n)), p.stdout
+        for x in lines:
+            assert x["world_size"] == n and x["gpus"] == n
+            assert x["backend"] == ("gloo" if n > 1 else None)
+    # a driver-style launch whose WORLD_SIZE disagrees with --gpus fails loudly
+    env2 = dict(env, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "4"], env=env2,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0 and "WORLD_SIZE=2" in (p.stderr + p.stdout)
