@@ -119,6 +119,9 @@ int64_t lp_possible_paths_remapped(const char *logformats, int max_depth, const 
 #define LP_OPT_CHUNK_LINES 4   /* one-format programs: lines per byte chunk the one-pass parse kernel
                                   aims for (1..64, 0 = default 54; a chunk's 65th line onwards is
                                   parsed from HBM by a second kernel) */
+#define LP_OPT_CHUNK_WAIT 5    /* tests: polls a chunk's wave makes for its first line number before it
+                                  leaves the chunk to the deferred pass (0 = default 16384; a negative
+                                  value: none, every chunk goes to the deferred pass) */
 int lp_set_option(lp_handle *h, int option, int64_t value);
 
 /* Capacity for the coming batches: columns for max_lines lines and at least
@@ -170,8 +173,10 @@ int64_t lp_line_record_json(lp_handle *h, int64_t i, char *out, size_t cap);
  * batch (capacity / arena estimates exceeded), out[6] = arena overflows the
  * final run left (lines sent to FALLBACK for want of arena; 0 normally),
  * out[7] = waves whose URI bytes exceeded the URI kernel's compact buffer
- * (their URI stages read the input from HBM directly).
- * Returns the words written. */
+ * (their URI stages read the input from HBM directly), out[8] = one-format
+ * programs: byte chunks redone by the deferred pass (their wave stopped
+ * waiting for its first line number; 0 normally, see LP_OPT_CHUNK_WAIT).
+ * Returns the words written (at most 9). */
 int lp_counters(lp_handle *h, uint64_t *out, int n);
 
 /* Device-side timing of the last batch, in milliseconds, measured with HIP

@@ -33,7 +33,7 @@ LIB_PATH = os.environ.get("LOGPARSER_AMD_LIB") or os.path.join(_HERE, "_lib", "l
 LP_OK, LP_E_INVALID, LP_E_MISSING, LP_E_UNSUPPORTED, LP_E_DEVICE, LP_E_NOMEM, LP_E_STATE = 0, -1, -2, -3, -4, -5, -6
 LINE_OK, LINE_BAD, LINE_FALLBACK = 0, 1, 2
 BUF_HOST, BUF_DEVICE = 0, 1
-OPT_FORCE_DIRECT, OPT_MAX_RETRIES, OPT_ARENA_BYTES, OPT_CHUNK_LINES = 1, 2, 3, 4
+OPT_FORCE_DIRECT, OPT_MAX_RETRIES, OPT_ARENA_BYTES, OPT_CHUNK_LINES, OPT_CHUNK_WAIT = 1, 2, 3, 4, 5
 ARENA_SHARDS = 64
 
 
@@ -234,10 +234,11 @@ class BatchResult:
             if rc != LP_OK:
                 raise EngineUnavailable("lp_line_status failed: %d" % rc)
         self.status = st[: self.n_lines]
-        c = (ctypes.c_uint64 * 8)()
-        L.lp_counters(parser._h, c, 8)
+        c = (ctypes.c_uint64 * 9)()
+        L.lp_counters(parser._h, c, 9)
         self.counters = {"lines": c[0], "ok": c[1], "bad": c[2], "fallback": c[3]}
-        self.diag = {"overflow_waves": c[4], "retries": c[5], "arena_ovf": c[6], "uri_overflow_waves": c[7]}
+        self.diag = {"overflow_waves": c[4], "retries": c[5], "arena_ovf": c[6], "uri_overflow_waves": c[7],
+                     "deferred_chunks": c[8]}
         t = (ctypes.c_float * 3)()
         L.lp_last_timing(parser._h, t, 3)
         self.timing_ms = {"total": t[0], "index": t[1], "parse": t[2]}
@@ -600,14 +601,14 @@ class HttpdLoglineParser:
         rc = L.lp_sync(self._h)
         if rc != LP_OK:
             raise EngineUnavailable("lp_sync failed: %d" % rc)
-        c = (ctypes.c_uint64 * 8)()
-        L.lp_counters(self._h, c, 8)
+        c = (ctypes.c_uint64 * 9)()
+        L.lp_counters(self._h, c, 9)
         t = (ctypes.c_float * 5)()
         L.lp_last_timing(self._h, t, 5)
         b = (ctypes.c_uint64 * 4)()
         L.lp_last_bytes(self._h, b, 4)
         return {"lines": c[0], "ok": c[1], "bad": c[2], "fallback": c[3], "overflow_waves": c[4], "retries": c[5],
-                "arena_ovf": c[6], "uri_overflow_waves": c[7],
+                "arena_ovf": c[6], "uri_overflow_waves": c[7], "deferred_chunks": c[8],
                 "ms_total": t[0], "ms_index": t[1], "ms_parse": t[2], "ms_parse_kernels": t[3], "ms_uri_kernels": t[4],
                 "bytes_in": b[0], "bytes_out": b[1], "bytes_parse_kernels": b[2], "bytes_uri_kernels": b[3]}
 

@@ -107,9 +107,11 @@ struct lp_handle {
     bool have_events = false;
     uint64_t counters[4]{};
     uint32_t chunk_lines = 0;      // LP_OPT_CHUNK_LINES (0: the kernel's default)
+    int32_t chunk_wait = 0;        // LP_OPT_CHUNK_WAIT (tests: 0 default, < 0 defer every chunk not yet reached)
     bool chunked = false;          // the last batch ran the chunked parse (line index inside the parse kernel)
     uint64_t ovf_waves = 0;        // waves of the last batch parsed by k_parse_overflow (chunked: lines by k_parse_ovf_lines)
     uint64_t uri_ovf_waves = 0;    // ... whose URI stages ran in k_uri_overflow
+    uint64_t deferred = 0;         // chunks of the last batch parsed by the deferred pass (normally 0)
     uint64_t shard_top[LP_ARENA_SHARDS]{};
     uint64_t arena_written = 0;
     uint64_t uri_src_bytes = 0;  // URI source bytes the URI kernels read (meta counters[5])
@@ -366,6 +368,7 @@ int enqueue(lp_handle* h, bool sync_count) {
         if (!pl.mean_line && cap > 0) pl.mean_line = (nbytes + cap - 1) / (uint64_t)cap;
         pl.chunked = chunked;
         pl.chunk_lines = h->chunk_lines;
+        pl.chunk_wait = h->chunk_wait;
         pl.lit_aware = false;
         for (int i = 0; i < P.n_elems; ++i) {
             const lp::ElemV e = lp::load_elem(P.elems + i);
@@ -376,10 +379,12 @@ int enqueue(lp_handle* h, bool sync_count) {
             // look-back words (zeroed), per-chunk counts, the queued line list
             const lp::ChunkPlan cp = lp::chunk_plan(pl);
             const size_t sb = align256(8 * (size_t)(cp.n_chunks + 1)), cb = align256(4 * lp::WC_WORDS * (size_t)(cp.n_chunks + 1));
-            if (!h->cstate.ensure(sb + cb + 4 * (size_t)(cap + 1))) return LP_E_NOMEM;
+            const size_t ob = align256(4 * (size_t)(cap + 1));
+            if (!h->cstate.ensure(sb + cb + ob + 4 * (size_t)(cp.n_chunks + 1))) return LP_E_NOMEM;
             C.chunk_state = h->cstate.as<uint64_t>();
             C.chunk_counts = h->cstate.as<uint32_t>(sb);
             C.ovf_lines = h->cstate.as<uint32_t>(sb + cb);
+            C.deferred_chunks = h->cstate.as<uint32_t>(sb + cb + ob);
             if (hipMemsetAsync(C.chunk_state, 0, sb, s) != hipSuccess) return LP_E_DEVICE;
         }
         h->host_args.prog = P;
@@ -452,6 +457,7 @@ int finish(lp_handle* h) {
             h->uri_src_bytes = m.counters[5];
             h->ovf_waves = h->chunked ? m.ovf_lines : m.ovf_waves;
             h->uri_ovf_waves = m.uri_ovf_waves;
+            h->deferred = h->chunked ? m.deferred : 0;
         } else {
             h->counters[0] = (uint64_t)n;
             h->counters[1] = h->counters[2] = 0;
@@ -642,6 +648,9 @@ int lp_set_option(lp_handle* h, int option, int64_t value) {
         if (value < 0 || value > 64) return LP_E_INVALID;
         h->chunk_lines = (uint32_t)value;
         return LP_OK;
+    case LP_OPT_CHUNK_WAIT:
+        h->chunk_wait = value < 0 ? -1 : (int32_t)std::min<int64_t>(value, 1 << 30);
+        return LP_OK;
     case LP_OPT_MAX_RETRIES:
         if (value < 0 || value > 16) return LP_E_INVALID;
         h->max_retries = (int)value;
@@ -779,10 +788,10 @@ int lp_counters(lp_handle* h, uint64_t* out, int n) {
     if (!h || !out) return LP_E_INVALID;
     const int st = ensure_synced(h);
     if (st != LP_OK) return st;
-    const uint64_t v[8] = {h->counters[0], h->counters[1], h->counters[2], h->counters[3], h->ovf_waves,
-                           (uint64_t)h->retries, h->arena_ovf, h->uri_ovf_waves};
-    for (int k = 0; k < n && k < 8; ++k) out[k] = v[k];
-    return n < 8 ? n : 8;
+    const uint64_t v[9] = {h->counters[0], h->counters[1], h->counters[2], h->counters[3], h->ovf_waves,
+                           (uint64_t)h->retries, h->arena_ovf, h->uri_ovf_waves, h->deferred};
+    for (int k = 0; k < n && k < 9; ++k) out[k] = v[k];
+    return n < 9 ? n : 9;
 }
 
 int lp_histograms(lp_handle* h, uint64_t* out, int out_on_device) {

@@ -44,6 +44,7 @@ struct ParseLaunch {
     void* mid_event = nullptr;  // hipEvent_t recorded between the parse kernels and the URI kernels
     bool chunked = false;       // one-format program: k_parse_chunks builds the line index itself
     uint32_t chunk_lines = 0;   // lines per byte chunk the chunked kernel aims for (0: default)
+    int32_t chunk_wait = 0;     // polls for a chunk's line number before deferring it (0: default, < 0: none)
     bool lit_aware = true;      // the program has a [^\s]* / "$request" element a shorter end of which can meet
                                 // its literal (the chunked kernel's instance with literal-aware first candidates)
 };
@@ -61,7 +62,7 @@ ChunkPlan chunk_plan(const ParseLaunch& a);
 // then meta->counters[0..4] += lines, ok, bad, fallback, arena bytes written.
 // Chunked (a.chunked): k_parse_chunks writes the line index, meta->n_lines /
 // cap_ovf and the lines' rows, k_parse_ovf_lines the lines it queued
-// (C.chunk_state: n_chunks + 1 words zeroed, C.chunk_counts: chunk_plan().n_chunks records,
+// (C.chunk_state zeroed, C.chunk_counts and C.deferred_chunks: chunk_plan().n_chunks records,
 // C.ovf_lines: cap_lines entries).  Otherwise the line index exists and the
 // staged waves, then the waves whose window did not fit LDS, run
 // (C.ovf_list and C.uri_ovf_list: parse_waves(cap_lines) + 1 entries each).

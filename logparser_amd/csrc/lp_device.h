@@ -660,16 +660,6 @@ __host__ __device__ LP_INLINE bool lit_at(const Program& P, const LN& L, int pos
     return true;
 }
 
-__host__ __device__ LP_INLINE bool time_us_bytes_ok(const Bytes28& c) {
-    if (!(c[0] >= '0' && c[0] <= '3') || !is_digit(c[1]) || c[2] != '/') return false;
-    if (!is_alpha(c[3]) || !is_alpha(c[4]) || !is_alpha(c[5]) || c[6] != '/') return false;
-    if (!(c[7] >= '1' && c[7] <= '9') || !is_digit(c[8]) || !is_digit(c[9]) || !is_digit(c[10]) || c[11] != ':') return false;
-    if (!is_digit(c[12]) || !is_digit(c[13]) || c[14] != ':' || !is_digit(c[15]) || !is_digit(c[16]) || c[17] != ':') return false;
-    if (!is_digit(c[18]) || !is_digit(c[19]) || c[20] != ' ') return false;
-    if (!(c[21] == '+' || c[21] == '|' || c[21] == '-')) return false;   // [\+|\-]
-    return is_digit(c[22]) && is_digit(c[23]) && is_digit(c[24]) && is_digit(c[25]);
-}
-
 template <typename LN>
 __host__ __device__ LP_INLINE bool time_us_ok(const LN& L, int p) {
     if (p + 26 > L.n) return false;
@@ -1261,134 +1251,6 @@ __host__ __device__ LP_INLINE bool match_first_leaf(const Program& P, const LN& 
     return ok && pos == L.n;
 }
 
-// A number token's bytes [p, p + len) (len <= 8, the two little-endian words
-// at p) in the element's class: [0-9]+, [0-9]+|-, [0-9a-fA-F]+, [0-9a-fA-F]+|-,
-// [1-9][0-9]* (TokenParser.java:35-59).
-__host__ __device__ LP_INLINE bool num_bytes_ok(int kind, uint32_t w0, uint32_t w1, int len) {
-    if (len <= 0 || len > 8) return false;
-    const uint32_t m0 = len >= 4 ? swar::HI : swar::HI & ((1u << (8 * len)) - 1u);
-    const uint32_t m1 = len >= 8 ? swar::HI : len <= 4 ? 0u : swar::HI & ((1u << (8 * (len - 4))) - 1u);
-    const bool hex = kind == EK_HEXNUMBER || kind == EK_CLFHEXNUMBER;
-    const uint32_t c0 = hex ? swar::hex(w0) : swar::digit(w0), c1 = hex ? swar::hex(w1) : swar::digit(w1);
-    bool ok = (c0 & m0) == m0 && (c1 & m1) == m1;
-    if (kind == EK_NONZERO) ok = ok && (w0 & 0xFFu) != '0';
-    if ((kind == EK_CLFNUMBER || kind == EK_CLFHEXNUMBER) && len == 1 && (w0 & 0xFFu) == '-') ok = true;
-    return ok;
-}
-
-// The first leaf of a one-format program on a line with class masks (the
-// kernels' LDS windows), speculatively: every element's end comes from the
-// QUOTE / WS mask planes alone, and the byte checks that do not move any end
-// (literals, the digits of a number token, a TIME_US value) are issued as
-// loads when the walk reaches them and compared one literal later (or at the
-// end), so that the chain of dependent LDS round trips is one mask read per
-// scanning token instead of two to four.  true implies that match_first_leaf
-// returns true with the same caps (each case below restates cand_first);
-// false decides nothing (the caller runs match_first_leaf, then the DFS).
-//   [^\s]*        the first WS byte (cand_first exactly, the !LA instance)
-//   number kinds  (det: the following literal does not start in the class)
-//                 the first byte of the following literal's first byte (' ' /
-//                 TAB -> the WS plane, '"' -> QUOTE, else a SWAR scan), all
-//                 bytes before it in the class checked: then the digit run
-//                 ends exactly there
-//   .* / .*?      the last occurrence of the following literal's first byte
-//                 <= the pruning bound / the first one (anchor_bwd / _fwd):
-//                 its check is the literal element's own (lit_last /
-//                 lit_first return that candidate exactly when the literal
-//                 matches there)
-//   TIME_US       p + 26, the 26 bytes checked
-// Other kinds (IP, NGINX lists, ...) -> false.
-template <typename LN, typename Caps>
-__host__ __device__ LP_INLINE bool match_spec_leaf(const Program& P, const LN& L, Caps& caps) {
-    static_assert(LN::has_masks, "the speculative first leaf reads the class masks");
-    int pos = 0;
-    bool ok = true;
-    // the pending literal: its two words at the position, literal bytes, mask
-    bool lpend = false;
-    uint32_t lw = 0, llit = 0, lkeep = 0;
-    // the pending number token: words at its start, length, kind
-    bool npend = false;
-    uint32_t nw0 = 0, nw1 = 0;
-    int nlen = 0, nkind = 0;
-    // the pending TIME_US value
-    bool tpend = false;
-    Bytes28 tb{};
-    const int ne = P.n_elems;
-    for (int i = 0; i < ne; ++i) {  // uniform loop (elements by scalar loads); a failed lane idles
-        const ElemV e = load_elem(P.elems + i);
-        if (!ok) continue;
-        if (e.kind == EK_LIT) {
-            // the previous literal's and number's words arrived with the mask
-            // reads since (LDS returns in order)
-            if (lpend) ok = ((lw ^ llit) & lkeep) == 0;
-            if (npend) ok = ok && num_bytes_ok(nkind, nw0, nw1, nlen);
-            npend = false;
-            const int len = e.lit_len;
-            if (pos + len > L.n) ok = false;
-            if (ok && len <= 4) {
-                lpend = true;
-                lw = load_u32_at(L, pos);
-                llit = e.lit4;
-                lkeep = len == 4 ? 0xFFFFFFFFu : ((1u << (8 * len)) - 1u);
-            } else {
-                lpend = false;
-                ok = ok && lit_at(P, L, pos, e);
-            }
-            pos += len;
-            continue;
-        }
-        int c = -1;
-        const uint32_t c0 = e.lit4 & 0xFFu;
-        switch (e.kind) {
-        case EK_NOSPACE: c = find_ws(L, pos, L.n); break;
-        case EK_NUMBER: case EK_CLFNUMBER: case EK_HEXNUMBER: case EK_CLFHEXNUMBER: case EK_NONZERO: {
-            if (e.last) c = L.n;
-            else if (!e.nlit || !e.det) break;  // c = -1: the literal may start with a digit
-            else if (c0 == ' ' || c0 == '\t') c = mfind_fwd(L, MC_WS, pos, L.n);
-            else c = anchor_fwd(L, e, pos, L.n);  // '"': the QUOTE plane; others a SWAR scan
-            if (c - pos > 8 || c <= pos || npend) { c = -1; break; }
-            npend = true;
-            nkind = e.kind;
-            nlen = c - pos;
-            nw0 = load_u32_at(L, pos);
-            nw1 = load_u32_at(L, pos + 4 <= L.n ? pos + 4 : L.n);
-            if (e.last) {  // no literal follows: check it now
-                if (!num_bytes_ok(nkind, nw0, nw1, nlen)) c = -1;
-                npend = false;
-            }
-            break;
-        }
-        case EK_TIME_US:
-            if (pos + 26 > L.n || tpend) break;
-            tpend = true;
-            tb = load28(L, pos);
-            c = pos + 26;
-            break;
-        case EK_ANY_GREEDY: {
-            if (e.last || !e.nlit) { c = L.n; break; }
-            const int hi = e.need > 1 ? kth_from_end(L, c0, e.need, pos) : L.n - 1;
-            c = hi < 0 ? -1 : anchor_bwd(L, e, hi, pos);
-            break;
-        }
-        case EK_ANY_LAZY: {
-            if (e.last) { c = L.n; break; }
-            if (!e.nlit) { c = pos; break; }
-            c = anchor_fwd(L, e, pos, L.n);
-            if (c >= L.n) c = -1;
-            break;
-        }
-        default: break;
-        }
-        if (c < 0) { ok = false; continue; }
-        if (e.cap >= 0) caps.set_u(e.cap, mkspan(pos, c));  // e.cap is uniform
-        pos = c;
-    }
-    if (lpend) ok = ok && ((lw ^ llit) & lkeep) == 0;
-    if (npend) ok = ok && num_bytes_ok(nkind, nw0, nw1, nlen);
-    if (tpend) ok = ok && time_us_bytes_ok(tb);
-    return ok && pos == L.n;
-}
-
 // The same first leaf for a lane of a several-format program: the lane's
 // own format's elements (LDS in the kernel, a lane-dependent index), caps
 // set by a select chain.  false also when an element needs the DFS's
@@ -1763,6 +1625,104 @@ __host__ __device__ LP_INLINE int strf_text(int table, int k, uint64_t& lo, uint
     return n;
 }
 
+// The element loop of parse_strf_time for a layout of fixed-width elements
+// (T.fixed_w: literals, fixed-width numbers, the 3-letter month / day names,
+// AM / PM, "+HHMM"; e.g. %d/%b/%Y %T) on a value of exactly that width and
+// all ASCII: the value's bytes are read once into registers (one aligned
+// word load per 4 bytes, all in flight together) and every element takes
+// its bytes at its fixed offset, instead of one dependent byte read per
+// byte.  Same fields and the same ST_BAD decisions as the general loop on
+// that subset (each case below restates its element); -1: not applicable,
+// the general loop decides.
+template <typename LN>
+__host__ __device__ LP_INLINE int strf_fixed(const TimeStage& T, const LN& L, int a, int b, RegArr<SF_NFIELDS>& fv,
+                                             uint32_t& has) {
+    const int W = T.fixed_w;
+    if (W <= 0 || b - a != W) return -1;
+    const uint32_t A = L.o + (uint32_t)a, W0 = A >> 2, sh = A & 3;
+    uint32_t w[9];
+    LP_UNROLL for (int j = 0; j < 9; ++j) w[j] = L.word_or0(W0 + (uint32_t)j);
+    RegArr<8> v;
+    uint32_t hi = 0;
+    LP_UNROLL for (int j = 0; j < 8; ++j) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        const uint32_t x = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
+#else
+        const uint32_t x = (uint32_t)((((uint64_t)w[j + 1] << 32) | w[j]) >> (8 * sh));
+#endif
+        v.v[j] = x;
+        const int r = W - 4 * j;  // the value's bytes in this word
+        hi |= r >= 4 ? (x & swar::HI) : r > 0 ? (x & swar::HI & ((1u << (8 * r)) - 1u)) : 0u;
+    }
+    if (hi) return -1;  // non-ASCII: the general loop (its text elements fall back)
+    auto byte = [&](int i) { return (v.get(i >> 2) >> (8 * (i & 3))) & 0xFFu; };  // i is uniform
+    auto low = [](uint32_t c) { return c | 0x20u; };
+    int off = 0;
+    for (int k = 0; k < T.n_ops; ++k) {
+        const uint32_t op = T.op[k];
+        const int kind = (int)(op & 0xFF), field = (int)((op >> 8) & 0xFF), width = (int)((op >> 16) & 0xFF);
+        const uint32_t arg = op >> 24;
+        uint32_t val = 0;
+        switch (kind) {
+        case SE_LIT: {  // CharLiteralPrinterParser, case-insensitive
+            const uint32_t c = byte(off);
+            if (!(c == arg || ((arg | 0x20u) - 'a' < 26u && low(c) == (arg | 0x20u)))) return ST_BAD;
+            ++off;
+            continue;
+        }
+        case SE_NUM: case SE_RED2: {  // fixed width, NOT_NEGATIVE; reduced: base 2000
+            for (int q = 0; q < width; ++q) {
+                const uint32_t d = byte(off + q) - '0';
+                if (d > 9) return ST_BAD;
+                val = val * 10 + d;
+            }
+            off += width;
+            if (kind == SE_RED2) val += 2000;
+            break;
+        }
+        case SE_TEXT: {  // every entry of these tables has the same length n: the first that matches
+            const int n = arg == ST_MON_SHORT || arg == ST_DOW_SHORT ? 3 : 2;
+            uint64_t tlo = 0;
+            for (int q = 0; q < n; ++q) tlo |= (uint64_t)low(byte(off + q)) << (8 * q);
+            const int nt = arg == ST_MON_SHORT ? 12 : arg == ST_DOW_SHORT ? 7 : 2;
+            const uint64_t m = (1ull << (8 * n)) - 1;
+            int best = -1;
+            for (int t = 0; t < nt; ++t) {
+                uint64_t elo;
+                uint32_t ehi;
+                strf_text((int)arg, t, elo, ehi);
+                if (best < 0 && ((tlo ^ elo) & m) == 0) best = t;
+            }
+            if (best < 0) return ST_BAD;
+            off += n;
+            val = arg == ST_AMPM_UP || arg == ST_AMPM_LOW ? (uint32_t)best : (uint32_t)best + 1;
+            break;
+        }
+        case SE_OFF: {  // appendOffset("+HHMM", "+0000")
+            const uint32_t sg = byte(off);
+            int of = 0;
+            if (!(sg == '+' && byte(off + 1) == '0' && byte(off + 2) == '0' && byte(off + 3) == '0' && byte(off + 4) == '0')) {
+                if (sg != '+' && sg != '-') return ST_BAD;
+                for (int q = 1; q <= 4; ++q) if (byte(off + q) - '0' > 9u) return ST_BAD;
+                const int oh = (int)(byte(off + 1) - '0') * 10 + (int)(byte(off + 2) - '0');
+                const int om = (int)(byte(off + 3) - '0') * 10 + (int)(byte(off + 4) - '0');
+                if (oh > 59 || om > 59) return ST_BAD;
+                of = (sg == '-' ? -1 : 1) * (oh * 3600 + om * 60);
+            }
+            off += 5;
+            val = (uint32_t)of;
+            break;
+        }
+        default: return -1;  // (not a fixed layout: fixed_w is 0 then)
+        }
+        // DateTimeParseContext.setParsedField: a field parsed twice must agree
+        if (((has >> field) & 1u) && fv.get(field) != val) return ST_BAD;
+        has |= 1u << field;
+        fv.set_u(field, val);
+    }
+    return ST_OK;
+}
+
 // StrfTimeStampDissector (hp/dissectors/StrfTimeStampDissector.java:44-70)
 // on the value [a, b): DateTimeFormatter.parse(text, ZonedDateTime::from)
 // with the elements of T (parseCaseInsensitive, strict), then JDK 8's
@@ -1788,7 +1748,14 @@ __host__ __device__ LP_INLINE int parse_strf_time(const TimeStage& T, const LN& 
     bool zone_utc = false;
     int pos = a;
     auto low = [](uint32_t c) { return c | 0x20u; };  // safe fold against lower-case ASCII letters
-    for (int k = 0; k < T.n_ops; ++k) {
+#if defined(LP_NO_STRF_FIXED)
+    const int fx = -1;
+#else
+    const int fx = strf_fixed(T, L, a, b, fv, has);
+#endif
+    if (fx == ST_BAD) return ST_BAD;
+    if (fx == ST_OK) pos = b;
+    for (int k = 0; k < T.n_ops && fx < 0; ++k) {
         const uint32_t op = T.op[k];
         const int kind = (int)(op & 0xFF), field = (int)((op >> 8) & 0xFF), width = (int)((op >> 16) & 0xFF);
         const uint32_t arg = op >> 24;
@@ -2453,12 +2420,7 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
         if (match_first_leaf_lane(P, elems + e0, ne, L, o.caps)) st = ST_OK;
         else o.caps.fill(0);  // the DFS sets its own
     } else {
-        // lines with class masks (the LDS windows; the !LA instance): the
-        // speculative first leaf, whose success is the first leaf's
-        if constexpr (LN::has_masks && !LA) {
-            if (P.spec_leaf && match_spec_leaf(P, L, o.caps)) st = ST_OK;
-        }
-        if (st != ST_OK && P.n_fmt == 1 && match_first_leaf<LA>(P, L, o.caps)) st = ST_OK;
+        if (P.n_fmt == 1 && match_first_leaf<LA>(P, L, o.caps)) st = ST_OK;
     }
     if (st != ST_OK) {
         const int e0 = P.fmt_elem0[fmt], ne = P.fmt_elem0[fmt + 1] - e0;

@@ -147,6 +147,7 @@ struct TimeStage {
     int32_t fmt;     // the LogFormat whose token this is
     int32_t kind;    // TK_*
     int32_t zone;    // TK_STRF: the pattern has %z or %Z (else the formatter's zone is UTC)
+    int32_t fixed_w; // TK_STRF: every op has a fixed width and they total fixed_w bytes (<= 32), else 0
     int32_t n_ops;
     uint32_t op[MAX_SF_OPS];
 };
@@ -262,10 +263,6 @@ struct Program {
     int32_t guard_setc[MAX_FMT];
     int32_t guard_setc_exp[MAX_FMT];
     int32_t n_secms, n_list, n_binip, n_pair;
-    // one LogFormat whose elements all have a speculative first-leaf rule
-    // (lp_device.h match_spec_leaf): the kernels try it before the exact
-    // first leaf
-    int32_t spec_leaf;
     SecmsStage secms[MAX_SECMS];
     ListStage list[MAX_LIST];
     BinipStage binip[MAX_BINIP];
@@ -351,7 +348,7 @@ struct Meta {
     unsigned long long fmt_state;    // routed LogFormat after the batch's last line
     unsigned long long uri_ovf_waves;// waves whose URI bytes exceed the URI kernel's compact buffer (direct path)
     unsigned long long ovf_lines;    // lines the chunked parse kernel queued for the direct kernel
-    unsigned long long pad[1];
+    unsigned long long deferred;     // chunks whose wave stopped waiting for its line number (second pass)
     unsigned long long shard_top[ARENA_SHARDS * 16];  // bump pointer of shard s at [16 s] (own 128-B line)
 };
 
@@ -399,9 +396,10 @@ struct Columns {
     // chunked parse (one-format programs: the line index built inside the
     // parse kernel): per byte chunk the decoupled look-back word, its status
     // counts, and the lines queued for the direct kernel
-    LP_G uint64_t* chunk_state;          // [n_chunks] aggregate / inclusive line counts, [n_chunks] the wave ticket
+    LP_G uint64_t* chunk_state;          // [n_chunks] aggregate / inclusive line counts
     LP_G uint32_t* chunk_counts;         // [n_chunks][WC_WORDS]
     LP_G uint32_t* ovf_lines;            // [cap_lines] line numbers
+    LP_G uint32_t* deferred_chunks;      // [n_chunks] chunks left to the deferred pass (Meta::deferred of them)
     int64_t cap_lines;                   // lines the columns hold
 };
 

@@ -213,18 +213,29 @@ __device__ __noinline__ void chunk_scanner(LP_G uint64_t* st, int64_t n_chunks) 
     }
 }
 
-// chunk c's first line number (the scanner's prefix minus the chunk's own count)
-__device__ __forceinline__ uint64_t chunk_base(LP_G uint64_t* st, int64_t c, uint64_t count) {
+// chunk c's first line number (the scanner's prefix minus the chunk's own
+// count), or ~0 when the scanner has not reached the chunk after
+// CHUNK_WAIT_MAX polls (~10 ms; in a normal launch it has long passed it):
+// the wave then leaves the chunk to the deferred pass instead of waiting on,
+// so that no wait depends on the order in which the dispatcher starts the
+// workgroups (a chunk whose wave was never started cannot hold the others).
+// (wait_max: LP_OPT_CHUNK_WAIT, tests; 0 = CHUNK_WAIT_MAX, < 0 = defer
+// without polling)
+constexpr uint32_t CHUNK_WAIT_MAX = 1u << 14;
+__device__ __forceinline__ uint64_t chunk_base(LP_G uint64_t* st, int64_t c, uint64_t count, int wait_max) {
+    if (wait_max < 0) return ~0ull;
     uint64_t v = 0;
+    const uint32_t lim = wait_max == 0 ? CHUNK_WAIT_MAX : (uint32_t)wait_max;
     if (threadIdx.x == 0) {
-        for (;;) {
+        for (uint32_t it = 0;; ++it) {
             v = __hip_atomic_load(&st[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (v & CS_INC) break;
+            if (it >= lim) { v = ~0ull; break; }
             __builtin_amdgcn_s_sleep(4);
         }
     }
     v = __shfl(v, 0);
-    return (v & CS_CNT) - count;
+    return v == ~0ull ? ~0ull : (v & CS_CNT) - count;
 }
 
 // Lines with rank >= 64 in a chunk (more than a wave's lanes): found again
@@ -260,41 +271,25 @@ __device__ __noinline__ void chunk_excess(const uint8_t* __restrict__ buf, uint6
     }
 }
 
-// Ticket 0: the scanner; ticket c + 1: chunk c of cb bytes, one wave.  The
-// role comes from an atomic ticket (chunk_state[n_chunks], zeroed with the
-// look-back words), not from blockIdx: a wave only ever waits for the scanner
-// and for chunks whose tickets were taken before its own, i.e. by waves that
-// are already resident, so every wait ends whatever order the dispatcher
-// starts the workgroups in (the decoupled look-back rule).
-// LDS: [elements][DFS stack][starts][window (win_cap)][mask planes (win_cap / 4)].
-// direct: every line goes to the direct kernel (LP_OPT_FORCE_DIRECT, tests).
+// Chunk c of cb bytes on one wave: stage its window, publish its line count,
+// phase 1 of its lines, then (its first line number known) the line index
+// entries and rows.  LDS: [elements][DFS stack][starts][window (win_cap)]
+// [mask planes (win_cap / 4)].  direct: every line goes to the direct kernel
+// (LP_OPT_FORCE_DIRECT, tests).
+// second: the deferred pass (the chunk's count is published and the scanner
+// has finished: the line number is read, not waited for).
 template <bool LA>
-__global__ __launch_bounds__(PW, 2) void k_parse_chunks(const uint8_t* __restrict__ buf, uint64_t nbytes,
-                                                     const DeviceArgs* __restrict__ args, uint32_t cb, uint32_t win_cap,
-                                                     uint32_t stk_words, int direct) {
-    const Program& P = args->prog;
-    const Columns& C = args->cols;
-    const int64_t n_chunks = (int64_t)((nbytes + cb - 1) / cb);
-    uint32_t ticket = 0;
-    if (threadIdx.x == 0)
-        ticket = (uint32_t)__hip_atomic_fetch_add(&C.chunk_state[n_chunks], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    ticket = (uint32_t)__builtin_amdgcn_readfirstlane((int)ticket);
-    if (ticket == 0) {
-        chunk_scanner(C.chunk_state, n_chunks);
-        return;
-    }
-    const int64_t c = (int64_t)ticket - 1;
+__device__ __forceinline__ void parse_chunk(const uint8_t* __restrict__ buf, uint64_t nbytes, const Program& P,
+                                            const Columns& C, const Elem* s_elems, uint8_t* smem, int64_t c,
+                                            int64_t n_chunks, uint32_t cb, uint32_t win_cap, uint32_t stk_words,
+                                            int direct, int wait_max, bool second) {
     const uint64_t c0 = (uint64_t)c * cb;
-    if (c0 >= nbytes) return;
     const uint64_t c1 = c0 + cb < nbytes ? c0 + cb : nbytes;
     const int lane = threadIdx.x;
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    Elem* s_elems = reinterpret_cast<Elem*>(smem);
     WaveStack stk{reinterpret_cast<uint32_t*>(smem + 16 * P.n_elems) + lane};
     uint32_t* starts = reinterpret_cast<uint32_t*>(smem + 16 * P.n_elems + 4 * stk_words);
     uint8_t* win = smem + 16 * P.n_elems + 4 * stk_words + 16 * ((4 * MAXS + 15) / 16);
     uint16_t* msk16 = reinterpret_cast<uint16_t*>(win + win_cap);
-    load_elems(P, s_elems);
     // window: 64 bytes before the chunk (its first start needs the byte
     // before it), the chunk, then the tail of its last line
     const uint64_t w0 = c0 >= 64 ? c0 - 64 : 0;
@@ -304,7 +299,7 @@ __global__ __launch_bounds__(PW, 2) void k_parse_chunks(const uint8_t* __restric
     if (first && lane == 0) starts[0] = 0;
     LP_PROF(0);
     const ChunkScan S = stage_chunk(buf, nbytes, w0, w1, t_lo, t_hi, first, win, msk16, starts);
-    chunk_publish(C.chunk_state, c, S.count);
+    if (!second) chunk_publish(C.chunk_state, c, S.count);
     LP_PROF(60);
     __syncthreads();  // starts[] written by every lane
     const uint32_t nl = S.count < (uint32_t)PW ? S.count : (uint32_t)PW;  // lines on this wave's lanes
@@ -335,7 +330,11 @@ __global__ __launch_bounds__(PW, 2) void k_parse_chunks(const uint8_t* __restric
     LP_PROF(1);
     if (lds_line) phase1<false, LA>(P, s_elems, L, o, stk, C, 0, S.clean, 0);
     LP_PROF(9);
-    const uint64_t base = chunk_base(C.chunk_state, c, S.count);
+    const uint64_t base = chunk_base(C.chunk_state, c, S.count, second ? (int)CHUNK_WAIT_MAX : wait_max);
+    if (base == ~0ull) {  // (never in a normal launch) the deferred pass redoes the chunk
+        if (lane == 0) C.deferred_chunks[atomicAdd(&C.meta->deferred, 1ull)] = (uint32_t)c;
+        return;
+    }
     LP_PROF(61);
     const int64_t cap = C.cap_lines;
     const int64_t li = (int64_t)base + lane;
@@ -364,6 +363,49 @@ __global__ __launch_bounds__(PW, 2) void k_parse_chunks(const uint8_t* __restric
     WC.bad = (uint32_t)__popcll(__ballot(row && o.status == ST_BAD));
     WC.store(C.chunk_counts, c);
     LP_PROF(62);
+}
+
+// Block 0: the scanner; block c + 1: chunk c.  Chunks whose wave stopped
+// waiting for the scanner (chunk_base) are redone by k_parse_deferred.
+template <bool LA>
+__global__ __launch_bounds__(PW, 2) void k_parse_chunks(const uint8_t* __restrict__ buf, uint64_t nbytes,
+                                                     const DeviceArgs* __restrict__ args, uint32_t cb, uint32_t win_cap,
+                                                     uint32_t stk_words, int direct, int wait_max) {
+    const Program& P = args->prog;
+    const Columns& C = args->cols;
+    const int64_t n_chunks = (int64_t)((nbytes + cb - 1) / cb);
+    if (blockIdx.x == 0) {
+        chunk_scanner(C.chunk_state, n_chunks);
+        return;
+    }
+    const int64_t c = (int64_t)blockIdx.x - 1;
+    if ((uint64_t)c * cb >= nbytes) return;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    Elem* s_elems = reinterpret_cast<Elem*>(smem);
+    load_elems(P, s_elems);
+    parse_chunk<LA>(buf, nbytes, P, C, s_elems, smem, c, n_chunks, cb, win_cap, stk_words, direct, wait_max, false);
+}
+
+// The deferred pass: the chunks in C.deferred_chunks (none in a normal
+// launch: its blocks return at once), after k_parse_chunks, whose scanner has
+// then finished, so their line numbers are read, not waited for.
+template <bool LA>
+__global__ __launch_bounds__(PW, 2) void k_parse_deferred(const uint8_t* __restrict__ buf, uint64_t nbytes,
+                                                       const DeviceArgs* __restrict__ args, uint32_t cb,
+                                                       uint32_t win_cap, uint32_t stk_words, int direct) {
+    const Program& P = args->prog;
+    const Columns& C = args->cols;
+    const uint64_t nd = C.meta->deferred;
+    if (blockIdx.x >= nd) return;
+    const int64_t n_chunks = (int64_t)((nbytes + cb - 1) / cb);
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    Elem* s_elems = reinterpret_cast<Elem*>(smem);
+    load_elems(P, s_elems);
+    for (uint64_t q = blockIdx.x; q < nd; q += gridDim.x) {
+        parse_chunk<LA>(buf, nbytes, P, C, s_elems, smem, (int64_t)C.deferred_chunks[q], n_chunks, cb, win_cap,
+                        stk_words, direct, 0, true);
+        __syncthreads();  // this chunk's LDS reads are done before the next one is staged
+    }
 }
 
 // The lines k_parse_chunks queued, 64 per wave on a persistent grid, read
@@ -624,12 +666,21 @@ int launch_parse(const ParseLaunch& a, const DeviceArgs* d_args, const Columns& 
         if (cp.n_chunks > 0) {
             // the instance per program shape: literal-aware first candidates
             // only for programs that have such an element
-            if (a.lit_aware)
-                hipLaunchKernelGGL(k_parse_chunks<true>, dim3((unsigned)cp.n_chunks + 1), dim3(PW), cp.lds, s, a.buf,
-                                   a.nbytes, d_args, cp.cb, cp.win_cap, cp.stk_words, a.force_direct ? 1 : 0);
-            else
-                hipLaunchKernelGGL(k_parse_chunks<false>, dim3((unsigned)cp.n_chunks + 1), dim3(PW), cp.lds, s, a.buf,
-                                   a.nbytes, d_args, cp.cb, cp.win_cap, cp.stk_words, a.force_direct ? 1 : 0);
+            // the chunks, then the deferred pass (its blocks return at once
+            // when no wave gave up waiting, the normal case)
+            const unsigned g0 = (unsigned)cp.n_chunks + 1, g1 = (unsigned)std::min<int64_t>(cp.n_chunks, 1024);
+            const int fd = a.force_direct ? 1 : 0;
+            if (a.lit_aware) {
+                hipLaunchKernelGGL(k_parse_chunks<true>, dim3(g0), dim3(PW), cp.lds, s, a.buf, a.nbytes, d_args, cp.cb,
+                                   cp.win_cap, cp.stk_words, fd, a.chunk_wait);
+                hipLaunchKernelGGL(k_parse_deferred<true>, dim3(g1), dim3(PW), cp.lds, s, a.buf, a.nbytes, d_args, cp.cb,
+                                   cp.win_cap, cp.stk_words, fd);
+            } else {
+                hipLaunchKernelGGL(k_parse_chunks<false>, dim3(g0), dim3(PW), cp.lds, s, a.buf, a.nbytes, d_args, cp.cb,
+                                   cp.win_cap, cp.stk_words, fd, a.chunk_wait);
+                hipLaunchKernelGGL(k_parse_deferred<false>, dim3(g1), dim3(PW), cp.lds, s, a.buf, a.nbytes, d_args, cp.cb,
+                                   cp.win_cap, cp.stk_words, fd);
+            }
             const size_t lds_ovf = 16 * (size_t)a.n_elems + 4 * (size_t)cp.stk_words;
             hipLaunchKernelGGL(k_parse_ovf_lines, dim3((unsigned)grid), dim3(PW), lds_ovf, s, a.buf, a.nbytes, d_args,
                                cp.stk_words);

@@ -262,6 +262,21 @@ static bool strf_compile(const std::string& f, TimeStage& T) {
         const bool num1 = k1 == SE_NUM || k1 == SE_NUMV || k1 == SE_PAD2 || k1 == SE_RED2;
         if ((k0 == SE_NUMV || k0 == SE_PAD2) && num1) return false;
     }
+    // a layout of fixed-width elements only (e.g. %d/%b/%Y %T): the device
+    // parses a value of exactly that width from registers (strf_fixed)
+    T.fixed_w = 0;
+    int w = 0;
+    for (int e = 0; e < T.n_ops && w >= 0; ++e) {
+        const int kind = T.op[e] & 0xFF, width = (T.op[e] >> 16) & 0xFF, arg = T.op[e] >> 24;
+        switch (kind) {
+        case SE_LIT: w += 1; break;
+        case SE_NUM: case SE_RED2: w += width; break;
+        case SE_TEXT: w = arg == ST_MON_SHORT || arg == ST_DOW_SHORT ? w + 3 : arg == ST_AMPM_UP || arg == ST_AMPM_LOW ? w + 2 : -1; break;
+        case SE_OFF: w += 5; break;
+        default: w = -1; break;
+        }
+    }
+    if (w > 0 && w <= 32) T.fixed_w = w;
     return true;
 }
 
@@ -1416,20 +1431,6 @@ void Plan::compile_program() {
         if (depth > P.max_stack) P.max_stack = depth;
     }
     if (P.max_stack > MAX_STACK) { device_ok_ = false; why_ = "too many backtracking elements"; return; }
-    // the speculative first leaf (match_spec_leaf) covers these element kinds
-    // (for the others it would only walk part of the line and give up)
-    P.spec_leaf = P.n_fmt == 1;
-    for (int i = 0; i < P.n_elems; ++i) {
-        const Elem& e = P.elems[i];
-        switch (e.kind) {
-        case EK_LIT: case EK_NOSPACE: case EK_TIME_US: break;
-        case EK_NUMBER: case EK_CLFNUMBER: case EK_HEXNUMBER: case EK_CLFHEXNUMBER: case EK_NONZERO:
-            if (!e.last && !(e.nlit && e.det)) P.spec_leaf = 0;
-            break;
-        case EK_ANY_GREEDY: case EK_ANY_LAZY: break;
-        default: P.spec_leaf = 0; break;
-        }
-    }
     int cur_fmt = 0;
     auto tk = [&](int oi) { return cur_fmt * 64 + oi; };  // (format, token slot) key of the stage maps
     // stages, walking the compiled tree from each captured token output.

@@ -87,38 +87,6 @@ int emu_parse_in(void* h, const char* buf, int64_t start, int len, char* out, in
 
 void emu_set_masks(int on) { g_masks_fwd(on); }
 
-// The speculative first leaf against the exact one on a line (staged as in
-// parse_impl's masked window): 0 the speculation declined, 1 both matched
-// with identical captures, 2 the speculation matched and the first leaf did
-// not (or their captures differ) -- never allowed; -1 not applicable.
-int emu_spec_check(void* h, const char* line, int len) {
-    Emu* e = (Emu*)h;
-    if (!e->plan.device_ok()) return -1;
-    const Program& P = e->plan.program();
-    if (!P.spec_leaf || lit_aware(P)) return -1;
-    const uint32_t off = (uint32_t)(len * 5 + 1) & 3u;
-    std::vector<uint8_t> buf(off, 0xFF);
-    buf.insert(buf.end(), line, line + len);
-    buf.push_back('\n');
-    const uint32_t hi = (off + (uint32_t)len + 4) & ~3u;
-    const uint32_t wn = (hi + 63) & ~63u;
-    std::vector<uint64_t> wbuf(wn / 8 + 8, ~0ull);
-    memcpy(wbuf.data(), buf.data(), std::min<size_t>(buf.size(), hi));
-    std::vector<uint64_t> masks(MC_N * (wn / 64));
-    build_masks((const uint8_t*)wbuf.data(), wn, masks.data());
-    MLine L{(const uint8_t*)wbuf.data(), off, len, masks.data()};
-    RegArr<MAX_TOK> c1, c2;
-    c1.fill(0);
-    c2.fill(0);
-    const bool s = match_spec_leaf(P, L, c1);
-    if (!s) return 0;
-    const bool f = match_first_leaf<false>(P, L, c2);
-    if (!f) return 2;
-    for (int k = 0; k < MAX_TOK; ++k)
-        if (c1.get(k) != c2.get(k)) return 2;
-    return 1;
-}
-
 // the planner's token table (plan.cpp) as canonical JSON; returns its length
 int emu_token_table(int nginx, char* out, int cap) {
     const std::string j = lp::token_table_json(nginx != 0);

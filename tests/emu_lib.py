@@ -53,8 +53,6 @@ def lib():
                                    ctypes.c_int]
         L.emu_describe.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]
         L.emu_set_masks.argtypes = [ctypes.c_int]
-        L.emu_spec_check.restype = ctypes.c_int
-        L.emu_spec_check.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]
         L.emu_casts.restype = ctypes.c_int
         L.emu_casts.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
         L.emu_possible_paths.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
@@ -115,10 +113,6 @@ class Emu:
             out.append((st, self.buf.value.decode("utf-8") if st in (0, 3) else None))
             start = end + 1
         return out
-
-    def spec_check(self, line):
-        """emu_spec_check: 0 declined, 1 matched like the first leaf, 2 mismatch, -1 n/a"""
-        return lib().emu_spec_check(self.h, line, len(line))
 
     def casts(self, target):
         c = lib().emu_casts(self.h, target.encode())

@@ -732,46 +732,3 @@ def test_type_remapping_same_type_planner(oracle, emu):
     assert o.parse(base % "/p?b=1")[0] == oracle.OK
     assert e.parse(base % "/p?b=1")[0] == 2
 
-
-SPEC_FORMATS = ["combined", "common", "combinedio", '%h %l %u %t "%r" %>s %b', '%h "%r" %b%>s "%{Referer}i"',
-                '%h %l %u %t "%r" %>s %b "%{Referer}i" "%{User-Agent}i" %D', '"%{User-Agent}i" %h %X %P',
-                '%{X-Forwarded-For}i %b', lpa.SYNTH_FORMATS[lpa.SYNTH_STRFTIME]]
-
-
-@pytest.mark.parametrize("fmt", SPEC_FORMATS)
-def test_spec_leaf_implies_first_leaf_emulated(oracle, emu, fmt):
-    """The speculative first leaf (lp_device.h match_spec_leaf: ends from the
-    mask planes, byte checks deferred) succeeds only where the exact first
-    leaf (match_first_leaf) succeeds, with the same captures -- on clean
-    synthetic lines, the demo log, mutated lines (truncations, missing /
-    extra quotes and spaces, TABs, bad numbers and dates) and byte-level
-    random edits."""
-    paths = oracle.possible_paths(fmt)
-    e = emu.Emu(fmt, paths)
-    if e.status != 0:
-        pytest.skip("not on device: " + e.err)
-    rng = random.Random(hash(fmt) & 0xFFFF)
-    base = lpa.synth_combined(11, 0, 1500).split(b"\n")[:-1]
-    if fmt == lpa.SYNTH_FORMATS[lpa.SYNTH_STRFTIME]:
-        base = lpa.synth(lpa.SYNTH_STRFTIME, 20261016, 0, 1500).split(b"\n")[:-1]
-    elif fmt in ("common", '%h %l %u %t "%r" %>s %b'):  # the combined lines without referer and agent
-        base = [l[:l.index(b' "', l.index(b'" ', l.index(b'] "') + 3) + 2)] for l in base]
-    elif fmt == "combinedio":
-        base = [l + b" %d %d" % (len(l), 3 * len(l)) for l in base]
-    lines = list(base)
-    for l in base:
-        lines.append(mutate(rng, l))
-        b = bytearray(l)
-        for _ in range(rng.randrange(1, 4)):  # random byte edits: quotes, spaces, digits, brackets
-            k = rng.randrange(len(b))
-            b[k] = rng.choice(b'" \t-0123456789[]/:aZ')
-        lines.append(bytes(b))
-        k = rng.randrange(len(l))
-        lines.append(l[:k] + rng.choice([b'"', b" ", b'" "', b"-", b"12"]) + l[k:])
-    res = [e.spec_check(l) for l in lines]
-    if res and res[0] == -1:
-        pytest.skip("no speculative leaf for this program")
-    bad = [l for l, r in zip(lines, res) if r == 2]
-    assert not bad, bad[:5]
-    if fmt in ("combined", "common", "combinedio", lpa.SYNTH_FORMATS[lpa.SYNTH_STRFTIME]):
-        assert res.count(1) > len(base) // 2, (res.count(0), res.count(1))

@@ -997,3 +997,20 @@ def test_chunk_geometry_gpu(oracle):
             if recs0[i] is not None:
                 assert r.record_json(i) == recs0[i], (cl, i)
         assert r.counters == r0.counters, cl
+    # every chunk whose line number is not known at its first poll goes to the
+    # deferred pass (LP_OPT_CHUNK_WAIT < 0): the same results; on a larger
+    # batch too (many chunks deferred, a deferred pass over many waves)
+    big = lpa.synth_combined(20261021, 0, 300000)
+    pb = lpa.HttpdLoglineParser("combined", fields)
+    rb0 = pb.parse_batch(big)
+    assert rb0.diag["deferred_chunks"] == 0
+    for d in (data, big):
+        ref = r0 if d is data else rb0
+        p = lpa.HttpdLoglineParser("combined", fields, options={lpa.OPT_CHUNK_WAIT: -1})
+        r = p.parse_batch(d)
+        assert r.diag["deferred_chunks"] > 0, r.diag
+        assert r.n_lines == ref.n_lines and (r.status == ref.status).all()
+        assert r.counters == ref.counters
+        for i in range(0, ref.n_lines, 1 if d is data else 37):
+            if int(ref.status[i]) == lpa.LINE_OK:
+                assert r.record_json(i) == ref.record_json(i), i

@@ -9,7 +9,7 @@ import sys
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ["LOGPARSER_AMD_LIB"] = os.path.join(ROOT, "logparser_amd", "_dbg", "liblogparser_amd_prof.so")
+os.environ["LOGPARSER_AMD_LIB"] = os.environ.get("LP_PROF_LIB") or os.path.join(ROOT, "logparser_amd", "_dbg", "liblogparser_amd_prof.so")
 sys.path.insert(0, ROOT)
 import torch  # noqa: E402,F401
 import logparser_amd as lpa  # noqa: E402
