@@ -2293,6 +2293,97 @@ __host__ __device__ LP_INLINE int uplist_items(const LN& L, int a, int b, F&& f)
     return k;
 }
 
+// The same split on a token of at most 32 bytes held in registers (TokReg:
+// its bytes aligned to its first byte, one word load per 4 bytes, and the
+// byte-class masks the split needs), so the scans are bit operations instead
+// of one dependent byte read per byte: the upstream lists of a line are split
+// twice (list_need, list_fill) and their items converted, and one lane's long
+// list held its whole wave.  Same steps as uplist_items, on the masks:
+// next_sep = the first separator bit in [q, e - 1), strip = the separator
+// bits at e - 2, trim = the first / last byte > ' '.
+struct TokReg {
+    RegArr<8> w;        // bytes 4j..4j+3 of the token in word j
+    uint32_t comma, colon, space, le;  // bit i: byte i is ',' / ':' / ' ' / <= ' '
+    __host__ __device__ LP_INLINE uint32_t byte(int i) const { return (w.get(i >> 2) >> (8 * (i & 3))) & 0xFFu; }
+};
+template <typename LN>
+__host__ __device__ LP_INLINE bool tok_load(const LN& L, int a, int b, TokReg& T) {
+    if (b - a > 32 || b < a) return false;
+    const uint32_t A = L.o + (uint32_t)a, W0 = A >> 2, sh = A & 3;
+    uint32_t x[9];
+    LP_UNROLL for (int j = 0; j < 9; ++j) x[j] = L.word_or0(W0 + (uint32_t)j);
+    T.comma = T.colon = T.space = T.le = 0;
+    LP_UNROLL for (int j = 0; j < 8; ++j) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        const uint32_t v = __builtin_amdgcn_alignbyte(x[j + 1], x[j], sh);
+#else
+        const uint32_t v = (uint32_t)((((uint64_t)x[j + 1] << 32) | x[j]) >> (8 * sh));
+#endif
+        T.w.v[j] = v;
+        T.comma |= bcls::nib(swar::eq(v, ',')) << (4 * j);
+        T.colon |= bcls::nib(swar::eq(v, ':')) << (4 * j);
+        T.space |= bcls::nib(swar::eq(v, ' ')) << (4 * j);
+        T.le |= bcls::nib(swar::lt(v, ' ' + 1)) << (4 * j);
+    }
+    return true;
+}
+__host__ __device__ LP_INLINE uint32_t bits_below(int e) { return e >= 32 ? ~0u : e <= 0 ? 0u : (1u << e) - 1u; }
+template <typename F>
+__host__ __device__ LP_INLINE int uplist_items_r(const TokReg& T, int a, int b, F&& f) {
+    const int n = b - a;
+    const uint32_t sp1 = T.space >> 1;  // bit q: byte q + 1 is ' '
+    const uint32_t sepc = T.comma & sp1 & bits_below(n - 1), sepk = T.colon & sp1 & bits_below(n - 1);
+    auto next_sep = [&](uint32_t sep, int q, int e) -> int {  // first separator q' >= q with q' + 1 < e, else e
+        const uint32_t m = sep & ~bits_below(q) & bits_below(e - 1);
+        return m ? __builtin_ctz(m) : e;
+    };
+    auto strip = [&](uint32_t sep, int s0, int e) {
+        while (e - s0 >= 2 && ((sep >> (e - 2)) & 1u)) e -= 2;
+        return e;
+    };
+    auto trim = [&](int& s0, int& e) {
+        const uint32_t m = ~T.le & ~bits_below(s0) & bits_below(e);
+        if (!m) { s0 = e; return; }
+        s0 = __builtin_ctz(m);
+        e = 32 - __builtin_clz(m);
+    };
+    int t = n;
+    if (next_sep(sepc, 0, n) < n) {
+        t = strip(sepc, 0, n);
+        if (t == 0) return 0;  // only empty servers
+    }
+    int k = 0;
+    for (int s0 = 0;;) {
+        const int e0 = next_sep(sepc, s0, t);
+        const int x0 = next_sep(sepk, s0, e0);
+        int va = s0, vb = x0, ra = s0, rb = x0;
+        if (x0 < e0) {
+            const int r1 = strip(sepk, x0 + 2, e0);
+            if (r1 > x0 + 2) {
+                ra = x0 + 2;
+                rb = next_sep(sepk, x0 + 2, e0);
+            } else if (x0 == s0) {
+                return -1;  // no parts at all
+            }
+        }
+        trim(va, vb);
+        trim(ra, rb);
+        f(k, a + va, a + vb, a + ra, a + rb);
+        ++k;
+        if (e0 >= t) break;
+        s0 = e0 + 2;
+    }
+    return k;
+}
+// secms_value on token bytes [s, e) (token-relative) in registers
+__host__ __device__ LP_INLINE int64_t secms_value_r(const TokReg& T, int s, int e) {
+    uint64_t sec = 0, frac = 0;
+    int q = s;
+    for (; q < e && T.byte(q) != '.'; ++q) sec = sec * 10u + (T.byte(q) - '0');
+    for (++q; q < e; ++q) frac = frac * 10u + (T.byte(q) - '0');
+    return (int64_t)(sec * 1000u + frac);
+}
+
 // ---- run histograms (lp_histograms, SURVEY.md §5 counters): one word per
 // OK line, reduced on demand: bits 0..15 token k present (not "-" and not
 // empty), bits 16..25 the response status code (100..599; 0: another value
@@ -2578,7 +2669,9 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
         const int k = P.secms[sm].tok;
         if ((o.tok_flags >> k) & 1u) continue;  // "-" never matches the token kinds; nothing to convert
         const uint32_t sp = o.caps.get(k);
-        const int64_t ms = secms_value(L, (int)(sp & 0xFFFFu), (int)(sp >> 16));
+        const int a = (int)(sp & 0xFFFFu), b = (int)(sp >> 16);
+        TokReg T;  // (a short value from registers: one word load per 4 bytes)
+        const int64_t ms = tok_load(L, a, b, T) ? secms_value_r(T, 0, b - a) : secms_value(L, a, b);
         o.smdone |= 1u << sm;
         o.sm_lo.set_u(sm, (uint32_t)(uint64_t)ms);
         o.sm_hi.set_u(sm, (uint32_t)((uint64_t)ms >> 32));
@@ -3515,7 +3608,10 @@ __host__ __device__ LP_INLINE uint32_t list_need(const Program& P, int fmt, cons
         const ListStage& S = P.list[j];
         if (S.fmt != fmt) continue;
         const uint32_t sp = C.tok_span[S.tok][li];
-        const int n = uplist_items(L, (int)(sp & 0xFFFFu), (int)(sp >> 16), [](int, int, int, int, int) {});
+        const int a = (int)(sp & 0xFFFFu), b = (int)(sp >> 16);
+        TokReg T;
+        const int n = tok_load(L, a, b, T) ? uplist_items_r(T, a, b, [](int, int, int, int, int) {})
+                                           : uplist_items(L, a, b, [](int, int, int, int, int) {});
         if (n > 0) need += 8 + (uint32_t)n * (S.secms ? LIST_ENT_MS : LIST_ENT);
     }
     return need;
@@ -3528,22 +3624,27 @@ __host__ __device__ LP_INLINE bool list_fill(const Program& P, int fmt, const LN
         const uint32_t sp = C.tok_span[S.tok][li];
         const int a = (int)(sp & 0xFFFFu), b = (int)(sp >> 16);
         const uint32_t ent = S.secms ? LIST_ENT_MS : LIST_ENT;
-        const int n = uplist_items(L, a, b, [](int, int, int, int, int) {});
+        TokReg T;
+        const bool reg = tok_load(L, a, b, T);  // (a short token: split from registers)
+        const int n = reg ? uplist_items_r(T, a, b, [](int, int, int, int, int) {})
+                          : uplist_items(L, a, b, [](int, int, int, int, int) {});
         if (n < 0) return false;
         const uint32_t off = (A.used + 7u) & ~7u;
         if (n > 0 && off + (uint32_t)n * ent > A.cap) return false;
         if (n > 0) A.used = off + (uint32_t)n * ent;
         LP_G uint8_t* tab = A.p + off;
-        uplist_items(L, a, b, [&](int k, int va, int vb, int ra, int rb) {
+        auto put = [&](int k, int va, int vb, int ra, int rb) {
             LP_G uint32_t* e32 = reinterpret_cast<LP_G uint32_t*>(tab + (uint32_t)k * ent);
             e32[0] = mkspan((uint32_t)va, (uint32_t)vb);
             e32[1] = mkspan((uint32_t)ra, (uint32_t)rb);
             if (S.secms) {
                 LP_G int64_t* e64 = reinterpret_cast<LP_G int64_t*>(tab + (uint32_t)k * ent + 8);
-                e64[0] = secms_value(L, va, vb);
-                e64[1] = secms_value(L, ra, rb);
+                e64[0] = reg ? secms_value_r(T, va - a, vb - a) : secms_value(L, va, vb);
+                e64[1] = reg ? secms_value_r(T, ra - a, rb - a) : secms_value(L, ra, rb);
             }
-        });
+        };
+        if (reg) uplist_items_r(T, a, b, put);
+        else uplist_items(L, a, b, put);
         C.l_count[j][li] = (uint32_t)n;
         C.l_tab[j][li] = n > 0 ? mkref(off, (uint32_t)n * ent, true) : 0ull;
     }
