@@ -97,11 +97,13 @@ __device__ __forceinline__ UriLane<NU> uri_lane(const Program& P, const Columns&
 // state: resume, fa, first_pct, rewr bit 1, the query table (slots, count,
 // s, lp).  L: the lane's line view (compact buffer with its UEV plane);
 // A.p / A.used: the line's region and where its table starts.
-template <typename CL>
+// SLOT: u differs between lanes (the k-th URI stage of each lane's own
+// LogFormat, -1 none): an event takes its owner line's table flag.
+template <bool SLOT, typename CL>
 __device__ __forceinline__ void uri_walk_coop(const Program& P, int u, const CL& L, bool part, int a, int b,
                                               uint32_t usep, const Arena& A, UriWalk& Wk) {
     const int lane = threadIdx.x;
-    const bool table = P.uri[u].want_query && P.uri[u].query_stage >= 0;  // uniform
+    const bool table = u >= 0 && P.uri[u].want_query && P.uri[u].query_stage >= 0;  // uniform unless SLOT
     const uint32_t cnt = part ? usep : 0u;
     uint32_t x = cnt;
     for (int d = 1; d < 64; d <<= 1) {
@@ -164,7 +166,8 @@ __device__ __forceinline__ void uri_walk_coop(const Program& P, int u, const CL&
         const int qfa = __shfl(q, mfa ? lsb64(mfa) : lane);
         const int fa_j = cfa >= 0 ? cfa : (mfa ? qfa : -1);  // the first '&' / '?' before me
         const bool pp = live && ((pct && !bad_pct) || c == '+');
-        const bool isB = table && live && aq && fa_j >= 0;   // a piece boundary after fa
+        const bool otable = SLOT ? __shfl((int)table, ow) != 0 : table;  // the owner line's stage has a table
+        const bool isB = otable && live && aq && fa_j >= 0;  // a piece boundary after fa
         const uint64_t BB = __ballot(isB), BPP = __ballot(pp);
         const uint64_t mB = BB & seg_lt, mP = BPP & seg_lt;
         const int qpb = __shfl(q, mB ? msb64(mB) : lane), qpp = __shfl(q, mP ? msb64(mP) : lane);
@@ -223,7 +226,10 @@ __device__ __forceinline__ void uri_walk_coop(const Program& P, int u, const CL&
 // Phase 2, the arena allocation and the query pieces of one wave; lu(u) is
 // the lane's line view of URI stage u (valid for every lane, empty stages
 // included: the query pass reads other lanes' views).
-template <int NU, int NQ, bool COOP, typename LU, typename LL>
+// SLOT (several LogFormats): pass k runs, on every lane, the k-th URI stage of
+// the lane's own LogFormat (URI stages by slot: the lanes of all formats
+// walk together instead of each format's stages under a partial mask).
+template <int NU, int NQ, bool COOP, bool SLOT, typename LU, typename LL>
 __device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, UriLane<NU>& U, LU&& lu, LL&& ll,
                                          bool active, int64_t li, int64_t wave, WaveCounts& WC) {
     const int lane = threadIdx.x;
@@ -292,8 +298,18 @@ __device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, Uri
     // phase 2 (lp_device.h phase2), stage by stage for the whole wave: the
     // compact path walks the stages' event bytes cooperatively
     const int nu = P.n_uri < NU ? P.n_uri : NU;
-    for (int u = 0; u < nu; ++u) {
-        const bool fmt_ok = live && o.status == ST_OK && P.uri[u].fmt == U.fmt;
+    for (int sl = 0; sl < nu; ++sl) {
+        int u = sl;  // this lane's stage of the pass
+        if constexpr (SLOT) {
+            u = -1;
+            for (int v = 0, c = 0; v < nu; ++v)
+                if (P.uri[v].fmt == U.fmt) {
+                    if (c == sl) u = v;
+                    ++c;
+                }
+            if (!__any(u >= 0)) break;  // no lane's LogFormat has a sl-th stage
+        }
+        const bool fmt_ok = live && o.status == ST_OK && u >= 0 && P.uri[u].fmt == U.fmt;
         const uint32_t sp = U.sp.get(u);
         const int a = (int)(sp & 0xFFFF), b = (int)(sp >> 16);
         const bool part = fmt_ok && b > a;
@@ -301,12 +317,12 @@ __device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, Uri
             C.u_flags[u][li] = 0;
             if (P.uri[u].query_stage >= 0) { C.q_count[P.uri[u].query_stage][li] = 0; C.q_params[P.uri[u].query_stage][li] = 0; }
         }
-        LP_PROF(10 + 2 * u);
+        LP_PROF(10 + 2 * sl);
         UriWalk Wk;
         if constexpr (COOP) {
-            LP_PROF(50 + 4 * u);
-            uri_walk_coop(P, u, lu(u), part, a, b, U.usep.get(u), A, Wk);
-            LP_PROF(51 + 4 * u);
+            LP_PROF(50 + 4 * sl);
+            uri_walk_coop<SLOT>(P, u, lu(u), part, a, b, U.usep.get(u), A, Wk);
+            LP_PROF(51 + 4 * sl);
         } else if (part) {
             uri_walk_fast(P, u, lu(u), a, b, U.usep.get(u), A, Wk);
         }
@@ -314,7 +330,7 @@ __device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, Uri
             const int st = uri_stage_rest(P, u, lu(u), a, b, U.usep.get(u), A, C, li, o, Wk);
             if (st != ST_OK) o.status = st;
         }
-        LP_PROF(11 + 2 * u);
+        LP_PROF(11 + 2 * sl);
     }
     if (live && lend && o.status == ST_OK) {
         bool filled = true;
@@ -460,7 +476,7 @@ __device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, Uri
 // The URI stages of one wave on the compact path: its lines' URI bytes
 // gathered into cbuf (CAP bytes) with their UEV plane, then uri_wave.
 // Returns false, having done nothing, when the wave's bytes exceed CAP.
-template <int NU, int NQ, uint32_t CAP>
+template <int NU, int NQ, bool SLOT, uint32_t CAP>
 __device__ __forceinline__ bool uri_compact(const uint8_t* __restrict__ buf, uint64_t nbytes, const Program& P,
                                             const Columns& C, int64_t wave, int64_t n_lines, uint32_t* cbuf,
                                             uint64_t* plane, WaveCounts& WC) {
@@ -581,13 +597,13 @@ __device__ __forceinline__ bool uri_compact(const uint8_t* __restrict__ buf, uin
         if (lin) f(LineT<lds_bytes>{(lds_bytes)cbuf, lorig, lend});
         else f(LineT<const LP_G uint8_t*>{lsp - lmis, lmis, lend});
     };
-    uri_wave<NU, NQ, true>(P, C, U, lu, ll, active, li, wave, WC);
+    uri_wave<NU, NQ, true, SLOT>(P, C, U, lu, ll, active, li, wave, WC);
     return true;
 }
 
 // 16 waves per CU: the LDS share allows them, and __launch_bounds__(64, 4)
 // (4 waves per SIMD) keeps the registers within 128
-template <int NU, int NQ>
+template <int NU, int NQ, bool SLOT>
 __global__ __launch_bounds__(PW, 4) void k_uri_lines(const uint8_t* __restrict__ buf, uint64_t nbytes,
                                                      const DeviceArgs* __restrict__ args) {
     const Program& P = args->prog;
@@ -598,7 +614,7 @@ __global__ __launch_bounds__(PW, 4) void k_uri_lines(const uint8_t* __restrict__
     __shared__ __attribute__((aligned(16))) uint32_t cbuf[URI_CAP / 4 + 16];
     __shared__ uint64_t plane[URI_CAP / 64 + 1];
     WaveCounts WC;
-    if (uri_compact<NU, NQ, URI_CAP>(buf, nbytes, P, C, wave, n_lines, cbuf, plane, WC)) WC.store(C, wave);
+    if (uri_compact<NU, NQ, SLOT, URI_CAP>(buf, nbytes, P, C, wave, n_lines, cbuf, plane, WC)) WC.store(C, wave);
     else if (threadIdx.x == 0) C.uri_ovf_list[atomicAdd(&C.meta->uri_ovf_waves, 1ull)] = (uint32_t)wave;
 }
 
@@ -607,7 +623,7 @@ __global__ __launch_bounds__(PW, 4) void k_uri_lines(const uint8_t* __restrict__
 // waves: their occupancy does not matter), and for a wave exceeding even
 // that, the lines' bytes read from HBM directly.
 constexpr uint32_t URI_CAP_OVF = 4 * URI_CAP;
-template <int NU, int NQ>
+template <int NU, int NQ, bool SLOT>
 __global__ __launch_bounds__(PW) void k_uri_overflow(const uint8_t* __restrict__ buf, uint64_t nbytes,
                                                      const DeviceArgs* __restrict__ args) {
     const Program& P = args->prog;
@@ -619,7 +635,7 @@ __global__ __launch_bounds__(PW) void k_uri_overflow(const uint8_t* __restrict__
     for (uint64_t q = blockIdx.x; q < nq; q += gridDim.x) {
         const int64_t wave = C.uri_ovf_list[q];
         WaveCounts WC;
-        if (!uri_compact<NU, NQ, URI_CAP_OVF>(buf, nbytes, P, C, wave, n_lines, cbuf, plane, WC)) {
+        if (!uri_compact<NU, NQ, SLOT, URI_CAP_OVF>(buf, nbytes, P, C, wave, n_lines, cbuf, plane, WC)) {
             const WaveLines W = wave_lines(C, wave, n_lines, nbytes);
             UriLane<NU> U = uri_lane<NU>(P, C, W.li, W.active);
             const LP_G uint8_t* ls = (const LP_G uint8_t*)(buf) + W.s;
@@ -627,7 +643,7 @@ __global__ __launch_bounds__(PW) void k_uri_overflow(const uint8_t* __restrict__
             const LineT<const LP_G uint8_t*> L{ls - mis, mis, crlf_len_hbm(buf, W)};
             auto lu = [&](int) { return L; };
             auto ll = [&](int lend, auto&& f) { f(LineT<const LP_G uint8_t*>{ls - mis, mis, lend}); };
-            uri_wave<NU, NQ, false>(P, C, U, lu, ll, W.active, W.li, wave, WC);
+            uri_wave<NU, NQ, false, SLOT>(P, C, U, lu, ll, W.active, W.li, wave, WC);
         }
         __syncthreads();
         WC.store(C, wave);
@@ -680,13 +696,19 @@ int launch_uri(const ParseLaunch& a, const DeviceArgs* d_args, hipStream_t s) {
     const int64_t grid = waves < 1024 ? waves : 1024;
     // most programs have at most two URI and two query stages (the request
     // URI and the referer): an instance keeping two of each
-    if (a.n_uri <= 2 && a.n_query <= 2) {
-        hipLaunchKernelGGL((k_uri_lines<2, 2>), dim3((unsigned)waves), dim3(PW), 0, s, a.buf, a.nbytes, d_args);
-        hipLaunchKernelGGL((k_uri_overflow<2, 2>), dim3((unsigned)grid), dim3(PW), 0, s, a.buf, a.nbytes, d_args);
-    } else {
-        hipLaunchKernelGGL((k_uri_lines<MAX_URI, MAX_QUERY>), dim3((unsigned)waves), dim3(PW), 0, s, a.buf,
+    // several LogFormats (not a.chunked): the instance running URI stages by slot
+    if (!a.chunked) {
+        hipLaunchKernelGGL((k_uri_lines<MAX_URI, MAX_QUERY, true>), dim3((unsigned)waves), dim3(PW), 0, s, a.buf,
                            a.nbytes, d_args);
-        hipLaunchKernelGGL((k_uri_overflow<MAX_URI, MAX_QUERY>), dim3((unsigned)grid), dim3(PW), 0, s, a.buf,
+        hipLaunchKernelGGL((k_uri_overflow<MAX_URI, MAX_QUERY, true>), dim3((unsigned)grid), dim3(PW), 0, s, a.buf,
+                           a.nbytes, d_args);
+    } else if (a.n_uri <= 2 && a.n_query <= 2) {
+        hipLaunchKernelGGL((k_uri_lines<2, 2, false>), dim3((unsigned)waves), dim3(PW), 0, s, a.buf, a.nbytes, d_args);
+        hipLaunchKernelGGL((k_uri_overflow<2, 2, false>), dim3((unsigned)grid), dim3(PW), 0, s, a.buf, a.nbytes, d_args);
+    } else {
+        hipLaunchKernelGGL((k_uri_lines<MAX_URI, MAX_QUERY, false>), dim3((unsigned)waves), dim3(PW), 0, s, a.buf,
+                           a.nbytes, d_args);
+        hipLaunchKernelGGL((k_uri_overflow<MAX_URI, MAX_QUERY, false>), dim3((unsigned)grid), dim3(PW), 0, s, a.buf,
                            a.nbytes, d_args);
     }
     if (a.derived) hipLaunchKernelGGL(k_derived_lines, dim3((unsigned)waves), dim3(PW), 0, s, a.buf, a.nbytes, d_args);
