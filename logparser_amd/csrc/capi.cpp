@@ -419,6 +419,15 @@ int finish(lp_handle* h) {
         if (hipStreamSynchronize(h->stream) != hipSuccess) return LP_E_DEVICE;
         lp::Meta m;
         if (hipMemcpy(&m, h->meta.p, sizeof m, hipMemcpyDeviceToHost) != hipSuccess) return LP_E_DEVICE;
+        if (m.err) {
+            // a kernel's self-check of its own bookkeeping failed (parse.hip check_fail)
+            fprintf(stderr,
+                    "logparser_amd: internal check failed %llu time(s); first: kind %llu values %llu %llu %llu %llu "
+                    "(batch %llu bytes, %llu lines)\n",
+                    m.err, m.err_info[0], m.err_info[1], m.err_info[2], m.err_info[3], m.err_info[4],
+                    (unsigned long long)h->nbytes, m.n_lines);
+            return LP_E_DEVICE;
+        }
         uint64_t top_max = 0;
         for (int s = 0; s < LP_ARENA_SHARDS; ++s) {
             h->shard_top[s] = m.shard_top[16 * s];

@@ -349,6 +349,11 @@ struct Meta {
     unsigned long long uri_ovf_waves;// waves whose URI bytes exceed the URI kernel's compact buffer (direct path)
     unsigned long long ovf_lines;    // lines the chunked parse kernel queued for the direct kernel
     unsigned long long deferred;     // chunks whose wave stopped waiting for its line number (second pass)
+    // self-checks of the chunked kernels' own bookkeeping (line index, queued
+    // lines): how many failed, and the first failure (kind, then four values;
+    // see check_fail in parse.hip).  Non-zero fails the batch (LP_E_DEVICE).
+    unsigned long long err;
+    unsigned long long err_info[15];  // (5 used; the rest keeps shard_top on its own 128-B lines)
     unsigned long long shard_top[ARENA_SHARDS * 16];  // bump pointer of shard s at [16 s] (own 128-B line)
 };
 

@@ -34,6 +34,32 @@ constexpr uint64_t CS_AGG = 1ull << 62, CS_INC = 1ull << 63, CS_CNT = CS_AGG - 1
 // the line index, written by the chunked parse kernel (read-only elsewhere)
 __device__ __forceinline__ LP_G uint64_t* line_off_w(const Columns& C) { return const_cast<LP_G uint64_t*>(C.line_off); }
 
+// Self-checks of the chunked kernels' own bookkeeping.  A failed check is
+// counted in Meta::err, the first failure's kind and values kept in
+// Meta::err_info, and the batch fails (LP_E_DEVICE, the values on stderr)
+// instead of a kernel reading a bad entry:
+//   CHK_OVF_LINE  a queued line k_parse_ovf_lines cannot take: q, li, line_off[li], line_off[li + 1]
+//   CHK_EXCESS    chunk_excess numbered a different count of lines than the staging pass: c, found, counted, base
+//   CHK_QUEUE     a queue append past its capacity: queue (0 lines, 1 chunks), index, entry, capacity
+constexpr uint64_t CHK_OVF_LINE = 1, CHK_EXCESS = 2, CHK_QUEUE = 3;
+__device__ __forceinline__ void check_fail(const Columns& C, uint64_t kind, uint64_t a, uint64_t b, uint64_t c,
+                                           uint64_t d) {
+    if (atomicAdd(&C.meta->err, 1ull) == 0) {
+        C.meta->err_info[0] = kind;
+        C.meta->err_info[1] = a;
+        C.meta->err_info[2] = b;
+        C.meta->err_info[3] = c;
+        C.meta->err_info[4] = d;
+    }
+}
+
+// Append line li to the queue of k_parse_ovf_lines (cap_lines + 1 entries).
+__device__ __forceinline__ void queue_line(const Columns& C, uint64_t li) {
+    const uint64_t q = atomicAdd(&C.meta->ovf_lines, 1ull);
+    if (q <= (uint64_t)C.cap_lines) C.ovf_lines[q] = (uint32_t)li;
+    else check_fail(C, CHK_QUEUE, 0, q, li, (uint64_t)C.cap_lines + 1);
+}
+
 // set bits of the wave mask b held by the lanes below this one
 __device__ __forceinline__ uint32_t below(uint64_t b) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
@@ -243,7 +269,7 @@ __device__ __forceinline__ uint64_t chunk_base(LP_G uint64_t* st, int64_t c, uin
 // queued for k_parse_ovf_lines.  Rare (very short lines).
 __device__ __noinline__ void chunk_excess(const uint8_t* __restrict__ buf, uint64_t nbytes, const Columns& C,
                                          const uint8_t* win, uint64_t w0, uint64_t w1, uint64_t t_lo, uint64_t t_hi,
-                                         uint32_t first, uint64_t base) {
+                                         uint32_t first, uint64_t base, int64_t chunk, uint32_t count) {
     const int lane = threadIdx.x;
     const int nv = (int)((w1 - w0 + 15) >> 4);
     uint32_t run = first;
@@ -266,9 +292,11 @@ __device__ __noinline__ void chunk_excess(const uint8_t* __restrict__ buf, uint6
             const uint64_t li = base + r;
             if ((int64_t)li >= C.cap_lines) continue;
             line_off_w(C)[li] = p + (uint64_t)__builtin_ctz(m) + 1;
-            C.ovf_lines[atomicAdd(&C.meta->ovf_lines, 1ull)] = (uint32_t)li;
+            queue_line(C, li);
         }
     }
+    // the staging pass counted (and published) `count` lines for this chunk
+    if (lane == 0 && run != count) check_fail(C, CHK_EXCESS, (uint64_t)chunk, run, count, base);
 }
 
 // Chunk c of cb bytes on one wave: stage its window, publish its line count,
@@ -332,7 +360,11 @@ __device__ __forceinline__ void parse_chunk(const uint8_t* __restrict__ buf, uin
     LP_PROF(9);
     const uint64_t base = chunk_base(C.chunk_state, c, S.count, second ? (int)CHUNK_WAIT_MAX : wait_max);
     if (base == ~0ull) {  // (never in a normal launch) the deferred pass redoes the chunk
-        if (lane == 0) C.deferred_chunks[atomicAdd(&C.meta->deferred, 1ull)] = (uint32_t)c;
+        if (lane == 0) {
+            const uint64_t q = atomicAdd(&C.meta->deferred, 1ull);
+            if (q < (uint64_t)n_chunks) C.deferred_chunks[q] = (uint32_t)c;
+            else check_fail(C, CHK_QUEUE, 1, q, (uint64_t)c, (uint64_t)n_chunks);
+        }
         return;
     }
     LP_PROF(61);
@@ -341,12 +373,12 @@ __device__ __forceinline__ void parse_chunk(const uint8_t* __restrict__ buf, uin
     const bool mine = has && li < cap;
     if (mine) line_off_w(C)[li] = w0 + s;
     const bool row = mine && lds_line;
-    if (mine && !lds_line) C.ovf_lines[atomicAdd(&C.meta->ovf_lines, 1ull)] = (uint32_t)li;
+    if (mine && !lds_line) queue_line(C, (uint64_t)li);
     if (row) {
         write_line(P, o, C, li);
         if (!P.has_phase2()) C.arena_base[li] = 0;  // no URI kernel: an empty region for every line
     }
-    if (S.count > (uint32_t)PW) chunk_excess(buf, nbytes, C, win, w0, w1, t_lo, t_hi, first, base);
+    if (S.count > (uint32_t)PW) chunk_excess(buf, nbytes, C, win, w0, w1, t_lo, t_hi, first, base, c, S.count);
     if (c == n_chunks - 1 && lane == 0) {
         // the batch's line count (Hadoop: a last line without terminator counts)
         const uint64_t total = base + S.count;
@@ -416,7 +448,8 @@ __global__ __launch_bounds__(PW) void k_parse_ovf_lines(const uint8_t* __restric
     const Program& P = args->prog;
     const Columns& C = args->cols;
     if (C.meta->cap_ovf) return;
-    const uint64_t nq = C.meta->ovf_lines;
+    const uint64_t nq = min((uint64_t)C.meta->ovf_lines, (uint64_t)C.cap_lines + 1);  // (queue_line checked the rest)
+    const uint64_t n_lines = C.meta->n_lines;
     if ((uint64_t)blockIdx.x * PW >= nq) return;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     Elem* s_elems = reinterpret_cast<Elem*>(smem);
@@ -426,12 +459,25 @@ __global__ __launch_bounds__(PW) void k_parse_ovf_lines(const uint8_t* __restric
     WaveCounts WC;
     for (uint64_t q0 = (uint64_t)blockIdx.x * PW; q0 < nq; q0 += (uint64_t)gridDim.x * PW) {
         const uint64_t q = q0 + threadIdx.x;
-        const bool active = q < nq;
+        bool active = q < nq;
         const int64_t li = active ? (int64_t)C.ovf_lines[q] : 0;
         uint64_t s = 0, e = 0;
         if (active) {
-            s = C.line_off[li];
-            e = C.line_off[li + 1] - 1;
+            // a queued line is one of the batch's lines, and its index entries
+            // bound a line of the buffer (the sentinel is nbytes or nbytes + 1)
+            uint64_t e1 = 0;
+            const bool in = (uint64_t)li < n_lines;
+            if (in) {
+                s = C.line_off[li];
+                e1 = C.line_off[li + 1];
+            }
+            if (!in || s >= e1 || e1 > nbytes + 1) {
+                check_fail(C, CHK_OVF_LINE, q, (uint64_t)li, s, e1);
+                active = false;
+                s = 0;
+            } else {
+                e = e1 - 1;
+            }
         }
         const uint64_t len = e - s;
         const int n0 = (int)(len > (uint64_t)0x7FFFFFFF ? 0x7FFFFFFF : len);
