@@ -326,12 +326,13 @@ int lp_casts(lp_handle *h, const char *target);
  * the GPU from the batch still in HBM (its input must still be valid):
  * valid / i64 / f64 / chars are then device buffers of the handle's device,
  * the call returns once they are filled.  Request cookies, raw-token query
- * strings, upstream list items (N.value / N.redirected, SECOND_MILLIS in ms and
- * us), BinaryIP and the first line / URI / query values are device columns.
- * LP_E_UNSUPPORTED names a path whose value only the host replay derives
- * (Set-Cookie values and attributes, a converter applied to an already
- * converted value) or a DOUBLE column of a string-valued path
- * (Double.parseDouble): build those from a host copy. */
+ * strings, Set-Cookie cookies and their value / expires / domain / comment /
+ * path attributes, upstream list items (N.value / N.redirected, SECOND_MILLIS
+ * in ms and us), BinaryIP and the first line / URI / query values are device
+ * columns.  LP_E_UNSUPPORTED names a path whose value only the host replay
+ * derives (a converter applied to an already converted value) or a DOUBLE
+ * column of a string-valued path (Double.parseDouble): build those from a
+ * host copy. */
 typedef struct lp_table_col {
     const char *path;
     int32_t kind;

@@ -113,6 +113,7 @@ struct lp_handle {
     uint64_t uri_ovf_waves = 0;    // ... whose URI stages ran in k_uri_overflow
     uint64_t deferred = 0;         // chunks of the last batch parsed by the deferred pass (normally 0)
     uint64_t shard_top[LP_ARENA_SHARDS]{};
+    lp::ParseLaunch last_launch{};  // the last enqueue's launch parameters (diagnostics)
     uint64_t arena_written = 0;
     uint64_t uri_src_bytes = 0;  // URI source bytes the URI kernels read (meta counters[5])
     int retries = 0;
@@ -269,6 +270,25 @@ void make_view(lp_handle* h, const lp_result& r, lp::ResultView& V) {
 // Enqueue the whole batch (index, routing, parse) with the current
 // capacities.  sync_count: count the lines first and size the buffers from
 // the exact count (the handle has no estimate yet).
+// One LogFormat of the Apache common / combined family: literals, [^\s]*,
+// the number kinds, .* / .*? and the %t time stamp, Apache time stages only,
+// no cookie / Set-Cookie guards, SECOND_MILLIS or BinaryIP stages (the parse
+// kernel's SIMPLE instance leaves the other kinds and stages out).
+bool simple_program(const lp::Program& P) {
+    if (P.n_fmt != 1 || P.n_secms || P.n_binip || P.guard_pct[0] || P.guard_setc[0]) return false;
+    for (int t = 0; t < P.n_time; ++t)
+        if (P.time[t].kind != lp::TK_APACHE) return false;
+    for (int i = 0; i < P.n_elems; ++i) {
+        switch (lp::load_elem(P.elems + i).kind) {
+        case lp::EK_LIT: case lp::EK_NOSPACE: case lp::EK_NUMBER: case lp::EK_CLFNUMBER: case lp::EK_HEXNUMBER:
+        case lp::EK_CLFHEXNUMBER: case lp::EK_NONZERO: case lp::EK_ANY_GREEDY: case lp::EK_ANY_LAZY:
+        case lp::EK_TIME_US: break;
+        default: return false;
+        }
+    }
+    return true;
+}
+
 int enqueue(lp_handle* h, bool sync_count) {
     hipStream_t s = h->stream;
     const uint64_t nbytes = h->nbytes;
@@ -375,6 +395,8 @@ int enqueue(lp_handle* h, bool sync_count) {
             if (e.nlit && !e.last && ((e.kind == lp::EK_NOSPACE && !e.det) || e.kind == lp::EK_NOSPACE3))
                 pl.lit_aware = true;
         }
+        pl.simple = simple_program(P);
+        h->last_launch = pl;
         if (chunked) {
             // look-back words (zeroed), per-chunk counts, the queued line list
             const lp::ChunkPlan cp = lp::chunk_plan(pl);
@@ -426,6 +448,14 @@ int finish(lp_handle* h) {
                     "(batch %llu bytes, %llu lines)\n",
                     m.err, m.err_info[0], m.err_info[1], m.err_info[2], m.err_info[3], m.err_info[4],
                     (unsigned long long)h->nbytes, m.n_lines);
+            if (m.err_info[0] == 2) {
+                const lp::ChunkPlan cp = lp::chunk_plan(h->last_launch);
+                fprintf(stderr,
+                        "  chunk_excess received w0 %llu w1 %llu t_lo %llu t_hi %llu first %llu win %llx nbytes %llu "
+                        "buf %llx (host: buf %llx cb %u win_cap %u)\n",
+                        m.err_info[5], m.err_info[6], m.err_info[7], m.err_info[8], m.err_info[9], m.err_info[10],
+                        m.err_info[11], m.err_info[12], (unsigned long long)(uintptr_t)h->d_buf, cp.cb, cp.win_cap);
+            }
             return LP_E_DEVICE;
         }
         uint64_t top_max = 0;

@@ -47,6 +47,7 @@ struct ParseLaunch {
     int32_t chunk_wait = 0;     // polls for a chunk's line number before deferring it (0: default, < 0: none)
     bool lit_aware = true;      // the program has a [^\s]* / "$request" element a shorter end of which can meet
                                 // its literal (the chunked kernel's instance with literal-aware first candidates)
+    bool simple = false;        // one format of the Apache common / combined family (capi simple_program)
 };
 // The chunked parse kernel's geometry: cb input bytes per chunk (one wave
 // each), an LDS window of win_cap bytes (the chunk, 64 bytes before it, the

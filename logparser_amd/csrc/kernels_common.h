@@ -68,6 +68,19 @@ __device__ __forceinline__ uint32_t term16(const uint8_t* p, uint64_t pos, uint6
     return term_bits(v, p, pos, nbytes);
 }
 
+// This lane's index in its wave (0..63; the parse / URI kernels run one wave
+// per workgroup, so it equals the workitem id x), from the hardware lane
+// count (v_mbcnt) instead of the workitem-ID register.  ROCm 7.2 (gfx950)
+// lost that register's value on some lanes across a non-inlined call made
+// under a partial EXEC mask (Program::has_phase2 inside `if (row)` in the
+// chunk kernel): the next callee (chunk_excess) then got wrong lane numbers,
+// scanned the wrong pieces of its window and numbered fewer lines than the
+// staging pass, leaving line_off entries unwritten (the round-5 aperture
+// fault in k_parse_ovf_lines).  mbcnt does not depend on it.
+__device__ __forceinline__ int lane_id() {
+    return (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+
 struct WaveStack {  // per-lane DFS stack, lane-interleaved (conflict-free)
     uint32_t* base;
     __device__ uint32_t& operator[](int k) const { return base[k * PW]; }
@@ -95,7 +108,7 @@ struct WaveLines {
 __device__ __forceinline__ WaveLines wave_lines(const Columns& C, int64_t wave, int64_t n_lines, uint64_t nbytes) {
     WaveLines W;
     W.li0 = wave * PW;
-    W.li = W.li0 + (int64_t)threadIdx.x;
+    W.li = W.li0 + (int64_t)lane_id();
     W.active = W.li < n_lines;
     W.lend = W.li0 + PW < n_lines ? W.li0 + PW : n_lines;
     W.s = W.e = 0;
@@ -124,7 +137,7 @@ __device__ __forceinline__ int crlf_len_hbm(const uint8_t* buf, const WaveLines&
 // guard scan of phase 1).
 __device__ __forceinline__ bool stage_window(const uint8_t* __restrict__ buf, uint64_t nbytes, uint64_t w0, uint64_t w1,
                                              uint8_t* win, uint16_t* msk16) {
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     const int nv = (int)((w1 - w0 + 15) >> 4);
     const int nv4 = (nv + 3) & ~3;  // whole 64-byte mask blocks
     uint32_t bad = 0;  // guard-failing bytes other than '\n' anywhere in the window
@@ -172,7 +185,7 @@ struct WaveCounts {
     uint32_t act = 0, ok = 0, bad = 0, written = 0;
     uint32_t gathered = 0;  // URI source bytes the URI kernel read (its roofline accounting)
     __device__ __forceinline__ void store(LP_G uint32_t* wave_counts, int64_t wave) const {
-        if (threadIdx.x == 0) {
+        if (lane_id() == 0) {
             uint4 c, d;
             c.x = act;
             c.y = ok;
@@ -217,7 +230,7 @@ __device__ __forceinline__ u32x4 load16(const uint8_t* __restrict__ buf, uint64_
 
 // LDS: [elements (n_elems x 16 B)][DFS stack][...]
 __device__ __forceinline__ void load_elems(const Program& P, Elem* s_elems) {
-    for (int k = threadIdx.x; k < P.n_elems; k += PW) s_elems[k] = P.elems[k];
+    for (int k = lane_id(); k < P.n_elems; k += PW) s_elems[k] = P.elems[k];
 }
 
 // k-th set bit (0-based) of m (k < popcount(m))
@@ -240,7 +253,7 @@ __device__ __forceinline__ int msb64(uint64_t m) { return 63 - (int)__builtin_cl
 // inclusive scan over the wave's lanes
 template <typename T>
 __device__ __forceinline__ T wave_incl_scan(T x) {
-    const int lane = threadIdx.x & 63;
+    const int lane = lane_id();
     for (int d = 1; d < 64; d <<= 1) {
         const T y = __shfl_up(x, d);
         if (lane >= d) x += y;

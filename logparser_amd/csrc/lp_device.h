@@ -18,7 +18,9 @@
 
 namespace lp {
 
-enum : int { ST_OK = 0, ST_BAD = 1, ST_FALLBACK = 2 };
+enum : int { ST_OK = 0, ST_BAD = 1, ST_FALLBACK = 2,
+             ST_REDO = 3 };  // (kernel-internal, never stored: the line needs the backtracking DFS, which
+                             // the one-pass chunk kernel leaves to the queued-line kernel; phase1<..., DFS = false>)
 
 // Profiling build only (-DLP_PROFILE): wave timestamps at fixed points,
 // stored per wave (the waves of blocks [PROF_W0, PROF_W0 + PROF_WAVES)),
@@ -898,7 +900,11 @@ __host__ __device__ LP_INLINE int uplist_ns_end(const Program& P, const ElemV& e
 // First candidate end of element e at position p (exact leftmost-first
 // order), -1 = none, -2 = FALLBACK.  '.' runs to the end of the line: the
 // fast-path guard already rejected every line terminator.
-template <bool LA = true, typename LN>
+// SIMPLE: an instance for programs whose elements are all literals,
+// [^\s]*, the number kinds, .* / .*? and TIME_US (the Apache common /
+// combined family): the other kinds' code is left out of it (-2, never
+// reached: the host picks the instance from the program).
+template <bool LA = true, bool SIMPLE = false, typename LN>
 __host__ __device__ LP_INLINE int cand_first(const Program& P, const ElemV& e, const LN& L, int p) {
     switch (e.kind) {
     case EK_NOSPACE: {
@@ -943,6 +949,7 @@ __host__ __device__ LP_INLINE int cand_first(const Program& P, const ElemV& e, c
     case EK_TIME_US: return time_us_ok(L, p) ? p + 26 : -1;
     case EK_CLF_IP:
     case EK_IP: {
+        if constexpr (SIMPLE) return -2;
         int q = ipv4_first(L, p);
         if (q >= 0) return q;
         // IPv6 alternative can only match empty at '-' (no hex/':'), so '-'
@@ -950,15 +957,17 @@ __host__ __device__ LP_INLINE int cand_first(const Program& P, const ElemV& e, c
         if (e.kind == EK_CLF_IP && p < L.n && L[p] == '-' && e.nlit && (e.lit4 & 0xFFu) != '-') return p + 1;
         return -2;  // resolved by match_line (ip_resolve)
     }
-    case EK_ANYCHAR: return p < L.n ? p + utf8_len(L[p]) : -1;  // '.': one char (the guard rejected line terminators)
-    case EK_DECIMAL: return decimal_at(L, p);
+    case EK_ANYCHAR: if constexpr (SIMPLE) return -2; else return p < L.n ? p + utf8_len(L[p]) : -1;  // '.': one char (the guard rejected line terminators)
+    case EK_DECIMAL: if constexpr (SIMPLE) return -2; else return decimal_at(L, p);
     case EK_MSEC: {
+        if constexpr (SIMPLE) return -2;
         const int d = digits_end(L, p);
         if (d == p || d + 4 > L.n || L[d] != '.' || !is_digit(L[d + 1]) || !is_digit(L[d + 2]) || !is_digit(L[d + 3]))
             return -1;
         return d - p > 18 ? -2 : d + 4;
     }
     case EK_NOSPACE3: {
+        if constexpr (SIMPLE) return -2;
         // only the maximal first and second runs can be followed by ' '; the
         // third run's ends come longest first (cand_next: one shorter), and
         // with a following literal the first that the literal follows is the
@@ -972,10 +981,11 @@ __host__ __device__ LP_INLINE int cand_first(const Program& P, const ElemV& e, c
         if (!LA || e.last || !e.nlit) return q3;
         return lit_last_call(P, L, e, q3, q2 + 1);
     }
-    case EK_UPLIST_DEC: return uplist_at(L, p, true);
-    case EK_UPLIST_NUM: return uplist_at(L, p, false);
-    case EK_UPLIST_NS: return uplist_ns_end(P, e, L, p);
+    case EK_UPLIST_DEC: if constexpr (SIMPLE) return -2; else return uplist_at(L, p, true);
+    case EK_UPLIST_NUM: if constexpr (SIMPLE) return -2; else return uplist_at(L, p, false);
+    case EK_UPLIST_NS: if constexpr (SIMPLE) return -2; else return uplist_ns_end(P, e, L, p);
     case EK_CACHE_STATUS: {
+        if constexpr (SIMPLE) return -2;
         // the alternatives in order; their first letters differ, so at most
         // one matches at p (the element has a single candidate)
         const char* alt[7] = {"MISS", "BYPASS", "EXPIRED", "STALE", "UPDATING", "REVALIDATED", "HIT"};
@@ -987,6 +997,7 @@ __host__ __device__ LP_INLINE int cand_first(const Program& P, const ElemV& e, c
         return -1;
     }
     case EK_TIME_ISO: {  // [1-9]ddd-[01]d-[0-3]dTdd:dd:dd[+|-]dd:dd
+        if constexpr (SIMPLE) return -2;
         if (p + 25 > L.n) return -1;
         const uint32_t c0 = L[p], s = L[p + 19];
         bool ok = c0 >= '1' && c0 <= '9' && L[p + 4] == '-' && L[p + 7] == '-' && L[p + 10] == 'T' &&
@@ -997,6 +1008,7 @@ __host__ __device__ LP_INLINE int cand_first(const Program& P, const ElemV& e, c
         return ok ? p + 25 : -1;
     }
     case EK_BINIP: {
+        if constexpr (SIMPLE) return -2;
         if (p + 16 > L.n) return -1;
         for (int k = p; k < p + 16; k += 4)
             if (L[k] != '\\' || L[k + 1] != 'x' || !is_hex(L[k + 2]) || !is_hex(L[k + 3])) return -1;
@@ -1087,8 +1099,8 @@ __host__ __device__ LP_INLINE bool ip_alt_end_possible(const Program& P, const L
     return ip_alt_ends(P, L, e, p, cur, ends);
 }
 
-// Next candidate after 'cur' (same priority order).
-template <typename LN>
+// Next candidate after 'cur' (same priority order).  SIMPLE: see cand_first.
+template <bool SIMPLE = false, typename LN>
 __host__ __device__ LP_INLINE int cand_next(const Program& P, const ElemV& e, const LN& L, int p, int cur) {
     switch (e.kind) {
     case EK_NOSPACE: return cur - 1 >= p ? cur - 1 : -1;
@@ -1107,6 +1119,7 @@ __host__ __device__ LP_INLINE int cand_next(const Program& P, const ElemV& e, co
     }
     case EK_TIME_US: return -1;
     case EK_CLF_IP: case EK_IP:
+        if constexpr (SIMPLE) return -2;
         if (L[p] == '-') return -1;
         // shorter IPv4 / IPv6 alternatives: exact only when none of them can
         // be followed by the rest of the format
@@ -1114,14 +1127,17 @@ __host__ __device__ LP_INLINE int cand_next(const Program& P, const ElemV& e, co
     case EK_ANYCHAR: case EK_MSEC: case EK_UPLIST_NS: case EK_BINIP: case EK_TIME_ISO: case EK_CACHE_STATUS:
         return -1;
     case EK_DECIMAL: {  // a shorter fraction
+        if constexpr (SIMPLE) return -2;
         const int d = digits_end(L, p);
         return cur - 1 >= d + 2 ? cur - 1 : -1;
     }
     case EK_NOSPACE3: {  // a shorter third run
+        if constexpr (SIMPLE) return -2;
         const int q2 = find_ws(L, find_ws(L, p, L.n) + 1, L.n);
         return cur - 1 >= q2 + 1 ? cur - 1 : -1;
     }
     case EK_UPLIST_DEC: case EK_UPLIST_NUM: {
+        if constexpr (SIMPLE) return -2;
         // Backtracking into X(?: *, *X(?: *: *X)?)* yields, in priority order,
         // every shorter end: fewer digits in an item's last run (followed by
         // a digit) and fewer items (item ends, descending).  Followed by the
@@ -1151,7 +1167,7 @@ struct NoCapsDfs {
 // (stack entries above the caller's; Nested = no further nesting).  Then the
 // token has no further candidate (-1); otherwise the line is FALLBACK, as
 // the priority order among the IPv6 branch's ends is not modelled.
-template <bool Nested = false, typename LN, typename EL, typename Caps, typename Stk>
+template <bool Nested = false, bool SIMPLE = false, typename LN, typename EL, typename Caps, typename Stk>
 __host__ __device__ LP_INLINE int match_line(const Program& P, const EL& elems, int ne, const LN& L, Caps& caps,
                                              Stk stk, int pos0 = 0, int sp0 = 0) {
     int i = 0, pos = pos0, sp = sp0;
@@ -1160,7 +1176,7 @@ __host__ __device__ LP_INLINE int match_line(const Program& P, const EL& elems, 
     // -1 when no alternative end of the IP element j at p (other than cur)
     // completes the match, -2 otherwise
     auto ip_resolve = [&](int j, int p, int cur, int spn) -> int {
-        if constexpr (Nested) {
+        if constexpr (Nested || SIMPLE) {
             return -2;
         } else {
             const ElemV e = load_elem(elems + j);
@@ -1171,7 +1187,7 @@ __host__ __device__ LP_INLINE int match_line(const Program& P, const EL& elems, 
             NoCapsDfs nc;
             bool hit = false;
             ends.each([&](int k) {
-                if (!hit && match_line<true>(P, elems + j + 1, ne - j - 1, L, nc, stk, p + k, spn) != ST_BAD) hit = true;
+                if (!hit && match_line<true, SIMPLE>(P, elems + j + 1, ne - j - 1, L, nc, stk, p + k, spn) != ST_BAD) hit = true;
             });
             return hit ? -2 : -1;
         }
@@ -1188,7 +1204,7 @@ __host__ __device__ LP_INLINE int match_line(const Program& P, const EL& elems, 
                 ok = lit_at(P, L, pos, e);
                 if (ok) { pos += e.lit_len; ++i; continue; }
             } else {
-                int c = cand_first(P, e, L, pos);
+                int c = cand_first<true, SIMPLE>(P, e, L, pos);
                 if (c == -2) c = ip_resolve(i, pos, -1, sp);
                 if (c == -2) return ST_FALLBACK;
                 ok = c >= 0;
@@ -1210,7 +1226,7 @@ __host__ __device__ LP_INLINE int match_line(const Program& P, const EL& elems, 
             uint32_t top = stk[sp - 1];
             int j = top & 63, p = (top >> 6) & 8191, cur = (top >> 19) & 8191;
             const ElemV e = load_elem(elems + j);
-            int c = cand_next(P, e, L, p, cur);
+            int c = cand_next<SIMPLE>(P, e, L, p, cur);
             if (c == -2) c = ip_resolve(j, p, cur, sp);
             if (c == -2) return ST_FALLBACK;
             if (c >= 0) {
@@ -1229,7 +1245,7 @@ __host__ __device__ LP_INLINE int match_line(const Program& P, const EL& elems, 
 // a one-format program, elements read from the Program with a uniform
 // index.  true: the line matches along that leaf (then it is the DFS's
 // result: its first complete match); false: decide with match_line.
-template <bool LA = true, typename LN, typename Caps>
+template <bool LA = true, bool SIMPLE = false, typename LN, typename Caps>
 __host__ __device__ LP_INLINE bool match_first_leaf(const Program& P, const LN& L, Caps& caps) {
     int pos = 0;
     bool ok = true;
@@ -1241,7 +1257,7 @@ __host__ __device__ LP_INLINE bool match_first_leaf(const Program& P, const LN& 
             ok = ok && lit_at(P, L, pos, e);
             pos += e.lit_len;
         } else if (ok) {
-            const int c = cand_first<LA>(P, e, L, pos);
+            const int c = cand_first<LA, SIMPLE>(P, e, L, pos);
             ok = c >= 0;
             if (e.cap >= 0) caps.set_u(e.cap, mkspan(pos, c));  // e.cap is uniform
             pos = ok ? c : pos;
@@ -1609,20 +1625,48 @@ __host__ __device__ LP_INLINE int32_t wf_week_based_year(int32_t y, int32_t days
 // Text of a strftime text element (default locale en_US, JDK 8 data),
 // lower-case, packed little-endian: months / days of week short and full,
 // "am" / "pm" (AMPM_OF_DAY SHORT is "AM" / "PM"; parsing is case-insensitive).
-__host__ __device__ LP_INLINE int strf_text(int table, int k, uint64_t& lo, uint32_t& hi) {
-    const char* const mon[12] = {"january", "february", "march", "april", "may", "june", "july", "august",
-                                 "september", "october", "november", "december"};
-    const char* const dow[7] = {"monday", "tuesday", "wednesday", "thursday", "friday", "saturday", "sunday"};
-    const char* const ap[2] = {"am", "pm"};
-    const char* t = table == ST_MON_SHORT || table == ST_MON_FULL ? mon[k] : table == ST_DOW_SHORT || table == ST_DOW_FULL ? dow[k] : ap[k];
+// The texts are compile-time constants (a constexpr table per kind, folded
+// into immediates where the entry is known): no per-call string walk -- the
+// earlier version packed each entry from its C string with one dependent
+// byte load per character, ~45 K cycles per wave for config 3's %b.
+constexpr uint64_t strf_pk8(const char* t) {
+    uint64_t v = 0;
+    for (int q = 0; q < 8 && t[q]; ++q) v |= (uint64_t)(uint8_t)t[q] << (8 * q);
+    return v;
+}
+constexpr int strf_len(const char* t) {
     int n = 0;
     while (t[n]) ++n;
-    if (table == ST_MON_SHORT || table == ST_DOW_SHORT) n = 3;  // "Jan" .. "Dec", "Mon" .. "Sun"
-    lo = 0;
-    hi = 0;
-    for (int q = 0; q < n && q < 8; ++q) lo |= (uint64_t)(uint8_t)t[q] << (8 * q);
-    if (n > 8) hi = (uint8_t)t[8];
     return n;
+}
+__host__ __device__ LP_INLINE int strf_text(int table, int k, uint64_t& lo, uint32_t& hi) {
+#define LP_STRF_MON "january", "february", "march", "april", "may", "june", "july", "august", "september", "october", \
+                    "november", "december"
+#define LP_STRF_DOW "monday", "tuesday", "wednesday", "thursday", "friday", "saturday", "sunday"
+    constexpr const char* mon[12] = {LP_STRF_MON};
+    constexpr const char* dow[7] = {LP_STRF_DOW};
+    constexpr uint64_t mon_lo[12] = {strf_pk8(mon[0]), strf_pk8(mon[1]), strf_pk8(mon[2]), strf_pk8(mon[3]),
+                                     strf_pk8(mon[4]), strf_pk8(mon[5]), strf_pk8(mon[6]), strf_pk8(mon[7]),
+                                     strf_pk8(mon[8]), strf_pk8(mon[9]), strf_pk8(mon[10]), strf_pk8(mon[11])};
+    constexpr uint8_t mon_n[12] = {(uint8_t)strf_len(mon[0]), (uint8_t)strf_len(mon[1]), (uint8_t)strf_len(mon[2]),
+                                   (uint8_t)strf_len(mon[3]), (uint8_t)strf_len(mon[4]), (uint8_t)strf_len(mon[5]),
+                                   (uint8_t)strf_len(mon[6]), (uint8_t)strf_len(mon[7]), (uint8_t)strf_len(mon[8]),
+                                   (uint8_t)strf_len(mon[9]), (uint8_t)strf_len(mon[10]), (uint8_t)strf_len(mon[11])};
+    constexpr uint64_t dow_lo[7] = {strf_pk8(dow[0]), strf_pk8(dow[1]), strf_pk8(dow[2]), strf_pk8(dow[3]),
+                                    strf_pk8(dow[4]), strf_pk8(dow[5]), strf_pk8(dow[6])};
+    constexpr uint8_t dow_n[7] = {(uint8_t)strf_len(dow[0]), (uint8_t)strf_len(dow[1]), (uint8_t)strf_len(dow[2]),
+                                  (uint8_t)strf_len(dow[3]), (uint8_t)strf_len(dow[4]), (uint8_t)strf_len(dow[5]),
+                                  (uint8_t)strf_len(dow[6])};
+#undef LP_STRF_MON
+#undef LP_STRF_DOW
+    hi = 0;
+    switch (table) {
+    case ST_MON_SHORT: lo = mon_lo[k] & 0xFFFFFFull; return 3;  // "Jan" .. "Dec"
+    case ST_MON_FULL: lo = mon_lo[k]; if (mon_n[k] > 8) hi = 'r'; return mon_n[k];  // "september"
+    case ST_DOW_SHORT: lo = dow_lo[k] & 0xFFFFFFull; return 3;  // "Mon" .. "Sun"
+    case ST_DOW_FULL: lo = dow_lo[k]; if (dow_n[k] > 8) hi = 'y'; return dow_n[k];  // "wednesday"
+    default: lo = k ? 0x6D70ull : 0x6D61ull; return 2;  // "pm" / "am"
+    }
 }
 
 // The element loop of parse_strf_time for a layout of fixed-width elements
@@ -1753,6 +1797,7 @@ __host__ __device__ LP_INLINE int parse_strf_time(const TimeStage& T, const LN& 
 #else
     const int fx = strf_fixed(T, L, a, b, fv, has);
 #endif
+    LP_PROF(14);
     if (fx == ST_BAD) return ST_BAD;
     if (fx == ST_OK) pos = b;
     for (int k = 0; k < T.n_ops && fx < 0; ++k) {
@@ -1982,8 +2027,10 @@ __host__ __device__ LP_INLINE int parse_strf_time(const TimeStage& T, const LN& 
         if (off > 64800 || off < -64800) return ST_BAD;
     }
     if (dy < 1 || dy > 9999) return ST_FALLBACK;
+    LP_PROF(15);
     int64_t es;
     time_fields(dy, dm, dd, th, tmi, tse, off, days, es, local, utc);
+    LP_PROF(16);
     epoch_ms = es * 1000 + (int64_t)(nos / 1000000);
     nanos = (uint32_t)nos;
     return ST_OK;
@@ -2475,7 +2522,16 @@ __host__ __device__ LP_INLINE uint32_t hist_word(const Program& P, const LN& L, 
 // a wave hold lines of different LogFormats, so the stages run by slot (the
 // k-th time / first-line stage of each lane's own format together) and the
 // first leaf is walked per lane.
-template <bool MULTI = false, bool LA = true, typename LN, typename EL, typename Stk, typename Cols>
+// SIMPLE: one LogFormat of the Apache common / combined family (cand_first)
+// with only Apache time stamps and no cookie / Set-Cookie guards, SECOND_MILLIS
+// or BinaryIP stages: the other stages' code is left out of the instance.
+// DFS = false: a line whose first leaf fails and that the prefilters do not
+// rule out gets ST_REDO instead of the backtracking DFS (the one-pass chunk
+// kernel queues it for k_parse_ovf_lines, which runs the whole phase 1:
+// neither the DFS's code nor its registers are in the hot kernel, and a
+// line that backtracks no longer holds the other lanes of its wave).
+template <bool MULTI = false, bool LA = true, bool SIMPLE = false, bool DFS = true, typename LN, typename EL, typename Stk,
+          typename Cols>
 __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, const LN& L, LineOut& o, Stk stk, Cols& C,
                                           int64_t li, bool clean = false, int fmt = 0) {
     o.status = ST_OK;
@@ -2511,12 +2567,13 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
         if (match_first_leaf_lane(P, elems + e0, ne, L, o.caps)) st = ST_OK;
         else o.caps.fill(0);  // the DFS sets its own
     } else {
-        if (P.n_fmt == 1 && match_first_leaf<LA>(P, L, o.caps)) st = ST_OK;
+        if (P.n_fmt == 1 && match_first_leaf<LA, SIMPLE>(P, L, o.caps)) st = ST_OK;
     }
     if (st != ST_OK) {
         const int e0 = P.fmt_elem0[fmt], ne = P.fmt_elem0[fmt + 1] - e0;
         if (P.n_fmt == 1 && (!fmt_tail_ok(P, elems + e0, ne, L) || count_quotes(L) < P.fmt_quotes[fmt])) st = ST_BAD;
-        else st = match_line(P, elems + e0, ne, L, o.caps, stk);
+        else if constexpr (DFS) st = match_line<false, SIMPLE>(P, elems + e0, ne, L, o.caps, stk);
+        else st = ST_REDO;
     }
     LP_PROF(4);
     if (st != ST_OK) { o.status = st; return; }
@@ -2549,7 +2606,7 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
     }
     // values the replay URL-decodes (request cookies, Utils.resilientUrlDecode):
     // ASCII, and every '%' followed by two hex digits, else FALLBACK
-    for (uint32_t gm = (uint32_t)P.guard_pct[fmt]; gm; gm &= gm - 1) {
+    if constexpr (!SIMPLE) for (uint32_t gm = (uint32_t)P.guard_pct[fmt]; gm; gm &= gm - 1) {
         const uint32_t sp = o.caps.get(__builtin_ctz(gm));
         const int a = sp & 0xFFFF, b = sp >> 16;
         if (find_fwd(L, a, b, [](uint32_t w) { return w & swar::HI; }) < b) { o.status = ST_FALLBACK; return; }
@@ -2558,7 +2615,7 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
             if (q + 2 >= b || !is_hex(L[q + 1]) || !is_hex(L[q + 2])) { o.status = ST_FALLBACK; return; }
     }
     // Set-Cookie lists the replay splits (the subset where HttpCookie.parse cannot throw)
-    for (uint32_t gm = (uint32_t)P.guard_setc[fmt]; gm; gm &= gm - 1) {
+    if constexpr (!SIMPLE) for (uint32_t gm = (uint32_t)P.guard_setc[fmt]; gm; gm &= gm - 1) {
         const int k = __builtin_ctz(gm);
         if (o.tok_flags & (1u << k)) continue;  // "-": null, nothing is dissected
         const uint32_t sp = o.caps.get(k);
@@ -2588,6 +2645,8 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
         if (T.kind == TK_APACHE) {
             if (!parse_apache_time(L, a, ep, lo, ut)) { o.status = ST_BAD; return; }
             ep *= 1000;
+        } else if constexpr (SIMPLE) {
+            continue;  // (not in this instance's programs)
         } else if (T.kind == TK_ISO) {
             if (!parse_iso_time(L, a, ep, lo, ut)) { o.status = ST_BAD; return; }
             ep *= 1000;
@@ -2664,7 +2723,7 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
         }
     }
     // ConvertSecondsWithMillisStringDissector on this format's SECOND_MILLIS tokens
-    for (int sm = 0; sm < P.n_secms; ++sm) {
+    if constexpr (!SIMPLE) for (int sm = 0; sm < P.n_secms; ++sm) {
         if (P.secms[sm].fmt != fmt) continue;
         const int k = P.secms[sm].tok;
         if ((o.tok_flags >> k) & 1u) continue;  // "-" never matches the token kinds; nothing to convert
@@ -2677,7 +2736,7 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
         o.sm_hi.set_u(sm, (uint32_t)((uint64_t)ms >> 32));
     }
     // BinaryIPDissector: "\xHH" x 4 (the element kind EK_BINIP proved the shape)
-    for (int bs = 0; bs < P.n_binip; ++bs) {
+    if constexpr (!SIMPLE) for (int bs = 0; bs < P.n_binip; ++bs) {
         if (P.binip[bs].fmt != fmt) continue;
         const uint32_t sp = o.caps.get(P.binip[bs].tok);
         const int a = (int)(sp & 0xFFFFu);
@@ -3661,8 +3720,49 @@ __host__ __device__ LP_INLINE bool list_fill(const Program& P, int fmt, const LN
 //     first '=' (not trimmed), value = the rest.
 // (Names are lower-cased and values resilientUrlDecode'd by the caller; the
 // phase-1 guard proved them ASCII with every '%' before two hex digits.)
+//   PK_SETC (ResponseSetCookieListDissector.dissect, :86-110): split(", ")
+//     (trailing empty parts dropped); a part whose lower-cased "expires=" starts
+//     within its last 15 chars ("expires=XXXXXXX".length()) waits and is joined
+//     with the next part by ", " (a later such part replaces it; one left at the
+//     end is dropped); each cookie string is named by HttpCookie.parse -- on the
+//     Netscape branch the phase-1 guard setcookie_ok proved: the first
+//     ';'-token's part before '=', trimmed -- and its value is the cookie string
+//     itself ([vs, ve) = the joined parts, contiguous in the line).
+template <typename LN, typename F>
+__host__ __device__ LP_INLINE int setc_pieces(const LN& L, int a, int b, F&& f) {
+    int t = b;
+    while (t - a >= 2 && L[t - 2] == ',' && L[t - 1] == ' ') t -= 2;
+    if (t == a) return 0;
+    int k = 0, prev = -1;
+    for (int s0 = a;;) {
+        int e0 = s0;
+        while (e0 < t && !(L[e0] == ',' && e0 + 1 < t && L[e0 + 1] == ' ')) ++e0;
+        int ei = -1;
+        for (int q = s0; q + 8 <= e0 && ei < 0; ++q)
+            if ((L[q] | 32u) == 'e' && ci_lit_at(L, q, e0, "expires=")) ei = q - s0;
+        if (ei >= 0 && (e0 - s0) - 15 < ei) {
+            prev = s0;
+        } else {
+            const int cs = prev >= 0 ? prev : s0;
+            prev = -1;
+            int q = cs;
+            while (q < e0 && L[q] == ';') ++q;
+            int eq = q;
+            while (eq < e0 && L[eq] != '=' && L[eq] != ';') ++eq;
+            int ns = q, ne = eq;
+            while (ns < ne && L[ns] <= ' ') ++ns;
+            while (ne > ns && L[ne - 1] <= ' ') --ne;
+            f(ns, ne, cs, e0, true);
+            ++k;
+        }
+        if (e0 >= t) break;
+        s0 = e0 + 2;
+    }
+    return k;
+}
 template <typename LN, typename F>
 __host__ __device__ LP_INLINE int pair_pieces(const LN& L, int a, int b, int kind, F&& f) {
+    if (kind == PK_SETC) return setc_pieces(L, a, b, f);
     const bool ck = kind == PK_COOKIE;
     auto is_sep = [&](int q, int e) { return ck ? sep_at(L, q, e, ';') : (q < e && L[q] == '&'); };
     const int sl = ck ? 2 : 1;
@@ -3719,7 +3819,7 @@ __host__ __device__ LP_INLINE uint32_t pair_need(const Program& P, int fmt, cons
         uint32_t bytes = 0;
         const int n = pair_pieces(L, (int)(sp & 0xFFFFu), (int)(sp >> 16), S.kind, [&](int ns, int ne, int vs, int ve, bool) {
             if (has_upper(L, ns, ne)) bytes += (uint32_t)(ne - ns) + 3;
-            if (has_escape(L, vs, ve)) bytes += (uint32_t)(ve - vs) + 3;
+            if (S.kind != PK_SETC && has_escape(L, vs, ve)) bytes += (uint32_t)(ve - vs) + 3;
         });
         if (n > 0) need += 8 + 16 * (uint32_t)n + bytes;
     }
@@ -3761,7 +3861,7 @@ __host__ __device__ LP_INLINE bool pair_fill(const Program& P, int fmt, const LN
                 A.used = (A.used + 3u) & ~3u;
             }
             if (eq) {
-                if (has_escape(L, vs, ve)) {
+                if (S.kind != PK_SETC && has_escape(L, vs, ve)) {  // (a cookie string is not decoded)
                     if (A.used + (uint32_t)(ve - vs) + 3 > A.cap) { ok = false; return; }
                     vref = url_decode_value(L, vs, ve, A);
                     A.used = (A.used + 3u) & ~3u;

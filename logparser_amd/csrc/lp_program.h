@@ -215,7 +215,10 @@ constexpr uint32_t LIST_ENT = 8, LIST_ENT_MS = 24;  // entry bytes without / wit
 //   PK_COOKIE: RequestCookieListDissector (dissectors/RequestCookieListDissector.java:79-110)
 //   PK_QUERY:  QueryStringFieldDissector on a raw token (%q, $args;
 //              dissectors/QueryStringFieldDissector.java:76-108)
-enum : int32_t { PK_COOKIE = 0, PK_QUERY = 1 };
+//   PK_SETC:   ResponseSetCookieListDissector (dissectors/ResponseSetCookieListDissector.java:86-110):
+//              the cookie strings of a Set-Cookie list, named by HttpCookie.parse
+//              (lower-cased), the value the cookie string itself (never decoded)
+enum : int32_t { PK_COOKIE = 0, PK_QUERY = 1, PK_SETC = 2 };
 struct PairStage {
     int32_t tok;
     int32_t fmt;
@@ -275,7 +278,7 @@ struct Program {
     alignas(4) uint8_t lit[MAX_LIT];
     // phase 2 runs (the URI kernel): URI stages or upstream list stages, whose
     // results live in the line's arena region
-    __host__ __device__ bool has_phase2() const { return n_uri > 0 || n_list > 0 || n_pair > 0; }
+    __host__ __device__ LP_INLINE bool has_phase2() const { return n_uri > 0 || n_list > 0 || n_pair > 0; }
     // literal pool byte i, read as a dword (scalar load for a uniform index)
     __host__ __device__ uint32_t lit_byte(int i) const {
         return (reinterpret_cast<const uint32_t*>(lit)[i >> 2] >> (8 * (i & 3))) & 0xFFu;

@@ -28,7 +28,12 @@ enum : int32_t {
     TC_LIST_MS,    // a = SECOND_MILLIS list stage, b = item, c bit 0: redirected, bit 1: MICROSECONDS
     TC_BINIP,      // a = BinaryIP stage: its bytes as signed decimals joined by '.'
     TC_PAIR,       // a = pair stage (cookie / raw query), b / c = offset / length of the name in TableArgs::names (the last occurrence)
+    TC_SETC,       // a = Set-Cookie pair stage | SC_* field << 8, b / c = the cookie name in TableArgs::names:
+                   // ResponseSetCookieDissector on the name's last cookie string
 };
+// ResponseSetCookieDissector outputs (dissectors/ResponseSetCookieDissector.java:49-58)
+enum : int32_t { SC_VALUE, SC_EXPIRES_S /* STRING:expires, seconds */, SC_EXPIRES_MS /* TIME.EPOCH:expires */,
+                 SC_DOMAIN, SC_COMMENT, SC_PATH };
 enum : int32_t { TF_EPOCH, TF_DAY, TF_MONTHNAME, TF_MONTH, TF_WEEK, TF_WEEKYEAR, TF_YEAR, TF_HOUR, TF_MINUTE,
                  TF_SECOND, TF_MILLI, TF_MICRO, TF_NANO, TF_DATE, TF_TIME };
 enum : int32_t { UP_QUERY, UP_PATH, UP_REF, UP_PROTOCOL, UP_HOST, UP_PORT };

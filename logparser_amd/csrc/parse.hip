@@ -88,7 +88,7 @@ struct ChunkScan {
 __device__ __forceinline__ ChunkScan stage_chunk(const uint8_t* __restrict__ buf, uint64_t nbytes, uint64_t w0,
                                                  uint64_t w1, uint64_t t_lo, uint64_t t_hi, uint32_t first,
                                                  uint8_t* win, uint16_t* msk16, uint32_t* starts) {
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     const int nv = (int)((w1 - w0 + 15) >> 4);
     const int nv4 = (nv + 3) & ~3;  // whole 64-byte mask blocks
     if ((nv & (PW - 1)) == 0 && w0 + 16ull * nv <= (nbytes & ~15ull)) {
@@ -193,12 +193,12 @@ __device__ __forceinline__ ChunkScan stage_chunk(const uint8_t* __restrict__ buf
 // ends.  Each state word is one 8-byte value (status bits and count), stored
 // and polled with agent-scope (sc1) accesses: no payload travels beside it.
 __device__ __forceinline__ void chunk_publish(LP_G uint64_t* st, int64_t c, uint64_t count) {
-    if (threadIdx.x == 0) __hip_atomic_store(&st[c], CS_AGG | count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane_id() == 0) __hip_atomic_store(&st[c], CS_AGG | count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __device__ __noinline__ void chunk_scanner(LP_G uint64_t* st, int64_t n_chunks) {
     constexpr int PER = 8;  // state words per lane per round
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     uint64_t run = 0;
     int64_t c = 0;
     while (c < n_chunks) {
@@ -252,7 +252,7 @@ __device__ __forceinline__ uint64_t chunk_base(LP_G uint64_t* st, int64_t c, uin
     if (wait_max < 0) return ~0ull;
     uint64_t v = 0;
     const uint32_t lim = wait_max == 0 ? CHUNK_WAIT_MAX : (uint32_t)wait_max;
-    if (threadIdx.x == 0) {
+    if (lane_id() == 0) {
         for (uint32_t it = 0;; ++it) {
             v = __hip_atomic_load(&st[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if (v & CS_INC) break;
@@ -270,7 +270,7 @@ __device__ __forceinline__ uint64_t chunk_base(LP_G uint64_t* st, int64_t c, uin
 __device__ __noinline__ void chunk_excess(const uint8_t* __restrict__ buf, uint64_t nbytes, const Columns& C,
                                          const uint8_t* win, uint64_t w0, uint64_t w1, uint64_t t_lo, uint64_t t_hi,
                                          uint32_t first, uint64_t base, int64_t chunk, uint32_t count) {
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     const int nv = (int)((w1 - w0 + 15) >> 4);
     uint32_t run = first;
     for (int k0 = 0; k0 < nv; k0 += PW) {
@@ -296,7 +296,19 @@ __device__ __noinline__ void chunk_excess(const uint8_t* __restrict__ buf, uint6
         }
     }
     // the staging pass counted (and published) `count` lines for this chunk
-    if (lane == 0 && run != count) check_fail(C, CHK_EXCESS, (uint64_t)chunk, run, count, base);
+    if (lane == 0 && run != count) {
+        check_fail(C, CHK_EXCESS, (uint64_t)chunk, run, count, base);
+        if (C.meta->err_info[1] == (uint64_t)chunk) {  // (this chunk's record: the arguments it received)
+            C.meta->err_info[5] = w0;
+            C.meta->err_info[6] = w1;
+            C.meta->err_info[7] = t_lo;
+            C.meta->err_info[8] = t_hi;
+            C.meta->err_info[9] = first;
+            C.meta->err_info[10] = (uint64_t)(uintptr_t)win;
+            C.meta->err_info[11] = nbytes;
+            C.meta->err_info[12] = (uint64_t)(uintptr_t)buf;
+        }
+    }
 }
 
 // Chunk c of cb bytes on one wave: stage its window, publish its line count,
@@ -306,14 +318,14 @@ __device__ __noinline__ void chunk_excess(const uint8_t* __restrict__ buf, uint6
 // (LP_OPT_FORCE_DIRECT, tests).
 // second: the deferred pass (the chunk's count is published and the scanner
 // has finished: the line number is read, not waited for).
-template <bool LA>
+template <bool LA, bool SIMPLE>
 __device__ __forceinline__ void parse_chunk(const uint8_t* __restrict__ buf, uint64_t nbytes, const Program& P,
                                             const Columns& C, const Elem* s_elems, uint8_t* smem, int64_t c,
                                             int64_t n_chunks, uint32_t cb, uint32_t win_cap, uint32_t stk_words,
                                             int direct, int wait_max, bool second) {
     const uint64_t c0 = (uint64_t)c * cb;
     const uint64_t c1 = c0 + cb < nbytes ? c0 + cb : nbytes;
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     WaveStack stk{reinterpret_cast<uint32_t*>(smem + 16 * P.n_elems) + lane};
     uint32_t* starts = reinterpret_cast<uint32_t*>(smem + 16 * P.n_elems + 4 * stk_words);
     uint8_t* win = smem + 16 * P.n_elems + 4 * stk_words + 16 * ((4 * MAXS + 15) / 16);
@@ -356,7 +368,11 @@ __device__ __forceinline__ void parse_chunk(const uint8_t* __restrict__ buf, uin
     o.status = ST_OK;
     o.tdone = o.smdone = o.bipdone = 0;
     LP_PROF(1);
-    if (lds_line) phase1<false, LA>(P, s_elems, L, o, stk, C, 0, S.clean, 0);
+#if defined(LP_DFS_IN_CHUNKS)  // (experiment builds: the backtracking DFS inside the chunk kernel, as before round 6)
+    if (lds_line) phase1<false, LA, SIMPLE, true>(P, s_elems, L, o, stk, C, 0, S.clean, 0);
+#else
+    if (lds_line) phase1<false, LA, SIMPLE, false>(P, s_elems, L, o, stk, C, 0, S.clean, 0);  // (no DFS: ST_REDO)
+#endif
     LP_PROF(9);
     const uint64_t base = chunk_base(C.chunk_state, c, S.count, second ? (int)CHUNK_WAIT_MAX : wait_max);
     if (base == ~0ull) {  // (never in a normal launch) the deferred pass redoes the chunk
@@ -372,13 +388,17 @@ __device__ __forceinline__ void parse_chunk(const uint8_t* __restrict__ buf, uin
     const int64_t li = (int64_t)base + lane;
     const bool mine = has && li < cap;
     if (mine) line_off_w(C)[li] = w0 + s;
-    const bool row = mine && lds_line;
-    if (mine && !lds_line) queue_line(C, (uint64_t)li);
+    // a line the window does not hold, or that needs the backtracking DFS,
+    // is queued for k_parse_ovf_lines (the whole phase 1, from HBM)
+    const bool redo = lds_line && o.status == ST_REDO;
+    const bool row = mine && lds_line && !redo;
+    if (mine && (!lds_line || redo)) queue_line(C, (uint64_t)li);
     if (row) {
         write_line(P, o, C, li);
         if (!P.has_phase2()) C.arena_base[li] = 0;  // no URI kernel: an empty region for every line
     }
-    if (S.count > (uint32_t)PW) chunk_excess(buf, nbytes, C, win, w0, w1, t_lo, t_hi, first, base, c, S.count);
+    if (S.count > (uint32_t)PW)
+        chunk_excess(buf, nbytes, C, win, w0, w1, t_lo, t_hi, first, base, c, S.count);
     if (c == n_chunks - 1 && lane == 0) {
         // the batch's line count (Hadoop: a last line without terminator counts)
         const uint64_t total = base + S.count;
@@ -399,7 +419,9 @@ __device__ __forceinline__ void parse_chunk(const uint8_t* __restrict__ buf, uin
 
 // Block 0: the scanner; block c + 1: chunk c.  Chunks whose wave stopped
 // waiting for the scanner (chunk_base) are redone by k_parse_deferred.
-template <bool LA>
+// SIMPLE: the instance for Apache common / combined family programs
+// (phase1; the host's simple_program picks it).
+template <bool LA, bool SIMPLE>
 __global__ __launch_bounds__(PW, 2) void k_parse_chunks(const uint8_t* __restrict__ buf, uint64_t nbytes,
                                                      const DeviceArgs* __restrict__ args, uint32_t cb, uint32_t win_cap,
                                                      uint32_t stk_words, int direct, int wait_max) {
@@ -415,13 +437,13 @@ __global__ __launch_bounds__(PW, 2) void k_parse_chunks(const uint8_t* __restric
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     Elem* s_elems = reinterpret_cast<Elem*>(smem);
     load_elems(P, s_elems);
-    parse_chunk<LA>(buf, nbytes, P, C, s_elems, smem, c, n_chunks, cb, win_cap, stk_words, direct, wait_max, false);
+    parse_chunk<LA, SIMPLE>(buf, nbytes, P, C, s_elems, smem, c, n_chunks, cb, win_cap, stk_words, direct, wait_max, false);
 }
 
 // The deferred pass: the chunks in C.deferred_chunks (none in a normal
 // launch: its blocks return at once), after k_parse_chunks, whose scanner has
 // then finished, so their line numbers are read, not waited for.
-template <bool LA>
+template <bool LA, bool SIMPLE>
 __global__ __launch_bounds__(PW, 2) void k_parse_deferred(const uint8_t* __restrict__ buf, uint64_t nbytes,
                                                        const DeviceArgs* __restrict__ args, uint32_t cb,
                                                        uint32_t win_cap, uint32_t stk_words, int direct) {
@@ -434,8 +456,8 @@ __global__ __launch_bounds__(PW, 2) void k_parse_deferred(const uint8_t* __restr
     Elem* s_elems = reinterpret_cast<Elem*>(smem);
     load_elems(P, s_elems);
     for (uint64_t q = blockIdx.x; q < nd; q += gridDim.x) {
-        parse_chunk<LA>(buf, nbytes, P, C, s_elems, smem, (int64_t)C.deferred_chunks[q], n_chunks, cb, win_cap,
-                        stk_words, direct, 0, true);
+        parse_chunk<LA, SIMPLE>(buf, nbytes, P, C, s_elems, smem, (int64_t)C.deferred_chunks[q], n_chunks, cb,
+                                win_cap, stk_words, direct, 0, true);
         __syncthreads();  // this chunk's LDS reads are done before the next one is staged
     }
 }
@@ -453,12 +475,12 @@ __global__ __launch_bounds__(PW) void k_parse_ovf_lines(const uint8_t* __restric
     if ((uint64_t)blockIdx.x * PW >= nq) return;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     Elem* s_elems = reinterpret_cast<Elem*>(smem);
-    WaveStack stk{reinterpret_cast<uint32_t*>(smem + 16 * P.n_elems) + threadIdx.x};
+    WaveStack stk{reinterpret_cast<uint32_t*>(smem + 16 * P.n_elems) + lane_id()};
     load_elems(P, s_elems);
     __syncthreads();
     WaveCounts WC;
     for (uint64_t q0 = (uint64_t)blockIdx.x * PW; q0 < nq; q0 += (uint64_t)gridDim.x * PW) {
-        const uint64_t q = q0 + threadIdx.x;
+        const uint64_t q = q0 + lane_id();
         bool active = q < nq;
         const int64_t li = active ? (int64_t)C.ovf_lines[q] : 0;
         uint64_t s = 0, e = 0;
@@ -487,7 +509,7 @@ __global__ __launch_bounds__(PW) void k_parse_ovf_lines(const uint8_t* __restric
         const LineT<const LP_G uint8_t*> L{ls - mis, mis, n};
         parse_wave<false>(P, s_elems, C, L, active, li, stk, false, WC);
     }
-    if (!P.has_phase2() && threadIdx.x == 0 && WC.act) {
+    if (!P.has_phase2() && lane_id() == 0 && WC.act) {
         atomicAdd(&C.meta->counters[0], (unsigned long long)WC.act);
         atomicAdd(&C.meta->counters[1], (unsigned long long)WC.ok);
         atomicAdd(&C.meta->counters[2], (unsigned long long)WC.bad);
@@ -516,7 +538,7 @@ __device__ __forceinline__ void parse_group(const uint8_t* __restrict__ buf, uin
         b1 = W.w1;
         rounds = mid < W.lend ? 2 : 1;
         if (b0 - a0 > win_cap || (rounds == 2 && b1 - a1 > win_cap)) {
-            if (threadIdx.x == 0) C.ovf_list[atomicAdd(&C.meta->ovf_waves, 1ull)] = (uint32_t)wave;
+            if (lane_id() == 0) C.ovf_list[atomicAdd(&C.meta->ovf_waves, 1ull)] = (uint32_t)wave;
             return;
         }
     }
@@ -527,7 +549,7 @@ __device__ __forceinline__ void parse_group(const uint8_t* __restrict__ buf, uin
         const uint64_t a = r ? a1 : a0, b = r ? b1 : b0;
         const bool clean = stage_window(buf, nbytes, a, b, win, msk16);
         __syncthreads();
-        const bool mine = W.active && (rounds == 1 || ((int)threadIdx.x >= PW / 2) == (r != 0));
+        const bool mine = W.active && (rounds == 1 || (lane_id() >= PW / 2) == (r != 0));
         const int n = mine ? crlf_len(W.n, W.n > 0 ? win[W.e - 1 - a] : 0u) : 0;
         const LineT<lds_bytes, lds_u64> L{(lds_bytes)win, mine ? (uint32_t)(W.s - a) : 0u, n,
                                           (lds_u64)reinterpret_cast<uint64_t*>(msk16)};
@@ -547,7 +569,7 @@ __global__ __launch_bounds__(PW, 2) void k_parse_lines(const uint8_t* __restrict
     if (wave * PW >= n_lines || C.meta->cap_ovf) return;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     Elem* s_elems = reinterpret_cast<Elem*>(smem);
-    WaveStack stk{reinterpret_cast<uint32_t*>(smem + 16 * P.n_elems) + threadIdx.x};
+    WaveStack stk{reinterpret_cast<uint32_t*>(smem + 16 * P.n_elems) + lane_id()};
     uint8_t* win = smem + 16 * P.n_elems + stk_words * 4;
     uint16_t* msk16 = reinterpret_cast<uint16_t*>(win + win_cap);
     load_elems(P, s_elems);
@@ -564,7 +586,7 @@ __global__ __launch_bounds__(PW) void k_parse_overflow(const uint8_t* __restrict
     const uint64_t nq = C.meta->ovf_waves;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     Elem* s_elems = reinterpret_cast<Elem*>(smem);
-    WaveStack stk{reinterpret_cast<uint32_t*>(smem + 16 * P.n_elems) + threadIdx.x};
+    WaveStack stk{reinterpret_cast<uint32_t*>(smem + 16 * P.n_elems) + lane_id()};
     load_elems(P, s_elems);
     __syncthreads();
     for (uint64_t q = blockIdx.x; q < nq; q += gridDim.x) {
@@ -593,7 +615,7 @@ __global__ __launch_bounds__(PW) void k_route_match(const uint8_t* __restrict__ 
     if (wave * PW >= n_lines || C.meta->cap_ovf) return;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     Elem* s_elems = reinterpret_cast<Elem*>(smem);
-    WaveStack stk{reinterpret_cast<uint32_t*>(smem + 16 * P.n_elems) + threadIdx.x};
+    WaveStack stk{reinterpret_cast<uint32_t*>(smem + 16 * P.n_elems) + lane_id()};
     uint8_t* win = smem + 16 * P.n_elems + stk_words * 4;
     uint16_t* msk16 = reinterpret_cast<uint16_t*>(win + win_cap);
     load_elems(P, s_elems);
@@ -711,22 +733,27 @@ int launch_parse(const ParseLaunch& a, const DeviceArgs* d_args, const Columns& 
         const ChunkPlan cp = chunk_plan(a);
         if (cp.n_chunks > 0) {
             // the instance per program shape: literal-aware first candidates
-            // only for programs that have such an element
-            // the chunks, then the deferred pass (its blocks return at once
+            // only for programs that have such an element, SIMPLE for the
+            // Apache common / combined family; the chunks, then the deferred pass (its blocks return at once
             // when no wave gave up waiting, the normal case)
             const unsigned g0 = (unsigned)cp.n_chunks + 1, g1 = (unsigned)std::min<int64_t>(cp.n_chunks, 1024);
             const int fd = a.force_direct ? 1 : 0;
-            if (a.lit_aware) {
-                hipLaunchKernelGGL(k_parse_chunks<true>, dim3(g0), dim3(PW), cp.lds, s, a.buf, a.nbytes, d_args, cp.cb,
-                                   cp.win_cap, cp.stk_words, fd, a.chunk_wait);
-                hipLaunchKernelGGL(k_parse_deferred<true>, dim3(g1), dim3(PW), cp.lds, s, a.buf, a.nbytes, d_args, cp.cb,
+            // (the instance per program shape: LA, SIMPLE)
+            auto run = [&](auto chunks, auto deferred) {
+                hipLaunchKernelGGL(chunks, dim3(g0), dim3(PW), cp.lds, s, a.buf, a.nbytes, d_args, cp.cb, cp.win_cap,
+                                   cp.stk_words, fd, a.chunk_wait);
+                hipLaunchKernelGGL(deferred, dim3(g1), dim3(PW), cp.lds, s, a.buf, a.nbytes, d_args, cp.cb,
                                    cp.win_cap, cp.stk_words, fd);
-            } else {
-                hipLaunchKernelGGL(k_parse_chunks<false>, dim3(g0), dim3(PW), cp.lds, s, a.buf, a.nbytes, d_args, cp.cb,
-                                   cp.win_cap, cp.stk_words, fd, a.chunk_wait);
-                hipLaunchKernelGGL(k_parse_deferred<false>, dim3(g1), dim3(PW), cp.lds, s, a.buf, a.nbytes, d_args, cp.cb,
-                                   cp.win_cap, cp.stk_words, fd);
-            }
+            };
+#if defined(LP_NO_SIMPLE)  // (experiment builds: every program on the general instances)
+            const bool simple = false;
+#else
+            const bool simple = a.simple;
+#endif
+            if (a.lit_aware && simple) run(k_parse_chunks<true, true>, k_parse_deferred<true, true>);
+            else if (a.lit_aware) run(k_parse_chunks<true, false>, k_parse_deferred<true, false>);
+            else if (simple) run(k_parse_chunks<false, true>, k_parse_deferred<false, true>);
+            else run(k_parse_chunks<false, false>, k_parse_deferred<false, false>);
             const size_t lds_ovf = 16 * (size_t)a.n_elems + 4 * (size_t)cp.stk_words;
             hipLaunchKernelGGL(k_parse_ovf_lines, dim3((unsigned)grid), dim3(PW), lds_ovf, s, a.buf, a.nbytes, d_args,
                                cp.stk_words);

@@ -1120,6 +1120,42 @@ bool Plan::table_src(const std::string& path, TableSrc out[MAX_FMT], std::string
                 ps = kv.second;
             }
         }
+        // ResponseSetCookieDissector outputs of a cookie of a Set-Cookie pair
+        // stage: "STRING:<list>.<cookie>.value|expires|domain|comment|path",
+        // "TIME.EPOCH:<list>.<cookie>.expires" (the cookie name may hold '.')
+        if (!pbest && (type == "STRING" || type == "TIME.EPOCH")) {
+            const size_t dot = name.rfind('.');
+            if (dot != std::string::npos && dot > 0) {
+                const std::string field = name.substr(dot + 1), stem = name.substr(0, dot);
+                int sf = -1;
+                if (type == "TIME.EPOCH") sf = field == "expires" ? SC_EXPIRES_MS : -1;
+                else if (field == "value") sf = SC_VALUE;
+                else if (field == "expires") sf = SC_EXPIRES_S;
+                else if (field == "domain") sf = SC_DOMAIN;
+                else if (field == "comment") sf = SC_COMMENT;
+                else if (field == "path") sf = SC_PATH;
+                const std::string* sbest = nullptr;
+                int ss = -1;
+                for (const auto& kv : tpair_[f]) {
+                    if (kv.second >= 0 && prog_.pair[kv.second].kind != PK_SETC) continue;
+                    const size_t c2 = kv.first.find(':');
+                    const std::string kname = kv.first.substr(c2 + 1);
+                    if (stem.size() > kname.size() + 1 && stem.compare(0, kname.size(), kname) == 0 &&
+                        stem[kname.size()] == '.' && (!sbest || kname.size() > sbest->size() - (c2 + 1))) {
+                        sbest = &kv.first;
+                        ss = kv.second;
+                    }
+                }
+                if (sbest && sf >= 0) {
+                    if (ss < 0) return false;
+                    const std::string cn = stem.substr(sbest->size() - sbest->find(':'));
+                    if (names.size() + cn.size() > (size_t)TABLE_NAMES) return false;
+                    out[f] = TableSrc{TC_SETC, ss | (sf << 8), (int32_t)names.size(), (int32_t)cn.size()};
+                    names += cn;
+                    continue;
+                }
+            }
+        }
         if (pbest) {
             if (ps < 0) return false;
             const std::string pn = name.substr(pbest->size() - pbest->find(':'));
@@ -1553,12 +1589,14 @@ void Plan::compile_program() {
                     treg("TIME.LOCALIZEDSTRING:" + complete, TableSrc{TC_TOKEN, oi, 0, 0});
                     break;
                 case D_SETCOOKIES: {
-                    // ResponseSetCookieListDissector / ResponseSetCookieDissector:
-                    // split, joined, named and dissected in the replay; the device
-                    // proves HttpCookie.parse and parseExpire cannot throw (setcookie_ok)
+                    // ResponseSetCookieListDissector: split, joined and named by the
+                    // URI kernel (a pair stage, PK_SETC); ResponseSetCookieDissector
+                    // on a cookie string by the device table (TC_SETC, table_src) and
+                    // the replay; the phase-1 guard proves HttpCookie.parse and
+                    // parseExpire cannot throw (setcookie_ok)
                     if (ok != O_TOKEN) { device_ok_ = false; why_ = "Set-Cookie list from a derived value"; return; }
                     P.guard_setc[cur_fmt] |= 1 << oi;
-                    thost(complete);
+                    if (!add_pair(oi, PK_SETC, "HTTP.SETCOOKIE:" + complete)) return;
                     const std::string pre = "HTTP.SETCOOKIE:" + complete + ".";
                     for (const auto& kv : compiled_)
                         if (kv.first.compare(0, pre.size(), pre) == 0) P.guard_setc_exp[cur_fmt] |= 1 << oi;
@@ -2180,54 +2218,29 @@ void Plan::run_phase(Ctx& c, const Instance& in, const std::string& name, const 
     }
     case D_SETCOOKIES: {
         // ResponseSetCookieListDissector.dissect (dissectors/ResponseSetCookieListDissector.java:79-110):
-        // split(", ") (trailing empty parts dropped), a part whose lower-cased
-        // "expires=" starts within its last 15 chars is joined with the next
-        // one, HttpCookie.parse names each cookie string (the device proved the
-        // Netscape branch: one cookie, the first ';'-token's name before '=',
-        // trimmed), lower-cased; the value is the cookie string itself
+        // the URI kernel's piece table (lp_device.h setc_pieces / pair_fill):
+        // per cookie string in order its lower-cased name and the string itself
         if (v.null || v.len == 0) return;
         const bool all = has("*");
-        uint32_t t = v.len;
-        while (t >= 2 && v.p[t - 2] == ',' && v.p[t - 1] == ' ') t -= 2;
-        if (t == 0) return;
-        int64_t prev = -1;
+        const int j = pair_of_tok_.at(t_fmt * 64 + oi);
+        const uint32_t n = R.p_count[j][i];
+        const uint8_t* tab = n ? c.arena + ref_off(R.p_tab[j][i]) : nullptr;
+        auto at = [&](uint64_t r) { return mstr((ref_arena(r) ? c.arena : c.line) + ref_off(r), ref_len(r)); };
         // (name, cookie string) in order; a name's further dissection reads
         // the Parsable's cache, which holds the LAST value added under that
         // name (core/Parsable.java:172-183, Parser.java:735-753)
         std::vector<std::pair<std::string, MVal>> got;
-        for (uint32_t s = 0; s <= t;) {
-            uint32_t e = s;
-            while (e < t && !(v.p[e] == ',' && e + 1 < t && v.p[e + 1] == ' ')) ++e;
-            int64_t ei = -1;
-            for (uint32_t q = s; q + 8 <= e && ei < 0; ++q) {
-                static const char ex[] = "expires=";
-                bool m = true;
-                for (int k = 0; k < 8 && m; ++k) m = (v.p[q + k] | (v.p[q + k] >= 'A' && v.p[q + k] <= 'Z' ? 32 : 0)) == ex[k];
-                if (m) ei = q - s;
-            }
-            if (ei >= 0 && (int64_t)(e - s) - 15 < ei) {
-                prev = s;
-            } else {
-                const uint32_t cs = prev >= 0 ? (uint32_t)prev : s;
-                prev = -1;
-                uint32_t q = cs;
-                while (q < e && v.p[q] == ';') ++q;
-                uint32_t eq = q;
-                while (eq < e && v.p[eq] != '=' && v.p[eq] != ';') ++eq;
-                uint32_t na = q, nb = eq;
-                while (na < nb && v.p[na] <= ' ') ++na;
-                while (nb > na && v.p[nb - 1] <= ' ') --nb;
-                std::string nm((const char*)v.p + na, nb - na);
-                for (auto& ch : nm) if (ch >= 'A' && ch <= 'Z') ch = char(ch + 32);
-                if (all || has(nm.c_str())) got.emplace_back(nm, mstr(v.p + cs, e - cs));
-            }
-            if (e >= t) break;
-            s = e + 2;
+        for (uint32_t k = 0; k < n; ++k) {
+            uint64_t e[2];
+            memcpy(e, tab + 16 * (size_t)k, 16);
+            const MVal nm = at(e[0]);
+            std::string ns((const char*)nm.p, nm.len);
+            if (all || has(ns.c_str())) got.emplace_back(std::move(ns), at(e[1]));
         }
         for (size_t k = 0; k < got.size(); ++k) {
             const MVal* last = &got[k].second;
-            for (size_t j = k + 1; j < got.size(); ++j)
-                if (got[j].first == got[k].first) last = &got[j].second;
+            for (size_t q = k + 1; q < got.size(); ++q)
+                if (got[q].first == got[k].first) last = &got[q].second;
             set_origin(O_NONE, 0);
             emit(c, name, "HTTP.SETCOOKIE", got[k].first, got[k].second, last);
         }

@@ -102,7 +102,7 @@ __device__ __forceinline__ UriLane<NU> uri_lane(const Program& P, const Columns&
 template <bool SLOT, typename CL>
 __device__ __forceinline__ void uri_walk_coop(const Program& P, int u, const CL& L, bool part, int a, int b,
                                               uint32_t usep, const Arena& A, UriWalk& Wk) {
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     const bool table = u >= 0 && P.uri[u].want_query && P.uri[u].query_stage >= 0;  // uniform unless SLOT
     const uint32_t cnt = part ? usep : 0u;
     uint32_t x = cnt;
@@ -232,7 +232,7 @@ __device__ __forceinline__ void uri_walk_coop(const Program& P, int u, const CL&
 template <int NU, int NQ, bool COOP, bool SLOT, typename LU, typename LL>
 __device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, UriLane<NU>& U, LU&& lu, LL&& ll,
                                          bool active, int64_t li, int64_t wave, WaveCounts& WC) {
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     const int nq = P.n_query < NQ ? P.n_query : NQ;
     uint32_t need = 0;
     if (U.ok)
@@ -480,7 +480,7 @@ template <int NU, int NQ, bool SLOT, uint32_t CAP>
 __device__ __forceinline__ bool uri_compact(const uint8_t* __restrict__ buf, uint64_t nbytes, const Program& P,
                                             const Columns& C, int64_t wave, int64_t n_lines, uint32_t* cbuf,
                                             uint64_t* plane, WaveCounts& WC) {
-    const int lane = threadIdx.x;
+    const int lane = lane_id();
     const int64_t li = wave * PW + lane;
     const bool active = li < n_lines;
     LP_PROF(23);
@@ -615,7 +615,7 @@ __global__ __launch_bounds__(PW, 4) void k_uri_lines(const uint8_t* __restrict__
     __shared__ uint64_t plane[URI_CAP / 64 + 1];
     WaveCounts WC;
     if (uri_compact<NU, NQ, SLOT, URI_CAP>(buf, nbytes, P, C, wave, n_lines, cbuf, plane, WC)) WC.store(C, wave);
-    else if (threadIdx.x == 0) C.uri_ovf_list[atomicAdd(&C.meta->uri_ovf_waves, 1ull)] = (uint32_t)wave;
+    else if (lane_id() == 0) C.uri_ovf_list[atomicAdd(&C.meta->uri_ovf_waves, 1ull)] = (uint32_t)wave;
 }
 
 // The waves k_uri_lines queued (their URI bytes exceed its compact buffer),
@@ -679,7 +679,7 @@ __global__ __launch_bounds__(PW) void k_derived_lines(const uint8_t* __restrict_
         if (st != ST_OK) C.status[W.li] = (uint8_t)st;
     }
     const uint32_t ok = (uint32_t)__popcll(__ballot(st == ST_OK)), bad = (uint32_t)__popcll(__ballot(st == ST_BAD));
-    if (threadIdx.x == 0) {
+    if (lane_id() == 0) {
         LP_G uint32_t* wc = C.wave_counts + WC_WORDS * (size_t)wave;
         const uint32_t act = wc[0];
         wc[1] = ok;

@@ -314,6 +314,42 @@ static int parse_impl(Emu* e, const char* line, int len, const uint8_t* base, ui
 
 static int g_masks_fwd(int on) { return g_masks = on; }
 
+// How the lines of a one-format program reach their match result in the
+// parse kernel's phase 1 (k_parse_chunks): out[0] lines, [1] the first DFS
+// leaf matches, [2] ruled out by the quote-count / line-tail prefilters,
+// [3] the backtracking DFS decides.  (Diagnostics for the kernel design:
+// which lines a lean first-leaf kernel would hand to the queued-line kernel.)
+int emu_leaf_stats(void* h, const char* data, int64_t n, int64_t* out) {
+    Emu* e = (Emu*)h;
+    if (!e->plan.device_ok()) return 2;
+    const Program& P = e->plan.program();
+    if (P.n_fmt != 1) return 3;
+    const bool la = lit_aware(P);
+    for (int k = 0; k < 4; ++k) out[k] = 0;
+    const uint8_t* base = (const uint8_t*)data;
+    for (int64_t s = 0; s < n;) {
+        int64_t t = s;
+        while (t < n && data[t] != '\n') ++t;
+        const uint32_t off = (uint32_t)s, len = (uint32_t)(t - s);
+        const uint32_t lo = off & ~63u, hi = (off + len + 4) & ~3u;
+        const uint32_t wn = ((hi - lo) + 63) & ~63u;
+        std::vector<uint64_t> wbuf(wn / 8 + 8, ~0ull);
+        memcpy(wbuf.data(), base + lo, std::min<uint64_t>(hi - lo, (uint64_t)n - lo));
+        std::vector<uint64_t> masks(MC_N * (wn / 64));
+        build_masks((const uint8_t*)wbuf.data(), wn, masks.data());
+        MLine L{(const uint8_t*)wbuf.data(), off - lo, (int)len, masks.data()};
+        RegArr<MAX_TOK> caps;
+        caps.fill(0);
+        ++out[0];
+        const bool leaf = la ? match_first_leaf<true>(P, L, caps) : match_first_leaf<false>(P, L, caps);
+        if (leaf) ++out[1];
+        else if (!fmt_tail_ok(P, P.elems, P.n_elems, L) || count_quotes(L) < P.fmt_quotes[0]) ++out[2];
+        else ++out[3];
+        s = t + 1;
+    }
+    return 0;
+}
+
 int emu_possible_paths(const char* fmt, int depth, char* out, int cap) {
     std::vector<std::string> paths;
     std::string err;

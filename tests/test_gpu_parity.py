@@ -927,14 +927,22 @@ def test_device_table_other_configs_gpu():
     millisecond columns) and 5 (three LogFormats, rows of formats without a
     path empty), and on type-remapped paths"""
     import remap_corpus as rc
-    from test_emu_parity import COOKIE_FMT, QS_FMT, UPSTREAM_FMT, cookie_lines, querystring_lines, upstream_lines
+    from test_emu_parity import (COOKIE_FMT, QS_FMT, UPSTREAM_FMT, SETCOOKIE_FMT, SETCOOKIE_FIELDS, cookie_lines,
+                                 querystring_lines, upstream_lines, setcookie_lines)
     cases = [(wl, lpa.SYNTH_FORMATS[wl], lpa.synth(wl, 5, 0, 20000), ()) for wl in (3, 4, 5)]
-    # request cookies and raw-token query strings (the URI kernel's pair stages), upstream address /
-    # status lists and the binary IP (its list stages, phase 1's BinaryIP stage)
+    # request cookies, raw-token query strings and Set-Cookie lists (the URI kernel's pair stages;
+    # ResponseSetCookieDissector's outputs from the device table), upstream address / status lists
+    # and the binary IP (its list stages, phase 1's BinaryIP stage)
     extra = {COOKIE_FMT: ["HTTP.COOKIE:request.cookies.session", "HTTP.COOKIE:request.cookies.theme"],
-             QS_FMT: ["STRING:request.querystring.aap", "STRING:request.querystring.res"]}
+             QS_FMT: ["STRING:request.querystring.aap", "STRING:request.querystring.res"],
+             SETCOOKIE_FMT: [f for f in SETCOOKIE_FIELDS[1] if f.startswith(("HTTP.SETCOOKIE:", "STRING:response",
+                                                                            "TIME.EPOCH:"))] +
+             ["HTTP.SETCOOKIE:response.cookies.session", "STRING:response.cookies.session.path",
+              "TIME.EPOCH:response.cookies.session.expires", "STRING:response.cookies.nba-1.expires",
+              "HTTP.SETCOOKIE:response.cookies.x.y", "STRING:response.cookies.x.y.value",
+              "STRING:response.cookies.x.y.domain", "STRING:response.cookies._ga.comment"]}
     for fmt, lines in ((COOKIE_FMT, cookie_lines(5000, 21)), (QS_FMT, querystring_lines(5000, 22)),
-                       (UPSTREAM_FMT, upstream_lines(5000, 23))):
+                       (UPSTREAM_FMT, upstream_lines(5000, 23)), (SETCOOKIE_FMT, setcookie_lines(5000, 32))):
         cases.append((6, fmt, b"".join(l + b"\n" for l in lines), ()))
     rlines = rc.corpus(3, 3000)
     cases.append((0, rc.FORMAT, b"".join(l + b"\n" for l in rlines), rc.REMAPS))
@@ -961,6 +969,34 @@ def test_device_table_other_configs_gpu():
             # columns (list items, SECOND_MILLIS -> MILLISECONDS -> MICROSECONDS, binary IPs, cookies, raw
             # query parameters included)
             assert host_only == [], host_only
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wl", [3, 4])
+def test_chunk_excess_instances_gpu(oracle, wl):
+    """Chunks of more than 64 lines (chunk_excess: their 65th line on queued
+    for k_parse_ovf_lines) and lines that need the backtracking DFS (queued
+    too: the chunk kernel has no DFS) on the kernel instances other than the
+    Apache common / combined one: config 3's strftime program and config 4's
+    literal-aware NGINX program, against the oracle line by line.  Regression
+    for the round-5 fault: chunk_excess numbered fewer lines than the staging
+    pass (wrong lane ids in the non-inlined call), leaving
+    line_off entries unwritten; the kernels' self-check (Meta::err) now fails
+    such a batch instead of faulting."""
+    rng = random.Random(11 + wl)
+    fmt = lpa.SYNTH_FORMATS[wl]
+    base = lpa.synth(wl, 20261022, 0, 4000).split(b"\n")[:-1]
+    lines = []
+    for i, l in enumerate(base):
+        lines.append(l)
+        if i % 400 == 5:
+            lines += [b"x"] * rng.randrange(70, 260)  # > 64 line starts in one chunk
+        if i % 300 == 17:
+            lines.append(b"-" * rng.randrange(1, 5))  # short lines between them
+    fields = paths(oracle)
+    s, r = gpu_vs_oracle(oracle, fmt, fields, lines)
+    assert s["ok"] > 3500, s
+    assert r.diag["overflow_waves"] > 1000, r.diag  # (chunked: lines queued for k_parse_ovf_lines)
 
 
 @pytest.mark.gpu
