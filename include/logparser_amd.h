@@ -122,6 +122,9 @@ int64_t lp_possible_paths_remapped(const char *logformats, int max_depth, const 
 #define LP_OPT_CHUNK_WAIT 5    /* tests: polls a chunk's wave makes for its first line number before it
                                   leaves the chunk to the deferred pass (0 = default 16384; a negative
                                   value: none, every chunk goes to the deferred pass) */
+#define LP_OPT_ONE_PASS 6      /* several LogFormats: 1 (default) one pass over the input (the chunk kernel
+                                  routes every line exactly one format matches; the rest after the
+                                  routing scan), 0 the line index, routing and parse passes */
 int lp_set_option(lp_handle *h, int option, int64_t value);
 
 /* Capacity for the coming batches: columns for max_lines lines and at least

@@ -33,7 +33,7 @@ LIB_PATH = os.environ.get("LOGPARSER_AMD_LIB") or os.path.join(_HERE, "_lib", "l
 LP_OK, LP_E_INVALID, LP_E_MISSING, LP_E_UNSUPPORTED, LP_E_DEVICE, LP_E_NOMEM, LP_E_STATE = 0, -1, -2, -3, -4, -5, -6
 LINE_OK, LINE_BAD, LINE_FALLBACK = 0, 1, 2
 BUF_HOST, BUF_DEVICE = 0, 1
-OPT_FORCE_DIRECT, OPT_MAX_RETRIES, OPT_ARENA_BYTES, OPT_CHUNK_LINES, OPT_CHUNK_WAIT = 1, 2, 3, 4, 5
+OPT_FORCE_DIRECT, OPT_MAX_RETRIES, OPT_ARENA_BYTES, OPT_CHUNK_LINES, OPT_CHUNK_WAIT, OPT_ONE_PASS = 1, 2, 3, 4, 5, 6
 ARENA_SHARDS = 64
 
 

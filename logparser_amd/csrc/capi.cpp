@@ -108,6 +108,7 @@ struct lp_handle {
     uint64_t counters[4]{};
     uint32_t chunk_lines = 0;      // LP_OPT_CHUNK_LINES (0: the kernel's default)
     int32_t chunk_wait = 0;        // LP_OPT_CHUNK_WAIT (tests: 0 default, < 0 defer every chunk not yet reached)
+    bool one_pass = true;          // LP_OPT_ONE_PASS: several LogFormats on the chunked one-pass path
     bool chunked = false;          // the last batch ran the chunked parse (line index inside the parse kernel)
     uint64_t ovf_waves = 0;        // waves of the last batch parsed by k_parse_overflow (chunked: lines by k_parse_ovf_lines)
     uint64_t uri_ovf_waves = 0;    // ... whose URI stages ran in k_uri_overflow
@@ -305,7 +306,10 @@ int enqueue(lp_handle* h, bool sync_count) {
     int64_t cap = h->cap_lines;
     // one LogFormat: the parse kernel finds the lines itself (k_parse_chunks);
     // several: the routing pass needs the line index first
-    const bool chunked = h->plan.device_ok() && P.n_fmt == 1;
+    // one pass: the parse kernel finds the lines itself (k_parse_chunks);
+    // several LogFormats route inside it too (LP_OPT_ONE_PASS 0: the line
+    // index, the routing passes, then the parse)
+    const bool chunked = h->plan.device_ok() && (P.n_fmt == 1 || h->one_pass);
     h->chunked = chunked;
     if (sync_count && chunked) {
         // first batch of a one-format handle: the line length of an 8 MiB
@@ -389,6 +393,7 @@ int enqueue(lp_handle* h, bool sync_count) {
         pl.chunked = chunked;
         pl.chunk_lines = h->chunk_lines;
         pl.chunk_wait = h->chunk_wait;
+        pl.multi = chunked && P.n_fmt > 1;
         pl.lit_aware = false;
         for (int i = 0; i < P.n_elems; ++i) {
             const lp::ElemV e = lp::load_elem(P.elems + i);
@@ -415,9 +420,10 @@ int enqueue(lp_handle* h, bool sync_count) {
             return LP_E_DEVICE;
         hipEventRecord(h->ev[2], s);
         const lp::DeviceArgs* d_args = h->args.as<lp::DeviceArgs>();
-        if (P.n_fmt > 1) {
+        if (P.n_fmt > 1 && !chunked) {
             // HttpdLogFormatDissector routing: every format's match per line,
-            // then the scan of the sticky active format
+            // then the scan of the sticky active format (one pass: inside
+            // launch_parse, after the chunk kernel)
             if (lp::launch_route_match(pl, d_args, s) != 0 || lp::launch_route(d_args, cap, s) != 0) return LP_E_DEVICE;
         }
         if (lp::launch_parse(pl, d_args, C, s) != 0) return LP_E_DEVICE;
@@ -686,6 +692,9 @@ int lp_set_option(lp_handle* h, int option, int64_t value) {
     case LP_OPT_CHUNK_LINES:
         if (value < 0 || value > 64) return LP_E_INVALID;
         h->chunk_lines = (uint32_t)value;
+        return LP_OK;
+    case LP_OPT_ONE_PASS:
+        h->one_pass = value != 0;
         return LP_OK;
     case LP_OPT_CHUNK_WAIT:
         h->chunk_wait = value < 0 ? -1 : (int32_t)std::min<int64_t>(value, 1 << 30);

@@ -48,6 +48,7 @@ struct ParseLaunch {
     bool lit_aware = true;      // the program has a [^\s]* / "$request" element a shorter end of which can meet
                                 // its literal (the chunked kernel's instance with literal-aware first candidates)
     bool simple = false;        // one format of the Apache common / combined family (capi simple_program)
+    bool multi = false;         // several LogFormats on the one-pass path (routing inside the chunk kernel)
 };
 // The chunked parse kernel's geometry: cb input bytes per chunk (one wave
 // each), an LDS window of win_cap bytes (the chunk, 64 bytes before it, the

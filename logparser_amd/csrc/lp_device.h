@@ -1387,9 +1387,16 @@ __host__ __device__ LP_INLINE bool line_text_ok(const LN& L) {
 // The match word of a line for sticky routing: bit f = format f matches,
 // bit 8+f = undecided on the device (FALLBACK).  Formats whose literal '"'
 // count or line tail rule them out skip the DFS.
-template <typename LN, typename EL, typename Stk>
+// DFS = false (the one-pass chunk kernel of several-format programs): a
+// format whose first leaf fails and that the prefilters do not rule out sets
+// `redo` instead of running the backtracking DFS (the line is then queued:
+// k_route_ovf computes its word with the DFS).
+// caps (the one-pass chunk kernel): the spans of the first format whose first
+// leaf matches (phase1<..., PRE> then starts from them instead of matching
+// that format again).
+template <bool DFS = true, typename LN, typename EL, typename Stk, typename Caps = NoCaps>
 __host__ __device__ LP_INLINE uint32_t fmt_match_word(const Program& P, const EL& elems, const LN& L, Stk stk,
-                                                      bool clean) {
+                                                      bool clean, bool* redo = nullptr, Caps* caps = nullptr) {
     const uint32_t all = (1u << P.n_fmt) - 1u;
     if (L.n > MAX_LINE) return all << 8;
     if (!clean && !line_text_ok(L)) return all << 8;
@@ -1401,12 +1408,27 @@ __host__ __device__ LP_INLINE uint32_t fmt_match_word(const Program& P, const EL
         if (quotes < P.fmt_quotes[f] || !fmt_tail_ok(P, elems + e0, ne, L)) continue;
         // the DFS's first leaf decides most lines of the format (exact: its
         // first complete match); the backtracking DFS the rest
-        if (match_first_leaf_lane(P, elems + e0, ne, L, nc)) {
+        if constexpr (!std::is_same<Caps, NoCaps>::value) {
+            if (!(m & 0xFFu)) {  // no format matched yet: capture this one's spans
+                caps->fill(0);
+                if (match_first_leaf_lane(P, elems + e0, ne, L, *caps)) {
+                    m |= 1u << f;
+                    continue;
+                }
+            } else if (match_first_leaf_lane(P, elems + e0, ne, L, nc)) {
+                m |= 1u << f;
+                continue;
+            }
+        } else if (match_first_leaf_lane(P, elems + e0, ne, L, nc)) {
             m |= 1u << f;
             continue;
         }
-        const int st = match_line(P, elems + e0, ne, L, nc, stk);
-        m |= st == ST_OK ? (1u << f) : st == ST_FALLBACK ? (256u << f) : 0u;
+        if constexpr (DFS) {
+            const int st = match_line(P, elems + e0, ne, L, nc, stk);
+            m |= st == ST_OK ? (1u << f) : st == ST_FALLBACK ? (256u << f) : 0u;
+        } else {
+            *redo = true;
+        }
     }
     return m;
 }
@@ -2530,8 +2552,11 @@ __host__ __device__ LP_INLINE uint32_t hist_word(const Program& P, const LN& L, 
 // kernel queues it for k_parse_ovf_lines, which runs the whole phase 1:
 // neither the DFS's code nor its registers are in the hot kernel, and a
 // line that backtracks no longer holds the other lanes of its wave).
-template <bool MULTI = false, bool LA = true, bool SIMPLE = false, bool DFS = true, typename LN, typename EL, typename Stk,
-          typename Cols>
+// PRE (several LogFormats, one pass): the line's format and its first-leaf
+// spans are already known (fmt_match_word captured them into o.caps, the
+// guard included): phase 1 starts after the match.
+template <bool MULTI = false, bool LA = true, bool SIMPLE = false, bool DFS = true, bool PRE = false, typename LN,
+          typename EL, typename Stk, typename Cols>
 __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, const LN& L, LineOut& o, Stk stk, Cols& C,
                                           int64_t li, bool clean = false, int fmt = 0) {
     o.status = ST_OK;
@@ -2540,7 +2565,7 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
     o.tdone = 0;
     o.smdone = 0;
     o.bipdone = 0;
-    o.caps.fill(0);
+    if constexpr (!PRE) o.caps.fill(0);
     o.fl_kind.fill(FL_NONE);
     o.fl_method.fill(0);
     o.fl_uri.fill(0);
@@ -2549,7 +2574,7 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
     // fast-path guard: TAB, printable ASCII and valid UTF-8 without the
     // chars java.util.regex '.' does not match (line_text_ok)
     LP_PROF(2);
-    if (!clean && !line_text_ok(L)) {
+    if (!PRE && !clean && !line_text_ok(L)) {
         o.status = ST_FALLBACK;
         return;
     }
@@ -2562,7 +2587,9 @@ __host__ __device__ LP_INLINE void phase1(const Program& P, const EL& elems, con
     // quote count or line tail already rules them out (exact; malformed
     // lines would otherwise backtrack while the rest of the wave waits).
     int st = ST_BAD;
-    if constexpr (MULTI) {
+    if constexpr (PRE) {
+        st = ST_OK;
+    } else if constexpr (MULTI) {
         const int e0 = P.fmt_elem0[fmt], ne = P.fmt_elem0[fmt + 1] - e0;
         if (match_first_leaf_lane(P, elems + e0, ne, L, o.caps)) st = ST_OK;
         else o.caps.fill(0);  // the DFS sets its own

@@ -318,7 +318,16 @@ __device__ __noinline__ void chunk_excess(const uint8_t* __restrict__ buf, uint6
 // (LP_OPT_FORCE_DIRECT, tests).
 // second: the deferred pass (the chunk's count is published and the scanner
 // has finished: the line number is read, not waited for).
-template <bool LA, bool SIMPLE>
+// MF: a program of several LogFormats (HttpdLogFormatDissector.java:173-204):
+// each lane first computes its line's match word without the DFS; a line
+// that exactly one format matches is routed to it whatever the sticky state
+// is (the active format, if it is not that one, fails, and the first that
+// matches becomes active), and one that no format matches is BAD whatever
+// the state is; so phase 1 runs here for those.  A line several formats
+// match, or whose word needs the DFS, is queued: k_route_ovf computes its
+// word, the routing scan (k_fmt_*) then gives every line its format, and
+// k_parse_ovf_lines parses it.  Every line's word is written to fmt_match.
+template <bool LA, bool SIMPLE, bool MF = false>
 __device__ __forceinline__ void parse_chunk(const uint8_t* __restrict__ buf, uint64_t nbytes, const Program& P,
                                             const Columns& C, const Elem* s_elems, uint8_t* smem, int64_t c,
                                             int64_t n_chunks, uint32_t cb, uint32_t win_cap, uint32_t stk_words,
@@ -368,11 +377,24 @@ __device__ __forceinline__ void parse_chunk(const uint8_t* __restrict__ buf, uin
     o.status = ST_OK;
     o.tdone = o.smdone = o.bipdone = 0;
     LP_PROF(1);
+    uint32_t mword = 0;  // MF: the line's match word (bit f: format f matches)
+    if constexpr (MF) {
+        if (lds_line) {
+            bool redo = false;
+            // (the spans of the first matching format's first leaf in o.caps)
+            mword = fmt_match_word<false>(P, s_elems, L, stk, S.clean, &redo, &o.caps);
+            const uint32_t mm = mword & 0xFFu;
+            if (redo || (mword >> 8) || (mm & (mm - 1))) o.status = ST_REDO;  // the DFS or the sticky state decides
+            else if (mm == 0) o.status = ST_BAD;  // no format matches: BAD in every state
+            else phase1<true, LA, false, false, true>(P, s_elems, L, o, stk, C, 0, S.clean, __builtin_ctz(mm));
+        }
+    } else {
 #if defined(LP_DFS_IN_CHUNKS)  // (experiment builds: the backtracking DFS inside the chunk kernel, as before round 6)
-    if (lds_line) phase1<false, LA, SIMPLE, true>(P, s_elems, L, o, stk, C, 0, S.clean, 0);
+        if (lds_line) phase1<false, LA, SIMPLE, true>(P, s_elems, L, o, stk, C, 0, S.clean, 0);
 #else
-    if (lds_line) phase1<false, LA, SIMPLE, false>(P, s_elems, L, o, stk, C, 0, S.clean, 0);  // (no DFS: ST_REDO)
+        if (lds_line) phase1<false, LA, SIMPLE, false>(P, s_elems, L, o, stk, C, 0, S.clean, 0);  // (no DFS: ST_REDO)
 #endif
+    }
     LP_PROF(9);
     const uint64_t base = chunk_base(C.chunk_state, c, S.count, second ? (int)CHUNK_WAIT_MAX : wait_max);
     if (base == ~0ull) {  // (never in a normal launch) the deferred pass redoes the chunk
@@ -388,6 +410,9 @@ __device__ __forceinline__ void parse_chunk(const uint8_t* __restrict__ buf, uin
     const int64_t li = (int64_t)base + lane;
     const bool mine = has && li < cap;
     if (mine) line_off_w(C)[li] = w0 + s;
+    if constexpr (MF) {
+        if (mine) C.fmt_match[li] = (uint16_t)mword;  // (a queued line's word: k_route_ovf)
+    }
     // a line the window does not hold, or that needs the backtracking DFS,
     // is queued for k_parse_ovf_lines (the whole phase 1, from HBM)
     const bool redo = lds_line && o.status == ST_REDO;
@@ -421,7 +446,7 @@ __device__ __forceinline__ void parse_chunk(const uint8_t* __restrict__ buf, uin
 // waiting for the scanner (chunk_base) are redone by k_parse_deferred.
 // SIMPLE: the instance for Apache common / combined family programs
 // (phase1; the host's simple_program picks it).
-template <bool LA, bool SIMPLE>
+template <bool LA, bool SIMPLE, bool MF>
 __global__ __launch_bounds__(PW, 2) void k_parse_chunks(const uint8_t* __restrict__ buf, uint64_t nbytes,
                                                      const DeviceArgs* __restrict__ args, uint32_t cb, uint32_t win_cap,
                                                      uint32_t stk_words, int direct, int wait_max) {
@@ -437,13 +462,14 @@ __global__ __launch_bounds__(PW, 2) void k_parse_chunks(const uint8_t* __restric
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     Elem* s_elems = reinterpret_cast<Elem*>(smem);
     load_elems(P, s_elems);
-    parse_chunk<LA, SIMPLE>(buf, nbytes, P, C, s_elems, smem, c, n_chunks, cb, win_cap, stk_words, direct, wait_max, false);
+    parse_chunk<LA, SIMPLE, MF>(buf, nbytes, P, C, s_elems, smem, c, n_chunks, cb, win_cap, stk_words, direct, wait_max,
+                                false);
 }
 
 // The deferred pass: the chunks in C.deferred_chunks (none in a normal
 // launch: its blocks return at once), after k_parse_chunks, whose scanner has
 // then finished, so their line numbers are read, not waited for.
-template <bool LA, bool SIMPLE>
+template <bool LA, bool SIMPLE, bool MF>
 __global__ __launch_bounds__(PW, 2) void k_parse_deferred(const uint8_t* __restrict__ buf, uint64_t nbytes,
                                                        const DeviceArgs* __restrict__ args, uint32_t cb,
                                                        uint32_t win_cap, uint32_t stk_words, int direct) {
@@ -456,8 +482,8 @@ __global__ __launch_bounds__(PW, 2) void k_parse_deferred(const uint8_t* __restr
     Elem* s_elems = reinterpret_cast<Elem*>(smem);
     load_elems(P, s_elems);
     for (uint64_t q = blockIdx.x; q < nd; q += gridDim.x) {
-        parse_chunk<LA, SIMPLE>(buf, nbytes, P, C, s_elems, smem, (int64_t)C.deferred_chunks[q], n_chunks, cb,
-                                win_cap, stk_words, direct, 0, true);
+        parse_chunk<LA, SIMPLE, MF>(buf, nbytes, P, C, s_elems, smem, (int64_t)C.deferred_chunks[q], n_chunks, cb,
+                                    win_cap, stk_words, direct, 0, true);
         __syncthreads();  // this chunk's LDS reads are done before the next one is staged
     }
 }
@@ -514,6 +540,39 @@ __global__ __launch_bounds__(PW) void k_parse_ovf_lines(const uint8_t* __restric
         atomicAdd(&C.meta->counters[1], (unsigned long long)WC.ok);
         atomicAdd(&C.meta->counters[2], (unsigned long long)WC.bad);
         atomicAdd(&C.meta->counters[3], (unsigned long long)(WC.act - WC.ok - WC.bad));
+    }
+}
+
+// Several LogFormats, one pass: the match words (with the DFS) of the lines
+// the chunk kernel queued, 64 per wave on a persistent grid, from HBM; the
+// routing scan (k_fmt_*) runs after it.
+__global__ __launch_bounds__(PW) void k_route_ovf(const uint8_t* __restrict__ buf, uint64_t nbytes,
+                                                  const DeviceArgs* __restrict__ args, uint32_t stk_words) {
+    const Program& P = args->prog;
+    const Columns& C = args->cols;
+    if (C.meta->cap_ovf) return;
+    const uint64_t nq = min((uint64_t)C.meta->ovf_lines, (uint64_t)C.cap_lines + 1);
+    const uint64_t n_lines = C.meta->n_lines;
+    if ((uint64_t)blockIdx.x * PW >= nq) return;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    Elem* s_elems = reinterpret_cast<Elem*>(smem);
+    WaveStack stk{reinterpret_cast<uint32_t*>(smem + 16 * P.n_elems) + lane_id()};
+    load_elems(P, s_elems);
+    __syncthreads();
+    for (uint64_t q0 = (uint64_t)blockIdx.x * PW; q0 < nq; q0 += (uint64_t)gridDim.x * PW) {
+        const uint64_t q = q0 + lane_id();
+        if (q >= nq) continue;
+        const int64_t li = (int64_t)C.ovf_lines[q];
+        if ((uint64_t)li >= n_lines) continue;  // (k_parse_ovf_lines reports it)
+        const uint64_t s = C.line_off[li], e1 = C.line_off[li + 1];
+        if (s >= e1 || e1 > nbytes + 1) continue;  // (idem)
+        const uint64_t e = e1 - 1, len = e - s;
+        const int n0 = (int)(len > (uint64_t)0x7FFFFFFF ? 0x7FFFFFFF : len);
+        const int n = crlf_len(n0, n0 > 0 ? buf[e - 1] : 0u);
+        const LP_G uint8_t* ls = (const LP_G uint8_t*)(buf) + s;
+        const uint32_t mis = (uint32_t)((uintptr_t)ls & 3);
+        const LineT<const LP_G uint8_t*> L{ls - mis, mis, n};
+        C.fmt_match[li] = (uint16_t)fmt_match_word(P, s_elems, L, stk, false);
     }
 }
 
@@ -750,11 +809,21 @@ int launch_parse(const ParseLaunch& a, const DeviceArgs* d_args, const Columns& 
 #else
             const bool simple = a.simple;
 #endif
-            if (a.lit_aware && simple) run(k_parse_chunks<true, true>, k_parse_deferred<true, true>);
-            else if (a.lit_aware) run(k_parse_chunks<true, false>, k_parse_deferred<true, false>);
-            else if (simple) run(k_parse_chunks<false, true>, k_parse_deferred<false, true>);
-            else run(k_parse_chunks<false, false>, k_parse_deferred<false, false>);
+            // (several LogFormats: one instance; their first leaves are walked per lane)
+            if (a.multi) run(k_parse_chunks<true, false, true>, k_parse_deferred<true, false, true>);
+            else if (a.lit_aware && simple) run(k_parse_chunks<true, true, false>, k_parse_deferred<true, true, false>);
+            else if (a.lit_aware) run(k_parse_chunks<true, false, false>, k_parse_deferred<true, false, false>);
+            else if (simple) run(k_parse_chunks<false, true, false>, k_parse_deferred<false, true, false>);
+            else run(k_parse_chunks<false, false, false>, k_parse_deferred<false, false, false>);
             const size_t lds_ovf = 16 * (size_t)a.n_elems + 4 * (size_t)cp.stk_words;
+            if (a.multi) {
+                // the queued lines' match words, then the sticky routing scan
+                // over every line's word (fmt_id of every line, the state after
+                // the batch)
+                hipLaunchKernelGGL(k_route_ovf, dim3((unsigned)grid), dim3(PW), lds_ovf, s, a.buf, a.nbytes, d_args,
+                                   cp.stk_words);
+                if (launch_route(d_args, a.cap_lines, s) != 0) return -1;
+            }
             hipLaunchKernelGGL(k_parse_ovf_lines, dim3((unsigned)grid), dim3(PW), lds_ovf, s, a.buf, a.nbytes, d_args,
                                cp.stk_words);
         }

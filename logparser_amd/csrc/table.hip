@@ -125,6 +125,67 @@ __device__ double decimal_to_double(const LP_G uint8_t* p, uint32_t n) {
     return ldexp((double)m, shift - k);
 }
 
+// ResponseSetCookieDissector.dissect (dissectors/ResponseSetCookieDissector.java:86-135) on one
+// cookie string [cp, cp + cn) -- the cookie's LAST cookie string (every
+// dissection of a name reads the Parsable's cached last value,
+// core/Parsable.java:172-183): split(";"), each part trimmed and split("=", 2),
+// key and value trimmed; part 0's value is "value", a later part keyed
+// "expires" / "domain" / "comment" / "path" delivers that output (the last such
+// part wins, ParsedRecord).  Out of line: the table kernels' other columns
+// keep their registers.  kind / p / n / l as TVal.
+__device__ __noinline__ void setcookie_attr(const LP_G uint8_t* cp, uint32_t cn, int fld, int& kind,
+                                            const LP_G uint8_t*& p, uint32_t& n, int64_t& l) {
+    auto pk = [](const char* k) {
+        uint64_t x = 0;
+        for (int q = 0; k[q]; ++q) x |= (uint64_t)(uint8_t)k[q] << (8 * q);
+        return x;
+    };
+    const uint64_t want = fld == SC_DOMAIN ? pk("domain") : fld == SC_COMMENT ? pk("comment") : fld == SC_PATH ? pk("path")
+                                                                                                    : pk("expires");
+    const uint32_t klen = fld == SC_DOMAIN ? 6u : fld == SC_COMMENT ? 7u : fld == SC_PATH ? 4u : 7u;
+    for (uint32_t ps = 0, part = 0; ps <= cn; ++part) {
+        uint32_t pe = ps;
+        while (pe < cn && cp[pe] != ';') ++pe;
+        uint32_t a = ps, b = pe;
+        while (a < b && cp[a] <= ' ') ++a;
+        while (b > a && cp[b - 1] <= ' ') --b;
+        uint32_t x = a;
+        while (x < b && cp[x] != '=') ++x;
+        uint32_t ka = a, kb = x, va = x < b ? x + 1 : b, vb = b;
+        while (kb > ka && cp[kb - 1] <= ' ') --kb;
+        while (va < vb && cp[va] <= ' ') ++va;
+        if (part == 0) {
+            if (fld == SC_VALUE) { kind = 1; p = cp + va; n = vb - va; }
+        } else if (fld != SC_VALUE && kb - ka == klen) {
+            uint64_t k = 0;
+            for (uint32_t q = 0; q < klen; ++q) k |= (uint64_t)cp[ka + q] << (8 * q);
+            if (k == want) {
+                if (fld == SC_EXPIRES_S || fld == SC_EXPIRES_MS) {
+                    // parseExpire: "EEE, dd-MMM-yyyy HH:mm:ss GMT" (the only layout the
+                    // phase-1 guard lets through) -> epoch seconds * 1000; STRING:expires
+                    // is that / 1000 (ResponseSetCookieDissector.java:104-107, 137-150)
+                    const LP_G uint8_t* d = cp + va;
+                    int mon = 1;
+                    for (int q = 0; q < 12; ++q)
+                        if (d[8] == (uint8_t)MONTH_TEXT[MONTH_OFF[q]] && d[9] == (uint8_t)MONTH_TEXT[MONTH_OFF[q] + 1] &&
+                            d[10] == (uint8_t)MONTH_TEXT[MONTH_OFF[q] + 2])
+                            mon = q + 1;
+                    auto d2 = [&](int q) { return (int)(d[q] - '0') * 10 + (int)(d[q + 1] - '0'); };
+                    const int64_t days = days_from_civil(d2(12) * 100 + d2(14), mon, d2(5));
+                    const int64_t ms = (days * 86400 + d2(17) * 3600 + d2(20) * 60 + d2(23)) * 1000;
+                    kind = 2;
+                    l = fld == SC_EXPIRES_S ? ms / 1000 : ms;
+                } else {
+                    kind = 1;
+                    p = cp + va;
+                    n = vb - va;
+                }
+            }
+        }
+        ps = pe + 1;
+    }
+}
+
 __device__ TVal tvalue(const Program& P, const Columns& C, const TableArgs& T, const TableSrc& s, int64_t i,
                        const LP_G uint8_t* line, const LP_G uint8_t* region) {
     TVal v;
@@ -280,13 +341,7 @@ __device__ TVal tvalue(const Program& P, const Columns& C, const TableArgs& T, c
         return v;
     }
     case TC_SETC: {
-        // ResponseSetCookieDissector.dissect (dissectors/ResponseSetCookieDissector.java:86-135) on
-        // the cookie's LAST cookie string (every dissection of a name reads the
-        // Parsable's cached last value, core/Parsable.java:172-183): split(";"),
-        // each part trimmed and split("=", 2), key and value trimmed; part 0's
-        // value is "value", a later part keyed "expires" / "domain" / "comment" /
-        // "path" delivers that output (the last such part wins, ParsedRecord)
-        const int j = s.a & 0xFF, fld = s.a >> 8;
+        const int j = s.a & 0xFF;
         const uint32_t cnt = C.p_count[j][i];
         const LP_G uint64_t* t = reinterpret_cast<const LP_G uint64_t*>(region + ref_off(C.p_tab[j][i]));
         uint64_t cref = 0;
@@ -299,49 +354,7 @@ __device__ TVal tvalue(const Program& P, const Columns& C, const TableArgs& T, c
             for (int q = 0; q < s.c && same; ++q) same = np[q] == T.names[s.b + q];
             if (same) { cref = t[2 * k + 1]; found = true; }
         }
-        if (!found) return v;
-        const LP_G uint8_t* cp = (ref_arena(cref) ? region : line) + ref_off(cref);
-        const uint32_t cn = ref_len(cref);
-        const char* key = fld == SC_DOMAIN ? "domain" : fld == SC_COMMENT ? "comment" : fld == SC_PATH ? "path" : "expires";
-        const uint32_t klen = fld == SC_DOMAIN ? 6u : fld == SC_COMMENT ? 7u : fld == SC_PATH ? 4u : 7u;
-        for (uint32_t ps = 0, part = 0; ps <= cn; ++part) {
-            uint32_t pe = ps;
-            while (pe < cn && cp[pe] != ';') ++pe;
-            uint32_t a = ps, b = pe;
-            while (a < b && cp[a] <= ' ') ++a;
-            while (b > a && cp[b - 1] <= ' ') --b;
-            uint32_t x = a;
-            while (x < b && cp[x] != '=') ++x;
-            uint32_t ka = a, kb = x, va = x < b ? x + 1 : b, vb = b;
-            while (kb > ka && cp[kb - 1] <= ' ') --kb;
-            while (va < vb && cp[va] <= ' ') ++va;
-            if (part == 0) {
-                if (fld == SC_VALUE) bytes(cp + va, vb - va);
-            } else if (fld != SC_VALUE && kb - ka == klen) {
-                bool m = true;
-                for (uint32_t q = 0; q < klen && m; ++q) m = cp[ka + q] == (uint8_t)key[q];
-                if (m) {
-                    if (fld == SC_EXPIRES_S || fld == SC_EXPIRES_MS) {
-                        // parseExpire: "EEE, dd-MMM-yyyy HH:mm:ss GMT" (the only layout the
-                        // phase-1 guard lets through) -> epoch seconds * 1000; STRING:expires
-                        // is that / 1000 (ResponseSetCookieDissector.java:104-107, 137-150)
-                        const LP_G uint8_t* d = cp + va;
-                        int mon = 1;
-                        for (int q = 0; q < 12; ++q)
-                            if (d[8] == (uint8_t)MONTH_TEXT[MONTH_OFF[q]] && d[9] == (uint8_t)MONTH_TEXT[MONTH_OFF[q] + 1] &&
-                                d[10] == (uint8_t)MONTH_TEXT[MONTH_OFF[q] + 2])
-                                mon = q + 1;
-                        auto d2 = [&](int q) { return (int)(d[q] - '0') * 10 + (int)(d[q + 1] - '0'); };
-                        const int64_t days = days_from_civil(d2(12) * 100 + d2(14), mon, d2(5));
-                        const int64_t ms = (days * 86400 + d2(17) * 3600 + d2(20) * 60 + d2(23)) * 1000;
-                        along(fld == SC_EXPIRES_S ? ms / 1000 : ms);
-                    } else {
-                        bytes(cp + va, vb - va);
-                    }
-                }
-            }
-            ps = pe + 1;
-        }
+        if (found) setcookie_attr((ref_arena(cref) ? region : line) + ref_off(cref), ref_len(cref), s.a >> 8, v.kind, v.p, v.n, v.l);
         return v;
     }
     case TC_QP: {  // the parameter's last occurrence (ParsedRecord: the last value wins)
@@ -516,23 +529,6 @@ __global__ __launch_bounds__(64 * CW) void k_table_chars(const DeviceArgs* __res
                 if (r + st < nrows && off[r + st] <= x0) r += st;
             uint32_t nxt = off[r + 1], beg = off[r], fl = s_flag[wv][r];
             uint64_t sp = s_src[wv][r];
-            // the common case: the word's 4 bytes are 4 consecutive source
-            // bytes of one row (a value in the input / arena): ONE unaligned
-            // dword load (gfx950 global loads take any byte alignment) instead
-            // of 4 byte loads
-            {
-                const uint32_t o = x0 - beg;
-                if (t0 == 0 && x0 + 4 <= nxt && !(fl & 1u) && !((fl & 2u) && o == 0)) {
-                    typedef uint32_t u32u __attribute__((aligned(1)));
-                    const uint32_t w = *(const LP_G u32u*)(reinterpret_cast<const LP_G uint8_t*>((uintptr_t)sp) + o - (fl >> 1));
-                    bv[u][0] = (uint8_t)w;
-                    bv[u][1] = (uint8_t)(w >> 8);
-                    bv[u][2] = (uint8_t)(w >> 16);
-                    bv[u][3] = (uint8_t)(w >> 24);
-                    have[u] = 15u;
-                    continue;
-                }
-            }
 #pragma unroll
             for (uint32_t t = 0; t < 4; ++t) {
                 const uint32_t x = x0 + t - t0;

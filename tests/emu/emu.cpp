@@ -148,7 +148,20 @@ static int run_line(const Program& P, const LN& L, const uint8_t* base, uint32_t
         fmt_state = fmt_apply(fmt_table(m, P.n_fmt), fmt_state);
         R.fmt_id.assign(1, (uint8_t)fmt_state);
     }
-    if (P.n_fmt > 1) phase1<true>(P, P.elems, L, o, stk, C, 0, false, (int)fmt_state);  // as k_parse_lines
+    bool pre = false;
+    if (P.n_fmt > 1) {
+        // as the one-pass chunk kernel (parse.hip parse_chunk<..., MF>): a line
+        // exactly one format matches without the DFS is parsed from the spans
+        // the routing word captured (phase1 PRE); the rest as k_parse_ovf_lines
+        // does after the routing scan (the whole phase 1 on the routed format)
+        bool redo = false;
+        const uint32_t w = fmt_match_word<false>(P, P.elems, L, stk, false, &redo, &o.caps);
+        const uint32_t mm = w & 0xFFu;
+        pre = !redo && !(w >> 8) && mm && !(mm & (mm - 1));
+        if (pre && (uint32_t)__builtin_ctz(mm) != fmt_state) return -2;  // (the state must agree: exactness check)
+    }
+    if (pre) phase1<true, true, false, false, true>(P, P.elems, L, o, stk, C, 0, false, (int)fmt_state);
+    else if (P.n_fmt > 1) phase1<false>(P, P.elems, L, o, stk, C, 0, false, (int)fmt_state);  // as k_parse_ovf_lines
     else if (lit_aware(P)) phase1<false, true>(P, P.elems, L, o, stk, C, 0, false, 0);  // as k_parse_chunks<true>
     else phase1<false, false>(P, P.elems, L, o, stk, C, 0, false, 0);            // as k_parse_chunks<false>
     write_line(P, o, C, 0);

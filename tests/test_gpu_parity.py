@@ -332,15 +332,18 @@ def test_strftime_config3_gpu(oracle):
     assert s["bad"] > 300 and s["ok"] > 1000, s
 
 
-def test_mixed_formats_gpu(oracle):
-    """Sticky multi-format routing on the device (match pass + scan of the
-    active format) against the stateful oracle on a mixed corpus, across
-    routing chunks and across two batches of one handle."""
+@pytest.mark.parametrize("one_pass", [1, 0])
+def test_mixed_formats_gpu(oracle, one_pass):
+    """Sticky multi-format routing on the device against the stateful oracle
+    on a mixed corpus (formats that are not mutually exclusive, mutated lines),
+    across routing chunks and across two batches of one handle: one pass
+    (routing inside the chunk kernel, the lines several formats match after
+    the scan) and the index / routing / parse passes (LP_OPT_ONE_PASS 0)."""
     from test_emu_parity import MIXED, mixed_lines, mutate
     fields = paths(oracle, MIXED)
     rng = random.Random(57)
     lines = [mutate(rng, l) if rng.random() < 0.05 else l for l in mixed_lines(30000, 58)]
-    p = lpa.HttpdLoglineParser(MIXED, fields)
+    p = lpa.HttpdLoglineParser(MIXED, fields, options={lpa.OPT_ONE_PASS: one_pass})
     o = oracle.Oracle(MIXED, fields)
     for part in (lines[:17000], lines[17000:]):
         r = p.parse_batch(b"".join(l + b"\n" for l in part))
@@ -993,7 +996,7 @@ def test_chunk_excess_instances_gpu(oracle, wl):
             lines += [b"x"] * rng.randrange(70, 260)  # > 64 line starts in one chunk
         if i % 300 == 17:
             lines.append(b"-" * rng.randrange(1, 5))  # short lines between them
-    fields = paths(oracle)
+    fields = paths(oracle, fmt)
     s, r = gpu_vs_oracle(oracle, fmt, fields, lines)
     assert s["ok"] > 3500, s
     assert r.diag["overflow_waves"] > 1000, r.diag  # (chunked: lines queued for k_parse_ovf_lines)

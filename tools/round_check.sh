@@ -1,6 +1,6 @@
 #!/bin/bash
 # One GPU call: every -m gpu test, smoke(), the default bench line (config 2,
-# 100 M lines), then configs 3 and 4 (bench lines only).  Each step under its
+# 100 M lines), then configs 3, 4 and 5 (bench lines only).  Each step under its
 # own time limit; stops at the first failure.
 #   tools/round_check.sh TAG [skip-tests]
 set -uo pipefail
@@ -18,7 +18,7 @@ if [ "${2:-}" != "skip-tests" ]; then
 fi
 timeout -k 10 600 python3 bench.py > "$O/bench.json" 2> "$O/bench.err" || { echo "bench failed"; tail "$O/bench.err"; exit 1; }
 python3 -c "import json;d=json.loads(open('$O/bench.json').read().strip().splitlines()[-1]);print('value',d['value'],d['kernel_ms'],d['roofline']['frac'],d.get('delivery',{}).get('table_chars_roofline_frac'))"
-for w in 3 4; do
+for w in 3 4 5; do
   timeout -k 10 500 python3 bench.py --workload $w --steps 3 --warmup 1 --no-cpu-baseline --no-delivery \
       > "$O/bench_config$w.json" 2> "$O/bench_config$w.err" || { echo "config $w failed"; tail "$O/bench_config$w.err"; exit 1; }
   python3 -c "import json;d=json.loads(open('$O/bench_config$w.json').read().strip().splitlines()[-1]);print($w, d['value'], d['kernel_ms'], d['roofline']['frac'])"
