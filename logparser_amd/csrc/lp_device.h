@@ -632,6 +632,8 @@ struct RegArr {
         (f((int)J, v[J]), ...);
     }
     __host__ __device__ LP_INLINE uint32_t get(int k) const { return get_(k, std::make_index_sequence<N>{}); }
+    // get with a wave-uniform index 0 <= k < N: one indexed register read
+    __host__ __device__ LP_INLINE uint32_t get_u(int k) const { return v[k]; }
     // set with a wave-uniform index: one indexed register write on the device
     // (the select chain of set() rewrites every element)
     __host__ __device__ LP_INLINE void set_u(int k, uint32_t x) {
@@ -1694,22 +1696,26 @@ __host__ __device__ LP_INLINE int strf_text(int table, int k, uint64_t& lo, uint
 // The element loop of parse_strf_time for a layout of fixed-width elements
 // (T.fixed_w: literals, fixed-width numbers, the 3-letter month / day names,
 // AM / PM, "+HHMM"; e.g. %d/%b/%Y %T) on a value of exactly that width and
-// all ASCII: the value's bytes are read once into registers (one aligned
-// word load per 4 bytes, all in flight together) and every element takes
-// its bytes at its fixed offset, instead of one dependent byte read per
-// byte.  Same fields and the same ST_BAD decisions as the general loop on
-// that subset (each case below restates its element); -1: not applicable,
-// the general loop decides.
+// all ASCII, from the host's plan of the layout (T.fx_*, plan.cpp
+// strf_compile): the value's bytes are read once into registers (one aligned
+// word load per 4 bytes, all in flight together); the literals and the digit
+// positions are checked for all 32 bytes at once with the plan's byte masks;
+// then each field takes its bytes at its fixed offset (a wave-uniform
+// indexed register read) -- no per-element dispatch over T.op.  Every check
+// the general loop makes on this subset fails it with ST_BAD, so checking
+// them all at once decides the same status; the plan exists only when no
+// field is given twice (the "must agree" check stays with the general loop).
+// -1: not applicable, the general loop decides.
 template <typename LN>
 __host__ __device__ LP_INLINE int strf_fixed(const TimeStage& T, const LN& L, int a, int b, RegArr<SF_NFIELDS>& fv,
                                              uint32_t& has) {
     const int W = T.fixed_w;
-    if (W <= 0 || b - a != W) return -1;
+    if (T.fx_n <= 0 || b - a != W) return -1;
     const uint32_t A = L.o + (uint32_t)a, W0 = A >> 2, sh = A & 3;
     uint32_t w[9];
     LP_UNROLL for (int j = 0; j < 9; ++j) w[j] = L.word_or0(W0 + (uint32_t)j);
     RegArr<8> v;
-    uint32_t hi = 0;
+    uint32_t hi = 0, bad = 0;
     LP_UNROLL for (int j = 0; j < 8; ++j) {
 #if defined(__HIP_DEVICE_COMPILE__)
         const uint32_t x = __builtin_amdgcn_alignbyte(w[j + 1], w[j], sh);
@@ -1719,73 +1725,70 @@ __host__ __device__ LP_INLINE int strf_fixed(const TimeStage& T, const LN& L, in
         v.v[j] = x;
         const int r = W - 4 * j;  // the value's bytes in this word
         hi |= r >= 4 ? (x & swar::HI) : r > 0 ? (x & swar::HI & ((1u << (8 * r)) - 1u)) : 0u;
+        // CharLiteralPrinterParser (case-insensitive) at the literal bytes
+        bad |= ((x | T.fx_fold[j]) ^ T.fx_lit[j]) & T.fx_litm[j];
+        // '0'..'9' at the digit bytes (ASCII: no carry leaves a byte)
+        const uint32_t t = x ^ 0x30303030u;
+        bad |= (t | (t + 0x06060606u)) & 0xF0F0F0F0u & T.fx_dig[j];
     }
     if (hi) return -1;  // non-ASCII: the general loop (its text elements fall back)
-    auto byte = [&](int i) { return (v.get(i >> 2) >> (8 * (i & 3))) & 0xFFu; };  // i is uniform
-    auto low = [](uint32_t c) { return c | 0x20u; };
-    int off = 0;
-    for (int k = 0; k < T.n_ops; ++k) {
-        const uint32_t op = T.op[k];
-        const int kind = (int)(op & 0xFF), field = (int)((op >> 8) & 0xFF), width = (int)((op >> 16) & 0xFF);
-        const uint32_t arg = op >> 24;
+    if (bad) return ST_BAD;
+    for (int k = 0; k < T.fx_n; ++k) {
+        const uint32_t f = T.fx_f[k];
+        const int off = (int)(f & 0xFF), width = (int)((f >> 8) & 0xFF), field = (int)((f >> 16) & 0xFF);
+        const uint32_t code = f >> 24;
+        // the field's bytes [off, off + 8) (off is wave-uniform)
+        const int wi = off >> 2, bs = 8 * (off & 3);
+        const uint64_t w01 = (uint64_t)v.get_u(wi) | (uint64_t)(wi + 1 < 8 ? v.get_u(wi + 1) : 0u) << 32;
+        const uint32_t w2 = wi + 2 < 8 ? v.get_u(wi + 2) : 0u;
+        const uint64_t u = bs ? (w01 >> bs) | ((uint64_t)w2 << (64 - bs)) : w01;
         uint32_t val = 0;
-        switch (kind) {
-        case SE_LIT: {  // CharLiteralPrinterParser, case-insensitive
-            const uint32_t c = byte(off);
-            if (!(c == arg || ((arg | 0x20u) - 'a' < 26u && low(c) == (arg | 0x20u)))) return ST_BAD;
-            ++off;
-            continue;
-        }
-        case SE_NUM: case SE_RED2: {  // fixed width, NOT_NEGATIVE; reduced: base 2000
-            for (int q = 0; q < width; ++q) {
-                const uint32_t d = byte(off + q) - '0';
-                if (d > 9) return ST_BAD;
-                val = val * 10 + d;
-            }
-            off += width;
-            if (kind == SE_RED2) val += 2000;
+        switch (code & 0xF) {
+        case FX_NUM: case FX_RED2:  // fixed width, NOT_NEGATIVE (digits checked above); reduced: base 2000
+            for (int q = 0; q < width; ++q) val = val * 10 + (uint32_t)((u >> (8 * q)) & 0xF);
+            if ((code & 0xF) == FX_RED2) val += 2000;
             break;
-        }
-        case SE_TEXT: {  // every entry of these tables has the same length n: the first that matches
-            const int n = arg == ST_MON_SHORT || arg == ST_DOW_SHORT ? 3 : 2;
-            uint64_t tlo = 0;
-            for (int q = 0; q < n; ++q) tlo |= (uint64_t)low(byte(off + q)) << (8 * q);
-            const int nt = arg == ST_MON_SHORT ? 12 : arg == ST_DOW_SHORT ? 7 : 2;
-            const uint64_t m = (1ull << (8 * n)) - 1;
+        case FX_TEXT: {  // TextPrinterParser: every entry of these tables has the same length
+            const uint32_t tb = code >> 4;
             int best = -1;
-            for (int t = 0; t < nt; ++t) {
-                uint64_t elo;
-                uint32_t ehi;
-                strf_text((int)arg, t, elo, ehi);
-                if (best < 0 && ((tlo ^ elo) & m) == 0) best = t;
+            if (tb == ST_MON_SHORT || tb == ST_DOW_SHORT) {
+                const uint32_t tlo = (uint32_t)u | 0x202020u;
+                if (tb == ST_MON_SHORT) {
+                    LP_UNROLL for (int t = 0; t < 12; ++t) {
+                        uint64_t elo; uint32_t ehi;
+                        strf_text(ST_MON_SHORT, t, elo, ehi);
+                        if (best < 0 && ((tlo ^ (uint32_t)elo) & 0xFFFFFFu) == 0) best = t;
+                    }
+                } else {
+                    LP_UNROLL for (int t = 0; t < 7; ++t) {
+                        uint64_t elo; uint32_t ehi;
+                        strf_text(ST_DOW_SHORT, t, elo, ehi);
+                        if (best < 0 && ((tlo ^ (uint32_t)elo) & 0xFFFFFFu) == 0) best = t;
+                    }
+                }
+                if (best < 0) return ST_BAD;
+                val = (uint32_t)best + 1;
+            } else {  // AM / PM
+                const uint32_t tlo = ((uint32_t)u | 0x2020u) & 0xFFFFu;
+                if (tlo == 0x6D61u) val = 0;       // "am"
+                else if (tlo == 0x6D70u) val = 1;  // "pm"
+                else return ST_BAD;
             }
-            if (best < 0) return ST_BAD;
-            off += n;
-            val = arg == ST_AMPM_UP || arg == ST_AMPM_LOW ? (uint32_t)best : (uint32_t)best + 1;
             break;
         }
-        case SE_OFF: {  // appendOffset("+HHMM", "+0000")
-            const uint32_t sg = byte(off);
-            int of = 0;
-            if (!(sg == '+' && byte(off + 1) == '0' && byte(off + 2) == '0' && byte(off + 3) == '0' && byte(off + 4) == '0')) {
-                if (sg != '+' && sg != '-') return ST_BAD;
-                for (int q = 1; q <= 4; ++q) if (byte(off + q) - '0' > 9u) return ST_BAD;
-                const int oh = (int)(byte(off + 1) - '0') * 10 + (int)(byte(off + 2) - '0');
-                const int om = (int)(byte(off + 3) - '0') * 10 + (int)(byte(off + 4) - '0');
-                if (oh > 59 || om > 59) return ST_BAD;
-                of = (sg == '-' ? -1 : 1) * (oh * 3600 + om * 60);
-            }
-            off += 5;
-            val = (uint32_t)of;
+        default: {  // FX_OFF, appendOffset("+HHMM", "+0000") (digits checked above)
+            const uint32_t sg = (uint32_t)u & 0xFF;
+            if (sg != '+' && sg != '-') return ST_BAD;
+            const int oh = (int)((u >> 8) & 0xF) * 10 + (int)((u >> 16) & 0xF);
+            const int om = (int)((u >> 24) & 0xF) * 10 + (int)((u >> 32) & 0xF);
+            if (oh > 59 || om > 59) return ST_BAD;
+            val = (uint32_t)((sg == '-' ? -1 : 1) * (oh * 3600 + om * 60));
             break;
         }
-        default: return -1;  // (not a fixed layout: fixed_w is 0 then)
         }
-        // DateTimeParseContext.setParsedField: a field parsed twice must agree
-        if (((has >> field) & 1u) && fv.get(field) != val) return ST_BAD;
-        has |= 1u << field;
         fv.set_u(field, val);
     }
+    has |= T.fx_has;
     return ST_OK;
 }
 

@@ -140,6 +140,10 @@ enum : uint8_t {
 enum : uint8_t { SE_LIT, SE_NUM, SE_NUMV, SE_PAD2, SE_RED2, SE_TEXT, SE_OFF, SE_ZONE };
 enum : uint8_t { ST_MON_SHORT, ST_MON_FULL, ST_DOW_SHORT, ST_DOW_FULL, ST_AMPM_UP, ST_AMPM_LOW };
 constexpr int MAX_SF_OPS = 128;
+// fields of a fixed-layout plan (TimeStage::fx_f): number, reduced number
+// (base 2000), a text table (ST_MON_SHORT / ST_DOW_SHORT / AMPM), offset "+HHMM"
+enum : uint8_t { FX_NUM, FX_RED2, FX_TEXT, FX_OFF };
+constexpr int MAX_FX = 12;
 // Stage structs hold 32-bit fields only: the kernels read them with scalar
 // (dword) loads.
 struct TimeStage {
@@ -150,6 +154,14 @@ struct TimeStage {
     int32_t fixed_w; // TK_STRF: every op has a fixed width and they total fixed_w bytes (<= 32), else 0
     int32_t n_ops;
     uint32_t op[MAX_SF_OPS];
+    // TK_STRF with fixed_w and no field parsed twice: the layout as byte
+    // masks over the value's 32 bytes (strf_fixed); fx_n = 0: no such plan
+    int32_t fx_n;                  // fields
+    uint32_t fx_has;               // their SF_* bits
+    uint32_t fx_lit[8], fx_litm[8]; // literal bytes (letters lower-case) and their positions
+    uint32_t fx_fold[8];           // 0x20 at the literal letters (case-insensitive)
+    uint32_t fx_dig[8];            // 0xFF at the bytes that must be ASCII digits
+    uint32_t fx_f[MAX_FX];         // offset | width << 8 | field << 16 | FX_* code << 24
 };
 
 // HttpFirstLineDissector on an HTTP.FIRSTLINE token

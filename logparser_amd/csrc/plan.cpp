@@ -277,6 +277,43 @@ static bool strf_compile(const std::string& f, TimeStage& T) {
         }
     }
     if (w > 0 && w <= 32) T.fixed_w = w;
+    // ... and as byte masks + field offsets (strf_fixed): a value of that
+    // width whose literals, digits and fields all check is the general loop's
+    // parse, any failing check its ST_BAD; a field given twice (the general
+    // loop's "must agree" check) keeps the general loop
+    T.fx_n = 0;
+    T.fx_has = 0;
+    for (int j = 0; j < 8; ++j) T.fx_lit[j] = T.fx_litm[j] = T.fx_fold[j] = T.fx_dig[j] = 0;
+    if (T.fixed_w > 0) {
+        int off = 0, nf = 0;
+        bool ok = true;
+        auto put = [&](uint32_t* a, int i, uint32_t byte) { a[i >> 2] |= byte << (8 * (i & 3)); };
+        for (int e = 0; e < T.n_ops && ok; ++e) {
+            const int kind = T.op[e] & 0xFF, field = (T.op[e] >> 8) & 0xFF, width = (T.op[e] >> 16) & 0xFF;
+            const int arg = T.op[e] >> 24;
+            if (kind == SE_LIT) {
+                const bool letter = ((arg | 0x20) - 'a') < 26;
+                put(T.fx_lit, off, letter ? (uint32_t)(arg | 0x20) : (uint32_t)arg);
+                put(T.fx_litm, off, 0xFF);
+                if (letter) put(T.fx_fold, off, 0x20);
+                ++off;
+                continue;
+            }
+            int code, n;
+            switch (kind) {
+            case SE_NUM: case SE_RED2: code = kind == SE_NUM ? FX_NUM : FX_RED2; n = width; break;
+            case SE_TEXT: code = FX_TEXT | (arg << 4); n = arg == ST_MON_SHORT || arg == ST_DOW_SHORT ? 3 : 2; break;
+            default: code = FX_OFF; n = 5; break;  // SE_OFF (fixed_w admits no other kind)
+            }
+            if (nf >= MAX_FX || (T.fx_has >> field) & 1u || n > 8) { ok = false; break; }
+            for (int q = 0; q < n; ++q)
+                if ((code == FX_NUM || code == FX_RED2) || (code == FX_OFF && q > 0)) put(T.fx_dig, off + q, 0xFF);
+            T.fx_f[nf++] = (uint32_t)off | (uint32_t)n << 8 | (uint32_t)field << 16 | (uint32_t)code << 24;
+            T.fx_has |= 1u << field;
+            off += n;
+        }
+        if (ok && off == T.fixed_w) T.fx_n = nf;
+    }
     return true;
 }
 

@@ -87,6 +87,31 @@ int emu_parse_in(void* h, const char* buf, int64_t start, int len, char* out, in
 
 void emu_set_masks(int on) { g_masks_fwd(on); }
 
+// parse_strf_time of the program's first time stage on the value v[0, len)
+// placed at byte offset `off` (0..3) of an aligned buffer, with the stage's
+// fixed-layout plan (use_fixed 1) or the general element loop only (0):
+// out = {status, epoch_ms, local, utc, nanos}; returns -1 without a strftime stage
+int emu_strf(void* h, const char* v, int len, int off, int use_fixed, int64_t* out) {
+    const Program& P = ((Emu*)h)->plan.program();
+    if (P.n_time < 1 || P.time[0].kind != TK_STRF) return -1;
+    TimeStage T = P.time[0];
+    if (!use_fixed) { T.fx_n = 0; T.fixed_w = 0; }
+    std::vector<uint8_t> buf((size_t)off, 0xA5);
+    buf.insert(buf.end(), v, v + len);
+    buf.resize(((buf.size() + 8 + 3) & ~(size_t)3) + 40, 0xA5);  // word reads past the value
+    const Line L{buf.data(), (uint32_t)off, len};
+    int64_t ep = 0;
+    uint64_t lo = 0, ut = 0;
+    uint32_t ns = 0;
+    const int st = parse_strf_time(T, L, 0, len, ep, lo, ut, ns);
+    out[0] = st;
+    out[1] = ep;
+    out[2] = (int64_t)lo;
+    out[3] = (int64_t)ut;
+    out[4] = ns;
+    return T.fx_n;
+}
+
 // the planner's token table (plan.cpp) as canonical JSON; returns its length
 int emu_token_table(int nginx, char* out, int cap) {
     const std::string j = lp::token_table_json(nginx != 0);

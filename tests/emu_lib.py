@@ -58,6 +58,9 @@ def lib():
         L.emu_possible_paths.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
         L.emu_token_table.restype = ctypes.c_int
         L.emu_token_table.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        L.emu_strf.restype = ctypes.c_int
+        L.emu_strf.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                               ctypes.POINTER(ctypes.c_int64)]
         _lib = L
     return _lib
 
@@ -113,6 +116,14 @@ class Emu:
             out.append((st, self.buf.value.decode("utf-8") if st in (0, 3) else None))
             start = end + 1
         return out
+
+    def strf(self, value, off, use_fixed):
+        """parse_strf_time of the first time stage on value (bytes) at byte
+        offset off of an aligned buffer, with the fixed-layout plan or the
+        general loop only: (plan fields, (status, epoch_ms, local, utc, nanos))"""
+        out = (ctypes.c_int64 * 5)()
+        n = lib().emu_strf(self.h, value, len(value), off, 1 if use_fixed else 0, out)
+        return n, tuple(out)
 
     def casts(self, target):
         c = lib().emu_casts(self.h, target.encode())

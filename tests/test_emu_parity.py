@@ -732,3 +732,46 @@ def test_type_remapping_same_type_planner(oracle, emu):
     assert o.parse(base % "/p?b=1")[0] == oracle.OK
     assert e.parse(base % "/p?b=1")[0] == 2
 
+
+
+def test_strftime_fixed_plan_edges_emulated(emu):
+    """strf_fixed (the fixed-layout plan: all literals and digit positions
+    checked at once with byte masks, fields at fixed offsets) decides every
+    value exactly as the general element loop: valid values at every byte
+    offset of a word, every single-byte mutation of them (digits, letters in
+    both cases, separators, non-ASCII), wrong widths, offsets "+0000" /
+    "-0000" / out-of-range, and a layout with a field given twice (no plan:
+    the general loop's "must agree" check)."""
+    import random
+    import strf_corpus
+    rng = random.Random(20261018)
+    cases = [("%d/%b/%Y %T", True), ("%a, %d %b %Y %T %z", True), ("%D %r", True), ("%Y-%j %H:%M", True),
+             ("%d/%b/%Y %I:%M %P", True), ("%F %T.msec_frac %z", True), ("%F %R:%S.usec_frac", True),
+             ("%d/%b/%Y %T %d", False), ("%a %A", False)]
+    alphabet = b"0123456789aAbBzZ:/ .,+-\x80\xc3"
+    n_vals = 0
+    for pat, plan in cases:
+        e = emu.Emu('%h [%{' + pat + '}t] "%r"', strf_corpus.FIELDS)
+        assert e.status == 0, (pat, e.err)
+        vals = []
+        for _ in range(40):
+            dt = strf_corpus.datetime.datetime(1971, 1, 1) + strf_corpus.datetime.timedelta(
+                seconds=rng.randrange(0, 60 * 365 * 86400), microseconds=rng.randrange(1000000))
+            v = strf_corpus.render(pat, dt, rng.choice([0, -300, 330, 60 * 14]))
+            vals.append(v.encode())
+        v0 = vals[0]
+        for i in range(len(v0)):  # every position, several replacement bytes
+            for c in rng.sample(alphabet, 6):
+                vals.append(v0[:i] + bytes([c]) + v0[i + 1:])
+        vals += [v0[:-1], v0 + b"0", v0.upper(), v0.lower(), b""]
+        if b"+" in v0 or b"-" in v0[-5:]:
+            k = len(v0) - 5
+            vals += [v0[:k] + z for z in (b"+0000", b"-0000", b"+1860", b"-0960", b"+2400", b"|0100", b"+0a00")]
+        for v in vals:
+            for off in range(4):
+                nf, fixed = e.strf(v, off, True)
+                _, general = e.strf(v, off, False)
+                assert (nf > 0) == plan, (pat, nf)
+                assert fixed == general, (pat, v, off, fixed, general)
+                n_vals += 1
+    assert n_vals > 3000
