@@ -54,7 +54,7 @@ struct ParseLaunch {
 // each), an LDS window of win_cap bytes (the chunk, 64 bytes before it, the
 // tail of its last line), n_chunks chunks.
 struct ChunkPlan {
-    uint32_t cb, win_cap, stk_words;
+    uint32_t cb, win_cap, stk_words, chunk_stk;  // stk_words: the queued lines' kernels; chunk_stk: the chunk kernels'
     int waves_per_cu;
     size_t lds;
     int64_t n_chunks;

@@ -28,7 +28,16 @@ namespace {
 // to Parser.parse.  Here the lines of a byte chunk are found by the wave that
 // parses them: a line belongs to the chunk holding its first byte.
 
-constexpr int MAXS = PW + 1;  // line starts a chunk keeps in LDS (its 64 lines and the next start)
+constexpr int MAXS = PW + 1;
+#ifndef LP_CHUNK_MAXW
+#define LP_CHUNK_MAXW 10  // waves per CU the chunk plan may size the LDS window for
+#endif
+#ifndef LP_CHUNK_LMAX
+#define LP_CHUNK_LMAX 54  // lines per chunk at most (one-format programs)
+#endif
+#ifndef LP_CHUNK_LMAX_MF
+#define LP_CHUNK_LMAX_MF 58  // the same for several-format programs (VGPR-bound at 8 waves per CU: 58 measured 6 % faster than 54 on config 5)
+#endif  // line starts a chunk keeps in LDS (its 64 lines and the next start)
 constexpr uint64_t CS_AGG = 1ull << 62, CS_INC = 1ull << 63, CS_CNT = CS_AGG - 1;
 
 // the line index, written by the chunked parse kernel (read-only elsewhere)
@@ -732,22 +741,52 @@ WindowPlan window_plan(const ParseLaunch& a) {
 ChunkPlan chunk_plan(const ParseLaunch& a) {
     ChunkPlan c{};
     c.stk_words = (uint32_t)(a.stack_depth > 0 ? a.stack_depth : 1) * PW;
-    const uint64_t fixed = 16 * (uint64_t)a.n_elems + 4 * (uint64_t)c.stk_words + 16 * ((4 * MAXS + 15) / 16);
+    // the chunk kernels run no DFS (ST_REDO lines are queued): no stack in
+    // their LDS (the queued lines' kernels have theirs)
+#if defined(LP_DFS_IN_CHUNKS)
+    c.chunk_stk = c.stk_words;
+#else
+    c.chunk_stk = 0;
+#endif
+    const uint64_t fixed = 16 * (uint64_t)a.n_elems + 4 * (uint64_t)c.chunk_stk + 16 * ((4 * MAXS + 15) / 16);
     const uint64_t per8 = 8 + MC_N;  // LDS bytes per 8 window bytes (window + mask planes)
     const uint64_t mean = a.mean_line ? a.mean_line : 256;
-    const uint64_t lines = a.chunk_lines ? a.chunk_lines : 54;  // measured best (tools/chunk_sweep.py): 8 waves per CU on config 2
     const uint64_t oh = std::max<uint64_t>(512, ((2 * mean + 63) & ~63ull));
+    // lines per chunk: at most 54 (measured best at 8 waves per CU, config 2:
+    // tools/chunk_sweep.py), and the count that puts the most lines in
+    // flight per CU (waves x lines) over the wave counts the registers allow
+    // (the several-format instance: 2 waves per SIMD); LP_OPT_CHUNK_LINES
+    // fixes the count
+    uint64_t lines = a.chunk_lines ? a.chunk_lines : 54;
+    if (!a.chunk_lines) {
+        const int maxw = a.multi ? 8 : LP_CHUNK_MAXW;
+        const uint64_t lmax = a.multi ? LP_CHUNK_LMAX_MF : LP_CHUNK_LMAX;
+        uint64_t best = 0;
+        for (int k = 8; k <= maxw; ++k) {
+            const uint64_t budget = 160 * 1024 / k - 640;
+            if (budget <= fixed) break;
+            const uint64_t capk = std::min<uint64_t>(((budget - fixed) * 8 / per8) & ~63ull, 48 * 1024) & ~1023ull;
+            const uint64_t lk = capk > 64 + oh + 63 ? std::min<uint64_t>(lmax, (capk - 64 - oh - 63) / mean) : 0;
+            if (lk >= 16 && (uint64_t)k * lk > best) {
+                best = (uint64_t)k * lk;
+                lines = lk;
+            }
+        }
+    }
     uint64_t cb = ((lines * mean) + 63) & ~63ull;
     if (cb < 1024) cb = 1024;
     const uint64_t need = cb + 64 + oh;
     uint64_t cap = 0;
     int waves = 0;
-    for (int k = 8; k >= 2 && !cap; --k) {
+    for (int k = LP_CHUNK_MAXW; k >= 2 && !cap; --k) {
         const uint64_t budget = 160 * 1024 / k - 640;
         if (budget <= fixed) continue;
         const uint64_t w = ((budget - fixed) * 8 / per8) & ~63ull;
         if (w >= need || k == 2) {
-            cap = std::min<uint64_t>(w, 48 * 1024) & ~1023ull;  // whole 1 KiB LDS-DMA blocks
+            // whole 1 KiB LDS-DMA blocks, no more than the chunk needs (a
+            // wave stages its whole window: a larger one only re-reads the
+            // next chunk's bytes)
+            cap = std::min<uint64_t>(std::min<uint64_t>(w, 48 * 1024), (need + 1023) & ~1023ull) & ~1023ull;
             waves = k;
         }
     }
@@ -800,9 +839,9 @@ int launch_parse(const ParseLaunch& a, const DeviceArgs* d_args, const Columns& 
             // (the instance per program shape: LA, SIMPLE)
             auto run = [&](auto chunks, auto deferred) {
                 hipLaunchKernelGGL(chunks, dim3(g0), dim3(PW), cp.lds, s, a.buf, a.nbytes, d_args, cp.cb, cp.win_cap,
-                                   cp.stk_words, fd, a.chunk_wait);
+                                   cp.chunk_stk, fd, a.chunk_wait);
                 hipLaunchKernelGGL(deferred, dim3(g1), dim3(PW), cp.lds, s, a.buf, a.nbytes, d_args, cp.cb,
-                                   cp.win_cap, cp.stk_words, fd);
+                                   cp.win_cap, cp.chunk_stk, fd);
             };
 #if defined(LP_NO_SIMPLE)  // (experiment builds: every program on the general instances)
             const bool simple = false;

@@ -411,6 +411,7 @@ __device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, Uri
                 piece(ow, g - ob, pqs[k], soffs[k]);
                 if (g < tot) t0[k] = *reinterpret_cast<const LP_G uint64_t*>(C.arena + oab + soffs[k]);
             }
+            LP_PROF(17);
             QPrep qp[QR];
             uint32_t mine = 0;
 #pragma unroll
@@ -421,6 +422,7 @@ __device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, Uri
                 if (g < tot) qp[k] = query_prep(OL, t0[k]);
                 mine += qp[k].need;
             }
+            LP_PROF(18);
             // the round's spilled bytes in one allocation from the wave's
             // shard (every owner is a line of this wave)
             uint32_t x = mine;
@@ -432,6 +434,7 @@ __device__ __forceinline__ void uri_wave(const Program& P, const Columns& C, Uri
             unsigned long long rbase = 0;
             if (lane == 63 && rtot) rbase = atomicAdd(&C.meta->shard_top[16 * shard], (unsigned long long)rtot);
             unsigned long long at = __shfl(rbase, 63) + x - mine;  // this lane's first piece in the shard
+            LP_PROF(19);
 #pragma unroll
             for (int k = 0; k < QR; ++k) {
                 if (g0 + (uint32_t)(k * PW) >= tot) continue;
@@ -485,6 +488,7 @@ __device__ __forceinline__ bool uri_compact(const uint8_t* __restrict__ buf, uin
     const bool active = li < n_lines;
     LP_PROF(23);
     UriLane<NU> U = uri_lane<NU>(P, C, li, active);
+    LP_PROF(27);
     // one region per line: the 16-byte input blocks holding all its URI
     // sources (request URI, referer, ...: close together in a line), in
     // line order; a block keeps its alignment, so the wave gathers whole
@@ -564,6 +568,7 @@ __device__ __forceinline__ bool uri_compact(const uint8_t* __restrict__ buf, uin
             v[k] = u32x4{0, 0, 0, 0};
             if (g < tot) v[k] = load16(buf, nbytes, src);
         }
+        LP_PROF(28);
 #pragma unroll
         for (int k = 0; k < GR; ++k) {
             const uint32_t g = g0 + (uint32_t)(k * PW + lane);

@@ -36,7 +36,8 @@ names = {0: "start", 1: "staged", 2: "phase1 entry", 3: "guard", 4: "match", 5: 
          13: "uri1 out", 21: "phase2 exit", 22: "query pieces", 23: "uri kernel start", 24: "uri copied",
          25: "uri plane", 26: "uri arena", 43: "scheme", 44: "auth end", 45: "ipv4", 46: "hostname", 47: "port",
          60: "chunk staged", 61: "line numbers", 62: "rows written",
-         14: "strf parsed", 15: "strf resolved", 16: "strf fields"}
+         14: "strf parsed", 15: "strf resolved", 16: "strf fields", 27: "uri lane", 28: "uri gather loads",
+         17: "q slots loaded", 18: "q prepared", 19: "q spill allocated"}
 for u in range(2):
     for j, nm in enumerate(["pass1", "authority", "path", "query", "frag"]):
         names[30 + 8 * u + j] = "u%d %s done" % (u, nm)
@@ -46,7 +47,7 @@ for u in range(2):
     names[52 + 4 * u] = "u%d gen walk" % u
 # the parse kernel, then the URI kernel (k_uri_lines): separate orders
 orders = [[0, 60, 1, 2, 3, 4, 5, 14, 15, 16, 6, 7, 9, 61, 62],
-          [23, 24, 25, 26, 10, 50, 51, 52, 30, 31, 32, 33, 34, 11, 12, 54, 55, 56, 38, 43, 44, 45, 46, 47, 39, 40, 41, 42, 13, 21, 22]]
+          [23, 27, 28, 24, 25, 26, 10, 50, 51, 52, 30, 31, 32, 33, 34, 11, 12, 54, 55, 56, 38, 43, 44, 45, 46, 47, 39, 40, 41, 42, 13, 21, 17, 18, 19, 22]]
 print("parse ms %.3f  waves profiled %d" % (st["ms_parse"], int((T[:, 0] != 0).sum())))
 for order in orders:
     acc = {}
