@@ -841,6 +841,92 @@ __host__ __device__ LP_INLINE int uplist_at(const LN& L, int p, bool dec) {
     return e;
 }
 
+// uplist_at on the 32 bytes at p read into registers at once (one aligned
+// word load per 4 bytes, all in flight together) and classified into bit
+// masks (digits, '.', ',', ':', ' '): the runs and separators are found with
+// bit scans instead of one dependent LDS read per byte (the first-leaf
+// candidate of $upstream_response_time was config 4's costliest element,
+// 17 K cycles per wave).  The same steps and results as uplist_at; a list
+// still going at the 32nd byte before the line ends: uplist_at decides.
+template <typename LN>
+__host__ __device__ LP_INLINE int uplist_at_regs(const LN& L, int p, bool dec) {
+    constexpr int UNK = -3;
+    const int avail = L.n - p;  // bytes to the line end
+    const bool open = avail > 32;  // the line goes on past the registers
+    const uint32_t A = L.o + (uint32_t)p, W0 = A >> 2, sh = A & 3;
+    uint32_t x[9];
+    LP_UNROLL for (int j = 0; j < 9; ++j) x[j] = L.word_or0(W0 + (uint32_t)j);
+    uint32_t dg = 0, dot = 0, com = 0, col = 0, sp = 0;
+    LP_UNROLL for (int j = 0; j < 8; ++j) {
+#if defined(__HIP_DEVICE_COMPILE__)
+        const uint32_t v = __builtin_amdgcn_alignbyte(x[j + 1], x[j], sh);
+#else
+        const uint32_t v = (uint32_t)((((uint64_t)x[j + 1] << 32) | x[j]) >> (8 * sh));
+#endif
+        dg |= bcls::nib(swar::digit(v)) << (4 * j);
+        dot |= bcls::nib(swar::eq(v, '.')) << (4 * j);
+        com |= bcls::nib(swar::eq(v, ',')) << (4 * j);
+        col |= bcls::nib(swar::eq(v, ':')) << (4 * j);
+        sp |= bcls::nib(swar::eq(v, ' ')) << (4 * j);
+    }
+    const uint32_t in = avail >= 32 ? ~0u : avail <= 0 ? 0u : (1u << avail) - 1u;  // bytes inside the line
+    dg &= in; dot &= in; com &= in; col &= in; sp &= in;
+    auto bit = [](uint32_t m, int q) { return q < 32 && ((m >> q) & 1u); };
+    // the first position >= q (q <= 32) not in m: the end of a run
+    auto run = [&](uint32_t m, int q) -> int {
+        const int r = q + (int)__builtin_ctzll(~((uint64_t)m >> q));
+        return r >= 32 && open ? UNK : r;
+    };
+    auto X = [&](int q) -> int {  // decimal_at / the digit run at q (relative)
+        if (q >= 32) return open ? UNK : -1;
+        const int d = run(dg, q);
+        if (d == UNK) return UNK;
+        if (!dec) return d > q ? d : -1;
+        if (d == q || d >= avail || !bit(dot, d)) return -1;
+        const int r = run(dg, d + 1);
+        if (r == UNK) return UNK;
+        if (r == d + 1) return -1;
+        if (d - q > 18 || r - d - 1 > 18) return -2;
+        return r;
+    };
+    auto spaces = [&](int q) -> int { return q >= 32 ? (open ? UNK : q) : run(sp, q); };
+    int e = X(0);
+    if (e == UNK) return UNK;
+    if (e < 0) return e;
+    for (;;) {
+        int q = spaces(e);
+        if (q == UNK) return UNK;
+        if (q >= avail || !bit(com, q)) break;
+        const int s = spaces(q + 1);
+        if (s == UNK) return UNK;
+        const int e2 = X(s);
+        if (e2 == UNK) return UNK;
+        if (e2 == -2) return -2;
+        if (e2 < 0) break;
+        e = e2;
+        q = spaces(e);
+        if (q == UNK) return UNK;
+        if (q < avail && bit(col, q)) {
+            const int s3 = spaces(q + 1);
+            if (s3 == UNK) return UNK;
+            const int e3 = X(s3);
+            if (e3 == UNK) return UNK;
+            if (e3 == -2) return -2;
+            if (e3 >= 0) e = e3;
+        }
+    }
+    // a ',' / ':' not followed by ' ' inside the list (e <= 32 here)
+    const uint32_t sep = (com | col) & (e >= 32 ? ~0u : (1u << e) - 1u);
+    if ((sep & ~(sp >> 1)) || (e > 0 && bit(sep, e - 1))) return -2;
+    return p + e;
+}
+
+template <typename LN>
+__host__ __device__ LP_INLINE int uplist_at_r(const LN& L, int p, bool dec) {
+    const int r = uplist_at_regs(L, p, dec);
+    return r == -3 ? uplist_at(L, p, dec) : r;
+}
+
 // The largest item end of the list at p that is < cur (-1 none).  The list
 // was accepted by uplist_at, so its items split cleanly.
 template <typename LN>
@@ -983,8 +1069,8 @@ __host__ __device__ LP_INLINE int cand_first(const Program& P, const ElemV& e, c
         if (!LA || e.last || !e.nlit) return q3;
         return lit_last_call(P, L, e, q3, q2 + 1);
     }
-    case EK_UPLIST_DEC: if constexpr (SIMPLE) return -2; else return uplist_at(L, p, true);
-    case EK_UPLIST_NUM: if constexpr (SIMPLE) return -2; else return uplist_at(L, p, false);
+    case EK_UPLIST_DEC: if constexpr (SIMPLE) return -2; else return uplist_at_r(L, p, true);
+    case EK_UPLIST_NUM: if constexpr (SIMPLE) return -2; else return uplist_at_r(L, p, false);
     case EK_UPLIST_NS: if constexpr (SIMPLE) return -2; else return uplist_ns_end(P, e, L, p);
     case EK_CACHE_STATUS: {
         if constexpr (SIMPLE) return -2;

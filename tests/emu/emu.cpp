@@ -87,6 +87,18 @@ int emu_parse_in(void* h, const char* buf, int64_t start, int len, char* out, in
 
 void emu_set_masks(int on) { g_masks_fwd(on); }
 
+// uplist_at (byte reads) and uplist_at_r (register masks) on the line
+// buf[0, len) at offset p, the line at byte offset `off` of an aligned
+// buffer: out = {uplist_at, uplist_at_r}
+void emu_uplist(const char* v, int len, int p, int off, int dec, int* out) {
+    std::vector<uint8_t> buf((size_t)off, 0xA5);
+    buf.insert(buf.end(), v, v + len);
+    buf.resize(((buf.size() + 8 + 3) & ~(size_t)3) + 40, 0xA5);
+    const Line L{buf.data(), (uint32_t)off, len};
+    out[0] = uplist_at(L, p, dec != 0);
+    out[1] = uplist_at_r(L, p, dec != 0);
+}
+
 // parse_strf_time of the program's first time stage on the value v[0, len)
 // placed at byte offset `off` (0..3) of an aligned buffer, with the stage's
 // fixed-layout plan (use_fixed 1) or the general element loop only (0):

@@ -58,6 +58,8 @@ def lib():
         L.emu_possible_paths.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
         L.emu_token_table.restype = ctypes.c_int
         L.emu_token_table.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        L.emu_uplist.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                 ctypes.POINTER(ctypes.c_int)]
         L.emu_strf.restype = ctypes.c_int
         L.emu_strf.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                ctypes.POINTER(ctypes.c_int64)]
@@ -139,6 +141,13 @@ class Emu:
             lib().emu_free(self.h)
         except Exception:
             pass
+
+
+def uplist(line, p, off, dec):
+    """(uplist_at, uplist_at_r) of the line (bytes) at p"""
+    out = (ctypes.c_int * 2)()
+    lib().emu_uplist(line, len(line), p, off, 1 if dec else 0, out)
+    return out[0], out[1]
 
 
 def possible_paths(logformat, depth=15):

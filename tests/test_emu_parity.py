@@ -775,3 +775,50 @@ def test_strftime_fixed_plan_edges_emulated(emu):
                 assert fixed == general, (pat, v, off, fixed, general)
                 n_vals += 1
     assert n_vals > 3000
+
+
+def test_upstream_list_register_scan_emulated(emu):
+    """uplist_at_r (the first-leaf candidate of NGINX upstream lists from
+    32 bytes in registers, bit masks for digits / '.' / ',' / ':' / ' ')
+    returns what uplist_at (one read per byte) returns: lists of 1-4 items
+    with ", " and " : " separators, space runs, separators without the
+    space or at the end, 19-digit runs, lists ending at the line end or
+    continuing, lists reaching byte 31, 32, 33 and beyond the registers,
+    at every byte offset of a word."""
+    import random
+    rng = random.Random(20261018)
+
+    def item(dec):
+        a = "".join(rng.choice("0123456789") for _ in range(rng.choice([1, 1, 2, 3, 19, 20])))
+        if not dec or rng.random() < 0.1:
+            return a
+        return a + "." + "".join(rng.choice("0123456789") for _ in range(rng.choice([0, 1, 3, 3, 19])))
+    seps = [", ", " : ", ",", ":", " , ", ",  ", " ", ", ,", ": ", "-", ""]
+    n = 0
+    for _ in range(6000):
+        dec = rng.random() < 0.7
+        k = rng.choice([1, 1, 2, 3, 4, 6])
+        s = item(dec)
+        for _ in range(k - 1):
+            s += rng.choice(seps[:2] * 4 + seps) + item(dec)
+        if rng.random() < 0.3:
+            s += rng.choice(seps)
+        pre = rng.choice(["", "x ", "12 ", "- - [a] "])
+        post = rng.choice(["", " ", " .", " p", "\" 200", " " * rng.randint(0, 40) + "x"])
+        line = (pre + s + post).encode()
+        p = len(pre)
+        for off in range(4):
+            a, b = emu.uplist(line, p, off, dec)
+            assert a == b, (line, p, off, dec, a, b)
+            n += 1
+    # every length around the register window
+    for L in range(28, 40):
+        for dec in (True, False):
+            body = ("0.1, " * 10)[:L] if dec else ("1, " * 16)[:L]
+            for post in ("", " p"):
+                line = (body + post).encode()
+                for off in range(4):
+                    a, b = emu.uplist(line, 0, off, dec)
+                    assert a == b, (line, off, dec, a, b)
+                    n += 1
+    assert n > 20000
