@@ -120,8 +120,9 @@ int64_t lp_possible_paths_remapped(const char *logformats, int max_depth, const 
                                   aims for (1..64, 0 = default 54; a chunk's 65th line onwards is
                                   parsed from HBM by a second kernel) */
 #define LP_OPT_CHUNK_WAIT 5    /* tests: polls a chunk's wave makes for its first line number before it
-                                  leaves the chunk to the deferred pass (0 = default 16384; a negative
-                                  value: none, every chunk goes to the deferred pass) */
+                                  leaves the chunk to the deferred pass (0 = default 16384; -1: none,
+                                  every chunk goes to the deferred pass; -2: the odd chunks go to it
+                                  without polling, the even ones wait as by default) */
 #define LP_OPT_ONE_PASS 6      /* several LogFormats: 1 (default) one pass over the input (the chunk kernel
                                   routes every line exactly one format matches; the rest after the
                                   routing scan), 0 the line index, routing and parse passes */

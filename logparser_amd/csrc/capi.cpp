@@ -697,7 +697,7 @@ int lp_set_option(lp_handle* h, int option, int64_t value) {
         h->one_pass = value != 0;
         return LP_OK;
     case LP_OPT_CHUNK_WAIT:
-        h->chunk_wait = value < 0 ? -1 : (int32_t)std::min<int64_t>(value, 1 << 30);
+        h->chunk_wait = value == -2 ? -2 : value < 0 ? -1 : (int32_t)std::min<int64_t>(value, 1 << 30);
         return LP_OK;
     case LP_OPT_MAX_RETRIES:
         if (value < 0 || value > 16) return LP_E_INVALID;
@@ -1069,8 +1069,11 @@ static int table_device(lp_handle* h, int64_t first, int64_t count, lp_table_col
     hipSetDevice(h->device);
     hipStream_t s = h->stream;
     if (!h->targs.ensure(sizeof(lp::TableArgs))) return LP_E_NOMEM;
-    const size_t scratch = lp::table_scratch_bytes(count);
+    int n_str = 0;
+    for (int c = 0; c < n_cols; ++c) n_str += cols[c].kind == LP_CAST_STRING ? 1 : 0;
+    const size_t scratch = lp::table_scratch_bytes(count, n_str);
     if (!h->tscratch.ensure(scratch)) return LP_E_NOMEM;
+    ta->srcw = reinterpret_cast<uint64_t*>((char*)h->tscratch.p + lp::table_srcw_offset(count));
     if (hipMemcpyAsync(h->targs.p, ta.get(), sizeof(lp::TableArgs), hipMemcpyHostToDevice, s) != hipSuccess) return LP_E_DEVICE;
     const lp::DeviceArgs* d_args = h->args.as<lp::DeviceArgs>();
     const lp::TableArgs* d_targs = h->targs.as<lp::TableArgs>();

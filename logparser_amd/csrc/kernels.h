@@ -98,7 +98,9 @@ int launch_histograms(const DeviceArgs* d_args, const uint8_t* buf, int64_t cap_
 // values / validity / STRING offsets of rows [ta.first, ta.first + ta.count)
 // (d_targs: ta on the device; buf: the batch's input); then, once the caller
 // checked the offsets' totals against its capacities, the STRING bytes
-size_t table_scratch_bytes(int64_t count);
+size_t table_scratch_bytes(int64_t count, int n_str);
+// where TableArgs::srcw starts in that scratch
+size_t table_srcw_offset(int64_t count);
 // mid (optional): recorded after k_table_values, before the offset scans
 int launch_table_values(const DeviceArgs* d_args, const TableArgs* d_targs, const TableArgs& ta, const uint8_t* buf,
                         void* scratch, size_t scratch_bytes, hipStream_t s, hipEvent_t mid = nullptr);

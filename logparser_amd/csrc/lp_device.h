@@ -635,7 +635,9 @@ struct RegArr {
     // get with a wave-uniform index 0 <= k < N: one indexed register read
     __host__ __device__ LP_INLINE uint32_t get_u(int k) const { return v[k]; }
     // set with a wave-uniform index: one indexed register write on the device
-    // (the select chain of set() rewrites every element)
+    // (the select chain of set() rewrites every element).  A lane-varying k
+    // is still correct but compiles to a waterfall loop: index by a lane's own
+    // stage (e.g. the SLOT URI instances' u) with set() / get()
     __host__ __device__ LP_INLINE void set_u(int k, uint32_t x) {
         if ((unsigned)k < (unsigned)N) v[k] = x;
     }

@@ -59,9 +59,17 @@ struct TableCol {
     LP_G uint8_t* chars;
 };
 
+// a STRING column's value of one row as k_table_values found it, for
+// k_table_chars (TableArgs::srcw): tag in bits 63:62 -- SW_PTR the bytes'
+// address (bit 61: a leading '&'), SW_LONG a long in bits 61:0 (two's
+// complement), SW_SLOW anything else (a formatted date / time / month name /
+// binary IP, or a long outside 62 bits): k_table_chars derives it again
+constexpr uint64_t SW_AMP = 1ull << 61, SW_LONG = 1ull << 62, SW_SLOW = 2ull << 62;
+
 struct TableArgs {
     int64_t first, count;
     int32_t n_cols, pad;
+    LP_G uint64_t* srcw;  // [STRING column rank][count] value words (scratch)
     TableCol cols[MAX_TABLE_COLS];
     uint8_t names[TABLE_NAMES];
 };

@@ -254,13 +254,14 @@ __device__ __noinline__ void chunk_scanner(LP_G uint64_t* st, int64_t n_chunks) 
 // the wave then leaves the chunk to the deferred pass instead of waiting on,
 // so that no wait depends on the order in which the dispatcher starts the
 // workgroups (a chunk whose wave was never started cannot hold the others).
-// (wait_max: LP_OPT_CHUNK_WAIT, tests; 0 = CHUNK_WAIT_MAX, < 0 = defer
-// without polling)
+// (wait_max: LP_OPT_CHUNK_WAIT, tests; 0 = CHUNK_WAIT_MAX, -1 = defer
+// without polling, -2 = defer the odd chunks without polling, the even ones
+// as normal: finished and deferred chunks side by side, deterministically)
 constexpr uint32_t CHUNK_WAIT_MAX = 1u << 14;
 __device__ __forceinline__ uint64_t chunk_base(LP_G uint64_t* st, int64_t c, uint64_t count, int wait_max) {
-    if (wait_max < 0) return ~0ull;
+    if (wait_max < 0 && (wait_max != -2 || (c & 1))) return ~0ull;
     uint64_t v = 0;
-    const uint32_t lim = wait_max == 0 ? CHUNK_WAIT_MAX : (uint32_t)wait_max;
+    const uint32_t lim = wait_max <= 0 ? CHUNK_WAIT_MAX : (uint32_t)wait_max;
     if (lane_id() == 0) {
         for (uint32_t it = 0;; ++it) {
             v = __hip_atomic_load(&st[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

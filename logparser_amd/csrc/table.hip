@@ -7,7 +7,8 @@
 //
 //   k_table_values  one lane per row: each column's value from the source the
 //                   planner named (lp_table.h), the validity byte, LONG /
-//                   DOUBLE values, and each STRING value's length
+//                   DOUBLE values, and each STRING value's length and where
+//                   its bytes are (TableArgs::srcw)
 //   (scan)          the lengths -> Arrow offsets (hipCUB inclusive sum)
 //   k_table_chars   one wave per 64 rows of a STRING column: the column's
 //                   bytes of those rows, written 4-byte word by word
@@ -397,11 +398,12 @@ __global__ __launch_bounds__(TB) void k_table_values(const DeviceArgs* __restric
     const LP_G uint8_t *line = nullptr, *region = nullptr;
     const bool ok = row_view(P, C, buf, i, line, region);
     const int fmt = ok && P.n_fmt > 1 ? (int)C.fmt_id[i] : 0;
-    for (int c = 0; c < T.n_cols; ++c) {
+    for (int c = 0, rank = 0; c < T.n_cols; ++c) {
         const TableCol& col = T.cols[c];
         bool valid = false;
         int64_t x = 0;
         double d = 0.0;
+        uint64_t w = 0;
         // the later delivery, then (a value that is none for the column) the earlier
         for (int pass = 0; pass < 2 && ok && !valid; ++pass) {
             const TableSrc& sc = pass ? col.alt[fmt] : col.src[fmt];
@@ -410,6 +412,12 @@ __global__ __launch_bounds__(TB) void k_table_values(const DeviceArgs* __restric
             valid = v.kind != 0;
             if (col.kind == 1) {  // STRING: its length now, its bytes after the scan
                 x = v.kind == 2 ? digits(v.l) : v.n + (v.amp ? 1u : 0u);
+                // where k_table_chars finds them (lp_table.h SW_*)
+                const uint64_t pa = (uint64_t)(uintptr_t)v.p;
+                if (v.kind == 1 && pa < SW_AMP) w = pa | (v.amp ? SW_AMP : 0ull);
+                else if (v.kind == 2 && v.l >= -(int64_t)SW_AMP && v.l < (int64_t)SW_AMP)
+                    w = SW_LONG | ((uint64_t)v.l & (SW_LONG - 1));
+                else w = SW_SLOW;
             } else if (col.kind == 2) {
                 x = v.l;
                 if (v.kind == 1) valid = parse_long(v.p, v.n, v.amp, x);
@@ -424,6 +432,7 @@ __global__ __launch_bounds__(TB) void k_table_values(const DeviceArgs* __restric
         if (col.kind == 1) {
             col.i64[k + 1] = valid ? x : 0;
             if (k == 0) col.i64[0] = 0;
+            T.srcw[(int64_t)rank++ * T.count + k] = valid ? w : 0;
         } else if (col.kind == 2) {
             if (valid) col.i64[k] = x;
         } else if (valid) {
@@ -470,30 +479,44 @@ __global__ __launch_bounds__(64 * CW) void k_table_chars(const DeviceArgs* __res
     const uint64_t D0 = (uint64_t)col.i64[k0], D1 = (uint64_t)col.i64[kend];
     uint32_t flag = 0;  // bit 0: bytes in the scratch; bit 1: a leading '&'
     uint64_t src = 0;
+    // the row's value as k_table_values found it (one coalesced word: no
+    // status -> line -> span chain here); a long is formatted into the wave's
+    // scratch, a SW_SLOW value derived again
+    const uint64_t w = k < kend ? T.srcw[(int64_t)blockIdx.y * T.count + k] : 0;
     if (k < kend && col.valid[k]) {
-        const LP_G uint8_t *line = nullptr, *region = nullptr;
-        if (row_view(P, C, buf, T.first + k, line, region)) {
-            const int fmt = P.n_fmt > 1 ? (int)C.fmt_id[T.first + k] : 0;
-            TVal v = tvalue(P, C, T, col.src[fmt], T.first + k, line, region);
-            if (v.kind == 0) v = tvalue(P, C, T, col.alt[fmt], T.first + k, line, region);  // the earlier delivery
-            uint8_t* f = &s_fmt[wv][lane * FMTB];
-            if (v.kind == 2) {
-                uint64_t u = v.l < 0 ? 0 - (uint64_t)v.l : (uint64_t)v.l;
-                const uint32_t n = digits(v.l);
-                uint32_t q = n;
-                do {
-                    f[--q] = (uint8_t)('0' + u % 10);
-                    u /= 10;
-                } while (u);
-                if (v.l < 0) f[0] = '-';
-                flag = 1;
-            } else if (v.kind == 3) {
-                for (uint32_t q = 0; q < v.n; ++q) f[q] = (uint8_t)v.buf[q];
-                flag = 1;
-            } else {
-                src = (uint64_t)(uintptr_t)v.p;
-                flag = v.amp ? 2u : 0u;
+        uint8_t* f = &s_fmt[wv][lane * FMTB];
+        TVal v;
+        if ((w >> 62) == 0) {
+            v.kind = 1;
+            v.p = reinterpret_cast<const LP_G uint8_t*>((uintptr_t)(w & (SW_AMP - 1)));
+            v.amp = (w & SW_AMP) != 0;
+        } else if ((w >> 62) == 1) {
+            v.kind = 2;
+            v.l = (int64_t)(w << 2) >> 2;
+        } else {
+            const LP_G uint8_t *line = nullptr, *region = nullptr;
+            if (row_view(P, C, buf, T.first + k, line, region)) {
+                const int fmt = P.n_fmt > 1 ? (int)C.fmt_id[T.first + k] : 0;
+                v = tvalue(P, C, T, col.src[fmt], T.first + k, line, region);
+                if (v.kind == 0) v = tvalue(P, C, T, col.alt[fmt], T.first + k, line, region);  // the earlier delivery
             }
+        }
+        if (v.kind == 2) {
+            uint64_t u = v.l < 0 ? 0 - (uint64_t)v.l : (uint64_t)v.l;
+            const uint32_t n = digits(v.l);
+            uint32_t q = n;
+            do {
+                f[--q] = (uint8_t)('0' + u % 10);
+                u /= 10;
+            } while (u);
+            if (v.l < 0) f[0] = '-';
+            flag = 1;
+        } else if (v.kind == 3) {
+            for (uint32_t q = 0; q < v.n; ++q) f[q] = (uint8_t)v.buf[q];
+            flag = 1;
+        } else {
+            src = (uint64_t)(uintptr_t)v.p;
+            flag = v.amp ? 2u : 0u;
         }
     }
     if (lane < nrows) {
@@ -566,10 +589,15 @@ __global__ __launch_bounds__(64 * CW) void k_table_chars(const DeviceArgs* __res
 
 }  // namespace
 
-size_t table_scratch_bytes(int64_t count) {
+// scratch: the scan's temporary storage, its sums, the STRING value words
+size_t table_srcw_offset(int64_t count) {
     size_t tmp = 0;
     hipcub::DeviceScan::InclusiveSum(nullptr, tmp, (const int64_t*)nullptr, (int64_t*)nullptr, (int)count);
-    return ((tmp + 255) & ~(size_t)255) + 8 * (size_t)count + 256;
+    return ((tmp + 255) & ~(size_t)255) + ((8 * (size_t)count + 255) & ~(size_t)255);
+}
+
+size_t table_scratch_bytes(int64_t count, int n_str) {
+    return table_srcw_offset(count) + 8 * (size_t)count * (size_t)n_str + 256;
 }
 
 int launch_table_values(const DeviceArgs* d_args, const TableArgs* d_targs, const TableArgs& ta, const uint8_t* buf,

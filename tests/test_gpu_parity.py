@@ -1043,11 +1043,22 @@ def test_chunk_geometry_gpu(oracle):
     pb = lpa.HttpdLoglineParser("combined", fields)
     rb0 = pb.parse_batch(big)
     assert rb0.diag["deferred_chunks"] == 0
-    for d in (data, big):
+    # -2: the odd chunks deferred, the even ones finished by k_parse_chunks
+    # (line_off boundaries between a finished and a deferred chunk; the last
+    # chunk's sentinel from either pass), and a small positive wait
+    n_chunks = {}  # (-1 defers every chunk: their number)
+    for d, wait in ((data, -1), (big, -1), (data, -2), (big, -2), (big, 8)):
         ref = r0 if d is data else rb0
-        p = lpa.HttpdLoglineParser("combined", fields, options={lpa.OPT_CHUNK_WAIT: -1})
+        p = lpa.HttpdLoglineParser("combined", fields, options={lpa.OPT_CHUNK_WAIT: wait})
         r = p.parse_batch(d)
-        assert r.diag["deferred_chunks"] > 0, r.diag
+        nd = r.diag["deferred_chunks"]
+        if wait == -1:
+            assert nd > 1, r.diag
+            n_chunks[id(d)] = nd
+        elif wait == -2:
+            assert 0 < nd <= n_chunks[id(d)] // 2 + 1, (nd, n_chunks[id(d)])  # the odd ones
+        else:
+            assert 0 <= nd <= n_chunks[id(d)], r.diag
         assert r.n_lines == ref.n_lines and (r.status == ref.status).all()
         assert r.counters == ref.counters
         for i in range(0, ref.n_lines, 1 if d is data else 37):
