@@ -567,15 +567,16 @@ def main():
     avg_pk, avg_uk = sum(pk_ms) / len(pk_ms), sum(uk_ms) / len(uk_ms)
     algo_bytes = stats["bytes_in"] + stats["bytes_out"]
     pass_gbs = algo_bytes / (avg_parse / 1e3) / 1e9
-    # the dominant kernel: k_parse_lines (the parse kernels' HIP-event time on
+    # the dominant kernel: k_parse_chunks (the parse kernels' HIP-event time on
     # the launch stream; their algorithmic bytes: the input once, the line
     # index, their columns)
     pk_bytes, uk_bytes = stats["bytes_parse_kernels"], stats["bytes_uri_kernels"]
     achieved = pk_bytes / (avg_pk / 1e3) / 1e9
     uri_gbs = uk_bytes / (avg_uk / 1e3) / 1e9 if avg_uk > 0 else 0.0
     with_pmc = wl == 2 and args.fields == "all"
-    # the dominant kernel: one LogFormat -> the one-pass chunked parse
-    pk_name = "k_parse_chunks" if len(fmt.split("\n")) == 1 else "k_parse_lines"
+    # the dominant kernel: the one-pass chunked parse (several LogFormats: its
+    # routing instance, k_parse_chunks<.., MF>, since round 6)
+    pk_name = "k_parse_chunks" if len(fmt.split("\n")) == 1 else "k_parse_chunks (several LogFormats: routing instance)"
 
     result = {
         "metric": "GB/s (and lines/s) of 'combined' log parsed per GPU and per 8xMI355X node",
@@ -637,7 +638,7 @@ def main():
                 "traffic": pmc_traffic(args.pmc_json, stats["lines"], lpa.LIB_PATH, "k_uri_lines") if with_pmc else None,
             },
             "parse_pass": {
-                "kernels": "k_parse_chunks / k_parse_lines + k_uri_lines (+ their overflow paths, counter reduction)",
+                "kernels": "k_parse_chunks (+ k_parse_deferred, k_route_ovf, k_parse_ovf_lines) + k_uri_lines (+ its overflow path, counter reduction)",
                 "ms": round(avg_parse, 3), "achieved": round(pass_gbs, 1), "frac": round(pass_gbs / HBM_PEAK_GBS, 4),
                 "algorithmic_bytes": int(algo_bytes), "bytes_per_line": round(algo_bytes / max(1, stats["lines"]), 1),
             },

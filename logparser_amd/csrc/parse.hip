@@ -35,6 +35,9 @@ constexpr int MAXS = PW + 1;
 #ifndef LP_CHUNK_LMAX
 #define LP_CHUNK_LMAX 54  // lines per chunk at most (one-format programs)
 #endif
+#ifndef LP_MF_WPE
+#define LP_MF_WPE 2  // waves per SIMD the several-format chunk instance is compiled for (its registers)
+#endif
 #ifndef LP_CHUNK_LMAX_MF
 #define LP_CHUNK_LMAX_MF 58  // the same for several-format programs (VGPR-bound at 8 waves per CU: 58 measured 6 % faster than 54 on config 5)
 #endif  // line starts a chunk keeps in LDS (its 64 lines and the next start)
@@ -457,7 +460,7 @@ __device__ __forceinline__ void parse_chunk(const uint8_t* __restrict__ buf, uin
 // SIMPLE: the instance for Apache common / combined family programs
 // (phase1; the host's simple_program picks it).
 template <bool LA, bool SIMPLE, bool MF>
-__global__ __launch_bounds__(PW, 2) void k_parse_chunks(const uint8_t* __restrict__ buf, uint64_t nbytes,
+__global__ __launch_bounds__(PW, MF ? LP_MF_WPE : 2) void k_parse_chunks(const uint8_t* __restrict__ buf, uint64_t nbytes,
                                                      const DeviceArgs* __restrict__ args, uint32_t cb, uint32_t win_cap,
                                                      uint32_t stk_words, int direct, int wait_max) {
     const Program& P = args->prog;
@@ -760,7 +763,7 @@ ChunkPlan chunk_plan(const ParseLaunch& a) {
     // fixes the count
     uint64_t lines = a.chunk_lines ? a.chunk_lines : 54;
     if (!a.chunk_lines) {
-        const int maxw = a.multi ? 8 : LP_CHUNK_MAXW;
+        const int maxw = a.multi ? 4 * LP_MF_WPE : LP_CHUNK_MAXW;
         const uint64_t lmax = a.multi ? LP_CHUNK_LMAX_MF : LP_CHUNK_LMAX;
         uint64_t best = 0;
         for (int k = 8; k <= maxw; ++k) {
