@@ -99,6 +99,40 @@ void emu_uplist(const char* v, int len, int p, int off, int dec, int* out) {
     out[1] = uplist_at_r(L, p, dec != 0);
 }
 
+// UpstreamListDissector's split of the token v[0, len) (at byte offset `off`
+// of an aligned buffer): uplist_items (byte reads) and, when tok_load takes
+// the token (at most 32 bytes), uplist_items_r (registers); per item its
+// four trimmed positions and secms_value / secms_value_r of the value and
+// redirected spans (digits '.' digits items only: dec).  out: [0] the byte
+// count, [1] the register count (-2: not loaded), then 16 items x 8 int64
+// for each version.  Returns 0.
+int emu_uplist_items(const char* v, int len, int off, int dec, int64_t* out) {
+    std::vector<uint8_t> buf((size_t)off, 0xA5);
+    buf.insert(buf.end(), v, v + len);
+    buf.resize(((buf.size() + 8 + 3) & ~(size_t)3) + 40, 0xA5);
+    const Line L{buf.data(), (uint32_t)off, len};
+    for (int k = 0; k < 2 + 2 * 16 * 8; ++k) out[k] = 0;
+    auto rec = [&](int64_t* o, auto&& sm) {
+        return [o, &sm](int k, int va, int vb, int ra, int rb) {
+            if (k >= 16) return;
+            int64_t* e = o + 8 * k;
+            e[0] = va; e[1] = vb; e[2] = ra; e[3] = rb;
+            e[4] = sm(va, vb);
+            e[5] = sm(ra, rb);
+        };
+    };
+    auto sm_b = [&](int a, int b) -> int64_t { return dec ? secms_value(L, a, b) : 0; };
+    out[0] = uplist_items(L, 0, len, rec(out + 2, sm_b));
+    TokReg T;
+    if (tok_load(L, 0, len, T)) {
+        auto sm_r = [&](int a, int b) -> int64_t { return dec ? secms_value_r(T, a, b) : 0; };
+        out[1] = uplist_items_r(T, 0, len, rec(out + 2 + 16 * 8, sm_r));
+    } else {
+        out[1] = -2;
+    }
+    return 0;
+}
+
 // parse_strf_time of the program's first time stage on the value v[0, len)
 // placed at byte offset `off` (0..3) of an aligned buffer, with the stage's
 // fixed-layout plan (use_fixed 1) or the general element loop only (0):

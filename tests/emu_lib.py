@@ -60,6 +60,9 @@ def lib():
         L.emu_token_table.argtypes = [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
         L.emu_uplist.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                  ctypes.POINTER(ctypes.c_int)]
+        L.emu_uplist_items.restype = ctypes.c_int
+        L.emu_uplist_items.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.POINTER(ctypes.c_int64)]
         L.emu_strf.restype = ctypes.c_int
         L.emu_strf.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                ctypes.POINTER(ctypes.c_int64)]
@@ -148,6 +151,21 @@ def uplist(line, p, off, dec):
     out = (ctypes.c_int * 2)()
     lib().emu_uplist(line, len(line), p, off, 1 if dec else 0, out)
     return out[0], out[1]
+
+
+def uplist_items(tok, off, dec):
+    """UpstreamListDissector split of the token (bytes) by uplist_items and
+    uplist_items_r: ((count, items), (count or -2, items)), an item being
+    (va, vb, ra, rb, value ms, redirected ms)"""
+    out = (ctypes.c_int64 * (2 + 2 * 16 * 8))()
+    lib().emu_uplist_items(tok, len(tok), off, 1 if dec else 0, out)
+    res = []
+    for v in range(2):
+        n = out[v]
+        base = 2 + 16 * 8 * v
+        items = [tuple(out[base + 8 * k + j] for j in range(6)) for k in range(max(0, min(n, 16)))]
+        res.append((n, items))
+    return tuple(res)
 
 
 def possible_paths(logformat, depth=15):

@@ -822,3 +822,44 @@ def test_upstream_list_register_scan_emulated(emu):
                     assert a == b, (line, off, dec, a, b)
                     n += 1
     assert n > 20000
+
+
+def test_upstream_list_split_register_edges_emulated(emu):
+    """uplist_items_r / secms_value_r (the URI kernel's list stage on a token
+    of at most 32 bytes held in registers) against uplist_items /
+    secms_value (one read per byte) on constructed edge tokens: lengths 31,
+    32 and 33 (33: not loaded, the byte path alone), a ', ' or ': ' separator
+    in the last two bytes, separators only, whitespace-only tokens, empty
+    servers, ': ' pairs without parts, at every byte offset of a word."""
+    import random
+    rng = random.Random(20261019)
+    toks = [b"", b" ", b"   ", b"\t \t", b", ", b", , ", b": ", b" : ", b",", b":", b"1, ", b"1: ", b"1, 2: ",
+            b", 1", b": 1", b"1 : 2", b"1,2", b"1:2", b"0.001, 0.002 : 0.003", b"1.5, -, 2.25"]
+    # lengths around the register window, the separator placed at its end
+    for L in (30, 31, 32, 33, 34):
+        for tail in (b", ", b": ", b",", b" ", b", 7", b": 7", b""):
+            body = b"0.1, 2.25 : 3.0, " * 4
+            t = body[: max(0, L - len(tail))] + tail
+            toks.append(t[:L])
+            toks.append((b" " * L)[:L])
+            toks.append((b", " * 20)[:L])
+            toks.append((b": " * 20)[:L])
+    for _ in range(3000):
+        n = rng.choice([rng.randint(0, 34), 31, 32, 33])
+        alpha = rng.choice([b"0123456789., :", b"0123456789., : \t", b"ab.1, :-"])
+        toks.append(bytes(rng.choice(alpha) for _ in range(n)))
+    n_reg = 0
+    for t in toks:
+        dec = all(c in b"0123456789." for c in t.replace(b", ", b"").replace(b": ", b"").replace(b" ", b""))
+        for off in range(4):
+            (nb, ib), (nr, ir) = emu.uplist_items(t, off, dec)
+            if len(t) > 32:
+                assert nr == -2, (t, nr)
+                continue
+            n_reg += 1
+            assert nr == nb, (t, off, nb, nr)
+            if dec:
+                assert ir == ib, (t, off, ib, ir)
+            else:
+                assert [x[:4] for x in ir] == [x[:4] for x in ib], (t, off, ib, ir)
+    assert n_reg > 5000
