@@ -36,7 +36,8 @@ constexpr int MAXS = PW + 1;
 #define LP_CHUNK_LMAX 54  // lines per chunk at most (one-format programs)
 #endif
 #ifndef LP_MF_WPE
-#define LP_MF_WPE 2  // waves per SIMD the several-format chunk instance is compiled for (its registers)
+#define LP_MF_WPE 3  // waves per SIMD the several-format chunk instance is compiled for: 3 (168 VGPRs, a few
+                     // spilled) measured 10 % faster parse kernels on config 5 than 2 (216 VGPRs), profiles/r06w/mfab
 #endif
 #ifndef LP_CHUNK_LMAX_MF
 #define LP_CHUNK_LMAX_MF 58  // the same for several-format programs (VGPR-bound at 8 waves per CU: 58 measured 6 % faster than 54 on config 5)
@@ -759,7 +760,7 @@ ChunkPlan chunk_plan(const ParseLaunch& a) {
     // lines per chunk: at most 54 (measured best at 8 waves per CU, config 2:
     // tools/chunk_sweep.py), and the count that puts the most lines in
     // flight per CU (waves x lines) over the wave counts the registers allow
-    // (the several-format instance: 2 waves per SIMD); LP_OPT_CHUNK_LINES
+    // (the several-format instance: LP_MF_WPE waves per SIMD); LP_OPT_CHUNK_LINES
     // fixes the count
     uint64_t lines = a.chunk_lines ? a.chunk_lines : 54;
     if (!a.chunk_lines) {

@@ -608,8 +608,11 @@ __device__ __forceinline__ bool uri_compact(const uint8_t* __restrict__ buf, uin
 
 // 16 waves per CU: the LDS share allows them, and __launch_bounds__(64, 4)
 // (4 waves per SIMD) keeps the registers within 128
+#ifndef LP_URI_SLOT_WPE
+#define LP_URI_SLOT_WPE 4  // waves per SIMD of the several-format (SLOT) instance
+#endif
 template <int NU, int NQ, bool SLOT>
-__global__ __launch_bounds__(PW, 4) void k_uri_lines(const uint8_t* __restrict__ buf, uint64_t nbytes,
+__global__ __launch_bounds__(PW, SLOT ? LP_URI_SLOT_WPE : 4) void k_uri_lines(const uint8_t* __restrict__ buf, uint64_t nbytes,
                                                      const DeviceArgs* __restrict__ args) {
     const Program& P = args->prog;
     const Columns& C = args->cols;
