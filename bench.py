@@ -611,6 +611,8 @@ def main():
             "backend": backend,
             "batches_per_step": len(batches),
         },
+        # this rank's (rank 0's) batch; with several ranks the all-reduced
+        # totals are status_counts_all_ranks
         "status_counts": {k: int(stats[k]) for k in ("lines", "ok", "bad", "fallback")},
         "parse_diag": {"overflow_waves": int(stats.get("overflow_waves", 0)), "retries": int(stats.get("retries", 0)),
                        "waves": (int(stats["lines"]) + 63) // 64},
@@ -661,6 +663,8 @@ def main():
         result["config"]["corpus_bytes_all_ranks"] = total_bytes
         if rank == 0:
             result["pcie_inclusive"] = pcie_inclusive(torch, parser, buf, batches, 8 << 30)
+    if world > 1:
+        result["status_counts_all_ranks"] = {k: int(counters[j]) for j, k in enumerate(("lines", "ok", "bad", "fallback"))}
     if rank == 0 and wl != 5 and not args.no_delivery:
         result["delivery"] = host_delivery(lpa, torch, parser, stats["lines"], wl)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
